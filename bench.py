@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Headline benchmark: CAR placement scoring, pod×node move evaluations / s.
+
+Workload (BASELINE.json configs[2]): 100k pods, 5k
+nodes, preferential-attachment relation tree, S = 4096 what-if scenarios per
+GPU.  One step = one pass of the hot path over one batch: librsk's CAR pipeline
+(car_prep + car_light + car_heavy) scores every pod in every scenario against
+every node — P·N·S evaluations — with all inputs resident in HBM.
+
+Multi-GPU (``torchrun --nproc-per-node N``): scenario sharding, rank r scores
+global scenarios [r·S, (r+1)·S) with no data-path collective; ``value`` is the
+whole-job rate (weak scaling).  Timing: barrier + device sync around exactly
+``--steps`` steps, max over ranks.  Per-kernel times come from HIP events on the
+stream the kernels run on (librsk's profiler).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(REPO, "kubernetes-rescheduling_amd"), REPO]
+
+import numpy as np  # noqa: E402
+
+METRIC = "pod×node move evaluations/sec at 100k pods×5k nodes; % of HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+CONFIGS = {
+    "headline": dict(P=100_000, N=5_000, S=4096, name="100k pods x 5k nodes, PA tree, 4096 scenarios/GPU (config 3)"),
+    "2k64": dict(P=2_000, N=64, S=1, name="2k pods x 64 nodes, single CAR round (config 2)"),
+    "1m50k": dict(P=1_000_000, N=50_000, S=64, name="1M pods x 50k nodes, 64 scenarios/GPU (config 4 sizes)"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def algorithmic_bytes(P, N, S, nnz, Q_light=None, light_rec_bytes=0):
+    """B = 4(P+1) + 4nnz + 4PS + 4N + 5NS + 4PS per batch."""
+    return 4 * (P + 1) + 4 * nnz + 4 * P * S + 4 * N + 5 * N * S + 4 * P * S
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="headline", choices=sorted(CONFIGS))
+    ap.add_argument("--scenarios", type=int, default=0, help="override S per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_headline.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from rsk import _lib, api, synth
+
+    cfg = dict(CONFIGS[args.config])
+    if args.scenarios:
+        cfg["S"] = args.scenarios
+    P, N, S = cfg["P"], cfg["N"], cfg["S"]
+    t0 = time.time()
+    c = synth.make_cluster(P, N, S=S, seed=0, s0=rank * S)
+    log(f"[bench] rank {rank}: generated {P}x{N}x{S} in {time.time() - t0:.1f}s")
+
+    ctx = _lib.Context(local)
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_stream(stream.cuda_stream)
+    plan = api.CarPlan(c.row_ptr, c.col_idx, ctx=ctx)
+    T = {k: torch.from_numpy(getattr(c, k)).to(dev) for k in ("assign", "cap_cpu", "use_cpu", "hazard")}
+    out_t = torch.empty(P * S, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+
+    def step():
+        plan.execute(T["assign"], S, T["cap_cpu"], T["use_cpu"], T["hazard"], N, out_t, None, device=True)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    ctx.reset_profiling()
+    ctx.set_profiling(True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    ctx.set_profiling(False)
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    kernels = {}
+    for name in ("car_prep", "car_light", "car_heavy"):
+        ms, n = ctx.kernel_time(name)
+        if n:
+            kernels[name] = {"avg_ms": ms / n, "launches": n, "per_step_ms": ms / args.steps}
+    ms_step = elapsed * 1e3 / args.steps
+    evals = P * N * S
+    value = world * evals / (ms_step / 1e3)
+
+    # parity spot check against the oracle on sampled rows of this rank's batch
+    from oracle import oracle as orc
+    deg = np.diff(c.row_ptr)
+    rng = np.random.default_rng(rank)
+    rows = np.unique(np.concatenate([np.argsort(deg)[-4:], rng.choice(P, 28, replace=False)])).astype(np.int32)
+    got = out_t.view(P, S)[torch.from_numpy(rows).to(dev).long()].cpu().numpy().reshape(-1)
+    exp, _ = orc.car(c.row_ptr, c.col_idx, c.assign, S, c.cap_cpu, c.use_cpu, c.hazard, N, rows=rows,
+                     threads=min(16, os.cpu_count() or 1))
+    parity_ok = bool(np.array_equal(got, exp))
+
+    # roofline: dominant kernel = car_light (light rows: deg <= 16); its algorithmic
+    # bytes = own assign slice + target slice per light row (8 B per cell) + its ELL rows
+    Q_light = int((deg <= 16).sum())
+    ell_w = {2: 4, 4: 8, 8: 12, 16: 20}
+    light_bytes = 8 * Q_light * S + 4 * sum(ell_w[min(w for w in ell_w if w >= max(int(d), 1))] for d in deg[deg <= 16])
+    B = algorithmic_bytes(P, N, S, c.nnz)
+    roof = None
+    if "car_light" in kernels:
+        t = kernels["car_light"]["avg_ms"] / 1e3
+        ach = light_bytes / t / 1e9
+        roof = {"bound": "hbm", "kernel": "car_light", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "algorithmic_bytes": light_bytes}
+        try:
+            with open(args.pmc_json) as f:
+                pmc = json.load(f)
+            entry = pmc.get(args.config, {}).get("car_light")
+            if entry and entry.get("S") == S:
+                roof["traffic"] = entry["hbm_bytes_per_launch"]
+                roof["traffic_source"] = os.path.relpath(args.pmc_json, REPO)
+        except (OSError, ValueError):
+            pass
+    step_ach = B / (ms_step / 1e3) / 1e9
+    roof_step = {"bound": "hbm", "achieved": round(step_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": round(step_ach / HBM_PEAK_GBS, 4), "algorithmic_bytes": B,
+                 "note": "whole CAR step (prep+light+heavy launches, wall clock) vs SURVEY §8d B"}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = min(16, os.cpu_count() or 1)
+        probe = np.arange(0, P, max(1, P // 8), dtype=np.int32)[:8]
+        t1 = time.perf_counter()
+        orc.car(c.row_ptr, c.col_idx, c.assign, S, c.cap_cpu, c.use_cpu, c.hazard, N, rows=probe, threads=threads)
+        per_row = (time.perf_counter() - t1) / len(probe)
+        nrows = int(max(8, min(P, args.cpu_seconds / max(per_row, 1e-9))))
+        sample = np.linspace(0, P - 1, nrows).astype(np.int32)
+        t1 = time.perf_counter()
+        orc.car(c.row_ptr, c.col_idx, c.assign, S, c.cap_cpu, c.use_cpu, c.hazard, N, rows=sample, threads=threads)
+        dt = time.perf_counter() - t1
+        cpu = {"value": round(nrows * S * N / dt, 1), "unit": "pod×node evals/s", "cores": threads, "kind": "port",
+               "sample": f"{nrows} evenly spaced pods x {S} scenarios x {N} nodes ({dt:.1f}s), oracle/rsk_oracle.c "
+                         f"literal CAR restatement, OpenMP {threads} threads",
+               "seconds": round(dt, 2)}
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "pod×node evals/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
+            "config": {"workload": cfg["name"], "pods": P, "nodes": N, "scenarios_per_gpu": S, "nnz": c.nnz,
+                       "max_degree": int(deg.max()), "parallelism": f"scenario-sharded x{world}"},
+            "roofline": roof, "roofline_step": roof_step, "cpu_baseline": cpu, "kernels": kernels,
+            "parity_sample_ok": parity_ok, "hbm_bytes_algorithmic_per_step": B,
+        }
+        print(json.dumps(line), flush=True)
+    plan.close()
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

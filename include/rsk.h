@@ -1,0 +1,148 @@
+/*
+ * rsk.h — C ABI of librsk.so, the MI355X (gfx950) placement-scoring library.
+ *
+ * The reference (ye0nj00/Kubernetes-Rescheduling) is pure Python: its
+ * placement policies are the five functions of rescheduling.py and there is no
+ * FFI.  This header is the boundary the drop-in Python module
+ * (kubernetes-rescheduling_amd/rescheduling.py) binds with ctypes; each entry
+ * point names the reference code it replaces.  No torch types cross it: only
+ * plain pointers, sizes and status codes.
+ *
+ * Conventions
+ *  - Every pointer argument is caller-owned.  With RSK_F_DEVICE in `flags`,
+ *    ALL array pointers of the call are device (HBM) pointers and the call is
+ *    asynchronous on the context's stream; otherwise they are host pointers
+ *    and the call is synchronous (inputs copied in, outputs copied back).
+ *  - Per-scenario arrays are scenario-minor: x[i*S + s] for pod/node/row i and
+ *    scenario s.  Per-node constants (cap_cpu, name_rank) are x[n].
+ *  - Placement results: >= 0 node index; RSK_TARGET_NONE (-1) where the
+ *    reference yields nodeName=None; RSK_TARGET_NO_CANDIDATE (-2) where it raises
+ *    (ValueError in communication(), RuntimeError in spread/binpack/random).
+ *  - Values: cap_cpu / use_cpu are millicores in [0, 2^31-1]; node indices in
+ *    [0, N); an assign entry outside [0, N) means "not on any node".
+ *  - Return codes below; rsk_last_error() gives a thread-local message.
+ *  - One context = one device + one stream.  A context is not shareable across
+ *    threads; separate contexts may run concurrently.
+ */
+#ifndef RSK_H
+#define RSK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSK_OK 0
+#define RSK_NO_CANDIDATE 1 /* some cell had no candidate node (host-pointer calls) */
+#define RSK_EINVAL 2       /* bad argument: null pointer, size or range */
+#define RSK_EHIP 3         /* HIP runtime error */
+#define RSK_ERCCL 4        /* reserved: collective error */
+
+#define RSK_F_DEVICE 1u    /* all array pointers are device pointers; async */
+
+#define RSK_TARGET_NONE (-1)
+#define RSK_TARGET_NO_CANDIDATE (-2)
+
+typedef struct rsk_ctx rsk_ctx;
+typedef struct rsk_car_plan rsk_car_plan;
+
+/* ---- library / context ---------------------------------------------------- */
+int rsk_version(void);                                /* 100*major + minor */
+const char *rsk_last_error(void);                     /* thread-local, never NULL */
+int rsk_ctx_create(int device, rsk_ctx **out);
+int rsk_ctx_destroy(rsk_ctx *ctx);
+/* Run subsequent work on `hip_stream` (a hipStream_t; NULL = the context's own). */
+int rsk_ctx_set_stream(rsk_ctx *ctx, void *hip_stream);
+int rsk_ctx_synchronize(rsk_ctx *ctx);
+/* Kernel timing with HIP events recorded on the context's stream around every
+ * launch of the named kernel ("car_light", "car_heavy", "car_prep", ...). */
+int rsk_ctx_set_profiling(rsk_ctx *ctx, int on);
+int rsk_ctx_kernel_time(rsk_ctx *ctx, const char *kernel, double *total_ms, int64_t *launches);
+int rsk_ctx_reset_profiling(rsk_ctx *ctx);
+
+/* ---- CAR (communication-aware rescheduling) -------------------------------
+ * Replaces the score loop and argmax of `communication`
+ * (rescheduling.py:183-214) for a batch of moving pods x scenarios.
+ *   row_ptr[P+1], col_idx[nnz] : pod->pod relation CSR: q in row p iff
+ *        dep(q) in relations[dep(p)] (main.py:31-52 at pod level).  Host
+ *        pointers.  Duplicates and the self edge are dropped by the plan (the
+ *        evicted pod is off the cluster, main.py:73).
+ *   rows[Q] : the moving pods (NULL = all P, Q ignored).  Host pointer.
+ * A plan uploads the CSR once and bins rows by degree; execute() may then run
+ * any number of scenario batches against it.                                  */
+int rsk_car_plan_create(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, int32_t P,
+                        const int32_t *rows, int32_t Q, rsk_car_plan **out);
+int rsk_car_plan_destroy(rsk_car_plan *plan);
+/*   assign[P*S], use_cpu[N*S], hazard[N*S] (0/1), cap_cpu[N]
+ *   out_target[Q*S] : node per (row, scenario), codes as above
+ *   out_score[Q*S]  : max_score of rescheduling.py:199, -1 when no candidate
+ *                     (may be NULL)                                            */
+int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, const int32_t *cap_cpu,
+                         const int32_t *use_cpu, const uint8_t *hazard, int32_t N,
+                         int32_t *out_target, int32_t *out_score, uint32_t flags);
+/* One-shot convenience: plan_create + execute + destroy. */
+int rsk_car_place(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, int32_t P,
+                  const int32_t *assign, int32_t S, const int32_t *cap_cpu, const int32_t *use_cpu,
+                  const uint8_t *hazard, int32_t N, const int32_t *rows, int32_t Q,
+                  int32_t *out_target, int32_t *out_score, uint32_t flags);
+
+/* ---- baselines --------------------------------------------------------------
+ * spread  (rescheduling.py:89-101): argmin over non-hazard n of
+ *         (pod_count[n*S+s], name_rank[n]) -> out_node[s].
+ * binpack (rescheduling.py:121-133): argmax of (cpu_pct[n*S+s], name_rank[n]).
+ * name_rank[n] = rank of node n's name in Python str (code point) order.      */
+int rsk_spread_place(rsk_ctx *ctx, const int32_t *pod_count, const int32_t *name_rank,
+                     const uint8_t *hazard, int32_t N, int32_t S, int32_t *out_node, uint32_t flags);
+int rsk_binpack_place(rsk_ctx *ctx, const int32_t *cpu_pct, const int32_t *name_rank,
+                      const uint8_t *hazard, int32_t N, int32_t S, int32_t *out_node, uint32_t flags);
+/* random (rescheduling.py:149-153) in two halves around the caller's RNG:
+ *   rsk_random_count:  out_count[s] = #non-hazard nodes (len(candidates))
+ *   rsk_random_select: out_node[s] = the r[s]-th non-hazard node in index order
+ *                      (candidates[r]); -2 when r is out of range.
+ * rsk_random_place draws r[s] = Random(seeds[s])._randbelow(count[s]) with a
+ * CPython-compatible MT19937 on the host and runs both halves.               */
+int rsk_random_count(rsk_ctx *ctx, const uint8_t *hazard, int32_t N, int32_t S, int32_t *out_count,
+                     uint32_t flags);
+int rsk_random_select(rsk_ctx *ctx, const uint8_t *hazard, int32_t N, int32_t S, const int32_t *r,
+                      int32_t *out_node, uint32_t flags);
+int rsk_random_place(rsk_ctx *ctx, const uint8_t *hazard, int32_t N, int32_t S, const uint64_t *seeds,
+                     int32_t *out_node, uint32_t flags);
+/* CPython random.Random(seed)._randbelow(n) (host only; 0 < n < 2^31). */
+int32_t rsk_py_randbelow(uint64_t seed, int32_t n);
+
+/* ---- per-node reductions and metrics (kernel 3) ---------------------------
+ * rsk_node_reduce: pod_count[N*S], cpu_sum[N*S], mem_sum[N*S] (NULL to skip)
+ *                  of the pods assigned to each (node, scenario).
+ * rsk_cpu_pct:     int(round(use / cap * 100)), -1 if cap == 0
+ *                  (get_resource_usage.py:37), fp64, round-half-even.
+ * rsk_detect:      hazard = pct >= threshold, most[s] = first max hazard node
+ *                  or -1 (harzard_detect.py:3-27).
+ * rsk_load_std:    population std of use/cap*100 over nodes with cap > 0,
+ *                  0.0 if none (nodemonitor.py:24-50); fp64.
+ * rsk_cut_cost:    directed count of related pairs on different nodes
+ *                  (communicationcost.py:37-45), unscheduled = -1 compares as
+ *                  None; missing[p] (may be NULL) adds relations to absent
+ *                  deployments.  The reference's cost is out_directed / 2.
+ * rsk_pick_max_pod: first pod with the largest pod_cpu on node most[s]
+ *                  (delete_replaced_pod.py:41-61), -1 if none.              */
+int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, const int32_t *pod_cpu,
+                    const int64_t *pod_mem, int32_t N, int32_t *pod_count, int64_t *cpu_sum,
+                    int64_t *mem_sum, uint32_t flags);
+int rsk_cpu_pct(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *cap_cpu, int32_t N, int32_t S,
+                int32_t *out_pct, uint32_t flags);
+int rsk_detect(rsk_ctx *ctx, const int32_t *cpu_pct, int32_t N, int32_t S, int32_t threshold,
+               uint8_t *out_hazard, int32_t *out_most, uint32_t flags);
+int rsk_load_std(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *cap_cpu, int32_t N, int32_t S,
+                 double *out_std, uint32_t flags);
+int rsk_cut_cost(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, int32_t P,
+                 const int32_t *assign, int32_t S, const int32_t *missing, int64_t *out_directed,
+                 uint32_t flags);
+int rsk_pick_max_pod(rsk_ctx *ctx, const int32_t *assign, const int32_t *pod_cpu, int32_t P, int32_t S,
+                     const int32_t *most, int32_t *out_pod, uint32_t flags);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSK_H */

@@ -1,0 +1,631 @@
+// rsk_car.hip — CAR (communication-aware rescheduling) placement on gfx950.
+//
+// Replaces the score loop + argmax of `communication` (reference
+// rescheduling.py:183-214) for a batch of moving pods x what-if scenarios.
+//
+// For moving pod p and scenario s:
+//   score[n] = #{q in row p of the relation CSR : assign[q,s] == n},  n not hazard
+//   target   = argmax score; ties (|best| > 1) -> largest cap-use, first index,
+//              None if that remaining CPU is < 0; a single best node wins even
+//              when overloaded; no candidate at all -> the reference's ValueError.
+//
+// The dense score row has N entries but only the nodes holding p's neighbours
+// can score > 0, so each (p, s) cell is a histogram of deg(p) node ids:
+//   * max score M > 0: the winner is among the neighbour nodes.  With the
+//     lexicographic key (count, remaining CPU, -node) the argmax is the
+//     reference's choice; |best| == 1 iff exactly M neighbour entries reach M.
+//   * M == 0: every non-hazard node ties at 0 -> a per-scenario constant
+//     ("zero case"), computed once by car_prep_kernel.
+//
+// Kernels (one HIP stream, all integer, no atomics on the decision path):
+//   car_prep_kernel   nodekey[n*S+s] = hazard ? KEY_HAZ : cap[n]-use[n*S+s]
+//                     (one packed word per node gather later) + zero case per s.
+//   car_light_kernel  rows with deg <= 16: lane = scenario (64 consecutive
+//                     scenarios per wave -> each neighbour row is one coalesced
+//                     256-B load), per-lane register histogram, ELL rows.
+//   car_heavy_kernel  rows with deg > 16: one workgroup per (row, scenario
+//                     group); neighbour node ids staged in LDS, per-wave LDS hash
+//                     histograms, coalesced nodekey lookups, cross-lane reduce.
+#include <algorithm>
+#include <climits>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "rsk_common.h"
+
+namespace rsk {
+
+constexpr int kKeyHaz = INT_MIN;
+constexpr int kLightMax = 16;
+constexpr int kMaxDegree = 4096;
+constexpr int kNumLight = 4;                       // buckets D = 16, 8, 4, 2
+constexpr int kLightD[kNumLight] = {16, 8, 4, 2};
+constexpr int kLightW[kNumLight] = {20, 12, 8, 4};  // ELL record ints: oi, d, q[D], pad to x4
+constexpr int kNumHeavy = 4;                       // (16,64] (64,256] (256,1024] (1024,4096]
+constexpr int kHeavyMax[kNumHeavy] = {64, 256, 1024, 4096};
+
+struct CarState {
+    int bc;  // best count (max score); 0 = no non-hazard neighbour node
+    int br;  // remaining CPU of the best node
+    int bn;  // best node index
+    int nm;  // neighbour entries whose count == bc  (= bc * |best|)
+};
+
+__device__ __forceinline__ void st_init(CarState &st) {
+    st.bc = 0;
+    st.br = INT_MIN;
+    st.bn = INT_MAX;
+    st.nm = 0;
+}
+
+__device__ __forceinline__ void st_add(CarState &st, int c, int r, int n) {
+    if (c > st.bc) {
+        st.bc = c; st.br = r; st.bn = n; st.nm = 1;
+    } else if (c == st.bc) {
+        st.nm += 1;
+        if (r > st.br || (r == st.br && n < st.bn)) { st.br = r; st.bn = n; }
+    }
+}
+
+__device__ __forceinline__ CarState st_combine(CarState a, const CarState &b) {
+    if (b.bc > a.bc) return b;
+    if (b.bc < a.bc) return a;
+    a.nm += b.nm;
+    if (b.br > a.br || (b.br == a.br && b.bn < a.bn)) { a.br = b.br; a.bn = b.bn; }
+    return a;
+}
+
+__device__ __forceinline__ CarState st_shfl_xor(const CarState &st, int off) {
+    CarState o;
+    o.bc = __shfl_xor(st.bc, off, 64);
+    o.br = __shfl_xor(st.br, off, 64);
+    o.bn = __shfl_xor(st.bn, off, 64);
+    o.nm = __shfl_xor(st.nm, off, 64);
+    return o;
+}
+
+__device__ __forceinline__ unsigned long long zc_pack(int rem, int n) {
+    return ((unsigned long long)((unsigned)rem ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)n);
+}
+
+// rescheduling.py:199-214 applied to the reduced state.
+__device__ __forceinline__ int car_finalize(const CarState &st, int s, const int *__restrict__ zc_cnt,
+                                            const unsigned long long *__restrict__ zc_key, int &score) {
+    if (st.bc == 0) {
+        const int c = zc_cnt[s];
+        if (c == 0) { score = -1; return RSK_TARGET_NO_CANDIDATE; }
+        const unsigned long long k = zc_key[s];
+        const int n = (int)(~(unsigned)(k & 0xffffffffull));
+        const int rem = (int)((unsigned)(k >> 32) ^ 0x80000000u);
+        score = 0;
+        if (c == 1) return n;
+        return rem >= 0 ? n : RSK_TARGET_NONE;
+    }
+    score = st.bc;
+    if (st.nm == st.bc) return st.bn;
+    return st.br >= 0 ? st.bn : RSK_TARGET_NONE;
+}
+
+// ---------------------------------------------------------------------------
+// K0: packed node key + per-scenario zero case.
+// Thread t -> (scenario s = t % S, node chunk t / S): consecutive lanes read
+// consecutive scenarios of one node, i.e. coalesced rows of use / hazard.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void car_prep_kernel(const int *__restrict__ cap, const int *__restrict__ use,
+                                                       const uint8_t *__restrict__ haz, int N, int S, int npb,
+                                                       unsigned total, int *__restrict__ nodekey,
+                                                       int *__restrict__ zc_cnt,
+                                                       unsigned long long *__restrict__ zc_key) {
+    const unsigned t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= total) return;
+    const int s = (int)(t % (unsigned)S);
+    const int n0 = (int)(t / (unsigned)S) * npb;
+    const int n1 = min(N, n0 + npb);
+    int cnt = 0;
+    unsigned long long best = 0;
+    for (int n = n0; n < n1; ++n) {
+        const size_t idx = (size_t)n * S + s;
+        const int h = haz[idx];
+        const int key = h ? kKeyHaz : cap[n] - use[idx];
+        nodekey[idx] = key;
+        if (!h) {
+            ++cnt;
+            const unsigned long long pk = zc_pack(key, n);
+            best = pk > best ? pk : best;
+        }
+    }
+    if (cnt) {
+        atomicAdd(&zc_cnt[s], cnt);
+        atomicMax(&zc_key[s], best);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K1: light rows (deg <= 16), ELL records, per-lane register histograms.
+// ---------------------------------------------------------------------------
+struct LightArgs {
+    const int *ell[kNumLight];
+    int n_items[kNumLight];
+    int task_items[kNumLight];   // items per wave task
+    int task_prefix[kNumLight + 1];
+    const int *assign;
+    const int *nodekey;
+    const int *zc_cnt;
+    const unsigned long long *zc_key;
+    int *out_target;
+    int *out_score;
+    int S, N, SL, PS, blocks_per_chunk;
+};
+
+template <int D, int PK, int W>
+__device__ __forceinline__ void light_task(const LightArgs &a, const int *__restrict__ ell, int item0,
+                                           int item_end, int slot, int s, bool lane_ok) {
+    const int S = a.S;
+    const int step = PK * a.PS;
+    for (int base = item0; base < item_end; base += step) {
+        int oi[PK], dg[PK], nd[PK][D], ky[PK][D];
+        bool v[PK];
+#pragma unroll
+        for (int k = 0; k < PK; ++k) {
+            const int it = base + k * a.PS + slot;
+            v[k] = lane_ok && it < item_end;
+            const int4 *rec = reinterpret_cast<const int4 *>(ell + (size_t)(v[k] ? it : item0) * W);
+            int r[W];
+#pragma unroll
+            for (int w = 0; w < W / 4; ++w) {
+                const int4 x = rec[w];
+                r[4 * w] = x.x; r[4 * w + 1] = x.y; r[4 * w + 2] = x.z; r[4 * w + 3] = x.w;
+            }
+            oi[k] = r[0];
+            dg[k] = v[k] ? r[1] : 0;
+#pragma unroll
+            for (int j = 0; j < D; ++j)
+                nd[k][j] = j < dg[k] ? a.assign[(size_t)r[2 + j] * S + s] : -1;
+        }
+#pragma unroll
+        for (int k = 0; k < PK; ++k)
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                const int n = nd[k][j];
+                const bool ok = (unsigned)n < (unsigned)a.N;
+                ky[k][j] = ok ? a.nodekey[(size_t)n * S + s] : kKeyHaz;
+                if (!ok) nd[k][j] = -1 - j;  // never equal to another entry
+            }
+#pragma unroll
+        for (int k = 0; k < PK; ++k) {
+            CarState st;
+            st_init(st);
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                if (ky[k][j] == kKeyHaz) continue;
+                int c = 0;
+#pragma unroll
+                for (int jj = 0; jj < D; ++jj) c += nd[k][jj] == nd[k][j];
+                st_add(st, c, ky[k][j], nd[k][j]);
+            }
+            if (v[k]) {
+                int sc;
+                const int t = car_finalize(st, s, a.zc_cnt, a.zc_key, sc);
+                const size_t o = (size_t)oi[k] * S + s;
+                a.out_target[o] = t;
+                if (a.out_score) a.out_score[o] = sc;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void car_light_kernel(LightArgs a) {
+    const int chunk = blockIdx.x / a.blocks_per_chunk;
+    const int wave = (blockIdx.x % a.blocks_per_chunk) * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (wave >= a.task_prefix[kNumLight]) return;
+    const int slot = lane / a.SL;
+    const int s = chunk * a.SL + lane % a.SL;
+    const bool lane_ok = slot < a.PS && s < a.S;
+    int b = 0;
+    while (wave >= a.task_prefix[b + 1]) ++b;
+    const int lt = wave - a.task_prefix[b];
+    const int item0 = lt * a.task_items[b];
+    const int item_end = min(a.n_items[b], item0 + a.task_items[b]);
+    switch (b) {
+        case 0: light_task<16, 1, 20>(a, a.ell[0], item0, item_end, slot, s, lane_ok); break;
+        case 1: light_task<8, 2, 12>(a, a.ell[1], item0, item_end, slot, s, lane_ok); break;
+        case 2: light_task<4, 4, 8>(a, a.ell[2], item0, item_end, slot, s, lane_ok); break;
+        default: light_task<2, 4, 4>(a, a.ell[3], item0, item_end, slot, s, lane_ok); break;
+    }
+}
+constexpr int kLightPK[kNumLight] = {1, 2, 4, 4};
+
+// ---------------------------------------------------------------------------
+// K2: heavy rows (deg > 16).  Workgroup = (row, group of G scenarios).
+//   phase 0  stage node ids ntile[si][j] (G-scenario row segments per neighbour)
+//   phase A  wave w < NT hashes scenario si's d node ids into its LDS table
+//   phase B  counts back into ctile[si][j]; table cleared for the next scenario
+//   phase C  thread -> (si = tid % G, j = tid / G + k*256/G): nodekey gathers are
+//            G consecutive scenarios of one node (coalesced), then a shuffle /
+//            LDS reduction of CarState per scenario.
+// ---------------------------------------------------------------------------
+struct HeavyItem {
+    int oi, rb, d, pad;
+};
+
+__device__ __forceinline__ int hash_insert(unsigned *keys, unsigned *cnts, unsigned mask, int n) {
+    const unsigned k = (unsigned)n + 1u;
+    unsigned h = (k * 2654435761u) & mask;
+    while (true) {
+        const unsigned prev = atomicCAS(&keys[h], 0u, k);
+        if (prev == 0u || prev == k) {
+            atomicAdd(&cnts[h], 1u);
+            return (int)h;
+        }
+        h = (h + 1u) & mask;
+    }
+}
+
+__global__ __launch_bounds__(256) void car_heavy_kernel(const HeavyItem *__restrict__ items, int n_items,
+                                                        const int *__restrict__ hcol,
+                                                        const int *__restrict__ assign,
+                                                        const int *__restrict__ nodekey, int S, int N, int G,
+                                                        int dpad, int H, int NT, const int *__restrict__ zc_cnt,
+                                                        const unsigned long long *__restrict__ zc_key,
+                                                        int *__restrict__ out_target, int *__restrict__ out_score) {
+    extern __shared__ __attribute__((aligned(16))) int lds[];
+    const int g = blockIdx.x / n_items;
+    const HeavyItem it = items[blockIdx.x % n_items];
+    const int s0 = g * G;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int *ntile = lds;                                       // [G][dpad]
+    int *ctile = ntile + G * dpad;                          // [G][dpad]
+    unsigned *tkey = reinterpret_cast<unsigned *>(ctile + G * dpad);  // [NT][H]
+    unsigned *tcnt = tkey + NT * H;                         // [NT][H]
+    CarState *red = reinterpret_cast<CarState *>(tcnt + NT * H);      // [4][G]
+
+    const int d = it.d;
+    for (int idx = tid; idx < d * G; idx += 256) {
+        const int j = idx / G, si = idx - j * G, s = s0 + si;
+        int v = -1;
+        if (s < S) {
+            const int a = assign[(size_t)hcol[it.rb + j] * S + s];
+            v = (unsigned)a < (unsigned)N ? a : -1;
+        }
+        ntile[si * dpad + j] = v;
+    }
+    for (int k = tid; k < NT * H; k += 256) { tkey[k] = 0u; tcnt[k] = 0u; }
+    __syncthreads();
+
+    if (wave < NT) {
+        unsigned *keys = tkey + wave * H, *cnts = tcnt + wave * H;
+        const unsigned mask = (unsigned)H - 1u;
+        for (int si = wave; si < G; si += NT) {
+            int *nrow = ntile + si * dpad, *crow = ctile + si * dpad;
+            for (int j = lane; j < d; j += 64) {
+                const int n = nrow[j];
+                crow[j] = n >= 0 ? hash_insert(keys, cnts, mask, n) : -1;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            for (int j = lane; j < d; j += 64) {
+                const int slot = crow[j];
+                crow[j] = slot >= 0 ? (int)cnts[slot] : 0;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            for (int k = lane; k < H; k += 64) { keys[k] = 0u; cnts[k] = 0u; }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        }
+    }
+    __syncthreads();
+
+    const int si = tid % G, jstep = 256 / G;
+    const int s = s0 + si;
+    CarState st;
+    st_init(st);
+    if (s < S) {
+        const int *nrow = ntile + si * dpad, *crow = ctile + si * dpad;
+        for (int j = tid / G; j < d; j += jstep) {
+            const int n = nrow[j];
+            if (n < 0) continue;
+            const int key = nodekey[(size_t)n * S + s];
+            if (key != kKeyHaz) st_add(st, crow[j], key, n);
+        }
+    }
+    for (int off = G; off < 64; off <<= 1) st = st_combine(st, st_shfl_xor(st, off));
+    if (lane < G) red[wave * G + lane] = st;
+    __syncthreads();
+    if (tid < G && s < S) {
+        CarState r = red[tid];
+        for (int w = 1; w < 4; ++w) r = st_combine(r, red[w * G + tid]);
+        int sc;
+        const int t = car_finalize(r, s, zc_cnt, zc_key, sc);
+        const size_t o = (size_t)it.oi * S + s;
+        out_target[o] = t;
+        if (out_score) out_score[o] = sc;
+    }
+}
+
+}  // namespace rsk
+
+using namespace rsk;
+
+struct rsk_car_plan {
+    rsk_ctx *ctx = nullptr;
+    int P = 0, Q = 0, max_deg = 0;
+    int n_light[kNumLight] = {0, 0, 0, 0};
+    DevBuf ell[kNumLight];
+    int n_heavy[kNumHeavy] = {0, 0, 0, 0};
+    int heavy_dmax[kNumHeavy] = {0, 0, 0, 0};
+    DevBuf heavy_items[kNumHeavy];
+    DevBuf hcol;
+    DevBuf nodekey, zc;
+    ~rsk_car_plan() {
+        for (auto &b : ell) b.release();
+        for (auto &b : heavy_items) b.release();
+        hcol.release();
+        nodekey.release();
+        zc.release();
+    }
+};
+
+namespace {
+
+int light_bucket(int d) {
+    if (d <= 2) return 3;
+    if (d <= 4) return 2;
+    if (d <= 8) return 1;
+    return 0;
+}
+
+int heavy_class(int d) {
+    for (int c = 0; c < kNumHeavy; ++c)
+        if (d <= kHeavyMax[c]) return c;
+    return -1;
+}
+
+int next_pow2(int x) {
+    int p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+struct HeavyGeom {
+    int G, dpad, H, NT;
+    size_t lds;
+};
+
+HeavyGeom heavy_geometry(int dmax, int S) {
+    // Largest scenario group G (<= 64, <= S rounded up to a power of two) and
+    // hash-table count NT that fit 64 KiB of LDS (2 workgroups per CU); failing
+    // that, anything up to the 160 KiB a single workgroup may declare.
+    HeavyGeom g;
+    g.dpad = dmax | 1;  // odd row pitch: scenario rows start on different banks
+    g.H = next_pow2(2 * dmax);
+    const int gmax = std::min(64, next_pow2(S));
+    const size_t limits[2] = {64 * 1024, 160 * 1024};
+    for (size_t lim : limits)
+        for (g.G = gmax; g.G >= 1; g.G >>= 1)
+            for (g.NT = 4; g.NT >= 1; g.NT >>= 1) {
+                g.lds = (size_t)2 * g.G * g.dpad * 4 + (size_t)g.NT * g.H * 8 + (size_t)4 * g.G * sizeof(CarState);
+                if (g.lds <= lim) return g;
+            }
+    g.G = 1;
+    g.NT = 1;
+    g.lds = (size_t)2 * g.dpad * 4 + (size_t)g.H * 8 + 4 * sizeof(CarState);
+    return g;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rsk_car_plan_create(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, int32_t P,
+                        const int32_t *rows, int32_t Q, rsk_car_plan **out) {
+    RSK_CHECK(out, "null output pointer");
+    *out = nullptr;
+    RSK_TRY(activate(ctx));
+    RSK_CHECK(P >= 0 && row_ptr, "bad CSR (P=%d)", P);
+    if (!rows) Q = P;
+    RSK_CHECK(Q >= 0, "bad row count %d", Q);
+    RSK_CHECK(row_ptr[0] == 0, "row_ptr[0] must be 0");
+    for (int32_t p = 0; p < P; ++p)
+        RSK_CHECK(row_ptr[p + 1] >= row_ptr[p], "row_ptr not monotone at %d", p);
+    const int64_t nnz = P ? row_ptr[P] : 0;
+    RSK_CHECK(nnz == 0 || col_idx, "null col_idx");
+    for (int64_t k = 0; k < nnz; ++k)
+        RSK_CHECK(col_idx[k] >= 0 && col_idx[k] < P, "col_idx[%lld]=%d out of range", (long long)k, col_idx[k]);
+
+    auto plan = new rsk_car_plan();
+    plan->ctx = ctx;
+    plan->P = P;
+    plan->Q = Q;
+    std::vector<std::vector<int>> ell(kNumLight);
+    std::vector<std::vector<HeavyItem>> hitems(kNumHeavy);
+    std::vector<int> hcol;
+    std::vector<int> nb;
+    for (int32_t i = 0; i < Q; ++i) {
+        const int p = rows ? rows[i] : i;
+        if (p < 0 || p >= P) {
+            delete plan;
+            set_error("rows[%d]=%d out of range", i, p);
+            return RSK_EINVAL;
+        }
+        nb.assign(col_idx + row_ptr[p], col_idx + row_ptr[p + 1]);
+        std::sort(nb.begin(), nb.end());
+        nb.erase(std::unique(nb.begin(), nb.end()), nb.end());
+        nb.erase(std::remove(nb.begin(), nb.end(), p), nb.end());
+        const int d = (int)nb.size();
+        plan->max_deg = std::max(plan->max_deg, d);
+        if (d <= kLightMax) {
+            const int b = light_bucket(d);
+            auto &e = ell[b];
+            const size_t o = e.size();
+            e.resize(o + kLightW[b], 0);
+            e[o] = i;
+            e[o + 1] = d;
+            for (int j = 0; j < d; ++j) e[o + 2 + j] = nb[j];
+            plan->n_light[b] += 1;
+        } else {
+            const int c = heavy_class(d);
+            if (c < 0) {
+                delete plan;
+                set_error("row %d has degree %d > %d (unsupported)", p, d, kMaxDegree);
+                return RSK_EINVAL;
+            }
+            hitems[c].push_back({i, (int)hcol.size(), d, 0});
+            hcol.insert(hcol.end(), nb.begin(), nb.end());
+            plan->n_heavy[c] += 1;
+            plan->heavy_dmax[c] = std::max(plan->heavy_dmax[c], d);
+        }
+    }
+    for (int b = 0; b < kNumLight; ++b) {
+        if (ell[b].empty()) continue;
+        int rc = plan->ell[b].reserve(ell[b].size() * 4);
+        if (rc == RSK_OK && hipMemcpy(plan->ell[b].ptr, ell[b].data(), ell[b].size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+            set_error("hipMemcpy ELL failed");
+            rc = RSK_EHIP;
+        }
+        if (rc != RSK_OK) { delete plan; return rc; }
+    }
+    for (int c = 0; c < kNumHeavy; ++c) {
+        if (hitems[c].empty()) continue;
+        int rc = plan->heavy_items[c].reserve(hitems[c].size() * sizeof(HeavyItem));
+        if (rc == RSK_OK && hipMemcpy(plan->heavy_items[c].ptr, hitems[c].data(), hitems[c].size() * sizeof(HeavyItem),
+                                      hipMemcpyHostToDevice) != hipSuccess) {
+            set_error("hipMemcpy heavy items failed");
+            rc = RSK_EHIP;
+        }
+        if (rc != RSK_OK) { delete plan; return rc; }
+    }
+    if (!hcol.empty()) {
+        int rc = plan->hcol.reserve(hcol.size() * 4);
+        if (rc == RSK_OK && hipMemcpy(plan->hcol.ptr, hcol.data(), hcol.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+            set_error("hipMemcpy heavy CSR failed");
+            rc = RSK_EHIP;
+        }
+        if (rc != RSK_OK) { delete plan; return rc; }
+    }
+    *out = plan;
+    return RSK_OK;
+}
+
+int rsk_car_plan_destroy(rsk_car_plan *plan) {
+    if (!plan) return RSK_OK;
+    (void)hipSetDevice(plan->ctx->device);
+    (void)hipStreamSynchronize(plan->ctx->stream);
+    delete plan;
+    return RSK_OK;
+}
+
+int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, const int32_t *cap_cpu,
+                         const int32_t *use_cpu, const uint8_t *hazard, int32_t N, int32_t *out_target,
+                         int32_t *out_score, uint32_t flags) {
+    RSK_CHECK(plan, "null plan");
+    rsk_ctx *ctx = plan->ctx;
+    RSK_TRY(activate(ctx));
+    RSK_CHECK(S > 0 && N > 0, "need S > 0 and N > 0 (S=%d N=%d)", S, N);
+    RSK_CHECK((int64_t)N * S < INT32_MAX && (int64_t)plan->P * S < ((int64_t)1 << 40),
+              "N*S too large (N=%d S=%d)", N, S);
+    RSK_CHECK(out_target, "null out_target");
+    const bool dev = (flags & RSK_F_DEVICE) != 0;
+    const size_t PS_ = (size_t)plan->P * S, NS = (size_t)N * S, QS = (size_t)plan->Q * S;
+
+    const int *d_assign, *d_cap, *d_use;
+    const uint8_t *d_haz;
+    int *d_target, *d_score = nullptr;
+    RSK_TRY(stage_in(ctx, 0, assign, PS_ * 4, dev, reinterpret_cast<const void **>(&d_assign)));
+    RSK_TRY(stage_in(ctx, 1, cap_cpu, (size_t)N * 4, dev, reinterpret_cast<const void **>(&d_cap)));
+    RSK_TRY(stage_in(ctx, 2, use_cpu, NS * 4, dev, reinterpret_cast<const void **>(&d_use)));
+    RSK_TRY(stage_in(ctx, 3, hazard, NS, dev, reinterpret_cast<const void **>(&d_haz)));
+    RSK_TRY(stage_out(ctx, 4, out_target, QS * 4, dev, reinterpret_cast<void **>(&d_target)));
+    if (out_score) RSK_TRY(stage_out(ctx, 5, out_score, QS * 4, dev, reinterpret_cast<void **>(&d_score)));
+
+    RSK_TRY(plan->nodekey.reserve(NS * 4));
+    RSK_TRY(plan->zc.reserve((size_t)S * 12 + 16));
+    int *d_key = plan->nodekey.as<int>();
+    unsigned long long *d_zkey = plan->zc.as<unsigned long long>();
+    int *d_zcnt = reinterpret_cast<int *>(d_zkey + S);
+    RSK_HIP(hipMemsetAsync(plan->zc.ptr, 0, (size_t)S * 12, ctx->stream));
+
+    {   // K0
+        const int target_threads = 256 * 2048;
+        int npb = (int)std::max<int64_t>(1, ceil_div((int64_t)N * S, target_threads));
+        const int64_t chunks = ceil_div(N, npb);
+        const unsigned total = (unsigned)(chunks * S);
+        ScopedTimer tm(ctx, "car_prep");
+        car_prep_kernel<<<dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, ctx->stream>>>(
+            d_cap, d_use, d_haz, N, S, npb, total, d_key, d_zcnt, d_zkey);
+        RSK_HIP(hipGetLastError());
+    }
+    {   // K1
+        LightArgs a;
+        std::memset(&a, 0, sizeof(a));
+        a.SL = std::min(S, 64);
+        a.PS = 64 / a.SL;
+        const int iters = 2;
+        a.task_prefix[0] = 0;
+        for (int b = 0; b < kNumLight; ++b) {
+            a.ell[b] = plan->ell[b].as<int>();
+            a.n_items[b] = plan->n_light[b];
+            a.task_items[b] = kLightPK[b] * a.PS * iters;
+            a.task_prefix[b + 1] = a.task_prefix[b] + (int)ceil_div(plan->n_light[b], a.task_items[b]);
+        }
+        const int tasks = a.task_prefix[kNumLight];
+        if (tasks > 0) {
+            a.assign = d_assign;
+            a.nodekey = d_key;
+            a.zc_cnt = d_zcnt;
+            a.zc_key = d_zkey;
+            a.out_target = d_target;
+            a.out_score = d_score;
+            a.S = S;
+            a.N = N;
+            a.blocks_per_chunk = (int)ceil_div(tasks, 4);
+            const int64_t chunks = ceil_div(S, a.SL);
+            const int64_t blocks = chunks * a.blocks_per_chunk;
+            RSK_CHECK(blocks < INT32_MAX, "light grid too large");
+            ScopedTimer tm(ctx, "car_light");
+            car_light_kernel<<<dim3((unsigned)blocks), dim3(256), 0, ctx->stream>>>(a);
+            RSK_HIP(hipGetLastError());
+        }
+    }
+    for (int c = 0; c < kNumHeavy; ++c) {   // K2
+        const int n = plan->n_heavy[c];
+        if (!n) continue;
+        const HeavyGeom g = heavy_geometry(plan->heavy_dmax[c], S);
+        RSK_CHECK(g.lds <= 160 * 1024, "heavy class %d needs %zu B of LDS", c, g.lds);
+        const int64_t groups = ceil_div(S, g.G);
+        RSK_CHECK(groups * n < INT32_MAX, "heavy grid too large");
+        if (g.lds > 64 * 1024)
+            RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&car_heavy_kernel),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds));
+        ScopedTimer tm(ctx, "car_heavy");
+        car_heavy_kernel<<<dim3((unsigned)(groups * n)), dim3(256), g.lds, ctx->stream>>>(
+            plan->heavy_items[c].as<HeavyItem>(), n, plan->hcol.as<int>(), d_assign, d_key, S, N, g.G, g.dpad,
+            g.H, g.NT, d_zcnt, d_zkey, d_target, d_score);
+        RSK_HIP(hipGetLastError());
+    }
+    if (!dev) {
+        RSK_TRY(copy_back(ctx, out_target, d_target, QS * 4, false));
+        if (out_score) RSK_TRY(copy_back(ctx, out_score, d_score, QS * 4, false));
+        RSK_HIP(hipStreamSynchronize(ctx->stream));
+        for (size_t k = 0; k < QS; ++k)
+            if (out_target[k] == RSK_TARGET_NO_CANDIDATE) return RSK_NO_CANDIDATE;
+    }
+    return RSK_OK;
+}
+
+int rsk_car_place(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, int32_t P, const int32_t *assign,
+                  int32_t S, const int32_t *cap_cpu, const int32_t *use_cpu, const uint8_t *hazard, int32_t N,
+                  const int32_t *rows, int32_t Q, int32_t *out_target, int32_t *out_score, uint32_t flags) {
+    rsk_car_plan *plan = nullptr;
+    RSK_TRY(rsk_car_plan_create(ctx, row_ptr, col_idx, P, rows, Q, &plan));
+    const int rc = rsk_car_plan_execute(plan, assign, S, cap_cpu, use_cpu, hazard, N, out_target, out_score, flags);
+    if (rc != RSK_OK && rc != RSK_NO_CANDIDATE) {
+        std::string keep = last_error();
+        rsk_car_plan_destroy(plan);
+        set_error("%s", keep.c_str());
+        return rc;
+    }
+    rsk_car_plan_destroy(plan);
+    return rc;
+}
+
+}  // extern "C"

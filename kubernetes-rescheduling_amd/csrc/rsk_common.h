@@ -1,0 +1,92 @@
+// rsk_common.h — shared internals of librsk.so (HIP, gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "rsk.h"
+
+namespace rsk {
+
+// Error reporting: thread-local last error, returned through rsk_last_error().
+void set_error(const char *fmt, ...);
+const char *last_error();
+
+#define RSK_HIP(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t _e = (expr);                                                          \
+        if (_e != hipSuccess) {                                                          \
+            ::rsk::set_error("%s:%d %s: %s", __FILE__, __LINE__, #expr, hipGetErrorString(_e)); \
+            return RSK_EHIP;                                                             \
+        }                                                                                \
+    } while (0)
+
+#define RSK_CHECK(cond, ...)                                                             \
+    do {                                                                                 \
+        if (!(cond)) {                                                                   \
+            ::rsk::set_error(__VA_ARGS__);                                               \
+            return RSK_EINVAL;                                                           \
+        }                                                                                \
+    } while (0)
+
+#define RSK_TRY(expr)                                                                    \
+    do {                                                                                 \
+        int _rc = (expr);                                                                \
+        if (_rc != RSK_OK) return _rc;                                                   \
+    } while (0)
+
+// Grow-only device scratch buffer owned by a context or plan.
+struct DevBuf {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+    int reserve(size_t need);
+    void release();
+    template <class T> T *as() const { return static_cast<T *>(ptr); }
+};
+
+struct EventPair {
+    hipEvent_t start, stop;
+};
+
+}  // namespace rsk
+
+struct rsk_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    bool profiling = false;
+    std::map<std::string, std::vector<rsk::EventPair>> pending;
+    std::map<std::string, std::pair<double, int64_t>> totals;
+    rsk::DevBuf host_stage[12];  // device staging for host-pointer calls
+    rsk::DevBuf work[6];         // per-call device workspace
+    std::vector<uint8_t> pinned;  // host scratch
+};
+
+namespace rsk {
+
+// Event-bracketed launches: `name` accumulates kernel time when profiling is on.
+struct ScopedTimer {
+    rsk_ctx *ctx;
+    const char *name;
+    hipEvent_t a = nullptr, b = nullptr;
+    ScopedTimer(rsk_ctx *c, const char *n);
+    ~ScopedTimer();
+};
+
+int activate(rsk_ctx *ctx);
+
+// Host-pointer staging: copy `bytes` from host `src` into context slot `slot`
+// and return the device pointer (or pass a device pointer straight through).
+int stage_in(rsk_ctx *ctx, int slot, const void *src, size_t bytes, bool device, const void **out);
+int stage_out(rsk_ctx *ctx, int slot, void *dst, size_t bytes, bool device, void **out);
+int copy_back(rsk_ctx *ctx, void *host_dst, const void *dev_src, size_t bytes, bool device);
+
+constexpr int kBlock = 256;
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace rsk

@@ -1,0 +1,687 @@
+// rsk_metrics.hip — spread / binpack / random placement and the per-node
+// reductions ("kernel 3") of the placement path, on gfx950.
+//
+// All per-scenario arrays are scenario-minor (x[n*S + s]).  Most kernels map
+// thread t -> (scenario s = t % S, node or pod chunk t / S), so one wave reads 64
+// consecutive scenarios of the same node / pod: a coalesced row.  Per-scenario
+// winners are combined with 64-bit integer atomicMax / atomicMin on packed
+// keys (order-independent, hence deterministic); floating-point sums use
+// fixed-order partials, never atomics.
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "rsk_common.h"
+
+namespace rsk {
+
+// chunk size so the grid has ~512K threads
+static int chunk_for(int64_t items, int S) {
+    const int64_t target = 256 * 2048;
+    return (int)std::max<int64_t>(1, ceil_div(items * S, target));
+}
+
+__device__ __forceinline__ unsigned long long pack_hi_lo(int hi, unsigned lo) {
+    return ((unsigned long long)((unsigned)hi ^ 0x80000000u) << 32) | (unsigned long long)lo;
+}
+
+// ---------------------------------------------------------------------------
+// spread (rescheduling.py:89-101): min (pod_count, name_rank) over non-hazard.
+// binpack (rescheduling.py:121-133): max (cpu_pct, name_rank).
+// key = (primary ^ sign) << 32 | rank; the winning rank maps back to its node.
+// ---------------------------------------------------------------------------
+template <bool kMin>
+__global__ __launch_bounds__(256) void pick_node_kernel(const int *__restrict__ val, const int *__restrict__ rank,
+                                                        const uint8_t *__restrict__ haz, int N, int S, int npb,
+                                                        unsigned total, unsigned long long *__restrict__ best) {
+    const unsigned t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= total) return;
+    const int s = (int)(t % (unsigned)S);
+    const int n0 = (int)(t / (unsigned)S) * npb, n1 = min(N, n0 + npb);
+    unsigned long long b = kMin ? ~0ull : 0ull;
+    bool any = false;
+    for (int n = n0; n < n1; ++n) {
+        const size_t idx = (size_t)n * S + s;
+        if (haz[idx]) continue;
+        const unsigned long long k = pack_hi_lo(val[idx], (unsigned)rank[n]);
+        b = kMin ? (k < b ? k : b) : (k > b ? k : b);
+        any = true;
+    }
+    if (any) {
+        if (kMin) atomicMin(&best[s], b);
+        else atomicMax(&best[s], b + 1ull);  // +1: 0 stays "no candidate"
+    }
+}
+
+__global__ void rank_inverse_kernel(const int *__restrict__ rank, int N, int *__restrict__ inv) {
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    if (n < N) {
+        const int r = rank[n];
+        if ((unsigned)r < (unsigned)N) inv[r] = n;
+    }
+}
+
+template <bool kMin>
+__global__ void pick_node_finish(const unsigned long long *__restrict__ best, const int *__restrict__ inv, int N,
+                                 int S, int *__restrict__ out) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (s >= S) return;
+    unsigned long long b = best[s];
+    if (kMin ? b == ~0ull : b == 0ull) { out[s] = RSK_TARGET_NO_CANDIDATE; return; }
+    if (!kMin) b -= 1ull;
+    const unsigned r = (unsigned)(b & 0xffffffffull);
+    out[s] = r < (unsigned)N ? inv[r] : RSK_TARGET_NO_CANDIDATE;
+}
+
+template <bool kMin>
+static int pick_node(rsk_ctx *ctx, const int32_t *val, const int32_t *name_rank, const uint8_t *hazard, int32_t N,
+                     int32_t S, int32_t *out_node, uint32_t flags, const char *tag) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK(N > 0 && S > 0 && (int64_t)N * S < INT32_MAX, "bad sizes N=%d S=%d", N, S);
+    RSK_CHECK(out_node, "null out_node");
+    const bool dev = flags & RSK_F_DEVICE;
+    const size_t NS = (size_t)N * S;
+    const int *d_val, *d_rank;
+    const uint8_t *d_haz;
+    int *d_out;
+    RSK_TRY(stage_in(ctx, 0, val, NS * 4, dev, reinterpret_cast<const void **>(&d_val)));
+    RSK_TRY(stage_in(ctx, 1, name_rank, (size_t)N * 4, dev, reinterpret_cast<const void **>(&d_rank)));
+    RSK_TRY(stage_in(ctx, 2, hazard, NS, dev, reinterpret_cast<const void **>(&d_haz)));
+    RSK_TRY(stage_out(ctx, 3, out_node, (size_t)S * 4, dev, reinterpret_cast<void **>(&d_out)));
+    RSK_TRY(ctx->work[0].reserve((size_t)S * 8));
+    RSK_TRY(ctx->work[1].reserve((size_t)N * 4));
+    auto *best = ctx->work[0].as<unsigned long long>();
+    int *inv = ctx->work[1].as<int>();
+    RSK_HIP(hipMemsetAsync(best, kMin ? 0xff : 0x00, (size_t)S * 8, ctx->stream));
+    RSK_HIP(hipMemsetAsync(inv, 0xff, (size_t)N * 4, ctx->stream));
+    const int npb = chunk_for(N, S);
+    const unsigned total = (unsigned)(ceil_div(N, npb) * S);
+    {
+        ScopedTimer tm(ctx, tag);
+        pick_node_kernel<kMin><<<(unsigned)ceil_div(total, 256), 256, 0, ctx->stream>>>(d_val, d_rank, d_haz, N, S,
+                                                                                         npb, total, best);
+        rank_inverse_kernel<<<(unsigned)ceil_div(N, 256), 256, 0, ctx->stream>>>(d_rank, N, inv);
+        pick_node_finish<kMin><<<(unsigned)ceil_div(S, 256), 256, 0, ctx->stream>>>(best, inv, N, S, d_out);
+        RSK_HIP(hipGetLastError());
+    }
+    if (!dev) {
+        RSK_TRY(copy_back(ctx, out_node, d_out, (size_t)S * 4, false));
+        RSK_HIP(hipStreamSynchronize(ctx->stream));
+        for (int s = 0; s < S; ++s)
+            if (out_node[s] == RSK_TARGET_NO_CANDIDATE) return RSK_NO_CANDIDATE;
+    }
+    return RSK_OK;
+}
+
+// ---------------------------------------------------------------------------
+// random (rescheduling.py:149-153): count candidates, then the r-th one.
+// count: per (node chunk, s) partial counts -> part[chunk][s] (+ atomic total).
+// select: per scenario, walk the chunk partials to the chunk holding r, then
+// the nodes of that chunk.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void count_free_kernel(const uint8_t *__restrict__ haz, int N, int S, int npb,
+                                                         unsigned total, int *__restrict__ part,
+                                                         int *__restrict__ count) {
+    const unsigned t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= total) return;
+    const int s = (int)(t % (unsigned)S), ch = (int)(t / (unsigned)S);
+    const int n0 = ch * npb, n1 = min(N, n0 + npb);
+    int c = 0;
+    for (int n = n0; n < n1; ++n) c += !haz[(size_t)n * S + s];
+    part[(size_t)ch * S + s] = c;
+    if (c) atomicAdd(&count[s], c);
+}
+
+__global__ __launch_bounds__(256) void select_free_kernel(const uint8_t *__restrict__ haz, int N, int S, int npb,
+                                                          int nchunks, const int *__restrict__ part,
+                                                          const int *__restrict__ r, int *__restrict__ out) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (s >= S) return;
+    int want = r[s];
+    if (want < 0) { out[s] = RSK_TARGET_NO_CANDIDATE; return; }
+    int ch = 0;
+    for (; ch < nchunks; ++ch) {
+        const int c = part[(size_t)ch * S + s];
+        if (want < c) break;
+        want -= c;
+    }
+    if (ch == nchunks) { out[s] = RSK_TARGET_NO_CANDIDATE; return; }
+    const int n0 = ch * npb, n1 = min(N, n0 + npb);
+    int t = RSK_TARGET_NO_CANDIDATE;
+    for (int n = n0; n < n1; ++n)
+        if (!haz[(size_t)n * S + s]) {
+            if (want == 0) { t = n; break; }
+            --want;
+        }
+    out[s] = t;
+}
+
+// CPython random.Random: MT19937 with init_by_array seeding (see rsk_py_randbelow).
+struct MT {
+    uint32_t mt[624];
+    int idx;
+    void init_genrand(uint32_t s) {
+        mt[0] = s;
+        for (int i = 1; i < 624; ++i) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
+        idx = 624;
+    }
+    void init_by_array(const uint32_t *key, int len) {
+        init_genrand(19650218u);
+        int i = 1, j = 0;
+        for (int k = (624 > len ? 624 : len); k; --k) {
+            mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1664525u)) + key[j] + (uint32_t)j;
+            ++i;
+            ++j;
+            if (i >= 624) { mt[0] = mt[623]; i = 1; }
+            if (j >= len) j = 0;
+        }
+        for (int k = 623; k; --k) {
+            mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1566083941u)) - (uint32_t)i;
+            ++i;
+            if (i >= 624) { mt[0] = mt[623]; i = 1; }
+        }
+        mt[0] = 0x80000000u;
+        idx = 624;
+    }
+    uint32_t next() {
+        if (idx >= 624) {
+            for (int k = 0; k < 624; ++k) {
+                const uint32_t y = (mt[k] & 0x80000000u) | (mt[(k + 1) % 624] & 0x7fffffffu);
+                mt[k] = mt[(k + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+            }
+            idx = 0;
+        }
+        uint32_t y = mt[idx++];
+        y ^= y >> 11;
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= y >> 18;
+        return y;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Kernel 3: node reductions and metrics.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void node_reduce_kernel(const int *__restrict__ assign, int P, int S,
+                                                          const int *__restrict__ pod_cpu,
+                                                          const long long *__restrict__ pod_mem, int N,
+                                                          int *__restrict__ cnt, unsigned long long *__restrict__ cpu,
+                                                          unsigned long long *__restrict__ mem) {
+    const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (size_t)P * S) return;
+    const int a = assign[t];
+    if ((unsigned)a >= (unsigned)N) return;
+    const int p = (int)(t / (size_t)S), s = (int)(t - (size_t)p * S);
+    const size_t o = (size_t)a * S + s;
+    atomicAdd(&cnt[o], 1);
+    atomicAdd(&cpu[o], (unsigned long long)(long long)pod_cpu[p]);
+    if (mem) atomicAdd(&mem[o], (unsigned long long)pod_mem[p]);
+}
+
+// get_resource_usage.py:37: int(round(u / c * 100)) — IEEE fp64 divide, then an
+// fp64 multiply (no FMA can form), then round-half-even (rint).
+__global__ __launch_bounds__(256) void cpu_pct_kernel(const int *__restrict__ use, const int *__restrict__ cap, int N,
+                                                      int S, int *__restrict__ pct) {
+    const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (size_t)N * S) return;
+    const int n = (int)(t / (size_t)S);
+    const int c = cap[n];
+    if (c == 0) { pct[t] = -1; return; }
+    const double q = (double)use[t] / (double)c;
+    pct[t] = (int)rint(q * 100.0);
+}
+
+// harzard_detect.py:3-27: hazard flag and the first node with the max pct.
+__global__ __launch_bounds__(256) void detect_kernel(const int *__restrict__ pct, int N, int S, int thr, int npb,
+                                                     unsigned total, uint8_t *__restrict__ haz,
+                                                     unsigned long long *__restrict__ most) {
+    const unsigned t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= total) return;
+    const int s = (int)(t % (unsigned)S);
+    const int n0 = (int)(t / (unsigned)S) * npb, n1 = min(N, n0 + npb);
+    unsigned long long b = 0;
+    for (int n = n0; n < n1; ++n) {
+        const size_t idx = (size_t)n * S + s;
+        const int v = pct[idx];
+        const bool h = v >= thr;
+        haz[idx] = h;
+        if (h) {
+            const unsigned long long k = pack_hi_lo(v, ~(unsigned)n);
+            b = k > b ? k : b;
+        }
+    }
+    if (b) atomicMax(&most[s], b);
+}
+
+__global__ void decode_first_max(const unsigned long long *__restrict__ key, int S, int *__restrict__ out) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (s >= S) return;
+    const unsigned long long k = key[s];
+    out[s] = k ? (int)(~(unsigned)(k & 0xffffffffull)) : -1;
+}
+
+// nodemonitor.py:24-46.  Per (node chunk, s): count, chunk mean and M2 (two
+// passes over the chunk, fp64); then per s a fixed-order Chan merge.
+__global__ __launch_bounds__(256) void std_partial_kernel(const int *__restrict__ use, const int *__restrict__ cap,
+                                                          int N, int S, int npb, unsigned total,
+                                                          double *__restrict__ pmean, double *__restrict__ pm2,
+                                                          int *__restrict__ pcnt) {
+    const unsigned t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= total) return;
+    const int s = (int)(t % (unsigned)S), ch = (int)(t / (unsigned)S);
+    const int n0 = ch * npb, n1 = min(N, n0 + npb);
+    double sum = 0.0;
+    int c = 0;
+    for (int n = n0; n < n1; ++n) {
+        const int cp = cap[n];
+        if (cp <= 0) continue;
+        sum += (double)use[(size_t)n * S + s] / (double)cp * 100.0;
+        ++c;
+    }
+    double mean = c ? sum / c : 0.0, m2 = 0.0;
+    for (int n = n0; n < n1; ++n) {
+        const int cp = cap[n];
+        if (cp <= 0) continue;
+        const double d = (double)use[(size_t)n * S + s] / (double)cp * 100.0 - mean;
+        m2 += d * d;
+    }
+    const size_t o = (size_t)ch * S + s;
+    pmean[o] = mean;
+    pm2[o] = m2;
+    pcnt[o] = c;
+}
+
+__global__ void std_merge_kernel(const double *__restrict__ pmean, const double *__restrict__ pm2,
+                                 const int *__restrict__ pcnt, int nchunks, int S, double *__restrict__ out) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (s >= S) return;
+    double mean = 0.0, m2 = 0.0;
+    long long n = 0;
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const size_t o = (size_t)ch * S + s;
+        const int nb = pcnt[o];
+        if (!nb) continue;
+        const double mb = pmean[o], delta = mb - mean;
+        const long long nt = n + nb;
+        mean += delta * ((double)nb / (double)nt);
+        m2 += pm2[o] + delta * delta * ((double)n * (double)nb / (double)nt);
+        n = nt;
+    }
+    out[s] = n ? sqrt(m2 / (double)n) : 0.0;
+}
+
+// communicationcost.py:37-45: directed count of related pairs on different nodes.
+__global__ __launch_bounds__(256) void cut_cost_kernel(const int *__restrict__ row_ptr, const int *__restrict__ col,
+                                                       int P, const int *__restrict__ assign, int S,
+                                                       const int *__restrict__ missing, int ppt, unsigned total,
+                                                       unsigned long long *__restrict__ out) {
+    const unsigned t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= total) return;
+    const int s = (int)(t % (unsigned)S);
+    const int p0 = (int)(t / (unsigned)S) * ppt, p1 = min(P, p0 + ppt);
+    unsigned long long c = 0;
+    for (int p = p0; p < p1; ++p) {
+        const int a = assign[(size_t)p * S + s];
+        for (int k = row_ptr[p]; k < row_ptr[p + 1]; ++k) c += a != assign[(size_t)col[k] * S + s];
+        if (missing && a != -1) c += (unsigned long long)missing[p];
+    }
+    if (c) atomicAdd(&out[s], c);
+}
+
+// delete_replaced_pod.py:41-61: first pod (list order) with the largest cpu > -1.
+__global__ __launch_bounds__(256) void pick_pod_kernel(const int *__restrict__ assign, const int *__restrict__ pod_cpu,
+                                                       int P, int S, const int *__restrict__ most, int ppt,
+                                                       unsigned total, unsigned long long *__restrict__ best) {
+    const unsigned t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= total) return;
+    const int s = (int)(t % (unsigned)S);
+    const int m = most[s];
+    if (m < 0) return;
+    const int p0 = (int)(t / (unsigned)S) * ppt, p1 = min(P, p0 + ppt);
+    unsigned long long b = 0;
+    for (int p = p0; p < p1; ++p) {
+        if (assign[(size_t)p * S + s] != m || pod_cpu[p] < 0) continue;
+        const unsigned long long k = pack_hi_lo(pod_cpu[p], ~(unsigned)p);
+        b = k > b ? k : b;
+    }
+    if (b) atomicMax(&best[s], b);
+}
+
+}  // namespace rsk
+
+using namespace rsk;
+
+extern "C" {
+
+int rsk_spread_place(rsk_ctx *ctx, const int32_t *pod_count, const int32_t *name_rank, const uint8_t *hazard,
+                     int32_t N, int32_t S, int32_t *out_node, uint32_t flags) {
+    return pick_node<true>(ctx, pod_count, name_rank, hazard, N, S, out_node, flags, "spread");
+}
+
+int rsk_binpack_place(rsk_ctx *ctx, const int32_t *cpu_pct, const int32_t *name_rank, const uint8_t *hazard,
+                      int32_t N, int32_t S, int32_t *out_node, uint32_t flags) {
+    return pick_node<false>(ctx, cpu_pct, name_rank, hazard, N, S, out_node, flags, "binpack");
+}
+
+static int random_count_impl(rsk_ctx *ctx, const uint8_t *d_haz, int N, int S, int **d_count, int *npb_out,
+                             int *nchunks_out) {
+    const int npb = chunk_for(N, S);
+    const int nchunks = (int)ceil_div(N, npb);
+    RSK_TRY(ctx->work[2].reserve((size_t)nchunks * S * 4));
+    RSK_TRY(ctx->work[3].reserve((size_t)S * 4));
+    RSK_HIP(hipMemsetAsync(ctx->work[3].ptr, 0, (size_t)S * 4, ctx->stream));
+    const unsigned total = (unsigned)((int64_t)nchunks * S);
+    ScopedTimer tm(ctx, "random_count");
+    count_free_kernel<<<(unsigned)ceil_div(total, 256), 256, 0, ctx->stream>>>(d_haz, N, S, npb, total,
+                                                                               ctx->work[2].as<int>(),
+                                                                               ctx->work[3].as<int>());
+    RSK_HIP(hipGetLastError());
+    *d_count = ctx->work[3].as<int>();
+    *npb_out = npb;
+    *nchunks_out = nchunks;
+    return RSK_OK;
+}
+
+int rsk_random_count(rsk_ctx *ctx, const uint8_t *hazard, int32_t N, int32_t S, int32_t *out_count,
+                     uint32_t flags) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK(N > 0 && S > 0 && (int64_t)N * S < INT32_MAX && out_count, "bad arguments");
+    const bool dev = flags & RSK_F_DEVICE;
+    const uint8_t *d_haz;
+    RSK_TRY(stage_in(ctx, 0, hazard, (size_t)N * S, dev, reinterpret_cast<const void **>(&d_haz)));
+    int *d_cnt, npb, nch;
+    RSK_TRY(random_count_impl(ctx, d_haz, N, S, &d_cnt, &npb, &nch));
+    if (dev) {
+        RSK_HIP(hipMemcpyAsync(out_count, d_cnt, (size_t)S * 4, hipMemcpyDeviceToDevice, ctx->stream));
+    } else {
+        RSK_TRY(copy_back(ctx, out_count, d_cnt, (size_t)S * 4, false));
+        RSK_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    return RSK_OK;
+}
+
+static int random_select_impl(rsk_ctx *ctx, const uint8_t *d_haz, int N, int S, const int *d_r, int *d_out) {
+    int *d_cnt, npb, nch;
+    RSK_TRY(random_count_impl(ctx, d_haz, N, S, &d_cnt, &npb, &nch));
+    ScopedTimer tm(ctx, "random_select");
+    select_free_kernel<<<(unsigned)ceil_div(S, 256), 256, 0, ctx->stream>>>(d_haz, N, S, npb, nch,
+                                                                            ctx->work[2].as<int>(), d_r, d_out);
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
+}
+
+int rsk_random_select(rsk_ctx *ctx, const uint8_t *hazard, int32_t N, int32_t S, const int32_t *r, int32_t *out_node,
+                      uint32_t flags) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK(N > 0 && S > 0 && (int64_t)N * S < INT32_MAX && r && out_node, "bad arguments");
+    const bool dev = flags & RSK_F_DEVICE;
+    const uint8_t *d_haz;
+    const int *d_r;
+    int *d_out;
+    RSK_TRY(stage_in(ctx, 0, hazard, (size_t)N * S, dev, reinterpret_cast<const void **>(&d_haz)));
+    RSK_TRY(stage_in(ctx, 1, r, (size_t)S * 4, dev, reinterpret_cast<const void **>(&d_r)));
+    RSK_TRY(stage_out(ctx, 2, out_node, (size_t)S * 4, dev, reinterpret_cast<void **>(&d_out)));
+    RSK_TRY(random_select_impl(ctx, d_haz, N, S, d_r, d_out));
+    if (!dev) {
+        RSK_TRY(copy_back(ctx, out_node, d_out, (size_t)S * 4, false));
+        RSK_HIP(hipStreamSynchronize(ctx->stream));
+        for (int s = 0; s < S; ++s)
+            if (out_node[s] == RSK_TARGET_NO_CANDIDATE) return RSK_NO_CANDIDATE;
+    }
+    return RSK_OK;
+}
+
+int32_t rsk_py_randbelow(uint64_t seed, int32_t n) {
+    if (n <= 0) return -1;
+    MT st;
+    uint32_t key[2];
+    int len = 0;
+    if (seed == 0) key[len++] = 0;
+    else {
+        key[len++] = (uint32_t)seed;
+        if (seed >> 32) key[len++] = (uint32_t)(seed >> 32);
+    }
+    st.init_by_array(key, len);
+    int k = 0;
+    while (k < 32 && ((uint32_t)n >> k)) ++k;
+    uint32_t r;
+    do r = st.next() >> (32 - k);
+    while (r >= (uint32_t)n);
+    return (int32_t)r;
+}
+
+int rsk_random_place(rsk_ctx *ctx, const uint8_t *hazard, int32_t N, int32_t S, const uint64_t *seeds,
+                     int32_t *out_node, uint32_t flags) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK(N > 0 && S > 0 && (int64_t)N * S < INT32_MAX && seeds && out_node, "bad arguments");
+    const bool dev = flags & RSK_F_DEVICE;
+    const uint8_t *d_haz;
+    int *d_out;
+    RSK_TRY(stage_in(ctx, 0, hazard, (size_t)N * S, dev, reinterpret_cast<const void **>(&d_haz)));
+    RSK_TRY(stage_out(ctx, 2, out_node, (size_t)S * 4, dev, reinterpret_cast<void **>(&d_out)));
+    int *d_cnt, npb, nch;
+    RSK_TRY(random_count_impl(ctx, d_haz, N, S, &d_cnt, &npb, &nch));
+    std::vector<int> cnt(S), r(S);
+    std::vector<uint64_t> h_seeds(S);
+    RSK_HIP(hipMemcpyAsync(cnt.data(), d_cnt, (size_t)S * 4, hipMemcpyDeviceToHost, ctx->stream));
+    if (dev) RSK_HIP(hipMemcpyAsync(h_seeds.data(), seeds, (size_t)S * 8, hipMemcpyDeviceToHost, ctx->stream));
+    else std::memcpy(h_seeds.data(), seeds, (size_t)S * 8);
+    RSK_HIP(hipStreamSynchronize(ctx->stream));
+    for (int s = 0; s < S; ++s) r[s] = cnt[s] > 0 ? rsk_py_randbelow(h_seeds[s], cnt[s]) : -1;
+    RSK_TRY(ctx->work[4].reserve((size_t)S * 4));
+    RSK_HIP(hipMemcpyAsync(ctx->work[4].ptr, r.data(), (size_t)S * 4, hipMemcpyHostToDevice, ctx->stream));
+    {
+        ScopedTimer tm(ctx, "random_select");
+        select_free_kernel<<<(unsigned)ceil_div(S, 256), 256, 0, ctx->stream>>>(d_haz, N, S, npb, nch,
+                                                                                ctx->work[2].as<int>(),
+                                                                                ctx->work[4].as<int>(), d_out);
+        RSK_HIP(hipGetLastError());
+    }
+    if (!dev) {
+        RSK_TRY(copy_back(ctx, out_node, d_out, (size_t)S * 4, false));
+    }
+    RSK_HIP(hipStreamSynchronize(ctx->stream));  // r[] lives on this host stack frame
+    if (!dev)
+        for (int s = 0; s < S; ++s)
+            if (out_node[s] == RSK_TARGET_NO_CANDIDATE) return RSK_NO_CANDIDATE;
+    return RSK_OK;
+}
+
+int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, const int32_t *pod_cpu,
+                    const int64_t *pod_mem, int32_t N, int32_t *pod_count, int64_t *cpu_sum, int64_t *mem_sum,
+                    uint32_t flags) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK(P >= 0 && S > 0 && N > 0 && (int64_t)N * S < INT32_MAX, "bad sizes");
+    RSK_CHECK(pod_count && cpu_sum && pod_cpu && (!mem_sum || pod_mem), "null argument");
+    const bool dev = flags & RSK_F_DEVICE;
+    const size_t PS = (size_t)P * S, NS = (size_t)N * S;
+    const int *d_assign, *d_cpu;
+    const int64_t *d_mem = nullptr;
+    int *d_cnt;
+    int64_t *d_cs, *d_ms = nullptr;
+    RSK_TRY(stage_in(ctx, 0, assign, PS * 4, dev, reinterpret_cast<const void **>(&d_assign)));
+    RSK_TRY(stage_in(ctx, 1, pod_cpu, (size_t)P * 4, dev, reinterpret_cast<const void **>(&d_cpu)));
+    if (mem_sum) RSK_TRY(stage_in(ctx, 2, pod_mem, (size_t)P * 8, dev, reinterpret_cast<const void **>(&d_mem)));
+    RSK_TRY(stage_out(ctx, 3, pod_count, NS * 4, dev, reinterpret_cast<void **>(&d_cnt)));
+    RSK_TRY(stage_out(ctx, 4, cpu_sum, NS * 8, dev, reinterpret_cast<void **>(&d_cs)));
+    if (mem_sum) RSK_TRY(stage_out(ctx, 5, mem_sum, NS * 8, dev, reinterpret_cast<void **>(&d_ms)));
+    RSK_HIP(hipMemsetAsync(d_cnt, 0, NS * 4, ctx->stream));
+    RSK_HIP(hipMemsetAsync(d_cs, 0, NS * 8, ctx->stream));
+    if (d_ms) RSK_HIP(hipMemsetAsync(d_ms, 0, NS * 8, ctx->stream));
+    if (PS) {
+        ScopedTimer tm(ctx, "node_reduce");
+        node_reduce_kernel<<<(unsigned)ceil_div(PS, 256), 256, 0, ctx->stream>>>(
+            d_assign, P, S, d_cpu, reinterpret_cast<const long long *>(d_mem), N, d_cnt,
+            reinterpret_cast<unsigned long long *>(d_cs), reinterpret_cast<unsigned long long *>(d_ms));
+        RSK_HIP(hipGetLastError());
+    }
+    if (!dev) {
+        RSK_TRY(copy_back(ctx, pod_count, d_cnt, NS * 4, false));
+        RSK_TRY(copy_back(ctx, cpu_sum, d_cs, NS * 8, false));
+        if (mem_sum) RSK_TRY(copy_back(ctx, mem_sum, d_ms, NS * 8, false));
+        RSK_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    return RSK_OK;
+}
+
+int rsk_cpu_pct(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *cap_cpu, int32_t N, int32_t S, int32_t *out_pct,
+                uint32_t flags) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK(N > 0 && S > 0 && (int64_t)N * S < INT32_MAX && out_pct, "bad arguments");
+    const bool dev = flags & RSK_F_DEVICE;
+    const size_t NS = (size_t)N * S;
+    const int *d_use, *d_cap;
+    int *d_out;
+    RSK_TRY(stage_in(ctx, 0, use_cpu, NS * 4, dev, reinterpret_cast<const void **>(&d_use)));
+    RSK_TRY(stage_in(ctx, 1, cap_cpu, (size_t)N * 4, dev, reinterpret_cast<const void **>(&d_cap)));
+    RSK_TRY(stage_out(ctx, 2, out_pct, NS * 4, dev, reinterpret_cast<void **>(&d_out)));
+    {
+        ScopedTimer tm(ctx, "cpu_pct");
+        cpu_pct_kernel<<<(unsigned)ceil_div(NS, 256), 256, 0, ctx->stream>>>(d_use, d_cap, N, S, d_out);
+        RSK_HIP(hipGetLastError());
+    }
+    if (!dev) {
+        RSK_TRY(copy_back(ctx, out_pct, d_out, NS * 4, false));
+        RSK_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    return RSK_OK;
+}
+
+int rsk_detect(rsk_ctx *ctx, const int32_t *cpu_pct, int32_t N, int32_t S, int32_t threshold, uint8_t *out_hazard,
+               int32_t *out_most, uint32_t flags) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK(N > 0 && S > 0 && (int64_t)N * S < INT32_MAX && out_hazard && out_most, "bad arguments");
+    const bool dev = flags & RSK_F_DEVICE;
+    const size_t NS = (size_t)N * S;
+    const int *d_pct;
+    uint8_t *d_haz;
+    int *d_most;
+    RSK_TRY(stage_in(ctx, 0, cpu_pct, NS * 4, dev, reinterpret_cast<const void **>(&d_pct)));
+    RSK_TRY(stage_out(ctx, 1, out_hazard, NS, dev, reinterpret_cast<void **>(&d_haz)));
+    RSK_TRY(stage_out(ctx, 2, out_most, (size_t)S * 4, dev, reinterpret_cast<void **>(&d_most)));
+    RSK_TRY(ctx->work[0].reserve((size_t)S * 8));
+    auto *key = ctx->work[0].as<unsigned long long>();
+    RSK_HIP(hipMemsetAsync(key, 0, (size_t)S * 8, ctx->stream));
+    const int npb = chunk_for(N, S);
+    const unsigned total = (unsigned)(ceil_div(N, npb) * S);
+    {
+        ScopedTimer tm(ctx, "detect");
+        detect_kernel<<<(unsigned)ceil_div(total, 256), 256, 0, ctx->stream>>>(d_pct, N, S, threshold, npb, total,
+                                                                               d_haz, key);
+        decode_first_max<<<(unsigned)ceil_div(S, 256), 256, 0, ctx->stream>>>(key, S, d_most);
+        RSK_HIP(hipGetLastError());
+    }
+    if (!dev) {
+        RSK_TRY(copy_back(ctx, out_hazard, d_haz, NS, false));
+        RSK_TRY(copy_back(ctx, out_most, d_most, (size_t)S * 4, false));
+        RSK_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    return RSK_OK;
+}
+
+int rsk_load_std(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *cap_cpu, int32_t N, int32_t S,
+                 double *out_std, uint32_t flags) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK(N > 0 && S > 0 && (int64_t)N * S < INT32_MAX && out_std, "bad arguments");
+    const bool dev = flags & RSK_F_DEVICE;
+    const size_t NS = (size_t)N * S;
+    const int *d_use, *d_cap;
+    double *d_out;
+    RSK_TRY(stage_in(ctx, 0, use_cpu, NS * 4, dev, reinterpret_cast<const void **>(&d_use)));
+    RSK_TRY(stage_in(ctx, 1, cap_cpu, (size_t)N * 4, dev, reinterpret_cast<const void **>(&d_cap)));
+    RSK_TRY(stage_out(ctx, 2, out_std, (size_t)S * 8, dev, reinterpret_cast<void **>(&d_out)));
+    const int npb = std::max(chunk_for(N, S), 16);
+    const int nch = (int)ceil_div(N, npb);
+    RSK_TRY(ctx->work[0].reserve((size_t)nch * S * 8));
+    RSK_TRY(ctx->work[1].reserve((size_t)nch * S * 8));
+    RSK_TRY(ctx->work[2].reserve((size_t)nch * S * 4));
+    const unsigned total = (unsigned)((int64_t)nch * S);
+    {
+        ScopedTimer tm(ctx, "load_std");
+        std_partial_kernel<<<(unsigned)ceil_div(total, 256), 256, 0, ctx->stream>>>(
+            d_use, d_cap, N, S, npb, total, ctx->work[0].as<double>(), ctx->work[1].as<double>(),
+            ctx->work[2].as<int>());
+        std_merge_kernel<<<(unsigned)ceil_div(S, 256), 256, 0, ctx->stream>>>(
+            ctx->work[0].as<double>(), ctx->work[1].as<double>(), ctx->work[2].as<int>(), nch, S, d_out);
+        RSK_HIP(hipGetLastError());
+    }
+    if (!dev) {
+        RSK_TRY(copy_back(ctx, out_std, d_out, (size_t)S * 8, false));
+        RSK_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    return RSK_OK;
+}
+
+int rsk_cut_cost(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, int32_t P, const int32_t *assign,
+                 int32_t S, const int32_t *missing, int64_t *out_directed, uint32_t flags) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK(P >= 0 && S > 0 && row_ptr && out_directed, "bad arguments");
+    const bool dev = flags & RSK_F_DEVICE;
+    int64_t nnz = 0;
+    if (dev) {
+        int32_t last = 0;
+        RSK_HIP(hipMemcpyAsync(&last, row_ptr + P, 4, hipMemcpyDeviceToHost, ctx->stream));
+        RSK_HIP(hipStreamSynchronize(ctx->stream));
+        nnz = last;
+    } else {
+        nnz = row_ptr[P];
+    }
+    const int *d_rp, *d_col, *d_assign, *d_miss = nullptr;
+    int64_t *d_out;
+    RSK_TRY(stage_in(ctx, 0, row_ptr, (size_t)(P + 1) * 4, dev, reinterpret_cast<const void **>(&d_rp)));
+    RSK_TRY(stage_in(ctx, 1, col_idx, (size_t)nnz * 4, dev, reinterpret_cast<const void **>(&d_col)));
+    RSK_TRY(stage_in(ctx, 2, assign, (size_t)P * S * 4, dev, reinterpret_cast<const void **>(&d_assign)));
+    if (missing) RSK_TRY(stage_in(ctx, 3, missing, (size_t)P * 4, dev, reinterpret_cast<const void **>(&d_miss)));
+    RSK_TRY(stage_out(ctx, 4, out_directed, (size_t)S * 8, dev, reinterpret_cast<void **>(&d_out)));
+    RSK_HIP(hipMemsetAsync(d_out, 0, (size_t)S * 8, ctx->stream));
+    if (P > 0) {
+        const int ppt = chunk_for(P, S);
+        const int64_t tot = ceil_div(P, ppt) * S;
+        RSK_CHECK(tot < INT32_MAX, "grid too large");
+        ScopedTimer tm(ctx, "cut_cost");
+        cut_cost_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, ctx->stream>>>(
+            d_rp, d_col, P, d_assign, S, d_miss, ppt, (unsigned)tot, reinterpret_cast<unsigned long long *>(d_out));
+        RSK_HIP(hipGetLastError());
+    }
+    if (!dev) {
+        RSK_TRY(copy_back(ctx, out_directed, d_out, (size_t)S * 8, false));
+        RSK_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    return RSK_OK;
+}
+
+int rsk_pick_max_pod(rsk_ctx *ctx, const int32_t *assign, const int32_t *pod_cpu, int32_t P, int32_t S,
+                     const int32_t *most, int32_t *out_pod, uint32_t flags) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK(P >= 0 && S > 0 && most && out_pod, "bad arguments");
+    const bool dev = flags & RSK_F_DEVICE;
+    const int *d_assign, *d_cpu, *d_most;
+    int *d_out;
+    RSK_TRY(stage_in(ctx, 0, assign, (size_t)P * S * 4, dev, reinterpret_cast<const void **>(&d_assign)));
+    RSK_TRY(stage_in(ctx, 1, pod_cpu, (size_t)P * 4, dev, reinterpret_cast<const void **>(&d_cpu)));
+    RSK_TRY(stage_in(ctx, 2, most, (size_t)S * 4, dev, reinterpret_cast<const void **>(&d_most)));
+    RSK_TRY(stage_out(ctx, 3, out_pod, (size_t)S * 4, dev, reinterpret_cast<void **>(&d_out)));
+    RSK_TRY(ctx->work[0].reserve((size_t)S * 8));
+    auto *key = ctx->work[0].as<unsigned long long>();
+    RSK_HIP(hipMemsetAsync(key, 0, (size_t)S * 8, ctx->stream));
+    if (P > 0) {
+        const int ppt = chunk_for(P, S);
+        const int64_t tot = ceil_div(P, ppt) * S;
+        RSK_CHECK(tot < INT32_MAX, "grid too large");
+        ScopedTimer tm(ctx, "pick_max_pod");
+        pick_pod_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, ctx->stream>>>(d_assign, d_cpu, P, S, d_most, ppt,
+                                                                               (unsigned)tot, key);
+        RSK_HIP(hipGetLastError());
+    }
+    decode_first_max<<<(unsigned)ceil_div(S, 256), 256, 0, ctx->stream>>>(key, S, d_out);
+    RSK_HIP(hipGetLastError());
+    if (!dev) {
+        RSK_TRY(copy_back(ctx, out_pod, d_out, (size_t)S * 4, false));
+        RSK_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    return RSK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,173 @@
+// rsk_runtime.hip — contexts, errors, staging and kernel timing for librsk.so.
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+#include "rsk_common.h"
+
+namespace rsk {
+
+static thread_local char g_err[1024] = "";
+
+void set_error(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+const char *last_error() { return g_err; }
+
+int DevBuf::reserve(size_t need) {
+    if (need <= bytes && ptr) return RSK_OK;
+    release();
+    size_t n = need < 256 ? 256 : need;
+    RSK_HIP(hipMalloc(&ptr, n));
+    bytes = n;
+    return RSK_OK;
+}
+
+void DevBuf::release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+}
+
+int activate(rsk_ctx *ctx) {
+    RSK_CHECK(ctx, "null context");
+    RSK_HIP(hipSetDevice(ctx->device));
+    return RSK_OK;
+}
+
+ScopedTimer::ScopedTimer(rsk_ctx *c, const char *n) : ctx(c), name(n) {
+    if (!ctx->profiling) return;
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) { a = b = nullptr; return; }
+    (void)hipEventRecord(a, ctx->stream);
+}
+
+ScopedTimer::~ScopedTimer() {
+    if (!a) return;
+    (void)hipEventRecord(b, ctx->stream);
+    ctx->pending[name].push_back({a, b});
+}
+
+int stage_in(rsk_ctx *ctx, int slot, const void *src, size_t bytes, bool device, const void **out) {
+    if (device || bytes == 0) { *out = src; return RSK_OK; }
+    RSK_CHECK(src, "null input pointer");
+    RSK_TRY(ctx->host_stage[slot].reserve(bytes));
+    RSK_HIP(hipMemcpyAsync(ctx->host_stage[slot].ptr, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    *out = ctx->host_stage[slot].ptr;
+    return RSK_OK;
+}
+
+int stage_out(rsk_ctx *ctx, int slot, void *dst, size_t bytes, bool device, void **out) {
+    if (device || bytes == 0) { *out = dst; return RSK_OK; }
+    RSK_TRY(ctx->host_stage[slot].reserve(bytes));
+    *out = ctx->host_stage[slot].ptr;
+    return RSK_OK;
+}
+
+int copy_back(rsk_ctx *ctx, void *host_dst, const void *dev_src, size_t bytes, bool device) {
+    if (device || bytes == 0 || !host_dst) return RSK_OK;
+    RSK_HIP(hipMemcpyAsync(host_dst, dev_src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    return RSK_OK;
+}
+
+}  // namespace rsk
+
+using namespace rsk;
+
+extern "C" {
+
+int rsk_version(void) { return 100; }
+
+const char *rsk_last_error(void) { return rsk::last_error(); }
+
+int rsk_ctx_create(int device, rsk_ctx **out) {
+    RSK_CHECK(out, "null output pointer");
+    *out = nullptr;
+    int n = 0;
+    RSK_HIP(hipGetDeviceCount(&n));
+    RSK_CHECK(device >= 0 && device < n, "device %d out of range (%d visible)", device, n);
+    RSK_HIP(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    RSK_HIP(hipGetDeviceProperties(&prop, device));
+    RSK_CHECK(std::strncmp(prop.gcnArchName, "gfx950", 6) == 0,
+              "librsk is built for gfx950 (MI355X); device %d is %s", device, prop.gcnArchName);
+    rsk_ctx *c = new rsk_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        set_error("hipStreamCreateWithFlags failed");
+        return RSK_EHIP;
+    }
+    c->stream = c->own_stream;
+    *out = c;
+    return RSK_OK;
+}
+
+int rsk_ctx_destroy(rsk_ctx *ctx) {
+    if (!ctx) return RSK_OK;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto &kv : ctx->pending)
+        for (auto &e : kv.second) { (void)hipEventDestroy(e.start); (void)hipEventDestroy(e.stop); }
+    for (auto &b : ctx->host_stage) b.release();
+    for (auto &b : ctx->work) b.release();
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+    return RSK_OK;
+}
+
+int rsk_ctx_set_stream(rsk_ctx *ctx, void *hip_stream) {
+    RSK_CHECK(ctx, "null context");
+    ctx->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->own_stream;
+    return RSK_OK;
+}
+
+int rsk_ctx_synchronize(rsk_ctx *ctx) {
+    RSK_TRY(activate(ctx));
+    RSK_HIP(hipStreamSynchronize(ctx->stream));
+    return RSK_OK;
+}
+
+int rsk_ctx_set_profiling(rsk_ctx *ctx, int on) {
+    RSK_CHECK(ctx, "null context");
+    ctx->profiling = on != 0;
+    return RSK_OK;
+}
+
+int rsk_ctx_kernel_time(rsk_ctx *ctx, const char *kernel, double *total_ms, int64_t *launches) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK(kernel && total_ms && launches, "null argument");
+    auto it = ctx->pending.find(kernel);
+    if (it != ctx->pending.end()) {
+        auto &acc = ctx->totals[kernel];
+        for (auto &e : it->second) {
+            RSK_HIP(hipEventSynchronize(e.stop));
+            float ms = 0.f;
+            RSK_HIP(hipEventElapsedTime(&ms, e.start, e.stop));
+            acc.first += ms;
+            acc.second += 1;
+            (void)hipEventDestroy(e.start);
+            (void)hipEventDestroy(e.stop);
+        }
+        it->second.clear();
+    }
+    auto t = ctx->totals.find(kernel);
+    *total_ms = t == ctx->totals.end() ? 0.0 : t->second.first;
+    *launches = t == ctx->totals.end() ? 0 : t->second.second;
+    return RSK_OK;
+}
+
+int rsk_ctx_reset_profiling(rsk_ctx *ctx) {
+    RSK_TRY(activate(ctx));
+    RSK_HIP(hipStreamSynchronize(ctx->stream));
+    for (auto &kv : ctx->pending)
+        for (auto &e : kv.second) { (void)hipEventDestroy(e.start); (void)hipEventDestroy(e.stop); }
+    ctx->pending.clear();
+    ctx->totals.clear();
+    return RSK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,166 @@
+"""ctypes binding of librsk.so (include/rsk.h).
+
+This is the only place Python touches the native library.  There is no CPU
+fallback: if the library or a gfx950 device is missing, every call raises
+:class:`RskError` (``HIP device required``) — the product path never degrades
+to host code.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from typing import Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("RSK_LIB", os.path.join(HERE, "librsk.so"))
+
+RSK_OK, RSK_NO_CANDIDATE, RSK_EINVAL, RSK_EHIP, RSK_ERCCL = 0, 1, 2, 3, 4
+RSK_F_DEVICE = 1
+TARGET_NONE, TARGET_NO_CANDIDATE = -1, -2
+
+_i32p = C.POINTER(C.c_int32)
+_i64p = C.POINTER(C.c_int64)
+_u8p = C.POINTER(C.c_uint8)
+_u64p = C.POINTER(C.c_uint64)
+_f64p = C.POINTER(C.c_double)
+_vp = C.c_void_p
+
+# name -> (restype, argtypes); every array argument is passed as c_void_p so the
+# same signature carries host (numpy) and device (HBM) pointers.
+SIGNATURES = {
+    "rsk_version": (C.c_int, []),
+    "rsk_last_error": (C.c_char_p, []),
+    "rsk_ctx_create": (C.c_int, [C.c_int, C.POINTER(_vp)]),
+    "rsk_ctx_destroy": (C.c_int, [_vp]),
+    "rsk_ctx_set_stream": (C.c_int, [_vp, _vp]),
+    "rsk_ctx_synchronize": (C.c_int, [_vp]),
+    "rsk_ctx_set_profiling": (C.c_int, [_vp, C.c_int]),
+    "rsk_ctx_kernel_time": (C.c_int, [_vp, C.c_char_p, _f64p, _i64p]),
+    "rsk_ctx_reset_profiling": (C.c_int, [_vp]),
+    "rsk_car_plan_create": (C.c_int, [_vp, _vp, _vp, C.c_int32, _vp, C.c_int32, C.POINTER(_vp)]),
+    "rsk_car_plan_destroy": (C.c_int, [_vp]),
+    "rsk_car_plan_execute": (C.c_int, [_vp, _vp, C.c_int32, _vp, _vp, _vp, C.c_int32, _vp, _vp, C.c_uint32]),
+    "rsk_car_place": (C.c_int, [_vp, _vp, _vp, C.c_int32, _vp, C.c_int32, _vp, _vp, _vp, C.c_int32, _vp,
+                                C.c_int32, _vp, _vp, C.c_uint32]),
+    "rsk_spread_place": (C.c_int, [_vp, _vp, _vp, _vp, C.c_int32, C.c_int32, _vp, C.c_uint32]),
+    "rsk_binpack_place": (C.c_int, [_vp, _vp, _vp, _vp, C.c_int32, C.c_int32, _vp, C.c_uint32]),
+    "rsk_random_count": (C.c_int, [_vp, _vp, C.c_int32, C.c_int32, _vp, C.c_uint32]),
+    "rsk_random_select": (C.c_int, [_vp, _vp, C.c_int32, C.c_int32, _vp, _vp, C.c_uint32]),
+    "rsk_random_place": (C.c_int, [_vp, _vp, C.c_int32, C.c_int32, _vp, _vp, C.c_uint32]),
+    "rsk_py_randbelow": (C.c_int32, [C.c_uint64, C.c_int32]),
+    "rsk_node_reduce": (C.c_int, [_vp, _vp, C.c_int32, C.c_int32, _vp, _vp, C.c_int32, _vp, _vp, _vp, C.c_uint32]),
+    "rsk_cpu_pct": (C.c_int, [_vp, _vp, _vp, C.c_int32, C.c_int32, _vp, C.c_uint32]),
+    "rsk_detect": (C.c_int, [_vp, _vp, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, C.c_uint32]),
+    "rsk_load_std": (C.c_int, [_vp, _vp, _vp, C.c_int32, C.c_int32, _vp, C.c_uint32]),
+    "rsk_cut_cost": (C.c_int, [_vp, _vp, _vp, C.c_int32, _vp, C.c_int32, _vp, _vp, C.c_uint32]),
+    "rsk_pick_max_pod": (C.c_int, [_vp, _vp, _vp, C.c_int32, C.c_int32, _vp, _vp, C.c_uint32]),
+}
+
+
+class RskError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"librsk error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path: Optional[str] = None):
+    """Load librsk.so and declare every signature.  Loading needs no GPU."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise RskError(RSK_EHIP, f"{p} not built (run python __graft_entry__.py build or make -C csrc)")
+        lib = C.CDLL(p)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def last_error() -> str:
+    return (load_library().rsk_last_error() or b"").decode(errors="replace")
+
+
+def check(rc: int, allow_no_candidate: bool = False) -> int:
+    if rc == RSK_OK or (allow_no_candidate and rc == RSK_NO_CANDIDATE):
+        return rc
+    raise RskError(rc, last_error())
+
+
+def ptr(a) -> Optional[int]:
+    """Raw pointer of a numpy array / torch tensor / int (None passes through)."""
+    if a is None:
+        return None
+    if isinstance(a, int):
+        return a
+    if isinstance(a, np.ndarray):
+        if not a.flags["C_CONTIGUOUS"]:
+            raise ValueError("array must be C-contiguous")
+        return a.ctypes.data
+    if hasattr(a, "data_ptr"):
+        if not a.is_contiguous():
+            raise ValueError("tensor must be contiguous")
+        return a.data_ptr()
+    raise TypeError(f"cannot take a pointer of {type(a).__name__}")
+
+
+class Context:
+    """One device + one stream (rsk_ctx).  Not shareable across threads."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = _vp()
+        check(self.lib.rsk_ctx_create(device, C.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.rsk_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+    def set_stream(self, stream_handle: Optional[int]):
+        check(self.lib.rsk_ctx_set_stream(self.handle, stream_handle))
+
+    def synchronize(self):
+        check(self.lib.rsk_ctx_synchronize(self.handle))
+
+    def set_profiling(self, on: bool):
+        check(self.lib.rsk_ctx_set_profiling(self.handle, int(on)))
+
+    def reset_profiling(self):
+        check(self.lib.rsk_ctx_reset_profiling(self.handle))
+
+    def kernel_time(self, name: str):
+        ms, n = C.c_double(), C.c_int64()
+        check(self.lib.rsk_ctx_kernel_time(self.handle, name.encode(), C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+
+_default_ctx: Optional[Context] = None
+
+
+def default_context() -> Context:
+    """Process-wide context on device 0 (LOCAL_RANK under torch.distributed)."""
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(int(os.environ.get("LOCAL_RANK", "0")))
+    return _default_ctx

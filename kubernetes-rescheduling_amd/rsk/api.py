@@ -1,0 +1,193 @@
+"""Array-level API over librsk.so (numpy host arrays or device tensors).
+
+Every function mirrors one entry point of include/rsk.h.  Host numpy arrays go
+through the synchronous host-pointer path; pass ``device=True`` with device
+tensors (anything exposing ``data_ptr()``) for the asynchronous HBM path on the
+context's stream.  Layouts are the batched ABI's: per-scenario arrays are
+scenario-minor, ``x[i*S + s]``.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+
+from ._lib import (RSK_F_DEVICE, Context, check, default_context, load_library, ptr)
+
+_I32 = np.int32
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+def _flags(device: bool) -> int:
+    return RSK_F_DEVICE if device else 0
+
+
+class CarPlan:
+    """A relation CSR uploaded once and binned by degree (rsk_car_plan_*).
+
+    ``rows`` are the moving pods (default: every pod).  ``execute`` scores one
+    batch of S scenarios; results are ``target[i*S + s]`` for ``rows[i]``.
+    """
+
+    def __init__(self, row_ptr, col_idx, rows=None, ctx: Optional[Context] = None):
+        self.ctx = ctx or default_context()
+        self.row_ptr = _c(row_ptr, _I32)
+        self.col_idx = _c(col_idx, _I32) if len(col_idx) else np.zeros(1, _I32)
+        self.P = int(self.row_ptr.shape[0] - 1)
+        self.rows = None if rows is None else _c(rows, _I32)
+        self.Q = self.P if rows is None else int(self.rows.shape[0])
+        import ctypes as C
+        h = C.c_void_p()
+        check(self.ctx.lib.rsk_car_plan_create(self.ctx.handle, ptr(self.row_ptr), ptr(self.col_idx), self.P,
+                                               ptr(self.rows), self.Q, C.byref(h)))
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.ctx.lib.rsk_car_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def execute(self, assign, S, cap_cpu, use_cpu, hazard, N, out_target=None, out_score=None,
+                device: bool = False, want_score: bool = False):
+        if device:
+            check(self.ctx.lib.rsk_car_plan_execute(self.handle, ptr(assign), S, ptr(cap_cpu), ptr(use_cpu),
+                                                    ptr(hazard), N, ptr(out_target), ptr(out_score),
+                                                    RSK_F_DEVICE))
+            return out_target, out_score
+        assign, cap_cpu, use_cpu = _c(assign, _I32), _c(cap_cpu, _I32), _c(use_cpu, _I32)
+        hazard = _c(hazard, np.uint8)
+        if assign.size != self.P * S or cap_cpu.size != N or use_cpu.size != N * S or hazard.size != N * S:
+            raise ValueError("array sizes do not match P, N, S")
+        tgt = np.empty(self.Q * S, _I32) if out_target is None else out_target
+        sc = (np.empty(self.Q * S, _I32) if out_score is None else out_score) if (want_score or out_score is not None) else None
+        check(self.ctx.lib.rsk_car_plan_execute(self.handle, ptr(assign), S, ptr(cap_cpu), ptr(use_cpu), ptr(hazard),
+                                                N, ptr(tgt), ptr(sc), 0), allow_no_candidate=True)
+        return tgt, sc
+
+
+def car_place(row_ptr, col_idx, assign, S, cap_cpu, use_cpu, hazard, N, rows=None, ctx=None, want_score=False):
+    """One-shot CAR scoring (host arrays): returns (target[Q*S], score or None)."""
+    plan = CarPlan(row_ptr, col_idx, rows=rows, ctx=ctx)
+    try:
+        return plan.execute(assign, S, cap_cpu, use_cpu, hazard, N, want_score=want_score)
+    finally:
+        plan.close()
+
+
+def spread_place(pod_count, name_rank, hazard, N, S, ctx=None, out=None, device=False):
+    ctx = ctx or default_context()
+    if device:
+        check(ctx.lib.rsk_spread_place(ctx.handle, ptr(pod_count), ptr(name_rank), ptr(hazard), N, S, ptr(out),
+                                       RSK_F_DEVICE))
+        return out
+    # converted arrays are held in locals: a pointer must not outlive its array
+    v, r, h = _c(pod_count, _I32), _c(name_rank, _I32), _c(hazard, np.uint8)
+    out = np.empty(S, _I32)
+    check(ctx.lib.rsk_spread_place(ctx.handle, ptr(v), ptr(r), ptr(h), N, S, ptr(out), 0), allow_no_candidate=True)
+    return out
+
+
+def binpack_place(cpu_pct, name_rank, hazard, N, S, ctx=None, out=None, device=False):
+    ctx = ctx or default_context()
+    if device:
+        check(ctx.lib.rsk_binpack_place(ctx.handle, ptr(cpu_pct), ptr(name_rank), ptr(hazard), N, S, ptr(out),
+                                        RSK_F_DEVICE))
+        return out
+    v, r, h = _c(cpu_pct, _I32), _c(name_rank, _I32), _c(hazard, np.uint8)
+    out = np.empty(S, _I32)
+    check(ctx.lib.rsk_binpack_place(ctx.handle, ptr(v), ptr(r), ptr(h), N, S, ptr(out), 0), allow_no_candidate=True)
+    return out
+
+
+def random_count(hazard, N, S, ctx=None):
+    ctx = ctx or default_context()
+    h = _c(hazard, np.uint8)
+    out = np.empty(S, _I32)
+    check(ctx.lib.rsk_random_count(ctx.handle, ptr(h), N, S, ptr(out), 0))
+    return out
+
+
+def random_select(hazard, N, S, r, ctx=None):
+    ctx = ctx or default_context()
+    h, rr = _c(hazard, np.uint8), _c(r, _I32)
+    out = np.empty(S, _I32)
+    check(ctx.lib.rsk_random_select(ctx.handle, ptr(h), N, S, ptr(rr), ptr(out), 0), allow_no_candidate=True)
+    return out
+
+
+def random_place(hazard, N, S, seeds, ctx=None):
+    ctx = ctx or default_context()
+    h, sd = _c(hazard, np.uint8), _c(seeds, np.uint64)
+    out = np.empty(S, _I32)
+    check(ctx.lib.rsk_random_place(ctx.handle, ptr(h), N, S, ptr(sd), ptr(out), 0), allow_no_candidate=True)
+    return out
+
+
+def py_randbelow(seed: int, n: int) -> int:
+    """CPython ``random.Random(seed)._randbelow(n)`` from librsk's host MT19937 (no GPU)."""
+    return int(load_library().rsk_py_randbelow(seed, n))
+
+
+def node_reduce(assign, P, S, pod_cpu, pod_mem, N, ctx=None):
+    ctx = ctx or default_context()
+    a, c = _c(assign, _I32), _c(pod_cpu, _I32)
+    m = None if pod_mem is None else _c(pod_mem, np.int64)
+    cnt = np.empty(N * S, _I32)
+    cpu = np.empty(N * S, np.int64)
+    mem = np.empty(N * S, np.int64) if m is not None else None
+    check(ctx.lib.rsk_node_reduce(ctx.handle, ptr(a), P, S, ptr(c), ptr(m), N, ptr(cnt), ptr(cpu), ptr(mem), 0))
+    return cnt, cpu, mem
+
+
+def cpu_pct(use_cpu, cap_cpu, N, S, ctx=None):
+    ctx = ctx or default_context()
+    u, c = _c(use_cpu, _I32), _c(cap_cpu, _I32)
+    out = np.empty(N * S, _I32)
+    check(ctx.lib.rsk_cpu_pct(ctx.handle, ptr(u), ptr(c), N, S, ptr(out), 0))
+    return out
+
+
+def detect(cpu_pct_arr, N, S, threshold=30, ctx=None):
+    ctx = ctx or default_context()
+    pc = _c(cpu_pct_arr, _I32)
+    haz = np.empty(N * S, np.uint8)
+    most = np.empty(S, _I32)
+    check(ctx.lib.rsk_detect(ctx.handle, ptr(pc), N, S, threshold, ptr(haz), ptr(most), 0))
+    return haz, most
+
+
+def load_std(use_cpu, cap_cpu, N, S, ctx=None):
+    ctx = ctx or default_context()
+    u, c = _c(use_cpu, _I32), _c(cap_cpu, _I32)
+    out = np.empty(S, np.float64)
+    check(ctx.lib.rsk_load_std(ctx.handle, ptr(u), ptr(c), N, S, ptr(out), 0))
+    return out
+
+
+def cut_cost(row_ptr, col_idx, assign, P, S, missing=None, ctx=None):
+    """Directed cut count per scenario (the reference reports it / 2)."""
+    ctx = ctx or default_context()
+    rp = _c(row_ptr, _I32)
+    col = _c(col_idx, _I32) if len(col_idx) else np.zeros(1, _I32)
+    a = _c(assign, _I32)
+    m = None if missing is None else _c(missing, _I32)
+    out = np.empty(S, np.int64)
+    check(ctx.lib.rsk_cut_cost(ctx.handle, ptr(rp), ptr(col), P, ptr(a), S, ptr(m), ptr(out), 0))
+    return out
+
+
+def pick_max_pod(assign, pod_cpu, P, S, most, ctx=None):
+    ctx = ctx or default_context()
+    a, c, m = _c(assign, _I32), _c(pod_cpu, _I32), _c(most, _I32)
+    out = np.empty(S, _I32)
+    check(ctx.lib.rsk_pick_max_pod(ctx.handle, ptr(a), ptr(c), P, S, ptr(m), ptr(out), 0))
+    return out

@@ -1,0 +1,256 @@
+"""GPU parity: librsk.so (gfx950) against the reference fixtures and the oracle.
+
+Bit-exact for every placement / integer output; fp64 metrics within 1e-9 rel
+(north_star allows 1e-5).  All calls go through the C-ABI (ctypes).
+"""
+import numpy as np
+import pytest
+
+from helpers import ALGOS, assert_dropin_matches
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from rsk import _lib
+    return _lib.default_context()
+
+
+# ---------------------------------------------------------------------------
+# drop-in module vs the reference's own decisions
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("algo", ALGOS)
+def test_dropin_workmodel_snapshots(ctx, wm_golden, algo):
+    for k, snap in enumerate(wm_golden["snapshots"]):
+        assert_dropin_matches(algo, snap, wm_golden["relation"], f"snapshot {k}")
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+def test_dropin_edge_cases(ctx, edge_golden, algo):
+    for case in edge_golden["cases"]:
+        assert_dropin_matches(algo, case, case["relations"], case["name"])
+
+
+# ---------------------------------------------------------------------------
+# batched CAR vs golden and oracle
+# ---------------------------------------------------------------------------
+
+def _dedup_csr(row_ptr, col_idx):
+    rp, ci = [0], []
+    for p in range(len(row_ptr) - 1):
+        nb = sorted(set(int(q) for q in col_idx[row_ptr[p]:row_ptr[p + 1]]) - {p})
+        ci += nb
+        rp.append(len(ci))
+    return np.array(rp, np.int32), np.array(ci, np.int32)
+
+
+def _check_car(ctx, row_ptr, col_idx, assign, S, cap, use, haz, N, rows=None, label=""):
+    from oracle import oracle as orc
+    from rsk import api
+    tgt, sc = api.car_place(row_ptr, col_idx, assign, S, cap, use, haz, N, rows=rows, ctx=ctx, want_score=True)
+    rp, ci = _dedup_csr(row_ptr, col_idx)
+    ot, osc = orc.car(rp, ci, assign, S, cap, use, haz, N, rows=rows)
+    bad = np.nonzero(tgt != ot)[0]
+    assert bad.size == 0, f"{label}: {bad.size} targets differ, first cell {bad[0]}: gpu {tgt[bad[0]]} oracle {ot[bad[0]]}"
+    assert np.array_equal(sc, osc), f"{label}: scores differ"
+    return tgt
+
+
+def test_car_synth_2k64_golden(ctx, synth_golden):
+    from rsk import api, synth
+    g = synth_golden["2k64"]
+    c = synth.make_cluster(g["P"], g["N"], S=g["S"], seed=0)
+    tgt, _ = api.car_place(c.row_ptr, c.col_idx, c.assign, c.S, c.cap_cpu, c.use_cpu, c.hazard, c.N, ctx=ctx)
+    t = tgt.reshape(c.P, c.S)
+    for sc in g["scenarios"]:
+        assert t[sc["pods"], sc["s"]].tolist() == sc["car_target"], f"scenario {sc['s']}"
+    _check_car(ctx, c.row_ptr, c.col_idx, c.assign, c.S, c.cap_cpu, c.use_cpu, c.hazard, c.N, label="2k64 all rows")
+
+
+def test_car_synth_100k_golden(ctx, synth_golden):
+    from rsk import api, synth
+    g = synth_golden["100k5k"]
+    c = synth.make_cluster(g["P"], g["N"], S=1, seed=0)
+    sc = g["scenarios"][0]
+    tgt, _ = api.car_place(c.row_ptr, c.col_idx, c.assign, 1, c.cap_cpu, c.use_cpu, c.hazard, c.N, ctx=ctx)
+    assert tgt[sc["pods"]].tolist() == sc["car_target"]
+
+
+def test_car_synth_100k_s64_sampled(ctx):
+    """Headline cluster with 64 scenarios; oracle on 1500 sampled rows incl. every heavy row."""
+    from oracle import oracle as orc
+    from rsk import api, synth
+    c = synth.make_cluster(100000, 5000, S=64, seed=0)
+    plan = api.CarPlan(c.row_ptr, c.col_idx, ctx=ctx)
+    tgt, sc = plan.execute(c.assign, c.S, c.cap_cpu, c.use_cpu, c.hazard, c.N, want_score=True)
+    deg = np.diff(c.row_ptr)
+    rng = np.random.default_rng(5)
+    rows = np.unique(np.concatenate([np.nonzero(deg > 16)[0], rng.choice(c.P, 1500, replace=False)]))
+    ot, osc = orc.car(c.row_ptr, c.col_idx, c.assign, c.S, c.cap_cpu, c.use_cpu, c.hazard, c.N, rows=rows, threads=8)
+    t = tgt.reshape(c.P, c.S)[rows].reshape(-1)
+    assert np.array_equal(t, ot)
+    assert np.array_equal(sc.reshape(c.P, c.S)[rows].reshape(-1), osc)
+
+
+def _random_case(rng, P, N, S, max_deg, hub_deg=(), p_haz=0.3, overload=0.2, tie_heavy=False):
+    rows = [[] for _ in range(P)]
+    for p in range(P):
+        d = int(rng.integers(0, max_deg + 1))
+        rows[p] = rng.integers(0, P, d).tolist()
+    for k, hd in enumerate(hub_deg):
+        if k < P:
+            rows[k] = rng.integers(0, P, hd).tolist() + [k, k]  # duplicates + self loop
+    row_ptr = np.zeros(P + 1, np.int32)
+    row_ptr[1:] = np.cumsum([len(r) for r in rows])
+    col_idx = np.array([q for r in rows for q in r], np.int32)
+    nn = max(1, N // 4) if tie_heavy else N
+    assign = rng.integers(-1, nn, P * S).astype(np.int32)
+    cap = rng.choice([4000, 8000], N).astype(np.int32)
+    if tie_heavy:
+        use = np.repeat(rng.choice([1000, 3000], N).astype(np.int32), S)
+    else:
+        use = rng.integers(0, 8000, N * S).astype(np.int32)
+    over = rng.random(N * S) < overload
+    use[over] = (np.repeat(cap, S)[over] + rng.integers(0, 3, over.sum())).astype(np.int32)
+    haz = (rng.random(N * S) < p_haz).astype(np.uint8)
+    return row_ptr, col_idx, assign, cap, use, haz
+
+
+@pytest.mark.parametrize("S", [1, 3, 64, 100, 130])
+def test_car_random_graphs(ctx, S):
+    rng = np.random.default_rng(100 + S)
+    for trial in range(4):
+        N = int(rng.choice([1, 2, 5, 40, 300]))
+        P = int(rng.integers(20, 400))
+        hubs = [17, 65, 300, 1100] if trial == 3 else [20, 70]
+        rp, ci, a, cap, use, haz = _random_case(rng, P, N, S, max_deg=int(rng.choice([2, 8, 16])), hub_deg=hubs,
+                                                p_haz=float(rng.choice([0.0, 0.3, 0.95])),
+                                                tie_heavy=bool(trial % 2))
+        _check_car(ctx, rp, ci, a, S, cap, use, haz, N, label=f"S={S} trial={trial} N={N} P={P}")
+
+
+def test_car_all_hazard_and_rows_subset(ctx):
+    rng = np.random.default_rng(7)
+    P, N, S = 300, 12, 70
+    rp, ci, a, cap, use, haz = _random_case(rng, P, N, S, max_deg=6, hub_deg=[40])
+    haz.reshape(N, S)[:, 5] = 1          # scenario 5: every node hazard -> ValueError cells
+    haz.reshape(N, S)[:, 6] = 1
+    haz.reshape(N, S)[3, 6] = 0          # scenario 6: exactly one candidate
+    rows = np.array([0, 5, 5, 299, 17, 0], np.int32)
+    tgt = _check_car(ctx, rp, ci, a, S, cap, use, haz, N, rows=rows, label="subset")
+    t = tgt.reshape(len(rows), S)
+    assert (t[:, 5] == -2).all()
+    assert (t[:, 6] == 3).all()
+
+
+def test_car_device_mode_matches_host(ctx):
+    import torch
+    from rsk import api, synth
+    c = synth.make_cluster(2000, 64, S=96, seed=3)
+    plan = api.CarPlan(c.row_ptr, c.col_idx, ctx=ctx)
+    host_t, host_s = plan.execute(c.assign, c.S, c.cap_cpu, c.use_cpu, c.hazard, c.N, want_score=True)
+    dev = torch.device("cuda", ctx.device)
+    T = {k: torch.from_numpy(getattr(c, k)).to(dev) for k in ("assign", "cap_cpu", "use_cpu", "hazard")}
+    out_t = torch.empty(c.P * c.S, dtype=torch.int32, device=dev)
+    out_s = torch.empty_like(out_t)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    try:
+        plan.execute(T["assign"], c.S, T["cap_cpu"], T["use_cpu"], T["hazard"], c.N, out_t, out_s, device=True)
+        torch.cuda.synchronize(dev)
+    finally:
+        ctx.set_stream(None)
+    assert np.array_equal(out_t.cpu().numpy(), host_t)
+    assert np.array_equal(out_s.cpu().numpy(), host_s)
+
+
+# ---------------------------------------------------------------------------
+# spread / binpack / random / kernel-3 reductions vs oracle
+# ---------------------------------------------------------------------------
+
+def test_baselines_vs_oracle(ctx, synth_golden):
+    from oracle import oracle as orc
+    from rsk import api, synth
+    c = synth.make_cluster(2000, 64, S=8, seed=0)
+    names = c.node_names()
+    rank = np.argsort(np.argsort(np.array(names))).astype(np.int32)
+    cnt, cpu, mem = api.node_reduce(c.assign, c.P, c.S, c.pod_cpu, c.pod_mem, c.N, ctx=ctx)
+    ocnt, ocpu, omem = orc.node_reduce(c.assign, c.P, c.S, c.pod_cpu, c.pod_mem, c.N)
+    assert np.array_equal(cnt, ocnt) and np.array_equal(cpu, ocpu) and np.array_equal(mem, omem)
+    assert np.array_equal(cpu.reshape(c.N, c.S) + c.bg_cpu[:, None], c.use_cpu.reshape(c.N, c.S))
+    sp = api.spread_place(cnt, rank, c.hazard, c.N, c.S, ctx=ctx)
+    bp = api.binpack_place(c.cpu_pct, rank, c.hazard, c.N, c.S, ctx=ctx)
+    assert np.array_equal(sp, orc.spread(cnt, rank, c.hazard, c.N, c.S))
+    assert np.array_equal(bp, orc.binpack(c.cpu_pct, rank, c.hazard, c.N, c.S))
+    seeds = np.array([sc["random_seed"] for sc in synth_golden["2k64"]["scenarios"]], np.uint64)
+    rd = api.random_place(c.hazard, c.N, c.S, seeds, ctx=ctx)
+    ord_, ocnt2 = orc.random(c.hazard, c.N, c.S, seeds)
+    assert np.array_equal(rd, ord_)
+    assert np.array_equal(api.random_count(c.hazard, c.N, c.S, ctx=ctx), ocnt2)
+    for sc in synth_golden["2k64"]["scenarios"]:
+        s = sc["s"]
+        assert (sp[s], bp[s], rd[s]) == (sc["spread"], sc["binpack"], sc["random"])
+
+
+def test_baselines_ties_and_empty(ctx):
+    from oracle import oracle as orc
+    from rsk import api
+    rng = np.random.default_rng(11)
+    for N, S in [(1, 1), (5, 7), (37, 64), (300, 129)]:
+        val = rng.integers(-1, 3, N * S).astype(np.int32)
+        rank = rng.permutation(N).astype(np.int32)
+        haz = (rng.random(N * S) < 0.4).astype(np.uint8)
+        haz.reshape(N, S)[:, 0] = 1
+        assert np.array_equal(api.spread_place(val, rank, haz, N, S, ctx=ctx), orc.spread(val, rank, haz, N, S))
+        assert np.array_equal(api.binpack_place(val, rank, haz, N, S, ctx=ctx), orc.binpack(val, rank, haz, N, S))
+        r = rng.integers(-1, N + 1, S).astype(np.int32)
+        got = api.random_select(haz, N, S, r, ctx=ctx)
+        for s in range(S):
+            free = [n for n in range(N) if not haz[n * S + s]]
+            exp = free[r[s]] if 0 <= r[s] < len(free) else -2
+            assert got[s] == exp
+
+
+def test_metrics_vs_oracle(ctx):
+    from oracle import oracle as orc
+    from rsk import api, synth
+    c = synth.make_cluster(3000, 97, S=33, seed=9)
+    pct = api.cpu_pct(c.use_cpu, c.cap_cpu, c.N, c.S, ctx=ctx)
+    assert np.array_equal(pct, orc.cpu_pct(c.use_cpu, c.cap_cpu, c.N, c.S))
+    assert np.array_equal(pct, c.cpu_pct)
+    haz, most = api.detect(pct, c.N, c.S, ctx=ctx)
+    oh, om = orc.detect(pct, c.N, c.S)
+    assert np.array_equal(haz, oh) and np.array_equal(most, om)
+    std = api.load_std(c.use_cpu, c.cap_cpu, c.N, c.S, ctx=ctx)
+    ostd = orc.load_std(c.use_cpu, c.cap_cpu, c.N, c.S)
+    np.testing.assert_allclose(std, ostd, rtol=1e-9, atol=1e-12)
+    npstd = np.std(c.use_cpu.reshape(c.N, c.S) / c.cap_cpu[:, None] * 100, axis=0)
+    np.testing.assert_allclose(std, npstd, rtol=1e-9)
+    cut = api.cut_cost(c.row_ptr, c.col_idx, c.assign, c.P, c.S, ctx=ctx)
+    assert np.array_equal(cut, orc.cut_cost(c.row_ptr, c.col_idx, c.assign, c.P, c.S))
+    pm = api.pick_max_pod(c.assign, c.pod_cpu, c.P, c.S, most, ctx=ctx)
+    assert np.array_equal(pm, orc.pick_max_pod(c.assign, c.pod_cpu, c.P, c.S, most))
+
+
+def test_cpu_pct_round_half_even(ctx, metrics_golden):
+    from rsk import api
+    pairs = np.array(metrics_golden["cpu_pct_corner"]["pairs"], np.int64)
+    got = api.cpu_pct(pairs[:, 0].astype(np.int32), pairs[:, 1].astype(np.int32), len(pairs), 1, ctx=ctx)
+    # N = len(pairs), S = 1: cap is per node, one node per pair
+    assert got.tolist() == metrics_golden["cpu_pct_corner"]["pct"]
+
+
+def test_cut_cost_golden(ctx, metrics_golden):
+    from rsk import api, workmodel
+    for case in metrics_golden["communication_cost"]:
+        inf = {}
+        for p in case["pods"]:
+            if p["namespace"] == "default":
+                inf[p["deployment"]] = p["node_name"]
+        names = list(inf)
+        nodes = {n: i for i, n in enumerate(sorted({v for v in inf.values() if v is not None}))}
+        assign = np.array([nodes[inf[d]] if inf[d] is not None else -1 for d in names], np.int32)
+        rp, ci, miss = workmodel.relation_csr(case["relation"], names, dedup=False)
+        d = int(api.cut_cost(rp, ci, assign, len(names), 1, miss, ctx=ctx)[0])
+        assert d / 2 == case["cost"]

@@ -1,0 +1,126 @@
+"""CPU: host-side logic and the C-ABI boundary (no GPU compute calls)."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+from helpers import assert_dropin_matches
+
+HEADER = os.path.join(REPO, "include", "rsk.h")
+
+
+def declared_symbols():
+    txt = open(HEADER, encoding="utf-8").read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(rsk_\w+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    from rsk import _lib
+    lib = _lib.load_library()
+    syms = declared_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(lib, s), f"librsk.so does not export {s}"
+    assert set(syms) == set(_lib.SIGNATURES), "ctypes signature table out of sync with include/rsk.h"
+    assert lib.rsk_version() >= 100
+
+
+def test_library_is_gfx950_code_object():
+    """The embedded device code object targets gfx950 (and nothing else)."""
+    so = os.path.join(REPO, "kubernetes-rescheduling_amd", "rsk", "librsk.so")
+    blob = open(so, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    assert not re.search(rb"amdgcn-amd-amdhsa--gfx9(0|4)\d", blob)
+
+
+def test_randbelow_host_mt_matches_cpython():
+    import random as pyrandom
+    from rsk import api
+    for seed in (0, 1, 7, 2**32 + 5, 123456789):
+        for n in (1, 2, 3, 17, 1000, 99991):
+            assert api.py_randbelow(seed, n) == pyrandom.Random(seed)._randbelow(n)
+
+
+def test_kubescheduling_dropin_matches_reference(wm_golden, edge_golden):
+    """kubescheduling is host-only (affinity merge + create): checkable without a GPU."""
+    for k, snap in enumerate(wm_golden["snapshots"]):
+        assert_dropin_matches("kubescheduling", snap, wm_golden["relation"], f"snapshot {k}")
+    for case in edge_golden["cases"]:
+        assert_dropin_matches("kubescheduling", case, case["relations"], case["name"])
+
+
+def test_merge_affinity_levels():
+    import rescheduling as R
+    orig = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": [{"a": 1}]},
+                             "preferred": [1]},
+            "podAffinity": {"x": 1}}
+    patch = R.exclude_hazard_nodes(["w1"])
+    out = R._merge_affinity(orig, patch)
+    terms = out["nodeAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"]["nodeSelectorTerms"]
+    assert terms[0] == {"a": 1} and terms[1]["matchExpressions"][0]["values"] == ["w1"]
+    assert orig["nodeAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"]["nodeSelectorTerms"] == [{"a": 1}]
+    assert out["podAffinity"] == {"x": 1} and out["nodeAffinity"]["preferred"] == [1]
+    assert R._merge_affinity(None, patch) == patch
+    assert R._merge_affinity({}, {"k": 1}) == {"k": 1}
+    # level-3 dicts are replaced, not merged
+    a = {"x": {"y": {"z": {"old": 1}}}}
+    assert R._merge_affinity(a, {"x": {"y": {"z": {"new": 2}}}}) == {"x": {"y": {"z": {"new": 2}}}}
+
+
+def test_workmodel_relation_matches_reference(wm_golden):
+    from rsk import workmodel
+    calls = wm_golden["workmodel_calls"]
+    wm = {s: {"external_services": [{"services": v}]} for s, v in calls.items()}
+    ours = workmodel.relation_from_workmodel(wm)
+    ref = wm_golden["relation"]
+    assert set(ours) == set(ref)
+    for k in ref:
+        assert set(ours[k]) == set(ref[k]), k
+        assert len(ours[k]) == len(set(ours[k]))
+    rp, ci, miss = workmodel.relation_csr(ref, list(ref))
+    assert rp[-1] == 38 and miss.sum() == 0  # 19 undirected edges, symmetrised
+
+
+def test_synth_generator_pins():
+    from rsk import synth
+    c = synth.make_cluster(2000, 64, S=3, seed=0)
+    assert c.nnz == 2 * (c.P - 1)
+    assert int(np.diff(c.row_ptr).max()) == 61
+    assert int(c.hazard.reshape(c.N, c.S)[:, 0].sum()) == 18
+    # scenario-minor layout and recomputed per-scenario usage
+    a = c.assign.reshape(c.P, c.S)
+    assert (a[:, 1] != a[:, 0]).sum() <= c.P // 100
+    use = c.use_cpu.reshape(c.N, c.S)
+    for s in range(c.S):
+        exp = c.bg_cpu + np.bincount(a[:, s], weights=c.pod_cpu, minlength=c.N)
+        assert np.array_equal(use[:, s], exp.astype(np.int32))
+
+
+def test_car_request_marshalling():
+    from rsk import cluster
+    cm = {"w1": {"node_cpu_capacity": 4000, "node_cpu_usage": 100, "pods": [
+        {"podname": "b", "deploymentname": "b"}, {"podname": "z", "deploymentname": None}]},
+          "w2": {"node_cpu_capacity": 4000, "node_cpu_usage": 200, "pods": [{"podname": "c", "deploymentname": "c"}]}}
+    req = cluster.car_request("a", ["w2"], cm, {"a": ["b", "c", "b"]}, ["w1", "w2", "w1"])
+    assert req.nodes == ["w1", "w2"]
+    assert req.hazard.tolist() == [0, 1]
+    assert req.assign.tolist() == [-1, 0]          # c sits on a hazard node: not scanned
+    assert req.row_ptr.tolist() == [0, 1, 1]
+    with pytest.raises(KeyError):
+        cluster.car_request("a", [], {"w1": cm["w1"]}, {}, ["w1", "w3"])
+
+
+def test_product_path_fails_loudly_without_gpu():
+    """No silent CPU fallback: without a device the drop-in raises RskError."""
+    import torch
+    if torch.cuda.device_count() > 0:
+        pytest.skip("GPU present")
+    import rescheduling as R
+    from rsk._lib import RskError
+    cm = {"w1": {"node_cpu_capacity": 4000, "node_cpu_usage": 100, "cpu_pct": 3, "pods": []}}
+    info = {"metadata": {"name": "a"}, "spec": {"template": {"spec": {"affinity": None}}}}
+    with pytest.raises(RskError):
+        R.communication(info, [], cm, {}, ["w1"])
