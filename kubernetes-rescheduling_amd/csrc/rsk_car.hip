@@ -42,8 +42,12 @@ constexpr int kMaxDegree = 4096;
 constexpr int kNumLight = 4;                       // buckets D = 16, 8, 4, 2
 constexpr int kLightD[kNumLight] = {16, 8, 4, 2};
 constexpr int kLightW[kNumLight] = {20, 12, 8, 4};  // ELL record ints: oi, d, q[D], pad to x4
-constexpr int kNumHeavy = 4;                       // (16,64] (64,256] (256,1024] (1024,4096]
+constexpr int kNumHeavy = 4;                       // (.,64] (64,256] (256,1024] (1024,4096]
 constexpr int kHeavyMax[kNumHeavy] = {64, 256, 1024, 4096};
+constexpr int kTileMax = 32;                       // tile path: deg <= 32
+constexpr int kNumTile = 5;                        // tile buckets D = 32, 16, 8, 4, 2
+constexpr int kTileW[kNumTile] = {36, 20, 12, 8, 4};
+constexpr int kTileCP = 256;                       // pods per tile
 
 struct CarState {
     int bc;  // best count (max score); 0 = no non-hazard neighbour node
@@ -142,25 +146,24 @@ __global__ __launch_bounds__(256) void car_prep_kernel(const int *__restrict__ c
 }
 
 // ---------------------------------------------------------------------------
-// K1: light rows (deg <= 16), ELL records, per-lane register histograms.
+// Register scorer shared by the light kernels.  A record is
+//   [out_row, deg, nb[0..D-1], pad]   (W ints, W % 4 == 0, int4-loadable)
+// and `fetch(nb)` returns the neighbour's node id in this lane's scenario.  Each
+// lane histograms its deg <= D node ids in registers (O(D^2) compares, no
+// memory), gathers one nodekey word per neighbour, and reduces CarState.
 // ---------------------------------------------------------------------------
-struct LightArgs {
-    const int *ell[kNumLight];
-    int n_items[kNumLight];
-    int task_items[kNumLight];   // items per wave task
-    int task_prefix[kNumLight + 1];
-    const int *assign;
+struct ScoreCtx {
     const int *nodekey;
     const int *zc_cnt;
     const unsigned long long *zc_key;
     int *out_target;
     int *out_score;
-    int S, N, SL, PS, blocks_per_chunk;
+    int S, N, PS;
 };
 
-template <int D, int PK, int W>
-__device__ __forceinline__ void light_task(const LightArgs &a, const int *__restrict__ ell, int item0,
-                                           int item_end, int slot, int s, bool lane_ok) {
+template <int D, int PK, int W, class Fetch>
+__device__ __forceinline__ void score_records(const ScoreCtx &a, const int *__restrict__ recs, int item0,
+                                              int item_end, int slot, int s, bool lane_ok, Fetch fetch) {
     const int S = a.S;
     const int step = PK * a.PS;
     for (int base = item0; base < item_end; base += step) {
@@ -170,7 +173,7 @@ __device__ __forceinline__ void light_task(const LightArgs &a, const int *__rest
         for (int k = 0; k < PK; ++k) {
             const int it = base + k * a.PS + slot;
             v[k] = lane_ok && it < item_end;
-            const int4 *rec = reinterpret_cast<const int4 *>(ell + (size_t)(v[k] ? it : item0) * W);
+            const int4 *rec = reinterpret_cast<const int4 *>(recs + (size_t)(v[k] ? it : item0) * W);
             int r[W];
 #pragma unroll
             for (int w = 0; w < W / 4; ++w) {
@@ -180,8 +183,7 @@ __device__ __forceinline__ void light_task(const LightArgs &a, const int *__rest
             oi[k] = r[0];
             dg[k] = v[k] ? r[1] : 0;
 #pragma unroll
-            for (int j = 0; j < D; ++j)
-                nd[k][j] = j < dg[k] ? a.assign[(size_t)r[2 + j] * S + s] : -1;
+            for (int j = 0; j < D; ++j) nd[k][j] = j < dg[k] ? fetch(r[2 + j]) : -1;
         }
 #pragma unroll
         for (int k = 0; k < PK; ++k)
@@ -215,6 +217,18 @@ __device__ __forceinline__ void light_task(const LightArgs &a, const int *__rest
     }
 }
 
+// K1a: direct light rows (deg <= 16 in sparse tiles): ELL records whose
+// neighbours are global pod ids; every neighbour row is a coalesced 256-B gather.
+struct LightArgs {
+    ScoreCtx sc;
+    const int *ell[kNumLight];
+    int n_items[kNumLight];
+    int task_items[kNumLight];   // items per wave task
+    int task_prefix[kNumLight + 1];
+    const int *assign;
+    int SL, blocks_per_chunk;
+};
+
 __global__ __launch_bounds__(256) void car_light_kernel(LightArgs a) {
     const int chunk = blockIdx.x / a.blocks_per_chunk;
     const int wave = (blockIdx.x % a.blocks_per_chunk) * 4 + (threadIdx.x >> 6);
@@ -222,20 +236,80 @@ __global__ __launch_bounds__(256) void car_light_kernel(LightArgs a) {
     if (wave >= a.task_prefix[kNumLight]) return;
     const int slot = lane / a.SL;
     const int s = chunk * a.SL + lane % a.SL;
-    const bool lane_ok = slot < a.PS && s < a.S;
+    const bool lane_ok = slot < a.sc.PS && s < a.sc.S;
     int b = 0;
     while (wave >= a.task_prefix[b + 1]) ++b;
     const int lt = wave - a.task_prefix[b];
     const int item0 = lt * a.task_items[b];
     const int item_end = min(a.n_items[b], item0 + a.task_items[b]);
+    const int *__restrict__ assign = a.assign;
+    const size_t S = (size_t)a.sc.S;
+    auto fetch = [=](int q) { return assign[(size_t)q * S + s]; };
     switch (b) {
-        case 0: light_task<16, 1, 20>(a, a.ell[0], item0, item_end, slot, s, lane_ok); break;
-        case 1: light_task<8, 2, 12>(a, a.ell[1], item0, item_end, slot, s, lane_ok); break;
-        case 2: light_task<4, 4, 8>(a, a.ell[2], item0, item_end, slot, s, lane_ok); break;
-        default: light_task<2, 4, 4>(a, a.ell[3], item0, item_end, slot, s, lane_ok); break;
+        case 0: score_records<16, 1, 20>(a.sc, a.ell[0], item0, item_end, slot, s, lane_ok, fetch); break;
+        case 1: score_records<8, 2, 12>(a.sc, a.ell[1], item0, item_end, slot, s, lane_ok, fetch); break;
+        case 2: score_records<4, 4, 8>(a.sc, a.ell[2], item0, item_end, slot, s, lane_ok, fetch); break;
+        default: score_records<2, 4, 4>(a.sc, a.ell[3], item0, item_end, slot, s, lane_ok, fetch); break;
     }
 }
 constexpr int kLightPK[kNumLight] = {1, 2, 4, 4};
+
+// K1b: tiled light rows (deg <= 32).  The plan orders pods by a DFS of the
+// relation graph (small subtrees first) and cuts the order into tiles of CP
+// pods, so ~96% of a light row's neighbours share its tile (100k/5k PA tree,
+// CP=256).  Workgroup = (tile, chunk of SL <= 64 scenarios):
+//   phase 1  every member row's SL-scenario slice -> LDS tile[CP][SL]: each
+//            assign row is read from HBM once per chunk (256 B, one wave load)
+//   phase 2  owner records (neighbour = ~slot for in-tile, pod id otherwise)
+//            score from LDS, external neighbours gather from global.
+struct TileArgs {
+    ScoreCtx sc;
+    const int *members;            // [T][CP] pod ids, -1 = pad
+    const int *rec[kNumTile];      // per bucket records, grouped by tile
+    const int *rec_off[kNumTile];  // per bucket [T+1]
+    const int *assign;
+    int SL, CP, T;
+};
+
+template <int D, int PK, int W>
+__device__ __forceinline__ void tile_bucket(const TileArgs &a, const int *lds, int b, int tile, int wave, int slot,
+                                            int sl, int s, bool lane_ok) {
+    const int r0 = a.rec_off[b][tile], r1 = a.rec_off[b][tile + 1];
+    const int per = PK * a.sc.PS;
+    const int *__restrict__ assign = a.assign;
+    const size_t S = (size_t)a.sc.S;
+    const int SL = a.SL;
+    auto fetch = [=](int e) { return e < 0 ? lds[(~e) * SL + sl] : assign[(size_t)e * S + s]; };
+    for (int g0 = r0 + wave * per; g0 < r1; g0 += 4 * per)
+        score_records<D, PK, W>(a.sc, a.rec[b], g0, min(r1, g0 + per), slot, s, lane_ok, fetch);
+}
+
+__global__ __launch_bounds__(256) void car_tile_kernel(TileArgs a) {
+    extern __shared__ __attribute__((aligned(16))) int lds[];  // [CP][SL]
+    const int chunk = blockIdx.x / a.T, tile = blockIdx.x % a.T;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int SL = a.SL, PS = a.sc.PS, CP = a.CP;
+    const int slot = lane / SL, sl = lane % SL;
+    const int s = chunk * SL + sl;
+    const bool lane_ok = slot < PS && s < a.sc.S;
+    const int *__restrict__ mem = a.members + (size_t)tile * CP;
+    const int *__restrict__ assign = a.assign;
+    const size_t S = (size_t)a.sc.S;
+#pragma unroll 8
+    for (int r0 = wave * PS; r0 < CP; r0 += 4 * PS) {
+        const int r = r0 + slot;
+        if (slot < PS && r < CP) {
+            const int q = mem[r];
+            lds[r * SL + sl] = (q >= 0 && s < a.sc.S) ? assign[(size_t)q * S + s] : -1;
+        }
+    }
+    __syncthreads();
+    tile_bucket<32, 1, 36>(a, lds, 0, tile, wave, slot, sl, s, lane_ok);
+    tile_bucket<16, 1, 20>(a, lds, 1, tile, wave, slot, sl, s, lane_ok);
+    tile_bucket<8, 2, 12>(a, lds, 2, tile, wave, slot, sl, s, lane_ok);
+    tile_bucket<4, 4, 8>(a, lds, 3, tile, wave, slot, sl, s, lane_ok);
+    tile_bucket<2, 8, 4>(a, lds, 4, tile, wave, slot, sl, s, lane_ok);
+}
 
 // ---------------------------------------------------------------------------
 // K2: heavy rows (deg > 16).  Workgroup = (row, group of G scenarios).
@@ -349,14 +423,24 @@ using namespace rsk;
 struct rsk_car_plan {
     rsk_ctx *ctx = nullptr;
     int P = 0, Q = 0, max_deg = 0;
+    // tiled light rows
+    int CP = kTileCP, T = 0, n_tile_owners = 0;
+    DevBuf members;
+    DevBuf trec[kNumTile], toff[kNumTile];
+    // direct light rows (owners in sparse tiles)
     int n_light[kNumLight] = {0, 0, 0, 0};
     DevBuf ell[kNumLight];
+    // heavy rows
     int n_heavy[kNumHeavy] = {0, 0, 0, 0};
     int heavy_dmax[kNumHeavy] = {0, 0, 0, 0};
     DevBuf heavy_items[kNumHeavy];
     DevBuf hcol;
+    // per-execute workspace
     DevBuf nodekey, zc;
     ~rsk_car_plan() {
+        members.release();
+        for (auto &b : trec) b.release();
+        for (auto &b : toff) b.release();
         for (auto &b : ell) b.release();
         for (auto &b : heavy_items) b.release();
         hcol.release();
@@ -371,6 +455,14 @@ int light_bucket(int d) {
     if (d <= 2) return 3;
     if (d <= 4) return 2;
     if (d <= 8) return 1;
+    return 0;
+}
+
+int tile_bucket_of(int d) {
+    if (d <= 2) return 4;
+    if (d <= 4) return 3;
+    if (d <= 8) return 2;
+    if (d <= 16) return 1;
     return 0;
 }
 
@@ -412,6 +504,171 @@ HeavyGeom heavy_geometry(int dmax, int S) {
     return g;
 }
 
+// Locality order of the pods: DFS over the (deduplicated) relation graph, each
+// node's DFS-tree children visited smallest subtree first, roots in pod order.
+// Consecutive runs of CP pods of this order become tiles.
+std::vector<int> locality_order(int P, const std::vector<int> &rp, const std::vector<int> &ci) {
+    std::vector<int> parent(P, -1), pre;
+    std::vector<char> seen(P, 0);
+    pre.reserve(P);
+    std::vector<std::pair<int, int>> st;  // (node, next edge)
+    for (int r = 0; r < P; ++r) {
+        if (seen[r]) continue;
+        seen[r] = 1;
+        pre.push_back(r);
+        st.push_back({r, rp[r]});
+        while (!st.empty()) {
+            auto &top = st.back();
+            const int u = top.first;
+            if (top.second >= rp[u + 1]) { st.pop_back(); continue; }
+            const int v = ci[top.second++];
+            if (seen[v]) continue;
+            seen[v] = 1;
+            parent[v] = u;
+            pre.push_back(v);
+            st.push_back({v, rp[v]});
+        }
+    }
+    std::vector<int> size(P, 1);
+    for (int k = P - 1; k >= 0; --k) {
+        const int v = pre[k];
+        if (parent[v] >= 0) size[parent[v]] += size[v];
+    }
+    std::vector<int> cptr(P + 1, 0), kids(P > 0 ? P : 1);
+    for (int v = 0; v < P; ++v) if (parent[v] >= 0) ++cptr[parent[v] + 1];
+    for (int v = 0; v < P; ++v) cptr[v + 1] += cptr[v];
+    {
+        std::vector<int> fill(cptr.begin(), cptr.end() - 1);
+        for (int k = 0; k < P; ++k) {
+            const int v = pre[k];
+            if (parent[v] >= 0) kids[fill[parent[v]]++] = v;
+        }
+    }
+    for (int u = 0; u < P; ++u)
+        std::stable_sort(kids.begin() + cptr[u], kids.begin() + cptr[u + 1],
+                         [&](int a, int b) { return size[a] < size[b]; });
+    std::vector<int> order;
+    order.reserve(P);
+    std::vector<int> stack;
+    for (int r = 0; r < P; ++r) {
+        if (parent[r] >= 0) continue;
+        stack.push_back(r);
+        while (!stack.empty()) {
+            const int u = stack.back();
+            stack.pop_back();
+            order.push_back(u);
+            for (int k = cptr[u + 1] - 1; k >= cptr[u]; --k) stack.push_back(kids[k]);
+        }
+    }
+    return order;
+}
+
+int upload(DevBuf &buf, const void *src, size_t bytes) {
+    if (!bytes) return RSK_OK;
+    RSK_TRY(buf.reserve(bytes));
+    RSK_HIP(hipMemcpy(buf.ptr, src, bytes, hipMemcpyHostToDevice));
+    return RSK_OK;
+}
+
+int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_idx, int32_t P, const int32_t *rows,
+               int32_t Q) {
+    // deduplicated adjacency without self edges (the evicted pod is off the cluster)
+    std::vector<int> rp(P + 1, 0), ci;
+    ci.reserve(P ? row_ptr[P] : 0);
+    std::vector<int> nb;
+    for (int p = 0; p < P; ++p) {
+        nb.assign(col_idx + row_ptr[p], col_idx + row_ptr[p + 1]);
+        std::sort(nb.begin(), nb.end());
+        nb.erase(std::unique(nb.begin(), nb.end()), nb.end());
+        nb.erase(std::remove(nb.begin(), nb.end(), p), nb.end());
+        ci.insert(ci.end(), nb.begin(), nb.end());
+        rp[p + 1] = (int)ci.size();
+    }
+    const int CP = plan->CP;
+    const std::vector<int> order = locality_order(P, rp, ci);
+    std::vector<int> pos(P);
+    for (int k = 0; k < P; ++k) pos[order[k]] = k;
+    const int ntiles = (P + CP - 1) / CP;
+
+    // owners per tile (rows with deg <= kTileMax)
+    std::vector<int> owners_in(ntiles, 0);
+    for (int i = 0; i < Q; ++i) {
+        const int p = rows ? rows[i] : i;
+        const int d = rp[p + 1] - rp[p];
+        plan->max_deg = std::max(plan->max_deg, d);
+        if (d <= kTileMax) ++owners_in[pos[p] / CP];
+    }
+    RSK_CHECK(plan->max_deg <= kMaxDegree, "a row has degree %d > %d (unsupported)", plan->max_deg, kMaxDegree);
+    const int min_owners = std::max(1, CP / 16);  // sparser tiles use the direct path
+    std::vector<int> tile_id(ntiles, -1);
+    int T = 0;
+    for (int t = 0; t < ntiles; ++t)
+        if (owners_in[t] >= min_owners) tile_id[t] = T++;
+
+    std::vector<std::vector<std::vector<int>>> trec(kNumTile, std::vector<std::vector<int>>(T));
+    std::vector<std::vector<int>> ell(kNumLight);
+    std::vector<std::vector<HeavyItem>> hitems(kNumHeavy);
+    std::vector<int> hcol;
+    for (int i = 0; i < Q; ++i) {
+        const int p = rows ? rows[i] : i;
+        const int d = rp[p + 1] - rp[p];
+        const int *nbp = ci.data() + rp[p];
+        const int tid = tile_id[pos[p] / CP];
+        if (d <= kTileMax && tid >= 0) {
+            const int b = tile_bucket_of(d);
+            auto &e = trec[b][tid];
+            const size_t o = e.size();
+            e.resize(o + kTileW[b], 0);
+            e[o] = i;
+            e[o + 1] = d;
+            for (int j = 0; j < d; ++j) {
+                const int q = nbp[j];
+                e[o + 2 + j] = (pos[q] / CP == pos[p] / CP) ? ~(pos[q] % CP) : q;
+            }
+            plan->n_tile_owners += 1;
+        } else if (d <= kLightMax) {
+            const int b = light_bucket(d);
+            auto &e = ell[b];
+            const size_t o = e.size();
+            e.resize(o + kLightW[b], 0);
+            e[o] = i;
+            e[o + 1] = d;
+            for (int j = 0; j < d; ++j) e[o + 2 + j] = nbp[j];
+            plan->n_light[b] += 1;
+        } else {
+            const int c = heavy_class(d);
+            hitems[c].push_back({i, (int)hcol.size(), d, 0});
+            hcol.insert(hcol.end(), nbp, nbp + d);
+            plan->n_heavy[c] += 1;
+            plan->heavy_dmax[c] = std::max(plan->heavy_dmax[c], d);
+        }
+    }
+    plan->T = T;
+    if (T > 0) {
+        std::vector<int> mem((size_t)T * CP, -1);
+        for (int t = 0; t < ntiles; ++t) {
+            if (tile_id[t] < 0) continue;
+            for (int k = 0; k < CP && t * CP + k < P; ++k) mem[(size_t)tile_id[t] * CP + k] = order[t * CP + k];
+        }
+        RSK_TRY(upload(plan->members, mem.data(), mem.size() * 4));
+        for (int b = 0; b < kNumTile; ++b) {
+            std::vector<int> flat, off(T + 1, 0);
+            for (int t = 0; t < T; ++t) {
+                flat.insert(flat.end(), trec[b][t].begin(), trec[b][t].end());
+                off[t + 1] = (int)(flat.size() / kTileW[b]);
+            }
+            RSK_TRY(upload(plan->toff[b], off.data(), off.size() * 4));
+            if (flat.empty()) flat.assign(kTileW[b], 0);  // keep a valid pointer
+            RSK_TRY(upload(plan->trec[b], flat.data(), flat.size() * 4));
+        }
+    }
+    for (int b = 0; b < kNumLight; ++b) RSK_TRY(upload(plan->ell[b], ell[b].data(), ell[b].size() * 4));
+    for (int c = 0; c < kNumHeavy; ++c)
+        RSK_TRY(upload(plan->heavy_items[c], hitems[c].data(), hitems[c].size() * sizeof(HeavyItem)));
+    RSK_TRY(upload(plan->hcol, hcol.data(), hcol.size() * 4));
+    return RSK_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -431,76 +688,18 @@ int rsk_car_plan_create(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col
     RSK_CHECK(nnz == 0 || col_idx, "null col_idx");
     for (int64_t k = 0; k < nnz; ++k)
         RSK_CHECK(col_idx[k] >= 0 && col_idx[k] < P, "col_idx[%lld]=%d out of range", (long long)k, col_idx[k]);
-
+    if (rows)
+        for (int32_t i = 0; i < Q; ++i) RSK_CHECK(rows[i] >= 0 && rows[i] < P, "rows[%d]=%d out of range", i, rows[i]);
     auto plan = new rsk_car_plan();
     plan->ctx = ctx;
     plan->P = P;
     plan->Q = Q;
-    std::vector<std::vector<int>> ell(kNumLight);
-    std::vector<std::vector<HeavyItem>> hitems(kNumHeavy);
-    std::vector<int> hcol;
-    std::vector<int> nb;
-    for (int32_t i = 0; i < Q; ++i) {
-        const int p = rows ? rows[i] : i;
-        if (p < 0 || p >= P) {
-            delete plan;
-            set_error("rows[%d]=%d out of range", i, p);
-            return RSK_EINVAL;
-        }
-        nb.assign(col_idx + row_ptr[p], col_idx + row_ptr[p + 1]);
-        std::sort(nb.begin(), nb.end());
-        nb.erase(std::unique(nb.begin(), nb.end()), nb.end());
-        nb.erase(std::remove(nb.begin(), nb.end(), p), nb.end());
-        const int d = (int)nb.size();
-        plan->max_deg = std::max(plan->max_deg, d);
-        if (d <= kLightMax) {
-            const int b = light_bucket(d);
-            auto &e = ell[b];
-            const size_t o = e.size();
-            e.resize(o + kLightW[b], 0);
-            e[o] = i;
-            e[o + 1] = d;
-            for (int j = 0; j < d; ++j) e[o + 2 + j] = nb[j];
-            plan->n_light[b] += 1;
-        } else {
-            const int c = heavy_class(d);
-            if (c < 0) {
-                delete plan;
-                set_error("row %d has degree %d > %d (unsupported)", p, d, kMaxDegree);
-                return RSK_EINVAL;
-            }
-            hitems[c].push_back({i, (int)hcol.size(), d, 0});
-            hcol.insert(hcol.end(), nb.begin(), nb.end());
-            plan->n_heavy[c] += 1;
-            plan->heavy_dmax[c] = std::max(plan->heavy_dmax[c], d);
-        }
-    }
-    for (int b = 0; b < kNumLight; ++b) {
-        if (ell[b].empty()) continue;
-        int rc = plan->ell[b].reserve(ell[b].size() * 4);
-        if (rc == RSK_OK && hipMemcpy(plan->ell[b].ptr, ell[b].data(), ell[b].size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
-            set_error("hipMemcpy ELL failed");
-            rc = RSK_EHIP;
-        }
-        if (rc != RSK_OK) { delete plan; return rc; }
-    }
-    for (int c = 0; c < kNumHeavy; ++c) {
-        if (hitems[c].empty()) continue;
-        int rc = plan->heavy_items[c].reserve(hitems[c].size() * sizeof(HeavyItem));
-        if (rc == RSK_OK && hipMemcpy(plan->heavy_items[c].ptr, hitems[c].data(), hitems[c].size() * sizeof(HeavyItem),
-                                      hipMemcpyHostToDevice) != hipSuccess) {
-            set_error("hipMemcpy heavy items failed");
-            rc = RSK_EHIP;
-        }
-        if (rc != RSK_OK) { delete plan; return rc; }
-    }
-    if (!hcol.empty()) {
-        int rc = plan->hcol.reserve(hcol.size() * 4);
-        if (rc == RSK_OK && hipMemcpy(plan->hcol.ptr, hcol.data(), hcol.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
-            set_error("hipMemcpy heavy CSR failed");
-            rc = RSK_EHIP;
-        }
-        if (rc != RSK_OK) { delete plan; return rc; }
+    const int rc = build_plan(plan, row_ptr, col_idx, P, rows, Q);
+    if (rc != RSK_OK) {
+        std::string keep = last_error();
+        delete plan;
+        set_error("%s", keep.c_str());
+        return rc;
     }
     *out = plan;
     return RSK_OK;
@@ -554,31 +753,57 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
             d_cap, d_use, d_haz, N, S, npb, total, d_key, d_zcnt, d_zkey);
         RSK_HIP(hipGetLastError());
     }
-    {   // K1
+    ScoreCtx sc;
+    sc.nodekey = d_key;
+    sc.zc_cnt = d_zcnt;
+    sc.zc_key = d_zkey;
+    sc.out_target = d_target;
+    sc.out_score = d_score;
+    sc.S = S;
+    sc.N = N;
+    const int SL = std::min(S, 64);
+    sc.PS = 64 / SL;
+    const int64_t chunks = ceil_div(S, SL);
+    if (plan->T > 0) {   // K1b tiles
+        TileArgs a;
+        std::memset(&a, 0, sizeof(a));
+        a.sc = sc;
+        a.members = plan->members.as<int>();
+        for (int b = 0; b < kNumTile; ++b) {
+            a.rec[b] = plan->trec[b].as<int>();
+            a.rec_off[b] = plan->toff[b].as<int>();
+        }
+        a.assign = d_assign;
+        a.SL = SL;
+        a.CP = plan->CP;
+        a.T = plan->T;
+        const size_t lds = (size_t)plan->CP * SL * 4;
+        const int64_t blocks = chunks * plan->T;
+        RSK_CHECK(blocks < INT32_MAX, "tile grid too large");
+        if (lds > 64 * 1024)
+            RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&car_tile_kernel),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        ScopedTimer tm(ctx, "car_tile");
+        car_tile_kernel<<<dim3((unsigned)blocks), dim3(256), lds, ctx->stream>>>(a);
+        RSK_HIP(hipGetLastError());
+    }
+    {   // K1a direct light rows
         LightArgs a;
         std::memset(&a, 0, sizeof(a));
-        a.SL = std::min(S, 64);
-        a.PS = 64 / a.SL;
+        a.sc = sc;
+        a.SL = SL;
         const int iters = 2;
         a.task_prefix[0] = 0;
         for (int b = 0; b < kNumLight; ++b) {
             a.ell[b] = plan->ell[b].as<int>();
             a.n_items[b] = plan->n_light[b];
-            a.task_items[b] = kLightPK[b] * a.PS * iters;
+            a.task_items[b] = kLightPK[b] * sc.PS * iters;
             a.task_prefix[b + 1] = a.task_prefix[b] + (int)ceil_div(plan->n_light[b], a.task_items[b]);
         }
         const int tasks = a.task_prefix[kNumLight];
         if (tasks > 0) {
             a.assign = d_assign;
-            a.nodekey = d_key;
-            a.zc_cnt = d_zcnt;
-            a.zc_key = d_zkey;
-            a.out_target = d_target;
-            a.out_score = d_score;
-            a.S = S;
-            a.N = N;
             a.blocks_per_chunk = (int)ceil_div(tasks, 4);
-            const int64_t chunks = ceil_div(S, a.SL);
             const int64_t blocks = chunks * a.blocks_per_chunk;
             RSK_CHECK(blocks < INT32_MAX, "light grid too large");
             ScopedTimer tm(ctx, "car_light");

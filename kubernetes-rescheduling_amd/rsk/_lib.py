@@ -70,6 +70,24 @@ _lib = None
 _lib_lock = threading.Lock()
 
 
+def _prefer_torch_runtime():
+    """Load PyTorch's HIP runtime before librsk.so when torch is installed.
+
+    PyTorch-ROCm ships its own libamdhip64 / libhsa-runtime64.  If librsk.so were
+    loaded first, the process would hold /opt/rocm's runtime too and torch would
+    later report "No HIP GPUs are available".  Loading torch first makes librsk's
+    libamdhip64.so.7 dependency resolve to the already-loaded runtime, so device
+    pointers and streams are shared.  Set RSK_NO_TORCH=1 to skip (no torch in the
+    process at all).
+    """
+    if os.environ.get("RSK_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load_library(path: Optional[str] = None):
     """Load librsk.so and declare every signature.  Loading needs no GPU."""
     global _lib
@@ -77,6 +95,7 @@ def load_library(path: Optional[str] = None):
         if _lib is not None and path is None:
             return _lib
         p = path or LIB_PATH
+        _prefer_torch_runtime()
         if not os.path.exists(p):
             raise RskError(RSK_EHIP, f"{p} not built (run python __graft_entry__.py build or make -C csrc)")
         lib = C.CDLL(p)
