@@ -113,13 +113,14 @@ def main():
         elapsed = float(e.item())
 
     kernels = {}
-    for name in ("car_prep", "car_light", "car_heavy"):
+    for name in ("car_prep", "car_tile", "car_light", "car_heavy"):
         ms, n = ctx.kernel_time(name)
         if n:
             kernels[name] = {"avg_ms": ms / n, "launches": n, "per_step_ms": ms / args.steps}
     ms_step = elapsed * 1e3 / args.steps
     evals = P * N * S
     value = world * evals / (ms_step / 1e3)
+    info = plan.info()
 
     # parity spot check against the oracle on sampled rows of this rank's batch
     from oracle import oracle as orc
@@ -131,27 +132,37 @@ def main():
                      threads=min(16, os.cpu_count() or 1))
     parity_ok = bool(np.array_equal(got, exp))
 
-    # roofline: dominant kernel = car_light (light rows: deg <= 16); its algorithmic
-    # bytes = own assign slice + target slice per light row (8 B per cell) + its ELL rows
-    Q_light = int((deg <= 16).sum())
-    ell_w = {2: 4, 4: 8, 8: 12, 16: 20}
-    light_bytes = 8 * Q_light * S + 4 * sum(ell_w[min(w for w in ell_w if w >= max(int(d), 1))] for d in deg[deg <= 16])
+    # Algorithmic bytes per launch of each kernel (DESIGN.md "Roofline accounting"):
+    #   car_tile : every pod's assign slice once (4·S per tiled pod) + target of its rows (4·S) + records
+    #   car_light: own slice + target of each direct row (8·S) + ELL records
+    #   car_heavy: own slice + target of each heavy row (8·S) + heavy CSR   (per step, over its launches)
+    #   car_prep : use + hazard (5·N·S) + cap (4·N)
+    tiled_pods = min(P, info["tiles"] * info["tile_pods"])
+    alg = {"car_tile": 4 * S * tiled_pods + 4 * S * info["tile_rows"] + info["tile_bytes"],
+           "car_light": 8 * S * info["direct_rows"] + info["direct_bytes"],
+           "car_heavy": 8 * S * info["heavy_rows"] + info["heavy_bytes"],
+           "car_prep": 5 * N * S + 4 * N}
     B = algorithmic_bytes(P, N, S, c.nnz)
     roof = None
-    if "car_light" in kernels:
-        t = kernels["car_light"]["avg_ms"] / 1e3
-        ach = light_bytes / t / 1e9
-        roof = {"bound": "hbm", "kernel": "car_light", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "algorithmic_bytes": light_bytes}
+    if kernels:
+        dom = max(kernels, key=lambda k: kernels[k]["per_step_ms"])
+        launches_per_step = kernels[dom]["launches"] / args.steps
+        bytes_per_launch = alg[dom] / launches_per_step
+        t = kernels[dom]["avg_ms"] / 1e3
+        ach = bytes_per_launch / t / 1e9
+        roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "algorithmic_bytes": int(bytes_per_launch)}
         try:
             with open(args.pmc_json) as f:
                 pmc = json.load(f)
-            entry = pmc.get(args.config, {}).get("car_light")
+            entry = pmc.get(args.config, {}).get(dom)
             if entry and entry.get("S") == S:
                 roof["traffic"] = entry["hbm_bytes_per_launch"]
                 roof["traffic_source"] = os.path.relpath(args.pmc_json, REPO)
         except (OSError, ValueError):
             pass
+    for k, v in kernels.items():
+        v["algorithmic_GBps"] = round(alg[k] / (v["per_step_ms"] / 1e3) / 1e9, 1)
     step_ach = B / (ms_step / 1e3) / 1e9
     roof_step = {"bound": "hbm", "achieved": round(step_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                  "frac": round(step_ach / HBM_PEAK_GBS, 4), "algorithmic_bytes": B,
@@ -182,7 +193,7 @@ def main():
             "config": {"workload": cfg["name"], "pods": P, "nodes": N, "scenarios_per_gpu": S, "nnz": c.nnz,
                        "max_degree": int(deg.max()), "parallelism": f"scenario-sharded x{world}"},
             "roofline": roof, "roofline_step": roof_step, "cpu_baseline": cpu, "kernels": kernels,
-            "parity_sample_ok": parity_ok, "hbm_bytes_algorithmic_per_step": B,
+            "parity_sample_ok": parity_ok, "hbm_bytes_algorithmic_per_step": B, "plan": info,
         }
         print(json.dumps(line), flush=True)
     plan.close()

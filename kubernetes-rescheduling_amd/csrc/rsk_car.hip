@@ -30,6 +30,7 @@
 #include <climits>
 #include <cstring>
 #include <numeric>
+#include <unordered_map>
 #include <vector>
 
 #include "rsk_common.h"
@@ -44,10 +45,11 @@ constexpr int kLightD[kNumLight] = {16, 8, 4, 2};
 constexpr int kLightW[kNumLight] = {20, 12, 8, 4};  // ELL record ints: oi, d, q[D], pad to x4
 constexpr int kNumHeavy = 4;                       // (.,64] (64,256] (256,1024] (1024,4096]
 constexpr int kHeavyMax[kNumHeavy] = {64, 256, 1024, 4096};
-constexpr int kTileMax = 32;                       // tile path: deg <= 32
-constexpr int kNumTile = 5;                        // tile buckets D = 32, 16, 8, 4, 2
-constexpr int kTileW[kNumTile] = {36, 20, 12, 8, 4};
+constexpr int kTileMax = 16;                       // tile path: deg <= 16
+constexpr int kNumTile = 4;                        // tile buckets D = 16, 8, 4, 2
+constexpr int kTileW[kNumTile] = {20, 12, 8, 4};
 constexpr int kTileCP = 256;                       // pods per tile
+constexpr int kTileXCap = 64;                      // max external rows appended to a tile image
 
 struct CarState {
     int bc;  // best count (max score); 0 = no non-hazard neighbour node
@@ -70,6 +72,13 @@ __device__ __forceinline__ void st_add(CarState &st, int c, int r, int n) {
         st.nm += 1;
         if (r > st.br || (r == st.br && n < st.bn)) { st.br = r; st.bn = n; }
     }
+}
+
+// Candidate key for the register scorers: count (6 bits, <= 32), remaining
+// CPU (32 bits, sign-flipped), 0x3ffffff - node (26 bits): N < 2^26.
+__device__ __forceinline__ unsigned long long pack_cand(int c, int rem, int n) {
+    return ((unsigned long long)c << 58) | ((unsigned long long)((unsigned)rem ^ 0x80000000u) << 26) |
+           (unsigned long long)(0x3ffffff - n);
 }
 
 __device__ __forceinline__ CarState st_combine(CarState a, const CarState &b) {
@@ -151,7 +160,18 @@ __global__ __launch_bounds__(256) void car_prep_kernel(const int *__restrict__ c
 // and `fetch(nb)` returns the neighbour's node id in this lane's scenario.  Each
 // lane histograms its deg <= D node ids in registers (O(D^2) compares, no
 // memory), gathers one nodekey word per neighbour, and reduces CarState.
+//
+// Every load is issued unconditionally from a clamped, always-valid address
+// and the result is selected afterwards: hipcc otherwise branches around each
+// guarded load and waits vmcnt(0) per element, serialising the whole gather.
 // ---------------------------------------------------------------------------
+// Load with a 32-bit element index: base stays in SGPRs and the offset is one
+// VGPR (global_load saddr form) instead of a 64-bit address pair per load.
+// Callers guarantee index * 4 < 2^32.
+__device__ __forceinline__ int ld32(const int *__restrict__ base, unsigned idx) {
+    return *reinterpret_cast<const int *>(reinterpret_cast<const char *>(base) + (idx << 2));
+}
+
 struct ScoreCtx {
     const int *nodekey;
     const int *zc_cnt;
@@ -165,6 +185,7 @@ template <int D, int PK, int W, class Fetch>
 __device__ __forceinline__ void score_records(const ScoreCtx &a, const int *__restrict__ recs, int item0,
                                               int item_end, int slot, int s, bool lane_ok, Fetch fetch) {
     const int S = a.S;
+    const int s_ld = min(s, S - 1);  // loads of inactive lanes stay in bounds
     const int step = PK * a.PS;
     for (int base = item0; base < item_end; base += step) {
         int oi[PK], dg[PK], nd[PK][D], ky[PK][D];
@@ -183,29 +204,49 @@ __device__ __forceinline__ void score_records(const ScoreCtx &a, const int *__re
             oi[k] = r[0];
             dg[k] = v[k] ? r[1] : 0;
 #pragma unroll
-            for (int j = 0; j < D; ++j) nd[k][j] = j < dg[k] ? fetch(r[2 + j]) : -1;
+            for (int j = 0; j < D; ++j) nd[k][j] = fetch(r[2 + j]);  // padding entries encode a valid source
         }
 #pragma unroll
         for (int k = 0; k < PK; ++k)
 #pragma unroll
             for (int j = 0; j < D; ++j) {
-                const int n = nd[k][j];
+                const int n = j < dg[k] ? nd[k][j] : -1;
                 const bool ok = (unsigned)n < (unsigned)a.N;
-                ky[k][j] = ok ? a.nodekey[(size_t)n * S + s] : kKeyHaz;
-                if (!ok) nd[k][j] = -1 - j;  // never equal to another entry
+                const int key = ld32(a.nodekey, (unsigned)(ok ? n : 0) * (unsigned)S + (unsigned)s_ld);
+                ky[k][j] = ok ? key : kKeyHaz;
+                nd[k][j] = ok ? n : -1 - j;  // never equal to another entry
             }
 #pragma unroll
         for (int k = 0; k < PK; ++k) {
-            CarState st;
-            st_init(st);
+            // symmetric pairwise equality: D(D-1)/2 compares, counts kept in VGPRs
+            int cnt[D];
+#pragma unroll
+            for (int j = 0; j < D; ++j) cnt[j] = 1;
+#pragma unroll
+            for (int j = 1; j < D; ++j)
+#pragma unroll
+                for (int jj = 0; jj < j; ++jj) {
+                    const int e = 1 - (int)min((unsigned)(nd[k][j] ^ nd[k][jj]), 1u);
+                    cnt[j] += e;
+                    cnt[jj] += e;
+                }
+            // lexicographic (count, remaining CPU, -node) as one u64: the max is the
+            // reference's choice among the best nodes
+            unsigned long long best = 0;
 #pragma unroll
             for (int j = 0; j < D; ++j) {
-                if (ky[k][j] == kKeyHaz) continue;
-                int c = 0;
-#pragma unroll
-                for (int jj = 0; jj < D; ++jj) c += nd[k][jj] == nd[k][j];
-                st_add(st, c, ky[k][j], nd[k][j]);
+                const unsigned long long key = ky[k][j] == kKeyHaz ? 0ull : pack_cand(cnt[j], ky[k][j], nd[k][j]);
+                best = key > best ? key : best;
             }
+            const int M = (int)(best >> 58);
+            int nm = 0;
+#pragma unroll
+            for (int j = 0; j < D; ++j) nm += (ky[k][j] != kKeyHaz) & (cnt[j] == M);
+            CarState st;
+            st.bc = M;
+            st.nm = nm;
+            st.br = (int)((unsigned)(best >> 26) ^ 0x80000000u);
+            st.bn = 0x3ffffff - (int)(best & 0x3ffffffull);
             if (v[k]) {
                 int sc;
                 const int t = car_finalize(st, s, a.zc_cnt, a.zc_key, sc);
@@ -217,8 +258,9 @@ __device__ __forceinline__ void score_records(const ScoreCtx &a, const int *__re
     }
 }
 
-// K1a: direct light rows (deg <= 16 in sparse tiles): ELL records whose
-// neighbours are global pod ids; every neighbour row is a coalesced 256-B gather.
+// K1a: direct light rows (deg <= 16, owners of sparse tiles): ELL records whose
+// neighbours are global pod ids (padding = pod 0); every neighbour row is one
+// coalesced 256-B gather.
 struct LightArgs {
     ScoreCtx sc;
     const int *ell[kNumLight];
@@ -244,7 +286,8 @@ __global__ __launch_bounds__(256) void car_light_kernel(LightArgs a) {
     const int item_end = min(a.n_items[b], item0 + a.task_items[b]);
     const int *__restrict__ assign = a.assign;
     const size_t S = (size_t)a.sc.S;
-    auto fetch = [=](int q) { return assign[(size_t)q * S + s]; };
+    const int s_ld = min(s, a.sc.S - 1);
+    auto fetch = [=](int q) { return assign[(size_t)q * S + s_ld]; };
     switch (b) {
         case 0: score_records<16, 1, 20>(a.sc, a.ell[0], item0, item_end, slot, s, lane_ok, fetch); break;
         case 1: score_records<8, 2, 12>(a.sc, a.ell[1], item0, item_end, slot, s, lane_ok, fetch); break;
@@ -256,19 +299,25 @@ constexpr int kLightPK[kNumLight] = {1, 2, 4, 4};
 
 // K1b: tiled light rows (deg <= 32).  The plan orders pods by a DFS of the
 // relation graph (small subtrees first) and cuts the order into tiles of CP
-// pods, so ~96% of a light row's neighbours share its tile (100k/5k PA tree,
-// CP=256).  Workgroup = (tile, chunk of SL <= 64 scenarios):
-//   phase 1  every member row's SL-scenario slice -> LDS tile[CP][SL]: each
-//            assign row is read from HBM once per chunk (256 B, one wave load)
-//   phase 2  owner records (neighbour = ~slot for in-tile, pod id otherwise)
-//            score from LDS, external neighbours gather from global.
+// pods; ~96% of a light row's neighbours share its tile (100k/5k PA tree,
+// CP=256) and the rest (a handful per tile) are appended to the tile as extra
+// rows.  Workgroup (8 waves) = (tile, chunk of SL <= 64 scenarios):
+//   phase 1  the tile's rows (members + externals), SL scenarios each -> LDS
+//            image[row][SL]: every assign row leaves HBM once per chunk as
+//            256-B loads, issued in batches with no dependent waits
+//   phase 2  owner records (neighbour = LDS row) score from LDS; only the
+//            nodekey word of each neighbour's node comes from L2.
+constexpr int kTileWaves = 8;
+constexpr int kTileBatch = 8;
+
 struct TileArgs {
     ScoreCtx sc;
-    const int *members;            // [T][CP] pod ids, -1 = pad
-    const int *rec[kNumTile];      // per bucket records, grouped by tile
+    const int *members;            // [T][RS] pod ids (pad = pod 0, never referenced)
+    const int *nrows;              // [T] rows of each tile image (<= RS)
+    const int *rec[kNumTile];      // per bucket records, grouped by tile; nb = image row
     const int *rec_off[kNumTile];  // per bucket [T+1]
     const int *assign;
-    int SL, CP, T;
+    int SL, RS, T;
 };
 
 template <int D, int PK, int W>
@@ -276,39 +325,44 @@ __device__ __forceinline__ void tile_bucket(const TileArgs &a, const int *lds, i
                                             int sl, int s, bool lane_ok) {
     const int r0 = a.rec_off[b][tile], r1 = a.rec_off[b][tile + 1];
     const int per = PK * a.sc.PS;
-    const int *__restrict__ assign = a.assign;
-    const size_t S = (size_t)a.sc.S;
     const int SL = a.SL;
-    auto fetch = [=](int e) { return e < 0 ? lds[(~e) * SL + sl] : assign[(size_t)e * S + s]; };
-    for (int g0 = r0 + wave * per; g0 < r1; g0 += 4 * per)
+    auto fetch = [=](int row) { return lds[row * SL + sl]; };
+    for (int g0 = r0 + wave * per; g0 < r1; g0 += kTileWaves * per)
         score_records<D, PK, W>(a.sc, a.rec[b], g0, min(r1, g0 + per), slot, s, lane_ok, fetch);
 }
 
-__global__ __launch_bounds__(256) void car_tile_kernel(TileArgs a) {
-    extern __shared__ __attribute__((aligned(16))) int lds[];  // [CP][SL]
+__global__ __launch_bounds__(kTileWaves * 64) void car_tile_kernel(TileArgs a) {
+    extern __shared__ __attribute__((aligned(16))) int lds[];  // [RS][SL]
     const int chunk = blockIdx.x / a.T, tile = blockIdx.x % a.T;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int SL = a.SL, PS = a.sc.PS, CP = a.CP;
+    const int SL = a.SL, PS = a.sc.PS;
     const int slot = lane / SL, sl = lane % SL;
     const int s = chunk * SL + sl;
     const bool lane_ok = slot < PS && s < a.sc.S;
-    const int *__restrict__ mem = a.members + (size_t)tile * CP;
+    const int *__restrict__ mem = a.members + (size_t)tile * a.RS;
     const int *__restrict__ assign = a.assign;
     const size_t S = (size_t)a.sc.S;
-#pragma unroll 8
-    for (int r0 = wave * PS; r0 < CP; r0 += 4 * PS) {
-        const int r = r0 + slot;
-        if (slot < PS && r < CP) {
-            const int q = mem[r];
-            lds[r * SL + sl] = (q >= 0 && s < a.sc.S) ? assign[(size_t)q * S + s] : -1;
+    const int s_ld = min(s, a.sc.S - 1);
+    const int nr = a.nrows[tile];
+    const bool writer = slot < PS;
+    for (int r0 = wave * PS; r0 < nr; r0 += kTileWaves * PS * kTileBatch) {
+        int q[kTileBatch], v[kTileBatch];
+#pragma unroll
+        for (int k = 0; k < kTileBatch; ++k) q[k] = mem[min(r0 + k * kTileWaves * PS + slot, a.RS - 1)];
+#pragma unroll
+        for (int k = 0; k < kTileBatch; ++k) v[k] = assign[(size_t)q[k] * S + s_ld];
+#pragma unroll
+        for (int k = 0; k < kTileBatch; ++k) {
+            const int r = r0 + k * kTileWaves * PS + slot;
+            if (writer && r < nr) lds[r * SL + sl] = v[k];
         }
     }
     __syncthreads();
-    tile_bucket<32, 1, 36>(a, lds, 0, tile, wave, slot, sl, s, lane_ok);
-    tile_bucket<16, 1, 20>(a, lds, 1, tile, wave, slot, sl, s, lane_ok);
-    tile_bucket<8, 2, 12>(a, lds, 2, tile, wave, slot, sl, s, lane_ok);
-    tile_bucket<4, 4, 8>(a, lds, 3, tile, wave, slot, sl, s, lane_ok);
-    tile_bucket<2, 8, 4>(a, lds, 4, tile, wave, slot, sl, s, lane_ok);
+
+    tile_bucket<16, 1, 20>(a, lds, 0, tile, wave, slot, sl, s, lane_ok);
+    tile_bucket<8, 2, 12>(a, lds, 1, tile, wave, slot, sl, s, lane_ok);
+    tile_bucket<4, 4, 8>(a, lds, 2, tile, wave, slot, sl, s, lane_ok);
+    tile_bucket<2, 8, 4>(a, lds, 3, tile, wave, slot, sl, s, lane_ok);
 }
 
 // ---------------------------------------------------------------------------
@@ -337,6 +391,7 @@ __device__ __forceinline__ int hash_insert(unsigned *keys, unsigned *cnts, unsig
     }
 }
 
+template <bool kDirect>
 __global__ __launch_bounds__(256) void car_heavy_kernel(const HeavyItem *__restrict__ items, int n_items,
                                                         const int *__restrict__ hcol,
                                                         const int *__restrict__ assign,
@@ -349,26 +404,60 @@ __global__ __launch_bounds__(256) void car_heavy_kernel(const HeavyItem *__restr
     const HeavyItem it = items[blockIdx.x % n_items];
     const int s0 = g * G;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // kDirect: per-wave count table over node ids, two u16 counters per word
+    // (H = ceil(N/2) words); otherwise an open-addressing hash of H slots.
     int *ntile = lds;                                       // [G][dpad]
     int *ctile = ntile + G * dpad;                          // [G][dpad]
-    unsigned *tkey = reinterpret_cast<unsigned *>(ctile + G * dpad);  // [NT][H]
-    unsigned *tcnt = tkey + NT * H;                         // [NT][H]
+    unsigned *tkey = reinterpret_cast<unsigned *>(ctile + G * dpad);  // [NT][H] (hash only)
+    unsigned *tcnt = kDirect ? tkey : tkey + NT * H;        // [NT][H]
     CarState *red = reinterpret_cast<CarState *>(tcnt + NT * H);      // [4][G]
 
     const int d = it.d;
-    for (int idx = tid; idx < d * G; idx += 256) {
-        const int j = idx / G, si = idx - j * G, s = s0 + si;
-        int v = -1;
-        if (s < S) {
-            const int a = assign[(size_t)hcol[it.rb + j] * S + s];
-            v = (unsigned)a < (unsigned)N ? a : -1;
+    // stage: G consecutive scenarios of each neighbour row; loads unconditional
+    // (clamped) and batched so they are all in flight before the LDS writes
+    constexpr int kB = 4;
+    for (int idx0 = tid; idx0 < d * G; idx0 += 256 * kB) {
+        int v[kB];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            const int idx = min(idx0 + k * 256, d * G - 1);
+            const int j = idx / G, si = idx - j * G;
+            v[k] = assign[(size_t)hcol[it.rb + j] * S + min(s0 + si, S - 1)];
         }
-        ntile[si * dpad + j] = v;
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            const int idx = idx0 + k * 256;
+            if (idx < d * G) {
+                const int j = idx / G, si = idx - j * G;
+                ntile[si * dpad + j] = (s0 + si < S && (unsigned)v[k] < (unsigned)N) ? v[k] : -1;
+            }
+        }
     }
     for (int k = tid; k < NT * H; k += 256) { tkey[k] = 0u; tcnt[k] = 0u; }
     __syncthreads();
 
-    if (wave < NT) {
+    if (kDirect && wave < NT) {
+        unsigned *cnts = tcnt + wave * H;
+        for (int si = wave; si < G; si += NT) {
+            const int *nrow = ntile + si * dpad;
+            int *crow = ctile + si * dpad;
+            for (int j = lane; j < d; j += 64) {
+                const int n = nrow[j];
+                if (n >= 0) atomicAdd(&cnts[n >> 1], 1u << ((n & 1) << 4));
+            }
+            __builtin_amdgcn_wave_barrier();
+            for (int j = lane; j < d; j += 64) {
+                const int n = nrow[j];
+                crow[j] = n >= 0 ? (int)((cnts[n >> 1] >> ((n & 1) << 4)) & 0xffffu) : 0;
+            }
+            __builtin_amdgcn_wave_barrier();
+            for (int j = lane; j < d; j += 64) {
+                const int n = nrow[j];
+                if (n >= 0) cnts[n >> 1] = 0u;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    } else if (!kDirect && wave < NT) {
         unsigned *keys = tkey + wave * H, *cnts = tcnt + wave * H;
         const unsigned mask = (unsigned)H - 1u;
         for (int si = wave; si < G; si += NT) {
@@ -393,13 +482,13 @@ __global__ __launch_bounds__(256) void car_heavy_kernel(const HeavyItem *__restr
     const int s = s0 + si;
     CarState st;
     st_init(st);
-    if (s < S) {
+    {
         const int *nrow = ntile + si * dpad, *crow = ctile + si * dpad;
+        const unsigned s_ld = (unsigned)min(s, S - 1);
         for (int j = tid / G; j < d; j += jstep) {
             const int n = nrow[j];
-            if (n < 0) continue;
-            const int key = nodekey[(size_t)n * S + s];
-            if (key != kKeyHaz) st_add(st, crow[j], key, n);
+            const int key = ld32(nodekey, (unsigned)max(n, 0) * (unsigned)S + s_ld);
+            if (s < S && n >= 0 && key != kKeyHaz) st_add(st, crow[j], key, n);
         }
     }
     for (int off = G; off < 64; off <<= 1) st = st_combine(st, st_shfl_xor(st, off));
@@ -424,8 +513,8 @@ struct rsk_car_plan {
     rsk_ctx *ctx = nullptr;
     int P = 0, Q = 0, max_deg = 0;
     // tiled light rows
-    int CP = kTileCP, T = 0, n_tile_owners = 0;
-    DevBuf members;
+    int CP = kTileCP, RS = kTileCP, T = 0, n_tile_owners = 0;
+    DevBuf members, nrows;
     DevBuf trec[kNumTile], toff[kNumTile];
     // direct light rows (owners in sparse tiles)
     int n_light[kNumLight] = {0, 0, 0, 0};
@@ -439,6 +528,7 @@ struct rsk_car_plan {
     DevBuf nodekey, zc;
     ~rsk_car_plan() {
         members.release();
+        nrows.release();
         for (auto &b : trec) b.release();
         for (auto &b : toff) b.release();
         for (auto &b : ell) b.release();
@@ -459,10 +549,9 @@ int light_bucket(int d) {
 }
 
 int tile_bucket_of(int d) {
-    if (d <= 2) return 4;
-    if (d <= 4) return 3;
-    if (d <= 8) return 2;
-    if (d <= 16) return 1;
+    if (d <= 2) return 3;
+    if (d <= 4) return 2;
+    if (d <= 8) return 1;
     return 0;
 }
 
@@ -480,27 +569,33 @@ int next_pow2(int x) {
 
 struct HeavyGeom {
     int G, dpad, H, NT;
+    bool direct;
     size_t lds;
 };
 
-HeavyGeom heavy_geometry(int dmax, int S) {
+constexpr int kDirectMaxN = 16384;  // direct count tables up to 32 KiB per wave
+
+HeavyGeom heavy_geometry(int dmax, int S, int N) {
     // Largest scenario group G (<= 64, <= S rounded up to a power of two) and
     // hash-table count NT that fit 64 KiB of LDS (2 workgroups per CU); failing
     // that, anything up to the 160 KiB a single workgroup may declare.
     HeavyGeom g;
     g.dpad = dmax | 1;  // odd row pitch: scenario rows start on different banks
-    g.H = next_pow2(2 * dmax);
+    g.direct = N <= kDirectMaxN;
+    g.H = g.direct ? (N + 1) / 2 : next_pow2(2 * dmax);
+    const size_t slot_bytes = g.direct ? 4 : 8;
     const int gmax = std::min(64, next_pow2(S));
     const size_t limits[2] = {64 * 1024, 160 * 1024};
     for (size_t lim : limits)
         for (g.G = gmax; g.G >= 1; g.G >>= 1)
             for (g.NT = 4; g.NT >= 1; g.NT >>= 1) {
-                g.lds = (size_t)2 * g.G * g.dpad * 4 + (size_t)g.NT * g.H * 8 + (size_t)4 * g.G * sizeof(CarState);
+                g.lds = (size_t)2 * g.G * g.dpad * 4 + (size_t)g.NT * g.H * slot_bytes +
+                        (size_t)4 * g.G * sizeof(CarState);
                 if (g.lds <= lim) return g;
             }
     g.G = 1;
     g.NT = 1;
-    g.lds = (size_t)2 * g.dpad * 4 + (size_t)g.H * 8 + 4 * sizeof(CarState);
+    g.lds = (size_t)2 * g.dpad * 4 + (size_t)g.H * slot_bytes + 4 * sizeof(CarState);
     return g;
 }
 
@@ -606,15 +701,35 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
         if (owners_in[t] >= min_owners) tile_id[t] = T++;
 
     std::vector<std::vector<std::vector<int>>> trec(kNumTile, std::vector<std::vector<int>>(T));
+    std::vector<std::vector<int>> ext_rows(T);             // external pods appended to each tile image
+    std::vector<std::unordered_map<int, int>> ext_slot(T);  // pod -> image row
     std::vector<std::vector<int>> ell(kNumLight);
     std::vector<std::vector<HeavyItem>> hitems(kNumHeavy);
     std::vector<int> hcol;
+    std::vector<int> fresh;
     for (int i = 0; i < Q; ++i) {
         const int p = rows ? rows[i] : i;
         const int d = rp[p + 1] - rp[p];
         const int *nbp = ci.data() + rp[p];
-        const int tid = tile_id[pos[p] / CP];
-        if (d <= kTileMax && tid >= 0) {
+        const int tile = pos[p] / CP;
+        const int tid = tile_id[tile];
+        bool tiled = d <= kTileMax && tid >= 0;
+        if (tiled) {  // externals of this row must fit the tile image
+            fresh.clear();
+            for (int j = 0; j < d; ++j) {
+                const int q = nbp[j];
+                if (pos[q] / CP != tile && !ext_slot[tid].count(q) &&
+                    std::find(fresh.begin(), fresh.end(), q) == fresh.end())
+                    fresh.push_back(q);
+            }
+            tiled = (int)(ext_rows[tid].size() + fresh.size()) <= kTileXCap;
+            if (tiled)
+                for (int q : fresh) {
+                    ext_slot[tid][q] = CP + (int)ext_rows[tid].size();
+                    ext_rows[tid].push_back(q);
+                }
+        }
+        if (tiled) {
             const int b = tile_bucket_of(d);
             auto &e = trec[b][tid];
             const size_t o = e.size();
@@ -623,7 +738,7 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
             e[o + 1] = d;
             for (int j = 0; j < d; ++j) {
                 const int q = nbp[j];
-                e[o + 2 + j] = (pos[q] / CP == pos[p] / CP) ? ~(pos[q] % CP) : q;
+                e[o + 2 + j] = pos[q] / CP == tile ? pos[q] % CP : ext_slot[tid][q];
             }
             plan->n_tile_owners += 1;
         } else if (d <= kLightMax) {
@@ -645,12 +760,22 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
     }
     plan->T = T;
     if (T > 0) {
-        std::vector<int> mem((size_t)T * CP, -1);
+        size_t xm = 0;
+        for (auto &e : ext_rows) xm = std::max(xm, e.size());
+        const int RS = CP + (int)((xm + 7) / 8 * 8);
+        plan->RS = RS;
+        std::vector<int> mem((size_t)T * RS, 0), nr(T, 0);
         for (int t = 0; t < ntiles; ++t) {
-            if (tile_id[t] < 0) continue;
-            for (int k = 0; k < CP && t * CP + k < P; ++k) mem[(size_t)tile_id[t] * CP + k] = order[t * CP + k];
+            const int id = tile_id[t];
+            if (id < 0) continue;
+            int k = 0;
+            for (; k < CP && t * CP + k < P; ++k) mem[(size_t)id * RS + k] = order[t * CP + k];
+            nr[id] = CP;  // short last tile: rows past its members are never referenced
+            for (size_t x = 0; x < ext_rows[id].size(); ++x) mem[(size_t)id * RS + CP + x] = ext_rows[id][x];
+            nr[id] = CP + (int)ext_rows[id].size();
         }
         RSK_TRY(upload(plan->members, mem.data(), mem.size() * 4));
+        RSK_TRY(upload(plan->nrows, nr.data(), nr.size() * 4));
         for (int b = 0; b < kNumTile; ++b) {
             std::vector<int> flat, off(T + 1, 0);
             for (int t = 0; t < T; ++t) {
@@ -705,6 +830,28 @@ int rsk_car_plan_create(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col
     return RSK_OK;
 }
 
+int rsk_car_plan_info(const rsk_car_plan *plan, int64_t *out, int n) {
+    RSK_CHECK(plan && out && n >= 0, "bad arguments");
+    int64_t light = 0, heavy = 0, tile_bytes = 0, ell_bytes = 0, heavy_bytes = (int64_t)plan->hcol.bytes;
+    for (int b = 0; b < kNumLight; ++b) {
+        light += plan->n_light[b];
+        ell_bytes += (int64_t)plan->n_light[b] * kLightW[b] * 4;
+    }
+    for (int c = 0; c < kNumHeavy; ++c) {
+        heavy += plan->n_heavy[c];
+        heavy_bytes += (int64_t)plan->n_heavy[c] * (int64_t)sizeof(HeavyItem);
+    }
+    if (plan->T > 0) {
+        tile_bytes = (int64_t)plan->T * plan->RS * 4 + (int64_t)plan->T * 4;
+        for (int b = 0; b < kNumTile; ++b) tile_bytes += (int64_t)plan->trec[b].bytes + (int64_t)plan->toff[b].bytes;
+    }
+    const int64_t v[10] = {plan->n_tile_owners, light, heavy, plan->T, plan->RS, plan->CP,
+                           tile_bytes, ell_bytes, heavy_bytes, plan->max_deg};
+    const int m = n < 10 ? n : 10;
+    for (int i = 0; i < m; ++i) out[i] = v[i];
+    return m;
+}
+
 int rsk_car_plan_destroy(rsk_car_plan *plan) {
     if (!plan) return RSK_OK;
     (void)hipSetDevice(plan->ctx->device);
@@ -720,8 +867,8 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     rsk_ctx *ctx = plan->ctx;
     RSK_TRY(activate(ctx));
     RSK_CHECK(S > 0 && N > 0, "need S > 0 and N > 0 (S=%d N=%d)", S, N);
-    RSK_CHECK((int64_t)N * S < INT32_MAX && (int64_t)plan->P * S < ((int64_t)1 << 40),
-              "N*S too large (N=%d S=%d)", N, S);
+    RSK_CHECK((int64_t)N * S < ((int64_t)1 << 30) && N < (1 << 26) && (int64_t)plan->P * S < ((int64_t)1 << 40),
+              "N*S too large (N=%d S=%d; need N*S < 2^30, N < 2^26)", N, S);
     RSK_CHECK(out_target, "null out_target");
     const bool dev = (flags & RSK_F_DEVICE) != 0;
     const size_t PS_ = (size_t)plan->P * S, NS = (size_t)N * S, QS = (size_t)plan->Q * S;
@@ -769,22 +916,23 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         std::memset(&a, 0, sizeof(a));
         a.sc = sc;
         a.members = plan->members.as<int>();
+        a.nrows = plan->nrows.as<int>();
         for (int b = 0; b < kNumTile; ++b) {
             a.rec[b] = plan->trec[b].as<int>();
             a.rec_off[b] = plan->toff[b].as<int>();
         }
         a.assign = d_assign;
         a.SL = SL;
-        a.CP = plan->CP;
+        a.RS = plan->RS;
         a.T = plan->T;
-        const size_t lds = (size_t)plan->CP * SL * 4;
+        const size_t lds = (size_t)plan->RS * SL * 4;
         const int64_t blocks = chunks * plan->T;
         RSK_CHECK(blocks < INT32_MAX, "tile grid too large");
         if (lds > 64 * 1024)
             RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&car_tile_kernel),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         ScopedTimer tm(ctx, "car_tile");
-        car_tile_kernel<<<dim3((unsigned)blocks), dim3(256), lds, ctx->stream>>>(a);
+        car_tile_kernel<<<dim3((unsigned)blocks), dim3(kTileWaves * 64), lds, ctx->stream>>>(a);
         RSK_HIP(hipGetLastError());
     }
     {   // K1a direct light rows
@@ -814,15 +962,16 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     for (int c = 0; c < kNumHeavy; ++c) {   // K2
         const int n = plan->n_heavy[c];
         if (!n) continue;
-        const HeavyGeom g = heavy_geometry(plan->heavy_dmax[c], S);
+        const HeavyGeom g = heavy_geometry(plan->heavy_dmax[c], S, N);
         RSK_CHECK(g.lds <= 160 * 1024, "heavy class %d needs %zu B of LDS", c, g.lds);
         const int64_t groups = ceil_div(S, g.G);
         RSK_CHECK(groups * n < INT32_MAX, "heavy grid too large");
+        auto kern = g.direct ? &car_heavy_kernel<true> : &car_heavy_kernel<false>;
         if (g.lds > 64 * 1024)
-            RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&car_heavy_kernel),
+            RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds));
         ScopedTimer tm(ctx, "car_heavy");
-        car_heavy_kernel<<<dim3((unsigned)(groups * n)), dim3(256), g.lds, ctx->stream>>>(
+        kern<<<dim3((unsigned)(groups * n)), dim3(256), g.lds, ctx->stream>>>(
             plan->heavy_items[c].as<HeavyItem>(), n, plan->hcol.as<int>(), d_assign, d_key, S, N, g.G, g.dpad,
             g.H, g.NT, d_zcnt, d_zkey, d_target, d_score);
         RSK_HIP(hipGetLastError());

@@ -42,6 +42,7 @@ SIGNATURES = {
     "rsk_ctx_reset_profiling": (C.c_int, [_vp]),
     "rsk_car_plan_create": (C.c_int, [_vp, _vp, _vp, C.c_int32, _vp, C.c_int32, C.POINTER(_vp)]),
     "rsk_car_plan_destroy": (C.c_int, [_vp]),
+    "rsk_car_plan_info": (C.c_int, [_vp, _vp, C.c_int]),
     "rsk_car_plan_execute": (C.c_int, [_vp, _vp, C.c_int32, _vp, _vp, _vp, C.c_int32, _vp, _vp, C.c_uint32]),
     "rsk_car_place": (C.c_int, [_vp, _vp, _vp, C.c_int32, _vp, C.c_int32, _vp, _vp, _vp, C.c_int32, _vp,
                                 C.c_int32, _vp, _vp, C.c_uint32]),

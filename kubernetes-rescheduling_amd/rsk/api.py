@@ -45,6 +45,15 @@ class CarPlan:
                                                ptr(self.rows), self.Q, C.byref(h)))
         self.handle = h
 
+    INFO_FIELDS = ("tile_rows", "direct_rows", "heavy_rows", "tiles", "tile_image_rows", "tile_pods",
+                   "tile_bytes", "direct_bytes", "heavy_bytes", "max_degree")
+
+    def info(self) -> dict:
+        """How the plan routed its rows (rsk_car_plan_info)."""
+        out = np.zeros(len(self.INFO_FIELDS), np.int64)
+        n = self.ctx.lib.rsk_car_plan_info(self.handle, ptr(out), len(out))
+        return {k: int(v) for k, v in zip(self.INFO_FIELDS[:n], out[:n])}
+
     def close(self):
         if getattr(self, "handle", None):
             self.ctx.lib.rsk_car_plan_destroy(self.handle)

@@ -131,6 +131,16 @@ def test_car_random_graphs(ctx, S):
         _check_car(ctx, rp, ci, a, S, cap, use, haz, N, label=f"S={S} trial={trial} N={N} P={P}")
 
 
+def test_car_heavy_hash_path_large_n(ctx):
+    """N > 16384 switches heavy rows from direct LDS count tables to the LDS hash."""
+    rng = np.random.default_rng(21)
+    for S in (1, 5, 64):
+        P, N = 600, 20000
+        rp, ci, a, cap, use, haz = _random_case(rng, P, N, S, max_deg=4, hub_deg=[40, 200, 700], p_haz=0.2)
+        a[:] = rng.integers(-1, 300, P * S)  # crowd the neighbours onto few nodes -> real counts and ties
+        _check_car(ctx, rp, ci, a, S, cap, use, haz, N, rows=np.arange(0, 60, dtype=np.int32), label=f"hash S={S}")
+
+
 def test_car_all_hazard_and_rows_subset(ctx):
     rng = np.random.default_rng(7)
     P, N, S = 300, 12, 70
