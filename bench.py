@@ -69,13 +69,15 @@ def main():
     dev = torch.device("cuda", local)
 
     from rsk import _lib, api, synth
+    from rsk import dist as rdist
 
     cfg = dict(CONFIGS[args.config])
     if args.scenarios:
         cfg["S"] = args.scenarios
     P, N, S = cfg["P"], cfg["N"], cfg["S"]
     t0 = time.time()
-    c = synth.make_cluster(P, N, S=S, seed=0, s0=rank * S)
+    shard = rdist.shard_for(rank, world, S)
+    c = synth.make_cluster(P, N, S=S, seed=0, s0=shard.s0)
     log(f"[bench] rank {rank}: generated {P}x{N}x{S} in {time.time() - t0:.1f}s")
 
     ctx = _lib.Context(local)
