@@ -115,7 +115,7 @@ def main():
         elapsed = float(e.item())
 
     kernels = {}
-    for name in ("car_prep", "car_tile", "car_light", "car_heavy"):
+    for name in ("car_prep", "car_tile", "car_light", "car_mid", "car_heavy"):
         ms, n = ctx.kernel_time(name)
         if n:
             kernels[name] = {"avg_ms": ms / n, "launches": n, "per_step_ms": ms / args.steps}
@@ -142,6 +142,7 @@ def main():
     tiled_pods = min(P, info["tiles"] * info["tile_pods"])
     alg = {"car_tile": 4 * S * tiled_pods + 4 * S * info["tile_rows"] + info["tile_bytes"],
            "car_light": 8 * S * info["direct_rows"] + info["direct_bytes"],
+           "car_mid": 8 * S * info["mid_rows"] + info["mid_bytes"],
            "car_heavy": 8 * S * info["heavy_rows"] + info["heavy_bytes"],
            "car_prep": 5 * N * S + 4 * N}
     B = algorithmic_bytes(P, N, S, c.nnz)

@@ -83,12 +83,11 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
                          const int32_t *use_cpu, const uint8_t *hazard, int32_t N,
                          int32_t *out_target, int32_t *out_score, uint32_t flags);
 /* Plan layout statistics (host, no GPU work): how the rows were routed.
- * out[0] rows on the LDS-tiled path     out[1] rows on the direct light path
- * out[2] rows on the heavy path         out[3] tiles        out[4] rows per tile image
- * out[5] pods per tile                  out[6] bytes of tile records + members
- * out[7] bytes of direct ELL records    out[8] bytes of heavy items + CSR
- * out[9] max row degree
- * Returns the number of fields written (<= n).                                  */
+ * out[0] rows on the LDS-tiled path (deg <= 16)   out[1] direct light rows (deg <= 16)
+ * out[2] mid rows (17..64)    out[3] heavy rows (> 64)    out[4] tiles
+ * out[5] rows per tile image  out[6] pods per tile        out[7] tile plan bytes
+ * out[8] direct record bytes  out[9] mid record bytes     out[10] heavy item + CSR bytes
+ * out[11] max row degree.  Returns the number of fields written (<= n).     */
 int rsk_car_plan_info(const rsk_car_plan *plan, int64_t *out, int n);
 /* One-shot convenience: plan_create + execute + destroy. */
 int rsk_car_place(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, int32_t P,

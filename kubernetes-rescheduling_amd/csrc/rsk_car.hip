@@ -18,14 +18,17 @@
 //     ("zero case"), computed once by car_prep_kernel.
 //
 // Kernels (one HIP stream, all integer, no atomics on the decision path):
-//   car_prep_kernel   nodekey[n*S+s] = hazard ? KEY_HAZ : cap[n]-use[n*S+s]
-//                     (one packed word per node gather later) + zero case per s.
-//   car_light_kernel  rows with deg <= 16: lane = scenario (64 consecutive
-//                     scenarios per wave -> each neighbour row is one coalesced
-//                     256-B load), per-lane register histogram, ELL rows.
-//   car_heavy_kernel  rows with deg > 16: one workgroup per (row, scenario
-//                     group); neighbour node ids staged in LDS, per-wave LDS hash
-//                     histograms, coalesced nodekey lookups, cross-lane reduce.
+//   car_prep_kernel   nodekey[n*S+s] = hazard ? KEY_HAZ : cap[n]-use[n*S+s] (one
+//                     gather word per node later) + the zero case per scenario.
+//   car_tile_kernel   deg <= 16 rows of dense tiles: LDS image of the tile's
+//                     assign rows (each row read from HBM once per chunk),
+//                     per-lane register histograms (lane = scenario).
+//   car_light_kernel  deg <= 16 rows of sparse tiles: same scorer, neighbour
+//                     rows gathered from global.
+//   car_mid_kernel    17 <= deg <= 64: per-lane bitonic sort of the neighbour
+//                     node ids in registers + run-length scan.
+//   car_heavy_kernel  deg > 64: node ids staged in LDS, per-wave LDS count
+//                     tables / hash, coalesced lookups, cross-lane reduce.
 #include <algorithm>
 #include <climits>
 #include <cstring>
@@ -38,18 +41,20 @@
 namespace rsk {
 
 constexpr int kKeyHaz = INT_MIN;
-constexpr int kLightMax = 16;
 constexpr int kMaxDegree = 4096;
+constexpr int kLightMax = 16;                      // register-histogram rows: deg <= 16
 constexpr int kNumLight = 4;                       // buckets D = 16, 8, 4, 2
-constexpr int kLightD[kNumLight] = {16, 8, 4, 2};
-constexpr int kLightW[kNumLight] = {20, 12, 8, 4};  // ELL record ints: oi, d, q[D], pad to x4
-constexpr int kNumHeavy = 4;                       // (.,64] (64,256] (256,1024] (1024,4096]
-constexpr int kHeavyMax[kNumHeavy] = {64, 256, 1024, 4096};
-constexpr int kTileMax = 16;                       // tile path: deg <= 16
-constexpr int kNumTile = 4;                        // tile buckets D = 16, 8, 4, 2
-constexpr int kTileW[kNumTile] = {20, 12, 8, 4};
+constexpr int kLightW[kNumLight] = {20, 12, 8, 4};  // record ints: oi, d, nb[D], pad to x4
+constexpr int kLightPK[kNumLight] = {1, 2, 4, 4};  // direct kernel: records per lane per step
+constexpr int kMidMax = 64;                        // sorted-register rows: 17 <= deg <= 64
+constexpr int kNumMid = 2;                         // buckets D = 32, 64
+constexpr int kMidW[kNumMid] = {36, 68};
+constexpr int kNumHeavy = 3;                       // (64,256] (256,1024] (1024,4096]
+constexpr int kHeavyMax[kNumHeavy] = {256, 1024, 4096};
 constexpr int kTileCP = 256;                       // pods per tile
 constexpr int kTileXCap = 64;                      // max external rows appended to a tile image
+constexpr int kTileWaves = 8;                      // waves per tile workgroup
+constexpr int kTileBatch = 12;                     // rows per wave per load batch (register path)
 
 struct CarState {
     int bc;  // best count (max score); 0 = no non-hazard neighbour node
@@ -74,13 +79,6 @@ __device__ __forceinline__ void st_add(CarState &st, int c, int r, int n) {
     }
 }
 
-// Candidate key for the register scorers: count (6 bits, <= 32), remaining
-// CPU (32 bits, sign-flipped), 0x3ffffff - node (26 bits): N < 2^26.
-__device__ __forceinline__ unsigned long long pack_cand(int c, int rem, int n) {
-    return ((unsigned long long)c << 58) | ((unsigned long long)((unsigned)rem ^ 0x80000000u) << 26) |
-           (unsigned long long)(0x3ffffff - n);
-}
-
 __device__ __forceinline__ CarState st_combine(CarState a, const CarState &b) {
     if (b.bc > a.bc) return b;
     if (b.bc < a.bc) return a;
@@ -96,6 +94,26 @@ __device__ __forceinline__ CarState st_shfl_xor(const CarState &st, int off) {
     o.bn = __shfl_xor(st.bn, off, 64);
     o.nm = __shfl_xor(st.nm, off, 64);
     return o;
+}
+
+// Candidate key of the register scorers: lexicographic (count, remaining CPU,
+// -node) as one u64 — count 7 bits (<= 64), remaining CPU 32 bits (sign
+// flipped), 0x1ffffff - node 25 bits (N < 2^25).  0 = no candidate.
+constexpr int kNodeBits = 25;
+constexpr unsigned kNodeMask = (1u << kNodeBits) - 1u;
+__device__ __forceinline__ unsigned long long pack_cand(int c, int rem, int n) {
+    return ((unsigned long long)c << (32 + kNodeBits)) |
+           ((unsigned long long)((unsigned)rem ^ 0x80000000u) << kNodeBits) |
+           (unsigned long long)(kNodeMask - (unsigned)n);
+}
+__device__ __forceinline__ int cand_count(unsigned long long k) { return (int)(k >> (32 + kNodeBits)); }
+__device__ __forceinline__ CarState cand_state(unsigned long long best, int nm) {
+    CarState st;
+    st.bc = cand_count(best);
+    st.nm = nm;
+    st.br = (int)((unsigned)(best >> kNodeBits) ^ 0x80000000u);
+    st.bn = (int)(kNodeMask - (unsigned)(best & kNodeMask));
+    return st;
 }
 
 __device__ __forceinline__ unsigned long long zc_pack(int rem, int n) {
@@ -118,6 +136,13 @@ __device__ __forceinline__ int car_finalize(const CarState &st, int s, const int
     score = st.bc;
     if (st.nm == st.bc) return st.bn;
     return st.br >= 0 ? st.bn : RSK_TARGET_NONE;
+}
+
+// Load with a 32-bit element index: the base stays in SGPRs and the offset is
+// one VGPR (global_load saddr form) instead of a 64-bit address pair per
+// in-flight load.  Callers guarantee index * 4 < 2^32.
+__device__ __forceinline__ int ld32(const int *__restrict__ base, unsigned idx) {
+    return *reinterpret_cast<const int *>(reinterpret_cast<const char *>(base) + (idx << 2));
 }
 
 // ---------------------------------------------------------------------------
@@ -155,23 +180,17 @@ __global__ __launch_bounds__(256) void car_prep_kernel(const int *__restrict__ c
 }
 
 // ---------------------------------------------------------------------------
-// Register scorer shared by the light kernels.  A record is
+// Register scorer for deg <= 16 rows.  A record is
 //   [out_row, deg, nb[0..D-1], pad]   (W ints, W % 4 == 0, int4-loadable)
-// and `fetch(nb)` returns the neighbour's node id in this lane's scenario.  Each
-// lane histograms its deg <= D node ids in registers (O(D^2) compares, no
-// memory), gathers one nodekey word per neighbour, and reduces CarState.
+// and `fetch(nb)` returns the neighbour's node id in this lane's scenario
+// (padding entries encode a valid source).  Each lane counts equal node ids
+// pairwise in registers, gathers one nodekey word per neighbour and keeps the
+// max packed candidate key.
 //
 // Every load is issued unconditionally from a clamped, always-valid address
-// and the result is selected afterwards: hipcc otherwise branches around each
-// guarded load and waits vmcnt(0) per element, serialising the whole gather.
+// and the result selected afterwards: hipcc otherwise branches around each
+// guarded load and waits vmcnt(0) per element, serialising the gather.
 // ---------------------------------------------------------------------------
-// Load with a 32-bit element index: base stays in SGPRs and the offset is one
-// VGPR (global_load saddr form) instead of a 64-bit address pair per load.
-// Callers guarantee index * 4 < 2^32.
-__device__ __forceinline__ int ld32(const int *__restrict__ base, unsigned idx) {
-    return *reinterpret_cast<const int *>(reinterpret_cast<const char *>(base) + (idx << 2));
-}
-
 struct ScoreCtx {
     const int *nodekey;
     const int *zc_cnt;
@@ -180,6 +199,32 @@ struct ScoreCtx {
     int *out_score;
     int S, N, PS;
 };
+
+template <int D>
+__device__ __forceinline__ CarState reduce_entries(const int (&nd)[D], const int (&ky)[D]) {
+    int cnt[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) cnt[j] = 1;
+#pragma unroll
+    for (int j = 1; j < D; ++j)
+#pragma unroll
+        for (int jj = 0; jj < j; ++jj) {
+            const int e = 1 - (int)min((unsigned)(nd[j] ^ nd[jj]), 1u);
+            cnt[j] += e;
+            cnt[jj] += e;
+        }
+    unsigned long long best = 0;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        const unsigned long long key = ky[j] == kKeyHaz ? 0ull : pack_cand(cnt[j], ky[j], nd[j]);
+        best = key > best ? key : best;
+    }
+    const int M = cand_count(best);
+    int nm = 0;
+#pragma unroll
+    for (int j = 0; j < D; ++j) nm += (ky[j] != kKeyHaz) & (cnt[j] == M);
+    return cand_state(best, nm);
+}
 
 template <int D, int PK, int W, class Fetch>
 __device__ __forceinline__ void score_records(const ScoreCtx &a, const int *__restrict__ recs, int item0,
@@ -204,7 +249,7 @@ __device__ __forceinline__ void score_records(const ScoreCtx &a, const int *__re
             oi[k] = r[0];
             dg[k] = v[k] ? r[1] : 0;
 #pragma unroll
-            for (int j = 0; j < D; ++j) nd[k][j] = fetch(r[2 + j]);  // padding entries encode a valid source
+            for (int j = 0; j < D; ++j) nd[k][j] = fetch(r[2 + j]);
         }
 #pragma unroll
         for (int k = 0; k < PK; ++k)
@@ -218,35 +263,7 @@ __device__ __forceinline__ void score_records(const ScoreCtx &a, const int *__re
             }
 #pragma unroll
         for (int k = 0; k < PK; ++k) {
-            // symmetric pairwise equality: D(D-1)/2 compares, counts kept in VGPRs
-            int cnt[D];
-#pragma unroll
-            for (int j = 0; j < D; ++j) cnt[j] = 1;
-#pragma unroll
-            for (int j = 1; j < D; ++j)
-#pragma unroll
-                for (int jj = 0; jj < j; ++jj) {
-                    const int e = 1 - (int)min((unsigned)(nd[k][j] ^ nd[k][jj]), 1u);
-                    cnt[j] += e;
-                    cnt[jj] += e;
-                }
-            // lexicographic (count, remaining CPU, -node) as one u64: the max is the
-            // reference's choice among the best nodes
-            unsigned long long best = 0;
-#pragma unroll
-            for (int j = 0; j < D; ++j) {
-                const unsigned long long key = ky[k][j] == kKeyHaz ? 0ull : pack_cand(cnt[j], ky[k][j], nd[k][j]);
-                best = key > best ? key : best;
-            }
-            const int M = (int)(best >> 58);
-            int nm = 0;
-#pragma unroll
-            for (int j = 0; j < D; ++j) nm += (ky[k][j] != kKeyHaz) & (cnt[j] == M);
-            CarState st;
-            st.bc = M;
-            st.nm = nm;
-            st.br = (int)((unsigned)(best >> 26) ^ 0x80000000u);
-            st.bn = 0x3ffffff - (int)(best & 0x3ffffffull);
+            const CarState st = reduce_entries<D>(nd[k], ky[k]);
             if (v[k]) {
                 int sc;
                 const int t = car_finalize(st, s, a.zc_cnt, a.zc_key, sc);
@@ -258,8 +275,8 @@ __device__ __forceinline__ void score_records(const ScoreCtx &a, const int *__re
     }
 }
 
-// K1a: direct light rows (deg <= 16, owners of sparse tiles): ELL records whose
-// neighbours are global pod ids (padding = pod 0); every neighbour row is one
+// K1a: direct rows (deg <= 16, owners of sparse tiles): records whose
+// neighbours are global pod ids (padding = pod 0); each neighbour row is one
 // coalesced 256-B gather.
 struct LightArgs {
     ScoreCtx sc;
@@ -295,44 +312,40 @@ __global__ __launch_bounds__(256) void car_light_kernel(LightArgs a) {
         default: score_records<2, 4, 4>(a.sc, a.ell[3], item0, item_end, slot, s, lane_ok, fetch); break;
     }
 }
-constexpr int kLightPK[kNumLight] = {1, 2, 4, 4};
 
-// K1b: tiled light rows (deg <= 32).  The plan orders pods by a DFS of the
-// relation graph (small subtrees first) and cuts the order into tiles of CP
-// pods; ~96% of a light row's neighbours share its tile (100k/5k PA tree,
-// CP=256) and the rest (a handful per tile) are appended to the tile as extra
-// rows.  Workgroup (8 waves) = (tile, chunk of SL <= 64 scenarios):
-//   phase 1  the tile's rows (members + externals), SL scenarios each -> LDS
-//            image[row][SL]: every assign row leaves HBM once per chunk as
-//            256-B loads, issued in batches with no dependent waits
-//   phase 2  owner records (neighbour = LDS row) score from LDS; only the
-//            nodekey word of each neighbour's node comes from L2.
-constexpr int kTileWaves = 8;
-constexpr int kTileBatch = 8;
-
+// K1b: tiled rows (deg <= 16).  The plan orders pods by a DFS of the relation
+// graph (small subtrees first) and cuts the order into tiles of CP pods; ~96%
+// of a light row's neighbours share its tile (100k/5k PA tree, CP=256) and the
+// rest (a handful per tile) are appended to the tile image as extra rows.
+// Workgroup (8 waves) = (tile, chunk of SL <= 64 scenarios):
+//   phase 1  the tile's image rows (members + externals), SL scenarios each ->
+//            LDS image[row][SL] — each assign row leaves HBM once per chunk as
+//            one 256-B LDS-DMA (global_load_lds_dword) per row when SL = 64 —
+//            and the tile's owner records (one contiguous blob) -> LDS.
+//   phase 2  owner records score from LDS; only each neighbour's nodekey word
+//            comes from L2; one 256-B target store per record.
 struct TileArgs {
     ScoreCtx sc;
-    const int *members;            // [T][RS] pod ids (pad = pod 0, never referenced)
-    const int *nrows;              // [T] rows of each tile image (<= RS)
-    const int *rec[kNumTile];      // per bucket records, grouped by tile; nb = image row
-    const int *rec_off[kNumTile];  // per bucket [T+1]
+    const int *members;       // [T][RS] pod ids (pad = pod 0, never referenced)
+    const int *nrows;         // [T] image rows of each tile (<= RS)
+    const int *blob;          // per-tile record blobs, concatenated
+    const int *blob_off;      // [T][kNumLight + 1] ints: blob start + bucket starts (absolute)
     const int *assign;
-    int SL, RS, T;
+    int SL, RS, T, blob_max;  // blob_max: largest blob (ints, multiple of 4)
 };
 
 template <int D, int PK, int W>
-__device__ __forceinline__ void tile_bucket(const TileArgs &a, const int *lds, int b, int tile, int wave, int slot,
-                                            int sl, int s, bool lane_ok) {
-    const int r0 = a.rec_off[b][tile], r1 = a.rec_off[b][tile + 1];
+__device__ __forceinline__ void tile_bucket(const TileArgs &a, const int *img, const int *recs, int nrec, int wave,
+                                            int slot, int sl, int s, bool lane_ok) {
     const int per = PK * a.sc.PS;
     const int SL = a.SL;
-    auto fetch = [=](int row) { return lds[row * SL + sl]; };
-    for (int g0 = r0 + wave * per; g0 < r1; g0 += kTileWaves * per)
-        score_records<D, PK, W>(a.sc, a.rec[b], g0, min(r1, g0 + per), slot, s, lane_ok, fetch);
+    auto fetch = [=](int row) { return img[row * SL + sl]; };
+    for (int g0 = wave * per; g0 < nrec; g0 += kTileWaves * per)
+        score_records<D, PK, W>(a.sc, recs, g0, min(nrec, g0 + per), slot, s, lane_ok, fetch);
 }
 
 __global__ __launch_bounds__(kTileWaves * 64) void car_tile_kernel(TileArgs a) {
-    extern __shared__ __attribute__((aligned(16))) int lds[];  // [RS][SL]
+    extern __shared__ __attribute__((aligned(16))) int lds[];  // image [RS][SL] then records [blob_max]
     const int chunk = blockIdx.x / a.T, tile = blockIdx.x % a.T;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int SL = a.SL, PS = a.sc.PS;
@@ -344,29 +357,158 @@ __global__ __launch_bounds__(kTileWaves * 64) void car_tile_kernel(TileArgs a) {
     const size_t S = (size_t)a.sc.S;
     const int s_ld = min(s, a.sc.S - 1);
     const int nr = a.nrows[tile];
-    const bool writer = slot < PS;
-    for (int r0 = wave * PS; r0 < nr; r0 += kTileWaves * PS * kTileBatch) {
-        int q[kTileBatch], v[kTileBatch];
+    int *img = lds;
+    int *recs = lds + a.RS * SL;
+
+    // phase 1a: owner record blob -> LDS (int4 copies, issued first: no dependency)
+    const int *bo = a.blob_off + (size_t)tile * (kNumLight + 2);
+    const int b0 = bo[0], b1 = bo[kNumLight + 1];
+    for (int i = threadIdx.x * 4; i < b1 - b0; i += kTileWaves * 64 * 4)
+        *reinterpret_cast<int4 *>(recs + i) = *reinterpret_cast<const int4 *>(a.blob + b0 + i);
+    // phase 1b: image rows
+    if (PS == 1) {
+        // one LDS-DMA wave instruction per row: lane l loads scenario chunk*64+l
+        // No branch between the DMAs (a per-row `if` splits basic blocks and the
+        // waitcnt pass then drains vmcnt(0) before every DMA): rows past the
+        // image's end re-load its last row into the same LDS row (same bytes).
+        // Row ids are wave-uniform: readfirstlane makes the member loads scalar
+        // (lgkmcnt), so they never share the vector-memory counter with the DMAs.
+        constexpr int kMaxRowsPerWave = (kTileCP + kTileXCap + kTileWaves - 1) / kTileWaves;
+        const int wu = __builtin_amdgcn_readfirstlane(wave);
+        int q[kMaxRowsPerWave];
 #pragma unroll
-        for (int k = 0; k < kTileBatch; ++k) q[k] = mem[min(r0 + k * kTileWaves * PS + slot, a.RS - 1)];
+        for (int k = 0; k < kMaxRowsPerWave; ++k) q[k] = mem[min(wu + k * kTileWaves, nr - 1)];
 #pragma unroll
-        for (int k = 0; k < kTileBatch; ++k) v[k] = assign[(size_t)q[k] * S + s_ld];
+        for (int k = 0; k < kMaxRowsPerWave; ++k) {
+            const int r = min(wu + k * kTileWaves, nr - 1);
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(assign + (size_t)q[k] * S + s_ld),
+                (__attribute__((address_space(3))) void *)(img + r * SL), 4, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        for (int r0 = wave * PS; r0 < nr; r0 += kTileWaves * PS * kTileBatch) {
+            int q[kTileBatch], v[kTileBatch];
 #pragma unroll
-        for (int k = 0; k < kTileBatch; ++k) {
-            const int r = r0 + k * kTileWaves * PS + slot;
-            if (writer && r < nr) lds[r * SL + sl] = v[k];
+            for (int k = 0; k < kTileBatch; ++k) q[k] = mem[min(r0 + k * kTileWaves * PS + slot, a.RS - 1)];
+#pragma unroll
+            for (int k = 0; k < kTileBatch; ++k) v[k] = assign[(size_t)q[k] * S + s_ld];
+#pragma unroll
+            for (int k = 0; k < kTileBatch; ++k) {
+                const int r = r0 + k * kTileWaves * PS + slot;
+                if (slot < PS && r < nr) img[r * SL + sl] = v[k];
+            }
         }
     }
     __syncthreads();
-
-    tile_bucket<16, 1, 20>(a, lds, 0, tile, wave, slot, sl, s, lane_ok);
-    tile_bucket<8, 2, 12>(a, lds, 1, tile, wave, slot, sl, s, lane_ok);
-    tile_bucket<4, 4, 8>(a, lds, 2, tile, wave, slot, sl, s, lane_ok);
-    tile_bucket<2, 8, 4>(a, lds, 3, tile, wave, slot, sl, s, lane_ok);
+    tile_bucket<16, 1, 20>(a, img, recs + (bo[1] - b0), (bo[2] - bo[1]) / 20, wave, slot, sl, s, lane_ok);
+    tile_bucket<8, 2, 12>(a, img, recs + (bo[2] - b0), (bo[3] - bo[2]) / 12, wave, slot, sl, s, lane_ok);
+    tile_bucket<4, 4, 8>(a, img, recs + (bo[3] - b0), (bo[4] - bo[3]) / 8, wave, slot, sl, s, lane_ok);
+    tile_bucket<2, 8, 4>(a, img, recs + (bo[4] - b0), (bo[5] - bo[4]) / 4, wave, slot, sl, s, lane_ok);
 }
 
 // ---------------------------------------------------------------------------
-// K2: heavy rows (deg > 16).  Workgroup = (row, group of G scenarios).
+// K1c: mid rows (17 <= deg <= 64), one wave per (row, 64-scenario chunk),
+// lane = scenario.  Each lane loads its deg node ids (coalesced 256-B rows),
+// sorts them with a bitonic network in registers (min/max only: no compare
+// masks, no memory), gathers one nodekey word per sorted entry, then scans the
+// runs: best packed candidate, then the number of best-count runs.
+// ---------------------------------------------------------------------------
+template <int D>
+__device__ __forceinline__ void bitonic_sort(int (&v)[D]) {
+#pragma unroll
+    for (int k = 2; k <= D; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const int lo = min(v[i], v[l]), hi = max(v[i], v[l]);
+                    if ((i & k) == 0) { v[i] = lo; v[l] = hi; }
+                    else { v[i] = hi; v[l] = lo; }
+                }
+            }
+}
+
+struct MidArgs {
+    ScoreCtx sc;
+    const int *rec[kNumMid];
+    int n_items[kNumMid];
+    int prefix[kNumMid + 1];   // waves (rows) per chunk, prefix over buckets
+    const int *assign;
+    int SL, blocks_per_chunk;
+};
+
+template <int D, int W>
+__device__ __forceinline__ void mid_row(const MidArgs &a, const int *__restrict__ rec, int slot, int s, bool lane_ok) {
+    const int S = a.sc.S;
+    const int s_ld = min(s, S - 1);
+    const int4 *r4 = reinterpret_cast<const int4 *>(rec);
+    int r[W];
+#pragma unroll
+    for (int w = 0; w < W / 4; ++w) {
+        const int4 x = r4[w];
+        r[4 * w] = x.x; r[4 * w + 1] = x.y; r[4 * w + 2] = x.z; r[4 * w + 3] = x.w;
+    }
+    const int oi = r[0], d = r[1];
+    int v[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) v[j] = a.assign[(size_t)r[2 + j] * (size_t)S + s_ld];
+#pragma unroll
+    for (int j = 0; j < D; ++j) v[j] = (j < d && (unsigned)v[j] < (unsigned)a.sc.N) ? v[j] : INT_MAX;
+    bitonic_sort<D>(v);
+    int ky[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+        ky[j] = ld32(a.sc.nodekey, (unsigned)(v[j] == INT_MAX ? 0 : v[j]) * (unsigned)S + (unsigned)s_ld);
+    unsigned long long best = 0;
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        c = (j > 0 && v[j] == v[j - 1]) ? c + 1 : 1;
+        const bool end = (j == D - 1) || v[j + (j < D - 1 ? 1 : 0)] != v[j];
+        const bool cand = end && v[j] != INT_MAX && ky[j] != kKeyHaz;
+        const unsigned long long key = cand ? pack_cand(c, ky[j], v[j]) : 0ull;
+        best = key > best ? key : best;
+    }
+    const int M = cand_count(best);
+    int runs = 0;
+    c = 0;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        c = (j > 0 && v[j] == v[j - 1]) ? c + 1 : 1;
+        const bool end = (j == D - 1) || v[j + (j < D - 1 ? 1 : 0)] != v[j];
+        runs += (end && v[j] != INT_MAX && ky[j] != kKeyHaz && c == M) ? 1 : 0;
+    }
+    const CarState st = cand_state(best, M * runs);
+    if (lane_ok) {
+        int sc;
+        const int t = car_finalize(st, s, a.sc.zc_cnt, a.sc.zc_key, sc);
+        const size_t o = (size_t)oi * S + s;
+        a.sc.out_target[o] = t;
+        if (a.sc.out_score) a.sc.out_score[o] = sc;
+    }
+}
+
+__global__ __launch_bounds__(256) void car_mid_kernel(MidArgs a) {
+    const int chunk = blockIdx.x / a.blocks_per_chunk;
+    const int wave = (blockIdx.x % a.blocks_per_chunk) * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (wave >= a.prefix[kNumMid]) return;
+    // a wave scores PS rows of one bucket, lanes split into PS slots of SL scenarios
+    const int slot = lane / a.SL;
+    const int s = chunk * a.SL + lane % a.SL;
+    const int b = wave >= a.prefix[1] ? 1 : 0;
+    const int item = (wave - a.prefix[b]) * a.sc.PS + slot;
+    const bool lane_ok = slot < a.sc.PS && s < a.sc.S && item < a.n_items[b];
+    const int it = min(item, a.n_items[b] - 1);
+    if (b == 0) mid_row<32, 36>(a, a.rec[0] + (size_t)it * 36, slot, s, lane_ok);
+    else mid_row<64, 68>(a, a.rec[1] + (size_t)it * 68, slot, s, lane_ok);
+}
+
+// ---------------------------------------------------------------------------
+// K2: heavy rows (deg > 64).  Workgroup = (row, group of G scenarios).
 //   phase 0  stage node ids ntile[si][j] (G-scenario row segments per neighbour)
 //   phase A  wave w < NT hashes scenario si's d node ids into its LDS table
 //   phase B  counts back into ctile[si][j]; table cleared for the next scenario
@@ -512,16 +654,18 @@ using namespace rsk;
 struct rsk_car_plan {
     rsk_ctx *ctx = nullptr;
     int P = 0, Q = 0, max_deg = 0;
-    // tiled light rows
-    int CP = kTileCP, RS = kTileCP, T = 0, n_tile_owners = 0;
-    DevBuf members, nrows;
-    DevBuf trec[kNumTile], toff[kNumTile];
-    // direct light rows (owners in sparse tiles)
+    // tiled rows (deg <= 16 in dense tiles)
+    int CP = kTileCP, RS = kTileCP, T = 0, n_tile_owners = 0, blob_max = 0;
+    DevBuf members, nrows, blob, blob_off;
+    // direct rows (deg <= 16 in sparse tiles)
     int n_light[kNumLight] = {0, 0, 0, 0};
     DevBuf ell[kNumLight];
-    // heavy rows
-    int n_heavy[kNumHeavy] = {0, 0, 0, 0};
-    int heavy_dmax[kNumHeavy] = {0, 0, 0, 0};
+    // mid rows (17..64)
+    int n_mid[kNumMid] = {0, 0};
+    DevBuf mid[kNumMid];
+    // heavy rows (> 64)
+    int n_heavy[kNumHeavy] = {0, 0, 0};
+    int heavy_dmax[kNumHeavy] = {0, 0, 0};
     DevBuf heavy_items[kNumHeavy];
     DevBuf hcol;
     // per-execute workspace
@@ -529,9 +673,10 @@ struct rsk_car_plan {
     ~rsk_car_plan() {
         members.release();
         nrows.release();
-        for (auto &b : trec) b.release();
-        for (auto &b : toff) b.release();
+        blob.release();
+        blob_off.release();
         for (auto &b : ell) b.release();
+        for (auto &b : mid) b.release();
         for (auto &b : heavy_items) b.release();
         hcol.release();
         nodekey.release();
@@ -548,12 +693,6 @@ int light_bucket(int d) {
     return 0;
 }
 
-int tile_bucket_of(int d) {
-    if (d <= 2) return 3;
-    if (d <= 4) return 2;
-    if (d <= 8) return 1;
-    return 0;
-}
 
 int heavy_class(int d) {
     for (int c = 0; c < kNumHeavy; ++c)
@@ -685,13 +824,13 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
     for (int k = 0; k < P; ++k) pos[order[k]] = k;
     const int ntiles = (P + CP - 1) / CP;
 
-    // owners per tile (rows with deg <= kTileMax)
+    // owners per tile (rows with deg <= kLightMax)
     std::vector<int> owners_in(ntiles, 0);
     for (int i = 0; i < Q; ++i) {
         const int p = rows ? rows[i] : i;
         const int d = rp[p + 1] - rp[p];
         plan->max_deg = std::max(plan->max_deg, d);
-        if (d <= kTileMax) ++owners_in[pos[p] / CP];
+        if (d <= kLightMax) ++owners_in[pos[p] / CP];
     }
     RSK_CHECK(plan->max_deg <= kMaxDegree, "a row has degree %d > %d (unsupported)", plan->max_deg, kMaxDegree);
     const int min_owners = std::max(1, CP / 16);  // sparser tiles use the direct path
@@ -700,10 +839,10 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
     for (int t = 0; t < ntiles; ++t)
         if (owners_in[t] >= min_owners) tile_id[t] = T++;
 
-    std::vector<std::vector<std::vector<int>>> trec(kNumTile, std::vector<std::vector<int>>(T));
+    std::vector<std::vector<std::vector<int>>> trec(kNumLight, std::vector<std::vector<int>>(T));
     std::vector<std::vector<int>> ext_rows(T);             // external pods appended to each tile image
     std::vector<std::unordered_map<int, int>> ext_slot(T);  // pod -> image row
-    std::vector<std::vector<int>> ell(kNumLight);
+    std::vector<std::vector<int>> ell(kNumLight), midr(kNumMid);
     std::vector<std::vector<HeavyItem>> hitems(kNumHeavy);
     std::vector<int> hcol;
     std::vector<int> fresh;
@@ -713,7 +852,7 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
         const int *nbp = ci.data() + rp[p];
         const int tile = pos[p] / CP;
         const int tid = tile_id[tile];
-        bool tiled = d <= kTileMax && tid >= 0;
+        bool tiled = d <= kLightMax && tid >= 0;
         if (tiled) {  // externals of this row must fit the tile image
             fresh.clear();
             for (int j = 0; j < d; ++j) {
@@ -730,10 +869,10 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
                 }
         }
         if (tiled) {
-            const int b = tile_bucket_of(d);
+            const int b = light_bucket(d);
             auto &e = trec[b][tid];
             const size_t o = e.size();
-            e.resize(o + kTileW[b], 0);
+            e.resize(o + kLightW[b], 0);
             e[o] = i;
             e[o + 1] = d;
             for (int j = 0; j < d; ++j) {
@@ -750,6 +889,15 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
             e[o + 1] = d;
             for (int j = 0; j < d; ++j) e[o + 2 + j] = nbp[j];
             plan->n_light[b] += 1;
+        } else if (d <= kMidMax) {
+            const int b = d <= 32 ? 0 : 1;
+            auto &e = midr[b];
+            const size_t o = e.size();
+            e.resize(o + kMidW[b], 0);
+            e[o] = i;
+            e[o + 1] = d;
+            for (int j = 0; j < d; ++j) e[o + 2 + j] = nbp[j];
+            plan->n_mid[b] += 1;
         } else {
             const int c = heavy_class(d);
             hitems[c].push_back({i, (int)hcol.size(), d, 0});
@@ -768,25 +916,29 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
         for (int t = 0; t < ntiles; ++t) {
             const int id = tile_id[t];
             if (id < 0) continue;
-            int k = 0;
-            for (; k < CP && t * CP + k < P; ++k) mem[(size_t)id * RS + k] = order[t * CP + k];
-            nr[id] = CP;  // short last tile: rows past its members are never referenced
+            for (int k = 0; k < CP && t * CP + k < P; ++k) mem[(size_t)id * RS + k] = order[t * CP + k];
             for (size_t x = 0; x < ext_rows[id].size(); ++x) mem[(size_t)id * RS + CP + x] = ext_rows[id][x];
-            nr[id] = CP + (int)ext_rows[id].size();
+            nr[id] = CP + (int)ext_rows[id].size();  // short last tile: rows past its members are never read
         }
         RSK_TRY(upload(plan->members, mem.data(), mem.size() * 4));
         RSK_TRY(upload(plan->nrows, nr.data(), nr.size() * 4));
-        for (int b = 0; b < kNumTile; ++b) {
-            std::vector<int> flat, off(T + 1, 0);
-            for (int t = 0; t < T; ++t) {
-                flat.insert(flat.end(), trec[b][t].begin(), trec[b][t].end());
-                off[t + 1] = (int)(flat.size() / kTileW[b]);
+        // per-tile record blob: buckets D = 16, 8, 4, 2 back to back, padded to 4 ints
+        std::vector<int> blob, boff((size_t)T * (kNumLight + 2));
+        for (int t = 0; t < T; ++t) {
+            int *bo = boff.data() + (size_t)t * (kNumLight + 2);
+            bo[0] = (int)blob.size();
+            for (int b = 0; b < kNumLight; ++b) {
+                bo[1 + b] = (int)blob.size();
+                blob.insert(blob.end(), trec[b][t].begin(), trec[b][t].end());
             }
-            RSK_TRY(upload(plan->toff[b], off.data(), off.size() * 4));
-            if (flat.empty()) flat.assign(kTileW[b], 0);  // keep a valid pointer
-            RSK_TRY(upload(plan->trec[b], flat.data(), flat.size() * 4));
+            bo[kNumLight + 1] = (int)blob.size();
+            plan->blob_max = std::max(plan->blob_max, bo[kNumLight + 1] - bo[0]);
         }
+        if (blob.empty()) blob.assign(4, 0);
+        RSK_TRY(upload(plan->blob, blob.data(), blob.size() * 4));
+        RSK_TRY(upload(plan->blob_off, boff.data(), boff.size() * 4));
     }
+    for (int b = 0; b < kNumMid; ++b) RSK_TRY(upload(plan->mid[b], midr[b].data(), midr[b].size() * 4));
     for (int b = 0; b < kNumLight; ++b) RSK_TRY(upload(plan->ell[b], ell[b].data(), ell[b].size() * 4));
     for (int c = 0; c < kNumHeavy; ++c)
         RSK_TRY(upload(plan->heavy_items[c], hitems[c].data(), hitems[c].size() * sizeof(HeavyItem)));
@@ -832,22 +984,26 @@ int rsk_car_plan_create(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col
 
 int rsk_car_plan_info(const rsk_car_plan *plan, int64_t *out, int n) {
     RSK_CHECK(plan && out && n >= 0, "bad arguments");
-    int64_t light = 0, heavy = 0, tile_bytes = 0, ell_bytes = 0, heavy_bytes = (int64_t)plan->hcol.bytes;
+    int64_t light = 0, mid = 0, heavy = 0, tile_bytes = 0, ell_bytes = 0, mid_bytes = 0;
+    int64_t heavy_bytes = (int64_t)plan->hcol.bytes;
     for (int b = 0; b < kNumLight; ++b) {
         light += plan->n_light[b];
         ell_bytes += (int64_t)plan->n_light[b] * kLightW[b] * 4;
+    }
+    for (int b = 0; b < kNumMid; ++b) {
+        mid += plan->n_mid[b];
+        mid_bytes += (int64_t)plan->n_mid[b] * kMidW[b] * 4;
     }
     for (int c = 0; c < kNumHeavy; ++c) {
         heavy += plan->n_heavy[c];
         heavy_bytes += (int64_t)plan->n_heavy[c] * (int64_t)sizeof(HeavyItem);
     }
-    if (plan->T > 0) {
-        tile_bytes = (int64_t)plan->T * plan->RS * 4 + (int64_t)plan->T * 4;
-        for (int b = 0; b < kNumTile; ++b) tile_bytes += (int64_t)plan->trec[b].bytes + (int64_t)plan->toff[b].bytes;
-    }
-    const int64_t v[10] = {plan->n_tile_owners, light, heavy, plan->T, plan->RS, plan->CP,
-                           tile_bytes, ell_bytes, heavy_bytes, plan->max_deg};
-    const int m = n < 10 ? n : 10;
+    if (plan->T > 0)
+        tile_bytes = (int64_t)plan->T * plan->RS * 4 + (int64_t)plan->T * 4 * (kNumLight + 3) +
+                     (int64_t)plan->blob.bytes;
+    const int64_t v[12] = {plan->n_tile_owners, light, mid, heavy, plan->T, plan->RS, plan->CP,
+                           tile_bytes, ell_bytes, mid_bytes, heavy_bytes, plan->max_deg};
+    const int m = n < 12 ? n : 12;
     for (int i = 0; i < m; ++i) out[i] = v[i];
     return m;
 }
@@ -867,8 +1023,8 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     rsk_ctx *ctx = plan->ctx;
     RSK_TRY(activate(ctx));
     RSK_CHECK(S > 0 && N > 0, "need S > 0 and N > 0 (S=%d N=%d)", S, N);
-    RSK_CHECK((int64_t)N * S < ((int64_t)1 << 30) && N < (1 << 26) && (int64_t)plan->P * S < ((int64_t)1 << 40),
-              "N*S too large (N=%d S=%d; need N*S < 2^30, N < 2^26)", N, S);
+    RSK_CHECK((int64_t)N * S < ((int64_t)1 << 30) && N < (1 << kNodeBits) && (int64_t)plan->P * S < ((int64_t)1 << 40),
+              "N*S too large (N=%d S=%d; need N*S < 2^30, N < 2^25)", N, S);
     RSK_CHECK(out_target, "null out_target");
     const bool dev = (flags & RSK_F_DEVICE) != 0;
     const size_t PS_ = (size_t)plan->P * S, NS = (size_t)N * S, QS = (size_t)plan->Q * S;
@@ -917,15 +1073,15 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         a.sc = sc;
         a.members = plan->members.as<int>();
         a.nrows = plan->nrows.as<int>();
-        for (int b = 0; b < kNumTile; ++b) {
-            a.rec[b] = plan->trec[b].as<int>();
-            a.rec_off[b] = plan->toff[b].as<int>();
-        }
+        a.blob = plan->blob.as<int>();
+        a.blob_off = plan->blob_off.as<int>();
         a.assign = d_assign;
         a.SL = SL;
         a.RS = plan->RS;
         a.T = plan->T;
-        const size_t lds = (size_t)plan->RS * SL * 4;
+        a.blob_max = plan->blob_max;
+        const size_t lds = (size_t)plan->RS * SL * 4 + (size_t)plan->blob_max * 4;
+        RSK_CHECK(lds <= 160 * 1024, "tile image needs %zu B of LDS", lds);
         const int64_t blocks = chunks * plan->T;
         RSK_CHECK(blocks < INT32_MAX, "tile grid too large");
         if (lds > 64 * 1024)
@@ -956,6 +1112,27 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
             RSK_CHECK(blocks < INT32_MAX, "light grid too large");
             ScopedTimer tm(ctx, "car_light");
             car_light_kernel<<<dim3((unsigned)blocks), dim3(256), 0, ctx->stream>>>(a);
+            RSK_HIP(hipGetLastError());
+        }
+    }
+    {   // K1c mid rows
+        MidArgs a;
+        std::memset(&a, 0, sizeof(a));
+        a.sc = sc;
+        a.SL = SL;
+        a.prefix[0] = 0;
+        for (int b = 0; b < kNumMid; ++b) {
+            a.rec[b] = plan->mid[b].as<int>();
+            a.n_items[b] = plan->n_mid[b];
+            a.prefix[b + 1] = a.prefix[b] + (int)ceil_div(plan->n_mid[b], sc.PS);
+        }
+        if (a.prefix[kNumMid] > 0) {
+            a.assign = d_assign;
+            a.blocks_per_chunk = (int)ceil_div(a.prefix[kNumMid], 4);
+            const int64_t blocks = chunks * a.blocks_per_chunk;
+            RSK_CHECK(blocks < INT32_MAX, "mid grid too large");
+            ScopedTimer tm(ctx, "car_mid");
+            car_mid_kernel<<<dim3((unsigned)blocks), dim3(256), 0, ctx->stream>>>(a);
             RSK_HIP(hipGetLastError());
         }
     }

@@ -45,8 +45,8 @@ class CarPlan:
                                                ptr(self.rows), self.Q, C.byref(h)))
         self.handle = h
 
-    INFO_FIELDS = ("tile_rows", "direct_rows", "heavy_rows", "tiles", "tile_image_rows", "tile_pods",
-                   "tile_bytes", "direct_bytes", "heavy_bytes", "max_degree")
+    INFO_FIELDS = ("tile_rows", "direct_rows", "mid_rows", "heavy_rows", "tiles", "tile_image_rows",
+                   "tile_pods", "tile_bytes", "direct_bytes", "mid_bytes", "heavy_bytes", "max_degree")
 
     def info(self) -> dict:
         """How the plan routed its rows (rsk_car_plan_info)."""
