@@ -31,6 +31,7 @@
 //                     tables / hash, coalesced lookups, cross-lane reduce.
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <unordered_map>
@@ -332,6 +333,7 @@ struct TileArgs {
     const int *blob_off;      // [T][kNumLight + 1] ints: blob start + bucket starts (absolute)
     const int *assign;
     int SL, RS, T, blob_max;  // blob_max: largest blob (ints, multiple of 4)
+    int ablate;               // profiling only (RSK_ABLATE_TILE): 1 skip image load, 2 skip scoring
 };
 
 template <int D, int PK, int W>
@@ -366,7 +368,9 @@ __global__ __launch_bounds__(kTileWaves * 64) void car_tile_kernel(TileArgs a) {
     for (int i = threadIdx.x * 4; i < b1 - b0; i += kTileWaves * 64 * 4)
         *reinterpret_cast<int4 *>(recs + i) = *reinterpret_cast<const int4 *>(a.blob + b0 + i);
     // phase 1b: image rows
-    if (PS == 1) {
+    if (a.ablate & 1) {
+        // profiling ablation: no image load (results are wrong)
+    } else if (PS == 1) {
         // one LDS-DMA wave instruction per row: lane l loads scenario chunk*64+l
         // No branch between the DMAs (a per-row `if` splits basic blocks and the
         // waitcnt pass then drains vmcnt(0) before every DMA): rows past the
@@ -401,6 +405,7 @@ __global__ __launch_bounds__(kTileWaves * 64) void car_tile_kernel(TileArgs a) {
         }
     }
     __syncthreads();
+    if (a.ablate & 2) return;  // profiling ablation: no scoring (results are wrong)
     tile_bucket<16, 1, 20>(a, img, recs + (bo[1] - b0), (bo[2] - bo[1]) / 20, wave, slot, sl, s, lane_ok);
     tile_bucket<8, 2, 12>(a, img, recs + (bo[2] - b0), (bo[3] - bo[2]) / 12, wave, slot, sl, s, lane_ok);
     tile_bucket<4, 4, 8>(a, img, recs + (bo[3] - b0), (bo[4] - bo[3]) / 8, wave, slot, sl, s, lane_ok);
@@ -625,12 +630,24 @@ __global__ __launch_bounds__(256) void car_heavy_kernel(const HeavyItem *__restr
     CarState st;
     st_init(st);
     {
+        // batches of kC independent gathers (a load-then-use loop body would
+        // serialise one L2 round trip per neighbour)
+        constexpr int kC = 8;
         const int *nrow = ntile + si * dpad, *crow = ctile + si * dpad;
         const unsigned s_ld = (unsigned)min(s, S - 1);
-        for (int j = tid / G; j < d; j += jstep) {
-            const int n = nrow[j];
-            const int key = ld32(nodekey, (unsigned)max(n, 0) * (unsigned)S + s_ld);
-            if (s < S && n >= 0 && key != kKeyHaz) st_add(st, crow[j], key, n);
+        for (int j0 = tid / G; j0 < d; j0 += jstep * kC) {
+            int n[kC], key[kC];
+#pragma unroll
+            for (int k = 0; k < kC; ++k) {
+                const int j = min(j0 + k * jstep, d - 1);
+                n[k] = nrow[j];
+                key[k] = ld32(nodekey, (unsigned)max(n[k], 0) * (unsigned)S + s_ld);
+            }
+#pragma unroll
+            for (int k = 0; k < kC; ++k) {
+                const int j = j0 + k * jstep;
+                if (j < d && s < S && n[k] >= 0 && key[k] != kKeyHaz) st_add(st, crow[j], key[k], n[k]);
+            }
         }
     }
     for (int off = G; off < 64; off <<= 1) st = st_combine(st, st_shfl_xor(st, off));
@@ -1080,6 +1097,8 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         a.RS = plan->RS;
         a.T = plan->T;
         a.blob_max = plan->blob_max;
+        static const int ablate = [] { const char *e = getenv("RSK_ABLATE_TILE"); return e ? atoi(e) : 0; }();
+        a.ablate = ablate;
         const size_t lds = (size_t)plan->RS * SL * 4 + (size_t)plan->blob_max * 4;
         RSK_CHECK(lds <= 160 * 1024, "tile image needs %zu B of LDS", lds);
         const int64_t blocks = chunks * plan->T;

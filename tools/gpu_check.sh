@@ -31,3 +31,9 @@ if [ "$MODE" = all ] || [ "$MODE" = pmc ]; then
     step pmc_write 240 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc -o write -f csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
     step pmc_l2 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmc -o l2 -f csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
 fi
+if [ "$MODE" = ablate ]; then
+    step bench_full 300 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline
+    RSK_ABLATE_TILE=2 step bench_noscore 300 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline
+    RSK_ABLATE_TILE=1 step bench_noload 300 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline
+    RSK_ABLATE_TILE=3 step bench_nothing 300 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline
+fi
