@@ -121,17 +121,28 @@ __device__ __forceinline__ unsigned long long zc_pack(int rem, int n) {
     return ((unsigned long long)((unsigned)rem ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)n);
 }
 
+// The per-scenario zero case (car_prep_kernel), loaded once per lane.
+struct ZeroCase {
+    int cnt;                  // non-hazard nodes in the scenario
+    unsigned long long key;   // packed (cap-use, ~node) max over them
+};
+
+__device__ __forceinline__ ZeroCase load_zc(const int *__restrict__ zc_cnt, const unsigned long long *__restrict__ zc_key,
+                                            int s) {
+    ZeroCase z;
+    z.cnt = zc_cnt[s];
+    z.key = zc_key[s];
+    return z;
+}
+
 // rescheduling.py:199-214 applied to the reduced state.
-__device__ __forceinline__ int car_finalize(const CarState &st, int s, const int *__restrict__ zc_cnt,
-                                            const unsigned long long *__restrict__ zc_key, int &score) {
+__device__ __forceinline__ int car_finalize(const CarState &st, const ZeroCase &z, int &score) {
     if (st.bc == 0) {
-        const int c = zc_cnt[s];
-        if (c == 0) { score = -1; return RSK_TARGET_NO_CANDIDATE; }
-        const unsigned long long k = zc_key[s];
-        const int n = (int)(~(unsigned)(k & 0xffffffffull));
-        const int rem = (int)((unsigned)(k >> 32) ^ 0x80000000u);
+        if (z.cnt == 0) { score = -1; return RSK_TARGET_NO_CANDIDATE; }
+        const int n = (int)(~(unsigned)(z.key & 0xffffffffull));
+        const int rem = (int)((unsigned)(z.key >> 32) ^ 0x80000000u);
         score = 0;
-        if (c == 1) return n;
+        if (z.cnt == 1) return n;
         return rem >= 0 ? n : RSK_TARGET_NONE;
     }
     score = st.bc;
@@ -233,6 +244,7 @@ __device__ __forceinline__ void score_records(const ScoreCtx &a, const int *__re
     const int S = a.S;
     const int s_ld = min(s, S - 1);  // loads of inactive lanes stay in bounds
     const int step = PK * a.PS;
+    const ZeroCase z = load_zc(a.zc_cnt, a.zc_key, s_ld);
     for (int base = item0; base < item_end; base += step) {
         int oi[PK], dg[PK], nd[PK][D], ky[PK][D];
         bool v[PK];
@@ -267,7 +279,7 @@ __device__ __forceinline__ void score_records(const ScoreCtx &a, const int *__re
             const CarState st = reduce_entries<D>(nd[k], ky[k]);
             if (v[k]) {
                 int sc;
-                const int t = car_finalize(st, s, a.zc_cnt, a.zc_key, sc);
+                const int t = car_finalize(st, z, sc);
                 const size_t o = (size_t)oi[k] * S + s;
                 a.out_target[o] = t;
                 if (a.out_score) a.out_score[o] = sc;
@@ -487,9 +499,10 @@ __device__ __forceinline__ void mid_row(const MidArgs &a, const int *__restrict_
         runs += (end && v[j] != INT_MAX && ky[j] != kKeyHaz && c == M) ? 1 : 0;
     }
     const CarState st = cand_state(best, M * runs);
+    const ZeroCase z = load_zc(a.sc.zc_cnt, a.sc.zc_key, s_ld);
     if (lane_ok) {
         int sc;
-        const int t = car_finalize(st, s, a.sc.zc_cnt, a.sc.zc_key, sc);
+        const int t = car_finalize(st, z, sc);
         const size_t o = (size_t)oi * S + s;
         a.sc.out_target[o] = t;
         if (a.sc.out_score) a.sc.out_score[o] = sc;
@@ -657,7 +670,7 @@ __global__ __launch_bounds__(256) void car_heavy_kernel(const HeavyItem *__restr
         CarState r = red[tid];
         for (int w = 1; w < 4; ++w) r = st_combine(r, red[w * G + tid]);
         int sc;
-        const int t = car_finalize(r, s, zc_cnt, zc_key, sc);
+        const int t = car_finalize(r, load_zc(zc_cnt, zc_key, s), sc);
         const size_t o = (size_t)it.oi * S + s;
         out_target[o] = t;
         if (out_score) out_score[o] = sc;
