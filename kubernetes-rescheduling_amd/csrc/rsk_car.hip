@@ -25,9 +25,9 @@
 //                     per-lane register histograms (lane = scenario).
 //   car_light_kernel  deg <= 16 rows of sparse tiles: same scorer, neighbour
 //                     rows gathered from global.
-//   car_mid_kernel    17 <= deg <= 64: per-lane bitonic sort of the neighbour
+//   car_mid_kernel    17 <= deg <= 128: per-lane bitonic sort of the neighbour
 //                     node ids in registers + run-length scan.
-//   car_heavy_kernel  deg > 64: node ids staged in LDS, per-wave LDS count
+//   car_heavy_kernel  deg > 128: node ids staged in LDS, per-wave LDS count
 //                     tables / hash, coalesced lookups, cross-lane reduce.
 #include <algorithm>
 #include <climits>
@@ -47,11 +47,11 @@ constexpr int kLightMax = 16;                      // register-histogram rows: d
 constexpr int kNumLight = 4;                       // buckets D = 16, 8, 4, 2
 constexpr int kLightW[kNumLight] = {20, 12, 8, 4};  // record ints: oi, d, nb[D], pad to x4
 constexpr int kLightPK[kNumLight] = {1, 2, 4, 4};  // direct kernel: records per lane per step
-constexpr int kMidMax = 64;                        // sorted-register rows: 17 <= deg <= 64
-constexpr int kNumMid = 2;                         // buckets D = 32, 64
-constexpr int kMidW[kNumMid] = {36, 68};
-constexpr int kNumHeavy = 3;                       // (64,256] (256,1024] (1024,4096]
-constexpr int kHeavyMax[kNumHeavy] = {256, 1024, 4096};
+constexpr int kMidMax = 128;                       // sorted-register rows: 17 <= deg <= 128
+constexpr int kNumMid = 3;                         // buckets D = 32, 64, 128
+constexpr int kMidW[kNumMid] = {36, 68, 132};
+constexpr int kNumHeavy = 3;                       // (128,512] (512,2048] (2048,4096]
+constexpr int kHeavyMax[kNumHeavy] = {512, 2048, 4096};
 constexpr int kTileCP = 256;                       // pods per tile
 constexpr int kTileXCap = 64;                      // max external rows appended to a tile image
 constexpr int kTileWaves = 8;                      // waves per tile workgroup
@@ -425,11 +425,11 @@ __global__ __launch_bounds__(kTileWaves * 64) void car_tile_kernel(TileArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// K1c: mid rows (17 <= deg <= 64), one wave per (row, 64-scenario chunk),
+// K1c: mid rows (17 <= deg <= 128), one wave per (row, 64-scenario chunk),
 // lane = scenario.  Each lane loads its deg node ids (coalesced 256-B rows),
 // sorts them with a bitonic network in registers (min/max only: no compare
-// masks, no memory), gathers one nodekey word per sorted entry, then scans the
-// runs: best packed candidate, then the number of best-count runs.
+// masks, no memory), then scans the sorted runs once, gathering nodekey words
+// 32 at a time: best packed candidate and the number of best-count runs.
 // ---------------------------------------------------------------------------
 template <int D>
 __device__ __forceinline__ void bitonic_sort(int (&v)[D]) {
@@ -462,43 +462,47 @@ __device__ __forceinline__ void mid_row(const MidArgs &a, const int *__restrict_
     const int S = a.sc.S;
     const int s_ld = min(s, S - 1);
     const int4 *r4 = reinterpret_cast<const int4 *>(rec);
-    int r[W];
+    const int2 hd = *reinterpret_cast<const int2 *>(rec);
+    const int oi = hd.x, d = hd.y;
+    // record: [oi, d, nb[0..D-1], pad]; neighbour ids read 4 at a time
+    int v[D];
 #pragma unroll
     for (int w = 0; w < W / 4; ++w) {
         const int4 x = r4[w];
-        r[4 * w] = x.x; r[4 * w + 1] = x.y; r[4 * w + 2] = x.z; r[4 * w + 3] = x.w;
-    }
-    const int oi = r[0], d = r[1];
-    int v[D];
+        const int q[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-    for (int j = 0; j < D; ++j) v[j] = a.assign[(size_t)r[2 + j] * (size_t)S + s_ld];
+        for (int t = 0; t < 4; ++t) {
+            const int j = 4 * w + t - 2;
+            if (j >= 0 && j < D) v[j] = ld32(a.assign, (unsigned)q[t] * (unsigned)S + (unsigned)s_ld);
+        }
+    }
 #pragma unroll
     for (int j = 0; j < D; ++j) v[j] = (j < d && (unsigned)v[j] < (unsigned)a.sc.N) ? v[j] : INT_MAX;
     bitonic_sort<D>(v);
-    int ky[D];
-#pragma unroll
-    for (int j = 0; j < D; ++j)
-        ky[j] = ld32(a.sc.nodekey, (unsigned)(v[j] == INT_MAX ? 0 : v[j]) * (unsigned)S + (unsigned)s_ld);
+    // one pass over the sorted ids: runs = distinct nodes; keys gathered kC at a time
+    constexpr int kC = 32;
     unsigned long long best = 0;
-    int c = 0;
+    int M = 0, R = 0, c = 0;
 #pragma unroll
-    for (int j = 0; j < D; ++j) {
-        c = (j > 0 && v[j] == v[j - 1]) ? c + 1 : 1;
-        const bool end = (j == D - 1) || v[j + (j < D - 1 ? 1 : 0)] != v[j];
-        const bool cand = end && v[j] != INT_MAX && ky[j] != kKeyHaz;
-        const unsigned long long key = cand ? pack_cand(c, ky[j], v[j]) : 0ull;
-        best = key > best ? key : best;
-    }
-    const int M = cand_count(best);
-    int runs = 0;
-    c = 0;
+    for (int j0 = 0; j0 < D; j0 += kC) {
+        int ky[kC];
 #pragma unroll
-    for (int j = 0; j < D; ++j) {
-        c = (j > 0 && v[j] == v[j - 1]) ? c + 1 : 1;
-        const bool end = (j == D - 1) || v[j + (j < D - 1 ? 1 : 0)] != v[j];
-        runs += (end && v[j] != INT_MAX && ky[j] != kKeyHaz && c == M) ? 1 : 0;
+        for (int t = 0; t < kC; ++t)
+            ky[t] = ld32(a.sc.nodekey, (unsigned)(v[j0 + t] == INT_MAX ? 0 : v[j0 + t]) * (unsigned)S + (unsigned)s_ld);
+#pragma unroll
+        for (int t = 0; t < kC; ++t) {
+            const int j = j0 + t;
+            c = (j > 0 && v[j] == v[j - (j > 0 ? 1 : 0)]) ? c + 1 : 1;
+            const bool end = (j == D - 1) || v[j + (j < D - 1 ? 1 : 0)] != v[j];
+            const bool cand = end && v[j] != INT_MAX && ky[t] != kKeyHaz;
+            const unsigned long long key = cand ? pack_cand(c, ky[t], v[j]) : 0ull;
+            best = key > best ? key : best;
+            const bool gt = cand && c > M, eq = cand && c == M;
+            R = gt ? 1 : (eq ? R + 1 : R);
+            M = gt ? c : M;
+        }
     }
-    const CarState st = cand_state(best, M * runs);
+    const CarState st = cand_state(best, M * R);
     const ZeroCase z = load_zc(a.sc.zc_cnt, a.sc.zc_key, s_ld);
     if (lane_ok) {
         int sc;
@@ -509,24 +513,34 @@ __device__ __forceinline__ void mid_row(const MidArgs &a, const int *__restrict_
     }
 }
 
+// kWide = false: buckets D = 32, 64; kWide = true: bucket D = 128 (its own
+// launch, so the 256-VGPR D=128 body does not lower the occupancy of the others)
+template <bool kWide>
 __global__ __launch_bounds__(256) void car_mid_kernel(MidArgs a) {
     const int chunk = blockIdx.x / a.blocks_per_chunk;
     const int wave = (blockIdx.x % a.blocks_per_chunk) * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (wave >= a.prefix[kNumMid]) return;
+    const int b_lo = kWide ? 2 : 0, b_hi = kWide ? 3 : 2;
+    if (wave >= a.prefix[b_hi] - a.prefix[b_lo]) return;
     // a wave scores PS rows of one bucket, lanes split into PS slots of SL scenarios
     const int slot = lane / a.SL;
     const int s = chunk * a.SL + lane % a.SL;
-    const int b = wave >= a.prefix[1] ? 1 : 0;
-    const int item = (wave - a.prefix[b]) * a.sc.PS + slot;
+    int b = b_lo;
+    while (wave >= a.prefix[b + 1] - a.prefix[b_lo]) ++b;
+    const int item = (wave - (a.prefix[b] - a.prefix[b_lo])) * a.sc.PS + slot;
     const bool lane_ok = slot < a.sc.PS && s < a.sc.S && item < a.n_items[b];
     const int it = min(item, a.n_items[b] - 1);
-    if (b == 0) mid_row<32, 36>(a, a.rec[0] + (size_t)it * 36, slot, s, lane_ok);
-    else mid_row<64, 68>(a, a.rec[1] + (size_t)it * 68, slot, s, lane_ok);
+    if (kWide) {
+        mid_row<128, 132>(a, a.rec[2] + (size_t)it * 132, slot, s, lane_ok);
+    } else if (b == 0) {
+        mid_row<32, 36>(a, a.rec[0] + (size_t)it * 36, slot, s, lane_ok);
+    } else {
+        mid_row<64, 68>(a, a.rec[1] + (size_t)it * 68, slot, s, lane_ok);
+    }
 }
 
 // ---------------------------------------------------------------------------
-// K2: heavy rows (deg > 64).  Workgroup = (row, group of G scenarios).
+// K2: heavy rows (deg > 128).  Workgroup = (row, group of G scenarios).
 //   phase 0  stage node ids ntile[si][j] (G-scenario row segments per neighbour)
 //   phase A  wave w < NT hashes scenario si's d node ids into its LDS table
 //   phase B  counts back into ctile[si][j]; table cleared for the next scenario
@@ -691,7 +705,7 @@ struct rsk_car_plan {
     int n_light[kNumLight] = {0, 0, 0, 0};
     DevBuf ell[kNumLight];
     // mid rows (17..64)
-    int n_mid[kNumMid] = {0, 0};
+    int n_mid[kNumMid] = {0, 0, 0};
     DevBuf mid[kNumMid];
     // heavy rows (> 64)
     int n_heavy[kNumHeavy] = {0, 0, 0};
@@ -920,7 +934,7 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
             for (int j = 0; j < d; ++j) e[o + 2 + j] = nbp[j];
             plan->n_light[b] += 1;
         } else if (d <= kMidMax) {
-            const int b = d <= 32 ? 0 : 1;
+            const int b = d <= 32 ? 0 : (d <= 64 ? 1 : 2);
             auto &e = midr[b];
             const size_t o = e.size();
             e.resize(o + kMidW[b], 0);
@@ -1158,13 +1172,16 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
             a.n_items[b] = plan->n_mid[b];
             a.prefix[b + 1] = a.prefix[b] + (int)ceil_div(plan->n_mid[b], sc.PS);
         }
-        if (a.prefix[kNumMid] > 0) {
-            a.assign = d_assign;
-            a.blocks_per_chunk = (int)ceil_div(a.prefix[kNumMid], 4);
+        a.assign = d_assign;
+        for (int wide = 0; wide < 2; ++wide) {
+            const int waves = wide ? a.prefix[3] - a.prefix[2] : a.prefix[2] - a.prefix[0];
+            if (waves <= 0) continue;
+            a.blocks_per_chunk = (int)ceil_div(waves, 4);
             const int64_t blocks = chunks * a.blocks_per_chunk;
             RSK_CHECK(blocks < INT32_MAX, "mid grid too large");
             ScopedTimer tm(ctx, "car_mid");
-            car_mid_kernel<<<dim3((unsigned)blocks), dim3(256), 0, ctx->stream>>>(a);
+            if (wide) car_mid_kernel<true><<<dim3((unsigned)blocks), dim3(256), 0, ctx->stream>>>(a);
+            else car_mid_kernel<false><<<dim3((unsigned)blocks), dim3(256), 0, ctx->stream>>>(a);
             RSK_HIP(hipGetLastError());
         }
     }

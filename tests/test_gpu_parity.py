@@ -131,6 +131,19 @@ def test_car_random_graphs(ctx, S):
         _check_car(ctx, rp, ci, a, S, cap, use, haz, N, label=f"S={S} trial={trial} N={N} P={P}")
 
 
+@pytest.mark.parametrize("S", [1, 64, 65])
+def test_car_degree_bucket_boundaries(ctx, S):
+    """Rows at every routing boundary: light/tile <= 16 < mid <= 32/64/128 < heavy classes."""
+    rng = np.random.default_rng(300 + S)
+    hubs = [2, 3, 4, 5, 8, 9, 16, 17, 31, 32, 33, 63, 64, 65, 127, 128, 129, 511, 512, 513]
+    P, N = 1400, 60
+    rp, ci, a, cap, use, haz = _random_case(rng, P, N, S, max_deg=3, hub_deg=hubs, p_haz=0.2)
+    _check_car(ctx, rp, ci, a, S, cap, use, haz, N, label=f"boundaries S={S}")
+    from rsk import api
+    info = api.CarPlan(rp, ci, ctx=ctx).info()
+    assert info["mid_rows"] >= 8 and info["heavy_rows"] >= 3 and info["tile_rows"] > 0, info
+
+
 def test_car_heavy_hash_path_large_n(ctx):
     """N > 16384 switches heavy rows from direct LDS count tables to the LDS hash."""
     rng = np.random.default_rng(21)
