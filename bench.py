@@ -135,16 +135,15 @@ def main():
     parity_ok = bool(np.array_equal(got, exp))
 
     # Algorithmic bytes per launch of each kernel (DESIGN.md "Roofline accounting"):
-    #   car_tile : every pod's assign slice once (4·S per tiled pod) + target of its rows (4·S) + records
-    #   car_light: own slice + target of each direct row (8·S) + ELL records
-    #   car_heavy: own slice + target of each heavy row (8·S) + heavy CSR   (per step, over its launches)
-    #   car_prep : use + hazard (5·N·S) + cap (4·N)
-    tiled_pods = min(P, info["tiles"] * info["tile_pods"])
-    alg = {"car_tile": 4 * S * tiled_pods + 4 * S * info["tile_rows"] + info["tile_bytes"],
-           "car_light": 8 * S * info["direct_rows"] + info["direct_bytes"],
-           "car_mid": 8 * S * info["mid_rows"] + info["mid_bytes"],
-           "car_heavy": 8 * S * info["heavy_rows"] + info["heavy_bytes"],
-           "car_prep": 5 * N * S + 4 * N}
+    #   car_tile : the assign slice of every distinct pod in the tile images once (4·S per pod)
+    #              + target of its rows (4·S) + the tile plan (image lists, records)
+    #   car_mid  : target of each mid row (4·S) + its own neighbour slices are re-reads (not counted) + records
+    #   car_heavy: target of each heavy row (4·S) + heavy items / CSR
+    #   car_prep : use + hazard (5·N·S) + cap (4·N) read, nodekey (4·N·S) written
+    alg = {"car_tile": 4 * S * info["image_pods_distinct"] + 4 * S * info["tile_rows"] + info["tile_bytes"],
+           "car_mid": 4 * S * info["mid_rows"] + info["mid_bytes"],
+           "car_heavy": 4 * S * info["heavy_rows"] + info["heavy_bytes"],
+           "car_prep": 9 * N * S + 4 * N}
     B = algorithmic_bytes(P, N, S, c.nnz)
     roof = None
     if kernels:

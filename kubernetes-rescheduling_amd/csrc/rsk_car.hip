@@ -11,23 +11,21 @@
 //
 // The dense score row has N entries but only the nodes holding p's neighbours
 // can score > 0, so each (p, s) cell is a histogram of deg(p) node ids:
-//   * max score M > 0: the winner is among the neighbour nodes.  With the
-//     lexicographic key (count, remaining CPU, -node) the argmax is the
-//     reference's choice; |best| == 1 iff exactly M neighbour entries reach M.
+//   * max score M > 0: the winner is among the neighbour nodes: the largest
+//     (count, remaining CPU, -node); |best| == 1 iff exactly M entries reach M.
 //   * M == 0: every non-hazard node ties at 0 -> a per-scenario constant
 //     ("zero case"), computed once by car_prep_kernel.
 //
 // Kernels (one HIP stream, all integer, no atomics on the decision path):
-//   car_prep_kernel   nodekey[n*S+s] = hazard ? KEY_HAZ : cap[n]-use[n*S+s] (one
-//                     gather word per node later) + the zero case per scenario.
-//   car_tile_kernel   deg <= 16 rows of dense tiles: LDS image of the tile's
-//                     assign rows (each row read from HBM once per chunk),
-//                     per-lane register histograms (lane = scenario).
-//   car_light_kernel  deg <= 16 rows of sparse tiles: same scorer, neighbour
-//                     rows gathered from global.
-//   car_mid_kernel    17 <= deg <= 128: per-lane bitonic sort of the neighbour
+//   car_prep_kernel   nodekey[n*S+s] = hazard ? KEY_HAZ : cap[n]-use[n*S+s]
+//                     (one gather word per node later) + the zero case.
+//   car_tile_kernel   deg <= 16 rows, grouped into tiles of <= 128 rows whose
+//                     neighbours (<= 160 image rows) are staged once per
+//                     scenario chunk in LDS together with their node keys;
+//                     scoring then runs from LDS with per-degree-class scorers.
+//   car_mid_kernel    17 <= deg <= 64: per-lane bitonic sort of the neighbour
 //                     node ids in registers + run-length scan.
-//   car_heavy_kernel  deg > 128: node ids staged in LDS, per-wave LDS count
+//   car_heavy_kernel  deg > 64: node ids staged in LDS, per-wave LDS count
 //                     tables / hash, coalesced lookups, cross-lane reduce.
 #include <algorithm>
 #include <climits>
@@ -41,21 +39,23 @@
 
 namespace rsk {
 
-constexpr int kKeyHaz = INT_MIN;
+constexpr int kKeyHaz = INT_MIN;  // cap - use never reaches INT_MIN (both in [0, 2^31))
 constexpr int kMaxDegree = 4096;
-constexpr int kLightMax = 16;                      // register-histogram rows: deg <= 16
-constexpr int kNumLight = 4;                       // buckets D = 16, 8, 4, 2
-constexpr int kLightW[kNumLight] = {20, 12, 8, 4};  // record ints: oi, d, nb[D], pad to x4
-constexpr int kLightPK[kNumLight] = {1, 2, 4, 4};  // direct kernel: records per lane per step
-constexpr int kMidMax = 128;                       // sorted-register rows: 17 <= deg <= 128
-constexpr int kNumMid = 3;                         // buckets D = 32, 64, 128
-constexpr int kMidW[kNumMid] = {36, 68, 132};
-constexpr int kNumHeavy = 3;                       // (128,512] (512,2048] (2048,4096]
+constexpr int kLightMax = 16;                      // LDS-tile rows: deg <= 16
+constexpr int kMidMax = 64;                        // sorted-register rows: 17 <= deg <= 64
+constexpr int kNumMid = 2;                         // buckets D = 32, 64
+constexpr int kMidW[kNumMid] = {36, 68};           // record ints: oi, d, nb[D], pad to x4
+constexpr int kNumHeavy = 3;                       // (64,512] (512,2048] (2048,4096]
 constexpr int kHeavyMax[kNumHeavy] = {512, 2048, 4096};
-constexpr int kTileCP = 256;                       // pods per tile
-constexpr int kTileXCap = 64;                      // max external rows appended to a tile image
-constexpr int kTileWaves = 8;                      // waves per tile workgroup
-constexpr int kTileBatch = 12;                     // rows per wave per load batch (register path)
+
+// Light-row tiles.
+constexpr int kTileOwners = 128;                   // max rows scored per tile (plan default: 64)
+constexpr int kTileRows = 160;                     // max image rows (distinct neighbours) per tile
+constexpr int kTileThreads = 256;                  // pipelined kernel geometry
+constexpr int kTileWaves = kTileThreads / 64;
+constexpr int kNumCls = 5;                         // degree classes d = 1, 2, 3-4, 5-8, 9-16
+constexpr int kClsW[kNumCls] = {2, 2, 4, 8, 12};   // record ints
+constexpr int kMetaW = 12;                         // tile meta ints (see TileArgs)
 
 struct CarState {
     int bc;  // best count (max score); 0 = no non-hazard neighbour node
@@ -97,8 +97,8 @@ __device__ __forceinline__ CarState st_shfl_xor(const CarState &st, int off) {
     return o;
 }
 
-// Candidate key of the register scorers: lexicographic (count, remaining CPU,
-// -node) as one u64 — count 7 bits (<= 64), remaining CPU 32 bits (sign
+// Candidate key of the sorted-register scorer: lexicographic (count, remaining
+// CPU, -node) as one u64 — count 7 bits (<= 64), remaining CPU 32 bits (sign
 // flipped), 0x1ffffff - node 25 bits (N < 2^25).  0 = no candidate.
 constexpr int kNodeBits = 25;
 constexpr unsigned kNodeMask = (1u << kNodeBits) - 1u;
@@ -135,16 +135,20 @@ __device__ __forceinline__ ZeroCase load_zc(const int *__restrict__ zc_cnt, cons
     return z;
 }
 
+// rescheduling.py:199-214 when no neighbour node is a candidate (max score 0):
+// every non-hazard node ties; `max` raises on an empty candidate list.
+__device__ __forceinline__ int zero_target(const ZeroCase &z, int &score) {
+    if (z.cnt == 0) { score = -1; return RSK_TARGET_NO_CANDIDATE; }
+    const int n = (int)(~(unsigned)(z.key & 0xffffffffull));
+    const int rem = (int)((unsigned)(z.key >> 32) ^ 0x80000000u);
+    score = 0;
+    if (z.cnt == 1) return n;
+    return rem >= 0 ? n : RSK_TARGET_NONE;
+}
+
 // rescheduling.py:199-214 applied to the reduced state.
 __device__ __forceinline__ int car_finalize(const CarState &st, const ZeroCase &z, int &score) {
-    if (st.bc == 0) {
-        if (z.cnt == 0) { score = -1; return RSK_TARGET_NO_CANDIDATE; }
-        const int n = (int)(~(unsigned)(z.key & 0xffffffffull));
-        const int rem = (int)((unsigned)(z.key >> 32) ^ 0x80000000u);
-        score = 0;
-        if (z.cnt == 1) return n;
-        return rem >= 0 ? n : RSK_TARGET_NONE;
-    }
+    if (st.bc == 0) return zero_target(z, score);
     score = st.bc;
     if (st.nm == st.bc) return st.bn;
     return st.br >= 0 ? st.bn : RSK_TARGET_NONE;
@@ -156,6 +160,22 @@ __device__ __forceinline__ int car_finalize(const CarState &st, const ZeroCase &
 __device__ __forceinline__ int ld32(const int *__restrict__ base, unsigned idx) {
     return *reinterpret_cast<const int *>(reinterpret_cast<const char *>(base) + (idx << 2));
 }
+
+// Bounds-checked debug build (make debug -> librsk_dbg.so, -DRSK_DEBUG_BOUNDS):
+// every tile-kernel global access checks its element index against the buffer
+// size; a violation sets a bit in rsk_dbg_flags (reported by execute) and the
+// access is redirected to element 0 instead of faulting the GPU.
+#ifdef RSK_DEBUG_BOUNDS
+__device__ unsigned rsk_dbg_flags;
+__device__ __forceinline__ unsigned dbg_bound(unsigned idx, unsigned lim, unsigned code) {
+    if (idx < lim) return idx;
+    atomicOr(&rsk_dbg_flags, code);
+    return 0u;
+}
+#define RSK_BOUND(idx, lim, code) dbg_bound((unsigned)(idx), (unsigned)(lim), (code))
+#else
+#define RSK_BOUND(idx, lim, code) (idx)
+#endif
 
 // ---------------------------------------------------------------------------
 // K0: packed node key + per-scenario zero case.
@@ -192,17 +212,523 @@ __global__ __launch_bounds__(256) void car_prep_kernel(const int *__restrict__ c
 }
 
 // ---------------------------------------------------------------------------
-// Register scorer for deg <= 16 rows.  A record is
-//   [out_row, deg, nb[0..D-1], pad]   (W ints, W % 4 == 0, int4-loadable)
-// and `fetch(nb)` returns the neighbour's node id in this lane's scenario
-// (padding entries encode a valid source).  Each lane counts equal node ids
-// pairwise in registers, gathers one nodekey word per neighbour and keeps the
-// max packed candidate key.
+// K1: light rows (deg <= 16) in LDS tiles.
 //
-// Every load is issued unconditionally from a clamped, always-valid address
-// and the result selected afterwards: hipcc otherwise branches around each
-// guarded load and waits vmcnt(0) per element, serialising the gather.
+// The plan groups the light rows (in DFS order of the relation graph, so a
+// row's neighbours are mostly its tile-mates) into tiles of <= 128 rows whose
+// distinct neighbours — the tile's image rows — number <= 160.  Workgroup =
+// (tile, chunk of SL = 2^lsl scenarios), 4 waves:
+//   phase 1  every image row's SL-scenario slice of assign (SL*4 contiguous
+//            bytes; each row leaves HBM once per chunk) -> registers, its node
+//            key per scenario gathered from nodekey (L2), both -> LDS
+//            nimg[row][SL], kimg[row][SL]; the tile's records -> LDS.
+//   phase 2  lanes = (record slot, scenario).  A record is
+//            [out_row, (deg,) neighbour image rows packed 2 x u16 per int];
+//            scorers specialised per degree class read node + key from LDS and
+//            store one target word per lane (SL*4 contiguous bytes per row).
+// Meta per tile (kMetaW ints): img_off, nrows, rec_off, rec_ints,
+// n[5] records per class, o4, o8, o16 class offsets (ints, 4-aligned).
 // ---------------------------------------------------------------------------
+struct TileArgs {
+    const int *img_pods;   // concatenated per-tile image pod lists
+    const int *meta;       // [T][kMetaW]
+    const int *recs;       // concatenated per-tile record blobs (16-B aligned)
+    const int *assign;
+    const int *nodekey;
+    const int *zc_cnt;
+    const unsigned long long *zc_key;
+    int *out_target;
+    int *out_score;
+    int S, N, T, lsl, rmax;  // SL = 1 << lsl scenarios per workgroup
+    int ablate;              // profiling only (RSK_ABLATE_TILE): 1 skip image load, 2 skip scoring
+    int order;               // 0 chunk-major, 1 tile-major grid (RSK_TILE_ORDER)
+    unsigned n_assign, n_out, n_pods, n_recs, n_key, n_meta;  // element counts (debug bounds build)
+};
+// records -> LDS in two int4 copies per thread: NT * 8 >= owners * 12 + 2 (checked by the host)
+
+// Element offsets: 32-bit (saddr form, one VGPR) when every offset * 4 < 2^32.
+template <bool kOff32>
+__device__ __forceinline__ size_t cell(unsigned i, unsigned S, unsigned s) {
+    if (kOff32) return (size_t)((i * S + s) << 2);
+    return ((size_t)i * S + s) << 2;
+}
+template <bool kOff32>
+__device__ __forceinline__ void st_cell(int *base, unsigned i, unsigned S, unsigned s, int v) {
+    *reinterpret_cast<int *>(reinterpret_cast<char *>(base) + cell<kOff32>(i, S, s)) = v;
+}
+
+// Per-lane constants of the scoring phase.  Lanes past the last scenario (a
+// partial chunk) and record slots past a class's end redo a valid cell — the
+// last scenario / the last record — and store the identical value again, so
+// no load, LDS access or store is ever guarded by a branch.
+struct TileLane {
+    int slot, PS;
+    int col;    // image column of the lane's (clamped) scenario
+    int s;      // clamped scenario
+    int zt, zs; // zero-case target / score of the scenario
+};
+
+template <bool kScore, bool kOff32>
+__device__ __forceinline__ void tile_emit(const TileArgs &a, int oi, const TileLane &L, int t, int sc) {
+#ifdef RSK_DEBUG_BOUNDS
+    if ((size_t)(unsigned)oi * a.S + L.s >= a.n_out || oi < 0) { atomicOr(&rsk_dbg_flags, 1u); return; }
+#endif
+    st_cell<kOff32>(a.out_target, (unsigned)oi, (unsigned)a.S, (unsigned)L.s, t);
+    if (kScore) st_cell<kOff32>(a.out_score, (unsigned)oi, (unsigned)a.S, (unsigned)L.s, sc);
+}
+
+__device__ __forceinline__ int2 img_at(const int2 *img, int row, int lsl, int col) { return img[(row << lsl) + col]; }
+
+// d == 1: the neighbour's node is the single best unless hazard (zero case).
+template <int U, bool kScore, bool kOff32, int NW = kTileWaves>
+__device__ __forceinline__ void tile_d1(const TileArgs &a, const int2 *img, const int *rec, int n, const TileLane &L,
+                                        int wave) {
+    const int step = NW * L.PS;
+    const int2 *r2 = reinterpret_cast<const int2 *>(rec);
+    for (int b0 = wave * L.PS; b0 < n; b0 += step * U) {
+        int2 r[U], e[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) r[u] = r2[min(b0 + u * step + L.slot, n - 1)];
+#pragma unroll
+        for (int u = 0; u < U; ++u) e[u] = img_at(img, r[u].y, a.lsl, L.col);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool h = e[u].y == kKeyHaz;
+            tile_emit<kScore, kOff32>(a, r[u].x, L, h ? L.zt : e[u].x, h ? L.zs : 1);
+        }
+    }
+}
+
+// d == 2: same node -> score 2; one hazard -> the other; two distinct
+// candidates -> tie of two: larger remaining CPU (then lower index), None if < 0.
+template <int U, bool kScore, bool kOff32, int NW = kTileWaves>
+__device__ __forceinline__ void tile_d2(const TileArgs &a, const int2 *img, const int *rec, int n, const TileLane &L,
+                                        int wave) {
+    const int step = NW * L.PS;
+    const int2 *r2 = reinterpret_cast<const int2 *>(rec);
+    for (int b0 = wave * L.PS; b0 < n; b0 += step * U) {
+        int2 r[U], e0[U], e1[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) r[u] = r2[min(b0 + u * step + L.slot, n - 1)];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            e0[u] = img_at(img, r[u].y & 0xffff, a.lsl, L.col);
+            e1[u] = img_at(img, (int)((unsigned)r[u].y >> 16), a.lsl, L.col);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int n0 = e0[u].x, k0 = e0[u].y, n1 = e1[u].x, k1 = e1[u].y;
+            const bool h0 = k0 == kKeyHaz, h1 = k1 == kKeyHaz;
+            const bool w0 = !h0 && (h1 || k0 > k1 || (k0 == k1 && n0 <= n1));
+            const int nb = w0 ? n0 : n1, kb = w0 ? k0 : k1;
+            const bool single = h0 || h1 || n0 == n1;
+            const int tt = single ? nb : (kb >= 0 ? nb : RSK_TARGET_NONE);
+            const bool zero = h0 && h1;
+            tile_emit<kScore, kOff32>(a, r[u].x, L, zero ? L.zt : tt, zero ? L.zs : (n0 == n1 ? 2 : 1));
+        }
+    }
+}
+
+// 0 or 3 <= d <= D: pairwise equality counts in registers, then the
+// lexicographic (count, key, -node) maximum over the candidates in 32-bit steps.
+template <int D, int W, bool kScore, bool kOff32, int NW = kTileWaves>
+__device__ __forceinline__ void tile_dn(const TileArgs &a, const int2 *img, const int *rec, int n, const TileLane &L,
+                                        int wave) {
+    const int step = NW * L.PS;
+    for (int b0 = wave * L.PS; b0 < n; b0 += step) {
+        const int4 *r4 = reinterpret_cast<const int4 *>(rec + min(b0 + L.slot, n - 1) * W);
+        int r[W];
+#pragma unroll
+        for (int w = 0; w < W / 4; ++w) {
+            const int4 x = r4[w];
+            r[4 * w] = x.x; r[4 * w + 1] = x.y; r[4 * w + 2] = x.z; r[4 * w + 3] = x.w;
+        }
+        const int d = r[1];
+        int nd[D], ky[D], c[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const unsigned pr = (unsigned)r[2 + j / 2];
+            const int2 e = img_at(img, (j & 1) ? (int)(pr >> 16) : (int)(pr & 0xffffu), a.lsl, L.col);
+            // padding entries (j >= d) read row 0: masked out of the counts
+            // (a node id no real entry can hold) and of the candidates
+            nd[j] = j < d ? e.x : -1 - j;
+            ky[j] = j < d ? e.y : kKeyHaz;
+            c[j] = 1;
+        }
+#pragma unroll
+        for (int j = 1; j < D; ++j)
+#pragma unroll
+            for (int i2 = 0; i2 < j; ++i2) {
+                const int eq = nd[j] == nd[i2];
+                c[j] += eq;
+                c[i2] += eq;
+            }
+        int M = 0;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            c[j] = ky[j] == kKeyHaz ? 0 : c[j];
+            M = max(M, c[j]);
+        }
+        int kb = INT_MIN;
+#pragma unroll
+        for (int j = 0; j < D; ++j) kb = max(kb, c[j] == M ? ky[j] : INT_MIN);
+        int nb = INT_MAX, nm = 0;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const bool m = c[j] == M;
+            nb = min(nb, (m && ky[j] == kb) ? nd[j] : INT_MAX);
+            nm += m;
+        }
+        const int tt = nm == M ? nb : (kb >= 0 ? nb : RSK_TARGET_NONE);
+        tile_emit<kScore, kOff32>(a, r[0], L, M == 0 ? L.zt : tt, M == 0 ? L.zs : M);
+    }
+}
+
+// Phase 1: image rows -> LDS as {node, key} pairs.  kVec: SL >= 4 and S % 4 == 0
+// (16-B loads of 4 scenarios).  Elements past the end redo the last element
+// (identical LDS writes), so nothing is guarded.
+template <bool kVec, bool kOff32, int NT>
+__device__ __forceinline__ void tile_load_image(const TileArgs &a, int2 *img, int img_off, int nrows, int s0) {
+    const unsigned S = (unsigned)a.S, N = (unsigned)a.N;
+    const int *__restrict__ pods = a.img_pods + img_off;
+    const char *__restrict__ asg = reinterpret_cast<const char *>(a.assign);
+    constexpr int kB = 5;
+    if (kVec) {
+        const int lq = a.lsl - 2;  // 16-B slots per row = SL / 4
+        const int qm = (1 << lq) - 1;
+        const int total = nrows << lq;
+        for (int b = 0; b < total; b += NT * kB) {
+            int e[kB], pod[kB];
+            int4 v[kB];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                e[u] = min(b + u * NT + (int)threadIdx.x, total - 1);
+                pod[u] = pods[e[u] >> lq];
+            }
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                const unsigned s = (unsigned)min(s0 + ((e[u] & qm) << 2), (int)S - 4);
+                v[u] = *reinterpret_cast<const int4 *>(asg + cell<kOff32>((unsigned)pod[u], S, s));
+            }
+            int k[kB][4];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                const int s = s0 + ((e[u] & qm) << 2);
+                const int nn[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int x = 0; x < 4; ++x) {
+                    const bool ok = (unsigned)nn[x] < N && s + x < (int)S;
+                    const int key = ld32(a.nodekey, ok ? (unsigned)nn[x] * S + (unsigned)(s + x) : 0u);
+                    k[u][x] = ok ? key : kKeyHaz;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                int4 *dst = reinterpret_cast<int4 *>(img + ((e[u] >> lq) << a.lsl) + ((e[u] & qm) << 2));
+                dst[0] = make_int4(v[u].x, k[u][0], v[u].y, k[u][1]);
+                dst[1] = make_int4(v[u].z, k[u][2], v[u].w, k[u][3]);
+            }
+        }
+    } else {
+        const int total = nrows << a.lsl;
+        const int msk = (1 << a.lsl) - 1;
+        for (int b = 0; b < total; b += NT * kB) {
+            int e[kB], pod[kB], v[kB];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                e[u] = min(b + u * NT + (int)threadIdx.x, total - 1);
+                pod[u] = pods[e[u] >> a.lsl];
+            }
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                const unsigned s = (unsigned)min(s0 + (e[u] & msk), (int)S - 1);
+                v[u] = *reinterpret_cast<const int *>(asg + cell<kOff32>((unsigned)pod[u], S, s));
+            }
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                const int s = s0 + (e[u] & msk);
+                const bool ok = (unsigned)v[u] < N && s < (int)S;
+                const int key = ld32(a.nodekey, ok ? (unsigned)v[u] * S + (unsigned)s : 0u);
+                img[e[u]] = make_int2(v[u], ok ? key : kKeyHaz);
+            }
+        }
+    }
+}
+
+template <bool kVec, bool kScore, bool kOff32, int NT>
+__global__ __launch_bounds__(NT) void car_tile_kernel(TileArgs a) {
+    constexpr int NW = NT / 64;
+    extern __shared__ __attribute__((aligned(16))) int lds[];  // img {node,key} [rmax][SL], then records
+    // chunk-major (default: concurrent workgroups share a chunk's nodekey
+    // slice in L2) or tile-major (a tile's chunks back to back: DRAM locality)
+    const int nchunk = (a.S + (1 << a.lsl) - 1) >> a.lsl;
+    const int tile = a.order ? blockIdx.x / nchunk : blockIdx.x % a.T;
+    const int chunk = a.order ? blockIdx.x % nchunk : blockIdx.x / a.T;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int SL = 1 << a.lsl;
+    const int s0 = chunk * SL;
+    int2 *img = reinterpret_cast<int2 *>(lds);
+    int *rec = lds + ((2 * a.rmax * SL + 3) & ~3);  // 16-B aligned for the int4 record reads
+    const int *m = a.meta + (size_t)tile * kMetaW;
+    const int img_off = m[0], nrows = m[1], rec_off = m[2], rec_ints = m[3];
+
+    // records -> LDS: at most 2 int4 per thread (static_assert above), clamped
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int i = min((int)threadIdx.x * 4 + k * NT * 4, rec_ints - 4);
+        *reinterpret_cast<int4 *>(rec + i) = *reinterpret_cast<const int4 *>(a.recs + rec_off + i);
+    }
+    if (!(a.ablate & 1) && nrows > 0) tile_load_image<kVec, kOff32, NT>(a, img, img_off, nrows, s0);
+
+    TileLane L;
+    L.PS = 64 >> a.lsl;
+    L.slot = lane >> a.lsl;
+    L.s = min(s0 + (lane & (SL - 1)), a.S - 1);
+    L.col = L.s - s0;
+    {
+        int zs;
+        L.zt = zero_target(load_zc(a.zc_cnt, a.zc_key, L.s), zs);
+        L.zs = zs;
+    }
+    __syncthreads();
+    if (a.ablate & 2) return;  // profiling ablation: no scoring (results are wrong)
+    const int n1 = m[4], n2 = m[5], n4 = m[6], n8 = m[7], n16 = m[8];
+    const int o4 = m[9], o8 = m[10], o16 = m[11];
+    if (n1) tile_d1<4, kScore, kOff32, NW>(a, img, rec, n1, L, wave);
+    if (n2) tile_d2<2, kScore, kOff32, NW>(a, img, rec + 2 * n1, n2, L, wave);
+    if (n4) tile_dn<4, 4, kScore, kOff32, NW>(a, img, rec + o4, n4, L, wave);
+    if (n8) tile_dn<8, 8, kScore, kOff32, NW>(a, img, rec + o8, n8, L, wave);
+    if (n16) tile_dn<16, 12, kScore, kOff32, NW>(a, img, rec + o16, n16, L, wave);
+}
+
+// ---------------------------------------------------------------------------
+// K1p: the same light-row tiles as a persistent, wave-specialised pipeline
+// (S % 4 == 0, SL = 32).  One workgroup per CU walks the items (tile, chunk)
+// blockIdx, blockIdx + gridDim, ... (chunk-major, so concurrent items share a
+// chunk's nodekey slice in L2).  Per stage t (one s_barrier each):
+//   loader waves (kLoadW)  write item t+1 into LDS buffer (t+1)&1 from the
+//                          registers filled earlier, then issue the gathers of
+//                          item t+2 (node keys, records, zero case), the assign
+//                          loads of item t+3 and the image pod ids of item t+4;
+//   scorer waves (kScoreW) score item t from buffer t&1 and store its targets.
+// Loaders never store and scorers never load from global memory, so neither
+// kind waits on the other's vector-memory traffic (vmcnt retires in issue
+// order): a loader's waits are exactly the loads it issued one stage earlier,
+// and a scorer never waits on its stores.  Out-of-range items are clamped to
+// a valid one (their loads are harmless repeats; nothing is scored).
+// ---------------------------------------------------------------------------
+constexpr int kPipeSL = 32, kPipeLsl = 5;
+constexpr int kLoadW = 4, kScoreW = 8;
+constexpr int kPipeThreads = (kLoadW + kScoreW) * 64;
+constexpr int kLdThreads = kLoadW * 64;
+constexpr int kLdSlots = (kTileRows * (kPipeSL / 4) + kLdThreads - 1) / kLdThreads;  // int4 image slots per loader
+constexpr int kLdRec = (kTileOwners * 12 / 4 + kLdThreads - 1) / kLdThreads;         // int4 record slots per loader
+constexpr int kBufHead = 80;                                                          // meta[12], zt[32], zs[32], pad
+constexpr int kBufInts = kBufHead + kTileRows * kPipeSL * 2 + kTileOwners * 12;
+
+struct PipeArgs {
+    TileArgs t;
+    int items;  // T * chunks
+};
+
+struct LdA {  // assign slices of one item (this loader thread's slots)
+    int4 v[kLdSlots];
+};
+struct LdK {  // node keys of one item + its records + zero case
+    int k[kLdSlots][4];
+    int4 rec[kLdRec];
+    int zt, zs;
+};
+struct LdP {
+    int pod[kLdSlots];
+};
+
+__device__ __forceinline__ int pipe_item(const PipeArgs &a, int j) {
+    // j-th item of this workgroup, clamped into [first, last] of its own items
+    const int n = (a.items - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    j = min(max(j, 0), n - 1);
+    return (int)blockIdx.x + j * (int)gridDim.x;
+}
+
+// Tile meta read through the constant address space: the plan never changes
+// during a launch, so these become scalar loads (lgkmcnt) instead of vector
+// loads that would queue behind the loaders' in-flight gathers.
+typedef const __attribute__((address_space(4))) int *cint_ptr;
+__device__ __forceinline__ cint_ptr const_ptr(const int *p) { return (cint_ptr)(uintptr_t)p; }
+
+struct ItemGeo {
+    int tile, s0, img_off, total, rec_off, rec_ints;
+    cint_ptr meta;
+};
+__device__ __forceinline__ ItemGeo pipe_geo(const PipeArgs &a, int item) {
+    ItemGeo g;
+    g.tile = item % a.t.T;
+    g.s0 = (item / a.t.T) * kPipeSL;
+    g.meta = const_ptr(a.t.meta) + (size_t)g.tile * kMetaW;
+    g.img_off = g.meta[0];
+    g.total = g.meta[1] << 3;  // 8 int4 slots per row
+    g.rec_off = g.meta[2];
+    g.rec_ints = g.meta[3];
+    return g;
+}
+
+__device__ __forceinline__ int ld_slot(int u, int lt, int total) { return min(u * kLdThreads + lt, max(total - 1, 0)); }
+
+__device__ __forceinline__ void ld_issue_p(const PipeArgs &a, int item, int lt, LdP &p) {
+    const ItemGeo g = pipe_geo(a, item);
+#pragma unroll
+    for (int u = 0; u < kLdSlots; ++u)
+        p.pod[u] = a.t.img_pods[RSK_BOUND(g.img_off + (ld_slot(u, lt, g.total) >> 3), a.t.n_pods, 2u)];
+}
+
+template <bool kOff32>
+__device__ __forceinline__ void ld_issue_a(const PipeArgs &a, int item, int lt, const LdP &p, LdA &A) {
+    const ItemGeo g = pipe_geo(a, item);
+    const unsigned S = (unsigned)a.t.S;
+    const char *asg = reinterpret_cast<const char *>(a.t.assign);
+#pragma unroll
+    for (int u = 0; u < kLdSlots; ++u) {
+        const int e = ld_slot(u, lt, g.total);
+        const unsigned s = (unsigned)min(g.s0 + ((e & 7) << 2), (int)S - 4);
+#ifdef RSK_DEBUG_BOUNDS
+        if ((size_t)(unsigned)p.pod[u] * S + s + 3 >= a.t.n_assign) { atomicOr(&rsk_dbg_flags, 4u); A.v[u] = make_int4(0, 0, 0, 0); continue; }
+#endif
+        A.v[u] = *reinterpret_cast<const int4 *>(asg + cell<kOff32>((unsigned)p.pod[u], S, s));
+    }
+}
+
+__device__ __forceinline__ void ld_issue_k(const PipeArgs &a, int item, int lt, const LdA &A, LdK &K, bool keys) {
+    const ItemGeo g = pipe_geo(a, item);
+    const int S = a.t.S;
+    const unsigned N = (unsigned)a.t.N;
+#pragma unroll
+    for (int u = 0; keys && u < kLdSlots; ++u) {
+        const int e = ld_slot(u, lt, g.total);
+        const int s = g.s0 + ((e & 7) << 2);
+        const int nn[4] = {A.v[u].x, A.v[u].y, A.v[u].z, A.v[u].w};
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+            const bool ok = (unsigned)nn[x] < N && s + x < S;
+            const int key = ld32(a.t.nodekey, RSK_BOUND(ok ? (unsigned)nn[x] * (unsigned)S + (unsigned)(s + x) : 0u, a.t.n_key, 8u));
+            K.k[u][x] = ok ? key : kKeyHaz;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < kLdRec; ++u) {
+        const int i = min(4 * (u * kLdThreads + lt), g.rec_ints - 4);
+        K.rec[u] = *reinterpret_cast<const int4 *>(a.t.recs + RSK_BOUND(g.rec_off + i + 3, a.t.n_recs, 16u) - 3);
+    }
+    const int s = min(g.s0 + (lt & (kPipeSL - 1)), S - 1);
+    int zs;
+    K.zt = zero_target(load_zc(a.t.zc_cnt, a.t.zc_key, s), zs);
+    K.zs = zs;
+}
+
+__device__ __forceinline__ void ld_write(const PipeArgs &a, int item, int lt, const LdA &A, const LdK &K, int *buf) {
+    const ItemGeo g = pipe_geo(a, item);
+    int2 *img = reinterpret_cast<int2 *>(buf + kBufHead);
+    int *rec = buf + kBufHead + kTileRows * kPipeSL * 2;
+#pragma unroll
+    for (int u = 0; u < kLdSlots; ++u) {
+        const int e = ld_slot(u, lt, g.total);
+        int4 *dst = reinterpret_cast<int4 *>(img + ((e >> 3) << kPipeLsl) + ((e & 7) << 2));
+        dst[0] = make_int4(A.v[u].x, K.k[u][0], A.v[u].y, K.k[u][1]);
+        dst[1] = make_int4(A.v[u].z, K.k[u][2], A.v[u].w, K.k[u][3]);
+    }
+#pragma unroll
+    for (int u = 0; u < kLdRec; ++u) {
+        const int i = min(4 * (u * kLdThreads + lt), g.rec_ints - 4);
+        *reinterpret_cast<int4 *>(rec + i) = K.rec[u];
+    }
+    if (lt == 0) {
+#pragma unroll
+        for (int i = 0; i < kMetaW; ++i) buf[i] = g.meta[i];
+    }
+    if (lt < kPipeSL) {
+        buf[kMetaW + lt] = K.zt;
+        buf[kMetaW + kPipeSL + lt] = K.zs;
+    }
+}
+
+__device__ __forceinline__ void pipe_barrier() {
+    // LDS writes / reads of this stage complete, then the workgroup barrier;
+    // never a vmcnt wait (loads and stores stay in flight across stages)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// One loader stage t, register sets named by role.
+template <bool kOff32>
+__device__ __forceinline__ void ld_stage(const PipeArgs &a, int t, int lt, int *bufs, LdA &A1, LdK &K1, LdA &A2,
+                                         LdK &K2, LdA &A3, LdP &P3, LdP &P4) {
+    // compiler fences keep the issue order = the order the next stage waits in
+    ld_write(a, pipe_item(a, t + 1), lt, A1, K1, bufs + ((t + 1) & 1) * kBufInts);
+    asm volatile("" ::: "memory");
+    ld_issue_k(a, pipe_item(a, t + 2), lt, A2, K2, !(a.t.ablate & 1));
+    asm volatile("" ::: "memory");
+    if (!(a.t.ablate & 1)) ld_issue_a<kOff32>(a, pipe_item(a, t + 3), lt, P3, A3);
+    asm volatile("" ::: "memory");
+    ld_issue_p(a, pipe_item(a, t + 4), lt, P4);
+    pipe_barrier();
+}
+
+template <bool kScore, bool kOff32>
+__device__ __forceinline__ void sc_stage(const PipeArgs &a, int t, int n_items, int sw, int lane, int *bufs) {
+    if (t >= 0 && t < n_items && !(a.t.ablate & 2)) {
+        const int *buf = bufs + (t & 1) * kBufInts;
+        const int2 *img = reinterpret_cast<const int2 *>(buf + kBufHead);
+        const int *rec = buf + kBufHead + kTileRows * kPipeSL * 2;
+        const int item = pipe_item(a, t);
+        const int s0 = (item / a.t.T) * kPipeSL;
+        TileLane L;
+        L.PS = 64 / kPipeSL;
+        L.slot = lane >> kPipeLsl;
+        L.s = min(s0 + (lane & (kPipeSL - 1)), a.t.S - 1);
+        L.col = L.s - s0;
+        L.zt = buf[kMetaW + L.col];
+        L.zs = buf[kMetaW + kPipeSL + L.col];
+        const int n1 = buf[4], n2 = buf[5], n4 = buf[6], n8 = buf[7], n16 = buf[8];
+        const int o4 = buf[9], o8 = buf[10], o16 = buf[11];
+        if (n1) tile_d1<4, kScore, kOff32, kScoreW>(a.t, img, rec, n1, L, sw);
+        if (n2) tile_d2<2, kScore, kOff32, kScoreW>(a.t, img, rec + 2 * n1, n2, L, sw);
+        if (n4) tile_dn<4, 4, kScore, kOff32, kScoreW>(a.t, img, rec + o4, n4, L, sw);
+        if (n8) tile_dn<8, 8, kScore, kOff32, kScoreW>(a.t, img, rec + o8, n8, L, sw);
+        if (n16) tile_dn<16, 12, kScore, kOff32, kScoreW>(a.t, img, rec + o16, n16, L, sw);
+    }
+    pipe_barrier();
+}
+
+template <bool kScore, bool kOff32>
+__global__ __launch_bounds__(kPipeThreads) void car_tile_pipe_kernel(PipeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) int lds[];  // 2 item buffers of kBufInts
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int n = (a.items - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    // stages t = -4 .. n-1, padded to a multiple of 6 (the loaders' register
+    // rotation period); padding stages touch only clamped items
+    const int t_end = -4 + ((n + 4 + 5) / 6) * 6;
+    if (wave < kLoadW) {
+        const int lt = threadIdx.x;
+        // zero-initialised: the prologue stages consume sets no stage has
+        // filled yet (their loads must still hit valid addresses: pod 0)
+        LdA A0 = {}, A1 = {}, A2 = {};
+        LdK K0 = {}, K1 = {};
+        LdP P0 = {}, P1 = {};
+        for (int t = -4; t < t_end; t += 6) {
+            // roles per stage: write (A,K) of t+1, K-issue from A of t+2, A-issue of t+3, P-issue of t+4
+            ld_stage<kOff32>(a, t + 0, lt, lds, A0, K1, A1, K0, A2, P1, P0);
+            ld_stage<kOff32>(a, t + 1, lt, lds, A1, K0, A2, K1, A0, P0, P1);
+            ld_stage<kOff32>(a, t + 2, lt, lds, A2, K1, A0, K0, A1, P1, P0);
+            ld_stage<kOff32>(a, t + 3, lt, lds, A0, K0, A1, K1, A2, P0, P1);
+            ld_stage<kOff32>(a, t + 4, lt, lds, A1, K1, A2, K0, A0, P1, P0);
+            ld_stage<kOff32>(a, t + 5, lt, lds, A2, K0, A0, K1, A1, P0, P1);
+        }
+    } else {
+        const int sw = wave - kLoadW;
+        for (int t = -4; t < t_end; ++t) sc_stage<kScore, kOff32>(a, t, n, sw, lane, lds);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Shared by the mid and heavy kernels.
 struct ScoreCtx {
     const int *nodekey;
     const int *zc_cnt;
@@ -212,220 +738,8 @@ struct ScoreCtx {
     int S, N, PS;
 };
 
-template <int D>
-__device__ __forceinline__ CarState reduce_entries(const int (&nd)[D], const int (&ky)[D]) {
-    int cnt[D];
-#pragma unroll
-    for (int j = 0; j < D; ++j) cnt[j] = 1;
-#pragma unroll
-    for (int j = 1; j < D; ++j)
-#pragma unroll
-        for (int jj = 0; jj < j; ++jj) {
-            const int e = 1 - (int)min((unsigned)(nd[j] ^ nd[jj]), 1u);
-            cnt[j] += e;
-            cnt[jj] += e;
-        }
-    unsigned long long best = 0;
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-        const unsigned long long key = ky[j] == kKeyHaz ? 0ull : pack_cand(cnt[j], ky[j], nd[j]);
-        best = key > best ? key : best;
-    }
-    const int M = cand_count(best);
-    int nm = 0;
-#pragma unroll
-    for (int j = 0; j < D; ++j) nm += (ky[j] != kKeyHaz) & (cnt[j] == M);
-    return cand_state(best, nm);
-}
-
-template <int D, int PK, int W, class Fetch>
-__device__ __forceinline__ void score_records(const ScoreCtx &a, const int *__restrict__ recs, int item0,
-                                              int item_end, int slot, int s, bool lane_ok, Fetch fetch) {
-    const int S = a.S;
-    const int s_ld = min(s, S - 1);  // loads of inactive lanes stay in bounds
-    const int step = PK * a.PS;
-    const ZeroCase z = load_zc(a.zc_cnt, a.zc_key, s_ld);
-    for (int base = item0; base < item_end; base += step) {
-        int oi[PK], dg[PK], nd[PK][D], ky[PK][D];
-        bool v[PK];
-#pragma unroll
-        for (int k = 0; k < PK; ++k) {
-            const int it = base + k * a.PS + slot;
-            v[k] = lane_ok && it < item_end;
-            const int4 *rec = reinterpret_cast<const int4 *>(recs + (size_t)(v[k] ? it : item0) * W);
-            int r[W];
-#pragma unroll
-            for (int w = 0; w < W / 4; ++w) {
-                const int4 x = rec[w];
-                r[4 * w] = x.x; r[4 * w + 1] = x.y; r[4 * w + 2] = x.z; r[4 * w + 3] = x.w;
-            }
-            oi[k] = r[0];
-            dg[k] = v[k] ? r[1] : 0;
-#pragma unroll
-            for (int j = 0; j < D; ++j) nd[k][j] = fetch(r[2 + j]);
-        }
-#pragma unroll
-        for (int k = 0; k < PK; ++k)
-#pragma unroll
-            for (int j = 0; j < D; ++j) {
-                const int n = j < dg[k] ? nd[k][j] : -1;
-                const bool ok = (unsigned)n < (unsigned)a.N;
-                const int key = ld32(a.nodekey, (unsigned)(ok ? n : 0) * (unsigned)S + (unsigned)s_ld);
-                ky[k][j] = ok ? key : kKeyHaz;
-                nd[k][j] = ok ? n : -1 - j;  // never equal to another entry
-            }
-#pragma unroll
-        for (int k = 0; k < PK; ++k) {
-            const CarState st = reduce_entries<D>(nd[k], ky[k]);
-            if (v[k]) {
-                int sc;
-                const int t = car_finalize(st, z, sc);
-                const size_t o = (size_t)oi[k] * S + s;
-                a.out_target[o] = t;
-                if (a.out_score) a.out_score[o] = sc;
-            }
-        }
-    }
-}
-
-// K1a: direct rows (deg <= 16, owners of sparse tiles): records whose
-// neighbours are global pod ids (padding = pod 0); each neighbour row is one
-// coalesced 256-B gather.
-struct LightArgs {
-    ScoreCtx sc;
-    const int *ell[kNumLight];
-    int n_items[kNumLight];
-    int task_items[kNumLight];   // items per wave task
-    int task_prefix[kNumLight + 1];
-    const int *assign;
-    int SL, blocks_per_chunk;
-};
-
-__global__ __launch_bounds__(256) void car_light_kernel(LightArgs a) {
-    const int chunk = blockIdx.x / a.blocks_per_chunk;
-    const int wave = (blockIdx.x % a.blocks_per_chunk) * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (wave >= a.task_prefix[kNumLight]) return;
-    const int slot = lane / a.SL;
-    const int s = chunk * a.SL + lane % a.SL;
-    const bool lane_ok = slot < a.sc.PS && s < a.sc.S;
-    int b = 0;
-    while (wave >= a.task_prefix[b + 1]) ++b;
-    const int lt = wave - a.task_prefix[b];
-    const int item0 = lt * a.task_items[b];
-    const int item_end = min(a.n_items[b], item0 + a.task_items[b]);
-    const int *__restrict__ assign = a.assign;
-    const size_t S = (size_t)a.sc.S;
-    const int s_ld = min(s, a.sc.S - 1);
-    auto fetch = [=](int q) { return assign[(size_t)q * S + s_ld]; };
-    switch (b) {
-        case 0: score_records<16, 1, 20>(a.sc, a.ell[0], item0, item_end, slot, s, lane_ok, fetch); break;
-        case 1: score_records<8, 2, 12>(a.sc, a.ell[1], item0, item_end, slot, s, lane_ok, fetch); break;
-        case 2: score_records<4, 4, 8>(a.sc, a.ell[2], item0, item_end, slot, s, lane_ok, fetch); break;
-        default: score_records<2, 4, 4>(a.sc, a.ell[3], item0, item_end, slot, s, lane_ok, fetch); break;
-    }
-}
-
-// K1b: tiled rows (deg <= 16).  The plan orders pods by a DFS of the relation
-// graph (small subtrees first) and cuts the order into tiles of CP pods; ~96%
-// of a light row's neighbours share its tile (100k/5k PA tree, CP=256) and the
-// rest (a handful per tile) are appended to the tile image as extra rows.
-// Workgroup (8 waves) = (tile, chunk of SL <= 64 scenarios):
-//   phase 1  the tile's image rows (members + externals), SL scenarios each ->
-//            LDS image[row][SL] — each assign row leaves HBM once per chunk as
-//            one 256-B LDS-DMA (global_load_lds_dword) per row when SL = 64 —
-//            and the tile's owner records (one contiguous blob) -> LDS.
-//   phase 2  owner records score from LDS; only each neighbour's nodekey word
-//            comes from L2; one 256-B target store per record.
-struct TileArgs {
-    ScoreCtx sc;
-    const int *members;       // [T][RS] pod ids (pad = pod 0, never referenced)
-    const int *nrows;         // [T] image rows of each tile (<= RS)
-    const int *blob;          // per-tile record blobs, concatenated
-    const int *blob_off;      // [T][kNumLight + 1] ints: blob start + bucket starts (absolute)
-    const int *assign;
-    int SL, RS, T, blob_max;  // blob_max: largest blob (ints, multiple of 4)
-    int ablate;               // profiling only (RSK_ABLATE_TILE): 1 skip image load, 2 skip scoring
-};
-
-template <int D, int PK, int W>
-__device__ __forceinline__ void tile_bucket(const TileArgs &a, const int *img, const int *recs, int nrec, int wave,
-                                            int slot, int sl, int s, bool lane_ok) {
-    const int per = PK * a.sc.PS;
-    const int SL = a.SL;
-    auto fetch = [=](int row) { return img[row * SL + sl]; };
-    for (int g0 = wave * per; g0 < nrec; g0 += kTileWaves * per)
-        score_records<D, PK, W>(a.sc, recs, g0, min(nrec, g0 + per), slot, s, lane_ok, fetch);
-}
-
-__global__ __launch_bounds__(kTileWaves * 64) void car_tile_kernel(TileArgs a) {
-    extern __shared__ __attribute__((aligned(16))) int lds[];  // image [RS][SL] then records [blob_max]
-    const int chunk = blockIdx.x / a.T, tile = blockIdx.x % a.T;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int SL = a.SL, PS = a.sc.PS;
-    const int slot = lane / SL, sl = lane % SL;
-    const int s = chunk * SL + sl;
-    const bool lane_ok = slot < PS && s < a.sc.S;
-    const int *__restrict__ mem = a.members + (size_t)tile * a.RS;
-    const int *__restrict__ assign = a.assign;
-    const size_t S = (size_t)a.sc.S;
-    const int s_ld = min(s, a.sc.S - 1);
-    const int nr = a.nrows[tile];
-    int *img = lds;
-    int *recs = lds + a.RS * SL;
-
-    // phase 1a: owner record blob -> LDS (int4 copies, issued first: no dependency)
-    const int *bo = a.blob_off + (size_t)tile * (kNumLight + 2);
-    const int b0 = bo[0], b1 = bo[kNumLight + 1];
-    for (int i = threadIdx.x * 4; i < b1 - b0; i += kTileWaves * 64 * 4)
-        *reinterpret_cast<int4 *>(recs + i) = *reinterpret_cast<const int4 *>(a.blob + b0 + i);
-    // phase 1b: image rows
-    if (a.ablate & 1) {
-        // profiling ablation: no image load (results are wrong)
-    } else if (PS == 1) {
-        // one LDS-DMA wave instruction per row: lane l loads scenario chunk*64+l
-        // No branch between the DMAs (a per-row `if` splits basic blocks and the
-        // waitcnt pass then drains vmcnt(0) before every DMA): rows past the
-        // image's end re-load its last row into the same LDS row (same bytes).
-        // Row ids are wave-uniform: readfirstlane makes the member loads scalar
-        // (lgkmcnt), so they never share the vector-memory counter with the DMAs.
-        constexpr int kMaxRowsPerWave = (kTileCP + kTileXCap + kTileWaves - 1) / kTileWaves;
-        const int wu = __builtin_amdgcn_readfirstlane(wave);
-        int q[kMaxRowsPerWave];
-#pragma unroll
-        for (int k = 0; k < kMaxRowsPerWave; ++k) q[k] = mem[min(wu + k * kTileWaves, nr - 1)];
-#pragma unroll
-        for (int k = 0; k < kMaxRowsPerWave; ++k) {
-            const int r = min(wu + k * kTileWaves, nr - 1);
-            __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void *)(assign + (size_t)q[k] * S + s_ld),
-                (__attribute__((address_space(3))) void *)(img + r * SL), 4, 0, 0);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-        for (int r0 = wave * PS; r0 < nr; r0 += kTileWaves * PS * kTileBatch) {
-            int q[kTileBatch], v[kTileBatch];
-#pragma unroll
-            for (int k = 0; k < kTileBatch; ++k) q[k] = mem[min(r0 + k * kTileWaves * PS + slot, a.RS - 1)];
-#pragma unroll
-            for (int k = 0; k < kTileBatch; ++k) v[k] = assign[(size_t)q[k] * S + s_ld];
-#pragma unroll
-            for (int k = 0; k < kTileBatch; ++k) {
-                const int r = r0 + k * kTileWaves * PS + slot;
-                if (slot < PS && r < nr) img[r * SL + sl] = v[k];
-            }
-        }
-    }
-    __syncthreads();
-    if (a.ablate & 2) return;  // profiling ablation: no scoring (results are wrong)
-    tile_bucket<16, 1, 20>(a, img, recs + (bo[1] - b0), (bo[2] - bo[1]) / 20, wave, slot, sl, s, lane_ok);
-    tile_bucket<8, 2, 12>(a, img, recs + (bo[2] - b0), (bo[3] - bo[2]) / 12, wave, slot, sl, s, lane_ok);
-    tile_bucket<4, 4, 8>(a, img, recs + (bo[3] - b0), (bo[4] - bo[3]) / 8, wave, slot, sl, s, lane_ok);
-    tile_bucket<2, 8, 4>(a, img, recs + (bo[4] - b0), (bo[5] - bo[4]) / 4, wave, slot, sl, s, lane_ok);
-}
-
 // ---------------------------------------------------------------------------
-// K1c: mid rows (17 <= deg <= 128), one wave per (row, 64-scenario chunk),
+// K2: mid rows (17 <= deg <= 64), one wave per (row, 64-scenario chunk),
 // lane = scenario.  Each lane loads its deg node ids (coalesced 256-B rows),
 // sorts them with a bitonic network in registers (min/max only: no compare
 // masks, no memory), then scans the sorted runs once, gathering nodekey words
@@ -513,181 +827,189 @@ __device__ __forceinline__ void mid_row(const MidArgs &a, const int *__restrict_
     }
 }
 
-// kWide = false: buckets D = 32, 64; kWide = true: bucket D = 128 (its own
-// launch, so the 256-VGPR D=128 body does not lower the occupancy of the others)
-template <bool kWide>
 __global__ __launch_bounds__(256) void car_mid_kernel(MidArgs a) {
     const int chunk = blockIdx.x / a.blocks_per_chunk;
     const int wave = (blockIdx.x % a.blocks_per_chunk) * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int b_lo = kWide ? 2 : 0, b_hi = kWide ? 3 : 2;
-    if (wave >= a.prefix[b_hi] - a.prefix[b_lo]) return;
+    if (wave >= a.prefix[kNumMid]) return;
     // a wave scores PS rows of one bucket, lanes split into PS slots of SL scenarios
     const int slot = lane / a.SL;
     const int s = chunk * a.SL + lane % a.SL;
-    int b = b_lo;
-    while (wave >= a.prefix[b + 1] - a.prefix[b_lo]) ++b;
-    const int item = (wave - (a.prefix[b] - a.prefix[b_lo])) * a.sc.PS + slot;
+    const int b = wave >= a.prefix[1] ? 1 : 0;
+    const int item = (wave - a.prefix[b]) * a.sc.PS + slot;
     const bool lane_ok = slot < a.sc.PS && s < a.sc.S && item < a.n_items[b];
     const int it = min(item, a.n_items[b] - 1);
-    if (kWide) {
-        mid_row<128, 132>(a, a.rec[2] + (size_t)it * 132, slot, s, lane_ok);
-    } else if (b == 0) {
-        mid_row<32, 36>(a, a.rec[0] + (size_t)it * 36, slot, s, lane_ok);
-    } else {
-        mid_row<64, 68>(a, a.rec[1] + (size_t)it * 68, slot, s, lane_ok);
-    }
+    if (b == 0) mid_row<32, 36>(a, a.rec[0] + (size_t)it * 36, slot, s, lane_ok);
+    else mid_row<64, 68>(a, a.rec[1] + (size_t)it * 68, slot, s, lane_ok);
 }
 
 // ---------------------------------------------------------------------------
-// K2: heavy rows (deg > 128).  Workgroup = (row, group of G scenarios).
-//   phase 0  stage node ids ntile[si][j] (G-scenario row segments per neighbour)
-//   phase A  wave w < NT hashes scenario si's d node ids into its LDS table
-//   phase B  counts back into ctile[si][j]; table cleared for the next scenario
-//   phase C  thread -> (si = tid % G, j = tid / G + k*256/G): nodekey gathers are
-//            G consecutive scenarios of one node (coalesced), then a shuffle /
-//            LDS reduction of CarState per scenario.
+// K3: hub rows (deg > 64).  Workgroup (4 waves) = (row, group of G scenarios).
+//   stage  col[si][j] = {node, key} of neighbour j in scenario s0+si: each
+//          neighbour row's G consecutive scenarios in one coalesced segment, its
+//          node keys gathered right away (hazard / unscheduled -> KEY_HAZ);
+//   score  wave w takes scenarios si = w, w+4, ...; lanes = neighbours:
+//          A count every candidate entry into the wave's own LDS table
+//          B max count M (wave max)
+//          C best (remaining CPU, -node) among the entries with count M, and
+//            their number nm = M * |best| (wave reductions)
+//          D clear the table for the next scenario.
+// Tables: two u16 counters per word indexed by node id when N <= 16384, else
+// an open-addressing hash (keys + counts) of next_pow2(2 * deg) slots.
 // ---------------------------------------------------------------------------
 struct HeavyItem {
     int oi, rb, d, pad;
 };
 
-__device__ __forceinline__ int hash_insert(unsigned *keys, unsigned *cnts, unsigned mask, int n) {
-    const unsigned k = (unsigned)n + 1u;
-    unsigned h = (k * 2654435761u) & mask;
-    while (true) {
-        const unsigned prev = atomicCAS(&keys[h], 0u, k);
-        if (prev == 0u || prev == k) {
-            atomicAdd(&cnts[h], 1u);
-            return (int)h;
-        }
-        h = (h + 1u) & mask;
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long w = __shfl_xor(v, o, 64);
+        v = w > v ? w : v;
     }
+    return v;
+}
+
+// (remaining CPU, -node) as one u64, 0 = none (node < 2^25)
+__device__ __forceinline__ unsigned long long pack_rn(int rem, int n) {
+    return ((unsigned long long)((unsigned)rem ^ 0x80000000u) << kNodeBits) | (unsigned long long)(kNodeMask - (unsigned)n);
 }
 
 template <bool kDirect>
-__global__ __launch_bounds__(256) void car_heavy_kernel(const HeavyItem *__restrict__ items, int n_items,
-                                                        const int *__restrict__ hcol,
-                                                        const int *__restrict__ assign,
-                                                        const int *__restrict__ nodekey, int S, int N, int G,
-                                                        int dpad, int H, int NT, const int *__restrict__ zc_cnt,
-                                                        const unsigned long long *__restrict__ zc_key,
-                                                        int *__restrict__ out_target, int *__restrict__ out_score) {
+struct HubTable {
+    unsigned *keys, *cnts;  // direct: cnts only (2 x u16 per word); hash: keys[H] + cnts[H]
+    unsigned mask;
+    __device__ __forceinline__ unsigned slot(int n) const {  // hash: the slot holding n (inserted)
+        const unsigned k = (unsigned)n + 1u;
+        unsigned h = (k * 2654435761u) & mask;
+        while (keys[h] != k) h = (h + 1u) & mask;
+        return h;
+    }
+    __device__ __forceinline__ void add(int n) const {
+        if (kDirect) {
+            atomicAdd(&cnts[n >> 1], 1u << ((n & 1) << 4));
+        } else {
+            const unsigned k = (unsigned)n + 1u;
+            unsigned h = (k * 2654435761u) & mask;
+            while (true) {
+                const unsigned prev = atomicCAS(&keys[h], 0u, k);
+                if (prev == 0u || prev == k) break;
+                h = (h + 1u) & mask;
+            }
+            atomicAdd(&cnts[h], 1u);
+        }
+    }
+    __device__ __forceinline__ int get(int n) const {
+        if (kDirect) return (int)((cnts[n >> 1] >> ((n & 1) << 4)) & 0xffffu);
+        return (int)cnts[slot(n)];
+    }
+    __device__ __forceinline__ void clear(int n) const { cnts[n >> 1] = 0u; }  // direct tables only
+};
+
+template <bool kDirect>
+__global__ __launch_bounds__(256) void car_hub_kernel(const HeavyItem *__restrict__ items, int n_items,
+                                                      const int *__restrict__ hcol, const int *__restrict__ assign,
+                                                      const int *__restrict__ nodekey, int S, int N, int lg, int dpad,
+                                                      int H, const int *__restrict__ zc_cnt,
+                                                      const unsigned long long *__restrict__ zc_key,
+                                                      int *__restrict__ out_target, int *__restrict__ out_score) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
-    const int g = blockIdx.x / n_items;
+    const int G = 1 << lg;
+    const int grp = blockIdx.x / n_items;
     const HeavyItem it = items[blockIdx.x % n_items];
-    const int s0 = g * G;
+    const int s0 = grp * G;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // kDirect: per-wave count table over node ids, two u16 counters per word
-    // (H = ceil(N/2) words); otherwise an open-addressing hash of H slots.
-    int *ntile = lds;                                       // [G][dpad]
-    int *ctile = ntile + G * dpad;                          // [G][dpad]
-    unsigned *tkey = reinterpret_cast<unsigned *>(ctile + G * dpad);  // [NT][H] (hash only)
-    unsigned *tcnt = kDirect ? tkey : tkey + NT * H;        // [NT][H]
-    CarState *red = reinterpret_cast<CarState *>(tcnt + NT * H);      // [4][G]
-
+    int2 *col = reinterpret_cast<int2 *>(lds);                       // [G][dpad]
+    unsigned *tabs = reinterpret_cast<unsigned *>(col + G * dpad);   // [4][H] (x2 for the hash)
     const int d = it.d;
-    // stage: G consecutive scenarios of each neighbour row; loads unconditional
-    // (clamped) and batched so they are all in flight before the LDS writes
-    constexpr int kB = 4;
-    for (int idx0 = tid; idx0 < d * G; idx0 += 256 * kB) {
-        int v[kB];
+    const int total = d << lg;
+    // stage: element e -> (neighbour j = e >> lg, scenario si = e & (G-1)); loads
+    // unconditional (clamped), duplicates rewrite identical values
+    constexpr int kB = 8;
+    for (int e0 = 0; e0 < total; e0 += 256 * kB) {
+        int e[kB], q[kB], n[kB];
 #pragma unroll
-        for (int k = 0; k < kB; ++k) {
-            const int idx = min(idx0 + k * 256, d * G - 1);
-            const int j = idx / G, si = idx - j * G;
-            v[k] = assign[(size_t)hcol[it.rb + j] * S + min(s0 + si, S - 1)];
+        for (int u = 0; u < kB; ++u) {
+            e[u] = min(e0 + u * 256 + tid, total - 1);
+            q[u] = hcol[it.rb + (e[u] >> lg)];
         }
 #pragma unroll
-        for (int k = 0; k < kB; ++k) {
-            const int idx = idx0 + k * 256;
-            if (idx < d * G) {
-                const int j = idx / G, si = idx - j * G;
-                ntile[si * dpad + j] = (s0 + si < S && (unsigned)v[k] < (unsigned)N) ? v[k] : -1;
-            }
+        for (int u = 0; u < kB; ++u) n[u] = assign[(size_t)q[u] * S + min(s0 + (e[u] & (G - 1)), S - 1)];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            const int si = e[u] & (G - 1), s = s0 + si;
+            const bool ok = (unsigned)n[u] < (unsigned)N && s < S;
+            const int key = ld32(nodekey, ok ? (unsigned)n[u] * (unsigned)S + (unsigned)s : 0u);
+            col[si * dpad + (e[u] >> lg)] = make_int2(n[u], ok ? key : kKeyHaz);
         }
     }
-    for (int k = tid; k < NT * H; k += 256) { tkey[k] = 0u; tcnt[k] = 0u; }
+    const int Hw = kDirect ? H : 2 * H;  // words per wave table
+    for (int k = tid; k < 4 * Hw; k += 256) tabs[k] = 0u;
     __syncthreads();
-
-    if (kDirect && wave < NT) {
-        unsigned *cnts = tcnt + wave * H;
-        for (int si = wave; si < G; si += NT) {
-            const int *nrow = ntile + si * dpad;
-            int *crow = ctile + si * dpad;
-            for (int j = lane; j < d; j += 64) {
-                const int n = nrow[j];
-                if (n >= 0) atomicAdd(&cnts[n >> 1], 1u << ((n & 1) << 4));
-            }
-            __builtin_amdgcn_wave_barrier();
-            for (int j = lane; j < d; j += 64) {
-                const int n = nrow[j];
-                crow[j] = n >= 0 ? (int)((cnts[n >> 1] >> ((n & 1) << 4)) & 0xffffu) : 0;
-            }
-            __builtin_amdgcn_wave_barrier();
-            for (int j = lane; j < d; j += 64) {
-                const int n = nrow[j];
-                if (n >= 0) cnts[n >> 1] = 0u;
-            }
-            __builtin_amdgcn_wave_barrier();
+    HubTable<kDirect> tb;
+    tb.cnts = tabs + wave * Hw + (kDirect ? 0 : H);
+    tb.keys = tabs + wave * Hw;
+    tb.mask = (unsigned)H - 1u;
+    for (int si = wave; si < G && s0 + si < S; si += 4) {
+        const int2 *c = col + si * dpad;
+        for (int j = lane; j < d; j += 64) {
+            const int2 x = c[j];
+            if (x.y != kKeyHaz) tb.add(x.x);
         }
-    } else if (!kDirect && wave < NT) {
-        unsigned *keys = tkey + wave * H, *cnts = tcnt + wave * H;
-        const unsigned mask = (unsigned)H - 1u;
-        for (int si = wave; si < G; si += NT) {
-            int *nrow = ntile + si * dpad, *crow = ctile + si * dpad;
-            for (int j = lane; j < d; j += 64) {
-                const int n = nrow[j];
-                crow[j] = n >= 0 ? hash_insert(keys, cnts, mask, n) : -1;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            for (int j = lane; j < d; j += 64) {
-                const int slot = crow[j];
-                crow[j] = slot >= 0 ? (int)cnts[slot] : 0;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            for (int k = lane; k < H; k += 64) { keys[k] = 0u; cnts[k] = 0u; }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        int M = 0;
+        for (int j = lane; j < d; j += 64) {
+            const int2 x = c[j];
+            if (x.y != kKeyHaz) M = max(M, tb.get(x.x));
         }
-    }
-    __syncthreads();
-
-    const int si = tid % G, jstep = 256 / G;
-    const int s = s0 + si;
-    CarState st;
-    st_init(st);
-    {
-        // batches of kC independent gathers (a load-then-use loop body would
-        // serialise one L2 round trip per neighbour)
-        constexpr int kC = 8;
-        const int *nrow = ntile + si * dpad, *crow = ctile + si * dpad;
-        const unsigned s_ld = (unsigned)min(s, S - 1);
-        for (int j0 = tid / G; j0 < d; j0 += jstep * kC) {
-            int n[kC], key[kC];
-#pragma unroll
-            for (int k = 0; k < kC; ++k) {
-                const int j = min(j0 + k * jstep, d - 1);
-                n[k] = nrow[j];
-                key[k] = ld32(nodekey, (unsigned)max(n[k], 0) * (unsigned)S + s_ld);
-            }
-#pragma unroll
-            for (int k = 0; k < kC; ++k) {
-                const int j = j0 + k * jstep;
-                if (j < d && s < S && n[k] >= 0 && key[k] != kKeyHaz) st_add(st, crow[j], key[k], n[k]);
+        M = wave_max_i(M);
+        unsigned long long best = 0;
+        int nm = 0;
+        for (int j = lane; j < d && M > 0; j += 64) {
+            const int2 x = c[j];
+            if (x.y != kKeyHaz && tb.get(x.x) == M) {
+                ++nm;
+                const unsigned long long k = pack_rn(x.y, x.x);
+                best = k > best ? k : best;
             }
         }
-    }
-    for (int off = G; off < 64; off <<= 1) st = st_combine(st, st_shfl_xor(st, off));
-    if (lane < G) red[wave * G + lane] = st;
-    __syncthreads();
-    if (tid < G && s < S) {
-        CarState r = red[tid];
-        for (int w = 1; w < 4; ++w) r = st_combine(r, red[w * G + tid]);
-        int sc;
-        const int t = car_finalize(r, load_zc(zc_cnt, zc_key, s), sc);
-        const size_t o = (size_t)it.oi * S + s;
-        out_target[o] = t;
-        if (out_score) out_score[o] = sc;
+        best = wave_max_u64(best);
+        nm = wave_sum_i(nm);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        if (kDirect) {
+            for (int j = lane; j < d; j += 64) {
+                const int2 x = c[j];
+                if (x.y != kKeyHaz) tb.clear(x.x);
+            }
+        } else {  // a probe may still need a slot another lane cleared: wipe the whole table
+            for (int k = lane; k < Hw; k += 64) tb.keys[k] = 0u;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        if (lane == 0) {
+            const int s = s0 + si;
+            int sc, t;
+            if (M == 0) {
+                t = zero_target(load_zc(zc_cnt, zc_key, s), sc);
+            } else {
+                sc = M;
+                const int rem = (int)((unsigned)(best >> kNodeBits) ^ 0x80000000u);
+                const int bn = (int)(kNodeMask - (unsigned)(best & kNodeMask));
+                t = nm == M ? bn : (rem >= 0 ? bn : RSK_TARGET_NONE);
+            }
+            const size_t o = (size_t)it.oi * S + s;
+            out_target[o] = t;
+            if (out_score) out_score[o] = sc;
+        }
     }
 }
 
@@ -698,14 +1020,13 @@ using namespace rsk;
 struct rsk_car_plan {
     rsk_ctx *ctx = nullptr;
     int P = 0, Q = 0, max_deg = 0;
-    // tiled rows (deg <= 16 in dense tiles)
-    int CP = kTileCP, RS = kTileCP, T = 0, n_tile_owners = 0, blob_max = 0;
-    DevBuf members, nrows, blob, blob_off;
-    // direct rows (deg <= 16 in sparse tiles)
-    int n_light[kNumLight] = {0, 0, 0, 0};
-    DevBuf ell[kNumLight];
+    // light rows (deg <= 16) in LDS tiles
+    int T = 0, rmax = 0, recmax = 0, n_tile_rows = 0;
+    int owners_cap = 128, rows_cap = 160;  // tile limits (RSK_TILE_OWNERS / RSK_TILE_ROWS)
+    int64_t img_rows_total = 0, img_pods_distinct = 0, n_img_pods = 0, n_recs = 0;
+    DevBuf img_pods, meta, recs;
     // mid rows (17..64)
-    int n_mid[kNumMid] = {0, 0, 0};
+    int n_mid[kNumMid] = {0, 0};
     DevBuf mid[kNumMid];
     // heavy rows (> 64)
     int n_heavy[kNumHeavy] = {0, 0, 0};
@@ -715,11 +1036,9 @@ struct rsk_car_plan {
     // per-execute workspace
     DevBuf nodekey, zc;
     ~rsk_car_plan() {
-        members.release();
-        nrows.release();
-        blob.release();
-        blob_off.release();
-        for (auto &b : ell) b.release();
+        img_pods.release();
+        meta.release();
+        recs.release();
         for (auto &b : mid) b.release();
         for (auto &b : heavy_items) b.release();
         hcol.release();
@@ -729,14 +1048,6 @@ struct rsk_car_plan {
 };
 
 namespace {
-
-int light_bucket(int d) {
-    if (d <= 2) return 3;
-    if (d <= 4) return 2;
-    if (d <= 8) return 1;
-    return 0;
-}
-
 
 int heavy_class(int d) {
     for (int c = 0; c < kNumHeavy; ++c)
@@ -751,7 +1062,7 @@ int next_pow2(int x) {
 }
 
 struct HeavyGeom {
-    int G, dpad, H, NT;
+    int lg, dpad, H;
     bool direct;
     size_t lds;
 };
@@ -759,26 +1070,21 @@ struct HeavyGeom {
 constexpr int kDirectMaxN = 16384;  // direct count tables up to 32 KiB per wave
 
 HeavyGeom heavy_geometry(int dmax, int S, int N) {
-    // Largest scenario group G (<= 64, <= S rounded up to a power of two) and
-    // hash-table count NT that fit 64 KiB of LDS (2 workgroups per CU); failing
-    // that, anything up to the 160 KiB a single workgroup may declare.
+    // Largest scenario group G = 2^lg (<= 64, <= next_pow2(S)) whose staged
+    // columns + 4 wave tables fit 80 KiB (2 workgroups per CU), else 160 KiB.
     HeavyGeom g;
-    g.dpad = dmax | 1;  // odd row pitch: scenario rows start on different banks
+    g.dpad = dmax | 1;
     g.direct = N <= kDirectMaxN;
     g.H = g.direct ? (N + 1) / 2 : next_pow2(2 * dmax);
-    const size_t slot_bytes = g.direct ? 4 : 8;
+    const size_t tab = (size_t)4 * (g.direct ? g.H : 2 * g.H) * 4;
     const int gmax = std::min(64, next_pow2(S));
-    const size_t limits[2] = {64 * 1024, 160 * 1024};
-    for (size_t lim : limits)
-        for (g.G = gmax; g.G >= 1; g.G >>= 1)
-            for (g.NT = 4; g.NT >= 1; g.NT >>= 1) {
-                g.lds = (size_t)2 * g.G * g.dpad * 4 + (size_t)g.NT * g.H * slot_bytes +
-                        (size_t)4 * g.G * sizeof(CarState);
-                if (g.lds <= lim) return g;
-            }
-    g.G = 1;
-    g.NT = 1;
-    g.lds = (size_t)2 * g.dpad * 4 + (size_t)g.H * slot_bytes + 4 * sizeof(CarState);
+    for (size_t lim : {(size_t)80 * 1024, (size_t)160 * 1024})
+        for (int G = gmax; G >= 1; G >>= 1) {
+            g.lds = (size_t)G * g.dpad * 8 + tab;
+            g.lg = 0;
+            while ((1 << g.lg) < G) ++g.lg;
+            if (g.lds <= lim) return g;
+        }
     return g;
 }
 
@@ -848,6 +1154,93 @@ int upload(DevBuf &buf, const void *src, size_t bytes) {
     return RSK_OK;
 }
 
+int light_class(int d) {  // d = 0 rows go to the generic class: all entries masked -> zero case
+    if (d == 1) return 0;
+    if (d == 2) return 1;
+    if (d <= 4) return 2;
+    if (d <= 8) return 3;
+    return 4;
+}
+
+// Light-row tiles: rows in DFS order are packed greedily into tiles of at most
+// kTileOwners rows whose distinct neighbours (the image rows) number at most
+// kTileRows.  On a relation tree in DFS order a tile's image is essentially its
+// own 128 pods plus ~5 external neighbours.
+struct TileBuilder {
+    std::vector<int> img_pods, meta, recs;
+    std::vector<int> cur_pods;
+    std::unordered_map<int, int> cur_slot;
+    std::vector<int> cur_rec[kNumCls];
+    int cur_rows = 0, T = 0, rmax = 0, recmax = 0;
+    int owners_cap = kTileOwners, rows_cap = kTileRows;
+    int64_t img_total = 0;
+
+    bool fits(const int *nb, int d) const {
+        if (cur_rows >= owners_cap) return false;
+        int fresh = 0;
+        for (int j = 0; j < d; ++j) {
+            if (cur_slot.count(nb[j])) continue;
+            bool dup = false;
+            for (int i = 0; i < j; ++i) dup |= nb[i] == nb[j];
+            fresh += !dup;
+        }
+        return (int)cur_pods.size() + fresh <= rows_cap;
+    }
+    void add(int oi, const int *nb, int d) {
+        int lr[kLightMax];
+        for (int j = 0; j < d; ++j) {
+            auto it = cur_slot.find(nb[j]);
+            if (it == cur_slot.end()) {
+                it = cur_slot.emplace(nb[j], (int)cur_pods.size()).first;
+                cur_pods.push_back(nb[j]);
+            }
+            lr[j] = it->second;
+        }
+        const int c = light_class(d);
+        auto &e = cur_rec[c];
+        const size_t o = e.size();
+        e.resize(o + kClsW[c], 0);
+        e[o] = oi;
+        if (c == 0) {
+            e[o + 1] = lr[0];
+        } else if (c == 1) {
+            e[o + 1] = lr[0] | (lr[1] << 16);
+        } else {
+            e[o + 1] = d;
+            for (int j = 0; j < d; ++j) e[o + 2 + j / 2] |= lr[j] << ((j & 1) * 16);
+        }
+        ++cur_rows;
+    }
+    void close() {
+        if (!cur_rows) return;
+        // every tile stages >= 1 image row (a tile of deg-0 rows stages pod 0,
+        // which no record reads): the loaders never see an empty image
+        if (cur_pods.empty()) cur_pods.push_back(0);
+        const int rec_off = (int)recs.size();
+        int n[kNumCls], off[kNumCls];
+        for (int c = 0; c < kNumCls; ++c) {
+            if (c == 2) while ((recs.size() - rec_off) % 4) recs.push_back(0);  // int4 records from here on
+            off[c] = (int)recs.size() - rec_off;
+            n[c] = (int)cur_rec[c].size() / kClsW[c];
+            recs.insert(recs.end(), cur_rec[c].begin(), cur_rec[c].end());
+            cur_rec[c].clear();
+        }
+        while ((recs.size() - rec_off) % 4) recs.push_back(0);
+        const int rec_ints = (int)recs.size() - rec_off;
+        const int m[kMetaW] = {(int)img_pods.size(), (int)cur_pods.size(), rec_off, rec_ints,
+                               n[0], n[1], n[2], n[3], n[4], off[2], off[3], off[4]};
+        meta.insert(meta.end(), m, m + kMetaW);
+        img_pods.insert(img_pods.end(), cur_pods.begin(), cur_pods.end());
+        img_total += (int64_t)cur_pods.size();
+        rmax = std::max(rmax, (int)cur_pods.size());
+        recmax = std::max(recmax, rec_ints);
+        ++T;
+        cur_pods.clear();
+        cur_slot.clear();
+        cur_rows = 0;
+    }
+};
+
 int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_idx, int32_t P, const int32_t *rows,
                int32_t Q) {
     // deduplicated adjacency without self edges (the evicted pod is off the cluster)
@@ -862,79 +1255,24 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
         ci.insert(ci.end(), nb.begin(), nb.end());
         rp[p + 1] = (int)ci.size();
     }
-    const int CP = plan->CP;
     const std::vector<int> order = locality_order(P, rp, ci);
     std::vector<int> pos(P);
     for (int k = 0; k < P; ++k) pos[order[k]] = k;
-    const int ntiles = (P + CP - 1) / CP;
 
-    // owners per tile (rows with deg <= kLightMax)
-    std::vector<int> owners_in(ntiles, 0);
+    std::vector<int> light;  // row indices i with deg <= 16, to be tiled in DFS order
+    std::vector<std::vector<int>> midr(kNumMid);
+    std::vector<std::vector<HeavyItem>> hitems(kNumHeavy);
+    std::vector<int> hcol;
     for (int i = 0; i < Q; ++i) {
         const int p = rows ? rows[i] : i;
         const int d = rp[p + 1] - rp[p];
         plan->max_deg = std::max(plan->max_deg, d);
-        if (d <= kLightMax) ++owners_in[pos[p] / CP];
-    }
-    RSK_CHECK(plan->max_deg <= kMaxDegree, "a row has degree %d > %d (unsupported)", plan->max_deg, kMaxDegree);
-    const int min_owners = std::max(1, CP / 16);  // sparser tiles use the direct path
-    std::vector<int> tile_id(ntiles, -1);
-    int T = 0;
-    for (int t = 0; t < ntiles; ++t)
-        if (owners_in[t] >= min_owners) tile_id[t] = T++;
-
-    std::vector<std::vector<std::vector<int>>> trec(kNumLight, std::vector<std::vector<int>>(T));
-    std::vector<std::vector<int>> ext_rows(T);             // external pods appended to each tile image
-    std::vector<std::unordered_map<int, int>> ext_slot(T);  // pod -> image row
-    std::vector<std::vector<int>> ell(kNumLight), midr(kNumMid);
-    std::vector<std::vector<HeavyItem>> hitems(kNumHeavy);
-    std::vector<int> hcol;
-    std::vector<int> fresh;
-    for (int i = 0; i < Q; ++i) {
-        const int p = rows ? rows[i] : i;
-        const int d = rp[p + 1] - rp[p];
+        RSK_CHECK(d <= kMaxDegree, "a row has degree %d > %d (unsupported)", d, kMaxDegree);
         const int *nbp = ci.data() + rp[p];
-        const int tile = pos[p] / CP;
-        const int tid = tile_id[tile];
-        bool tiled = d <= kLightMax && tid >= 0;
-        if (tiled) {  // externals of this row must fit the tile image
-            fresh.clear();
-            for (int j = 0; j < d; ++j) {
-                const int q = nbp[j];
-                if (pos[q] / CP != tile && !ext_slot[tid].count(q) &&
-                    std::find(fresh.begin(), fresh.end(), q) == fresh.end())
-                    fresh.push_back(q);
-            }
-            tiled = (int)(ext_rows[tid].size() + fresh.size()) <= kTileXCap;
-            if (tiled)
-                for (int q : fresh) {
-                    ext_slot[tid][q] = CP + (int)ext_rows[tid].size();
-                    ext_rows[tid].push_back(q);
-                }
-        }
-        if (tiled) {
-            const int b = light_bucket(d);
-            auto &e = trec[b][tid];
-            const size_t o = e.size();
-            e.resize(o + kLightW[b], 0);
-            e[o] = i;
-            e[o + 1] = d;
-            for (int j = 0; j < d; ++j) {
-                const int q = nbp[j];
-                e[o + 2 + j] = pos[q] / CP == tile ? pos[q] % CP : ext_slot[tid][q];
-            }
-            plan->n_tile_owners += 1;
-        } else if (d <= kLightMax) {
-            const int b = light_bucket(d);
-            auto &e = ell[b];
-            const size_t o = e.size();
-            e.resize(o + kLightW[b], 0);
-            e[o] = i;
-            e[o + 1] = d;
-            for (int j = 0; j < d; ++j) e[o + 2 + j] = nbp[j];
-            plan->n_light[b] += 1;
+        if (d <= kLightMax) {
+            light.push_back(i);
         } else if (d <= kMidMax) {
-            const int b = d <= 32 ? 0 : (d <= 64 ? 1 : 2);
+            const int b = d <= 32 ? 0 : 1;
             auto &e = midr[b];
             const size_t o = e.size();
             e.resize(o + kMidW[b], 0);
@@ -950,44 +1288,48 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
             plan->heavy_dmax[c] = std::max(plan->heavy_dmax[c], d);
         }
     }
-    plan->T = T;
-    if (T > 0) {
-        size_t xm = 0;
-        for (auto &e : ext_rows) xm = std::max(xm, e.size());
-        const int RS = CP + (int)((xm + 7) / 8 * 8);
-        plan->RS = RS;
-        std::vector<int> mem((size_t)T * RS, 0), nr(T, 0);
-        for (int t = 0; t < ntiles; ++t) {
-            const int id = tile_id[t];
-            if (id < 0) continue;
-            for (int k = 0; k < CP && t * CP + k < P; ++k) mem[(size_t)id * RS + k] = order[t * CP + k];
-            for (size_t x = 0; x < ext_rows[id].size(); ++x) mem[(size_t)id * RS + CP + x] = ext_rows[id][x];
-            nr[id] = CP + (int)ext_rows[id].size();  // short last tile: rows past its members are never read
-        }
-        RSK_TRY(upload(plan->members, mem.data(), mem.size() * 4));
-        RSK_TRY(upload(plan->nrows, nr.data(), nr.size() * 4));
-        // per-tile record blob: buckets D = 16, 8, 4, 2 back to back, padded to 4 ints
-        std::vector<int> blob, boff((size_t)T * (kNumLight + 2));
-        for (int t = 0; t < T; ++t) {
-            int *bo = boff.data() + (size_t)t * (kNumLight + 2);
-            bo[0] = (int)blob.size();
-            for (int b = 0; b < kNumLight; ++b) {
-                bo[1 + b] = (int)blob.size();
-                blob.insert(blob.end(), trec[b][t].begin(), trec[b][t].end());
-            }
-            bo[kNumLight + 1] = (int)blob.size();
-            plan->blob_max = std::max(plan->blob_max, bo[kNumLight + 1] - bo[0]);
-        }
-        if (blob.empty()) blob.assign(4, 0);
-        RSK_TRY(upload(plan->blob, blob.data(), blob.size() * 4));
-        RSK_TRY(upload(plan->blob_off, boff.data(), boff.size() * 4));
+    std::stable_sort(light.begin(), light.end(), [&](int x, int y) {
+        return pos[rows ? rows[x] : x] < pos[rows ? rows[y] : y];
+    });
+    TileBuilder tb;
+    tb.owners_cap = plan->owners_cap;
+    tb.rows_cap = plan->rows_cap;
+    for (int i : light) {
+        const int p = rows ? rows[i] : i;
+        const int d = rp[p + 1] - rp[p];
+        const int *nbp = ci.data() + rp[p];
+        if (!tb.fits(nbp, d)) tb.close();
+        tb.add(i, nbp, d);
+    }
+    tb.close();
+    plan->T = tb.T;
+    plan->rmax = std::max(1, tb.rmax);
+    plan->recmax = tb.recmax;
+    plan->n_tile_rows = (int)light.size();
+    plan->img_rows_total = tb.img_total;
+    {
+        std::vector<char> seen(P, 0);
+        for (int q : tb.img_pods) seen[q] = 1;
+        plan->img_pods_distinct = std::count(seen.begin(), seen.end(), 1);
+    }
+    plan->n_img_pods = (int64_t)tb.img_pods.size();
+    plan->n_recs = std::max<int64_t>(4, (int64_t)tb.recs.size());
+    if (tb.T > 0) {
+        RSK_TRY(upload(plan->img_pods, tb.img_pods.data(), tb.img_pods.size() * 4));
+        RSK_TRY(upload(plan->meta, tb.meta.data(), tb.meta.size() * 4));
+        if (tb.recs.empty()) tb.recs.assign(4, 0);
+        RSK_TRY(upload(plan->recs, tb.recs.data(), tb.recs.size() * 4));
     }
     for (int b = 0; b < kNumMid; ++b) RSK_TRY(upload(plan->mid[b], midr[b].data(), midr[b].size() * 4));
-    for (int b = 0; b < kNumLight; ++b) RSK_TRY(upload(plan->ell[b], ell[b].data(), ell[b].size() * 4));
     for (int c = 0; c < kNumHeavy; ++c)
         RSK_TRY(upload(plan->heavy_items[c], hitems[c].data(), hitems[c].size() * sizeof(HeavyItem)));
     RSK_TRY(upload(plan->hcol, hcol.data(), hcol.size() * 4));
     return RSK_OK;
+}
+
+int env_int(const char *name, int dflt) {
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
 }
 
 }  // namespace
@@ -1013,6 +1355,8 @@ int rsk_car_plan_create(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col
         for (int32_t i = 0; i < Q; ++i) RSK_CHECK(rows[i] >= 0 && rows[i] < P, "rows[%d]=%d out of range", i, rows[i]);
     auto plan = new rsk_car_plan();
     plan->ctx = ctx;
+    plan->owners_cap = std::min(kTileOwners, std::max(8, env_int("RSK_TILE_OWNERS", 128)));
+    plan->rows_cap = std::min(kTileRows, std::max(kLightMax, env_int("RSK_TILE_ROWS", plan->owners_cap + 32)));
     plan->P = P;
     plan->Q = Q;
     const int rc = build_plan(plan, row_ptr, col_idx, P, rows, Q);
@@ -1028,12 +1372,8 @@ int rsk_car_plan_create(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col
 
 int rsk_car_plan_info(const rsk_car_plan *plan, int64_t *out, int n) {
     RSK_CHECK(plan && out && n >= 0, "bad arguments");
-    int64_t light = 0, mid = 0, heavy = 0, tile_bytes = 0, ell_bytes = 0, mid_bytes = 0;
+    int64_t mid = 0, heavy = 0, mid_bytes = 0;
     int64_t heavy_bytes = (int64_t)plan->hcol.bytes;
-    for (int b = 0; b < kNumLight; ++b) {
-        light += plan->n_light[b];
-        ell_bytes += (int64_t)plan->n_light[b] * kLightW[b] * 4;
-    }
     for (int b = 0; b < kNumMid; ++b) {
         mid += plan->n_mid[b];
         mid_bytes += (int64_t)plan->n_mid[b] * kMidW[b] * 4;
@@ -1042,12 +1382,11 @@ int rsk_car_plan_info(const rsk_car_plan *plan, int64_t *out, int n) {
         heavy += plan->n_heavy[c];
         heavy_bytes += (int64_t)plan->n_heavy[c] * (int64_t)sizeof(HeavyItem);
     }
-    if (plan->T > 0)
-        tile_bytes = (int64_t)plan->T * plan->RS * 4 + (int64_t)plan->T * 4 * (kNumLight + 3) +
-                     (int64_t)plan->blob.bytes;
-    const int64_t v[12] = {plan->n_tile_owners, light, mid, heavy, plan->T, plan->RS, plan->CP,
-                           tile_bytes, ell_bytes, mid_bytes, heavy_bytes, plan->max_deg};
-    const int m = n < 12 ? n : 12;
+    const int64_t tile_bytes = plan->T > 0 ? (int64_t)(plan->img_pods.bytes + plan->meta.bytes + plan->recs.bytes) : 0;
+    const int64_t v[14] = {plan->n_tile_rows, 0, mid, heavy, plan->T, plan->rmax, plan->owners_cap,
+                           tile_bytes, 0, mid_bytes, heavy_bytes, plan->max_deg, plan->img_rows_total,
+                           plan->img_pods_distinct};
+    const int m = n < 14 ? n : 14;
     for (int i = 0; i < m; ++i) out[i] = v[i];
     return m;
 }
@@ -1100,6 +1439,81 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
             d_cap, d_use, d_haz, N, S, npb, total, d_key, d_zcnt, d_zkey);
         RSK_HIP(hipGetLastError());
     }
+    if (plan->T > 0) {   // K1 light-row tiles
+        TileArgs a;
+        std::memset(&a, 0, sizeof(a));
+        a.img_pods = plan->img_pods.as<int>();
+        a.meta = plan->meta.as<int>();
+        a.recs = plan->recs.as<int>();
+        a.assign = d_assign;
+        a.nodekey = d_key;
+        a.zc_cnt = d_zcnt;
+        a.zc_key = d_zkey;
+        a.out_target = d_target;
+        a.out_score = d_score;
+        a.S = S;
+        a.N = N;
+        a.T = plan->T;
+        a.rmax = plan->rmax;
+        a.n_assign = (unsigned)std::min<size_t>(PS_, UINT32_MAX);
+        a.n_out = (unsigned)std::min<size_t>(QS, UINT32_MAX);
+        a.n_pods = (unsigned)plan->n_img_pods;
+        a.n_recs = (unsigned)plan->n_recs;
+        a.n_key = (unsigned)NS;
+        a.n_meta = (unsigned)plan->T * kMetaW;
+        static const int sl_max = [] { int v = env_int("RSK_TILE_SL", 32); return v >= 1 && v <= 64 ? v : 32; }();
+        int SL = std::min(next_pow2(S), next_pow2(sl_max));
+        a.lsl = 0;
+        while ((1 << a.lsl) < SL) ++a.lsl;
+        static const int ablate = env_int("RSK_ABLATE_TILE", 0);
+        static const int order = env_int("RSK_TILE_ORDER", 0);
+        a.order = order;
+        a.ablate = ablate;
+        const bool vec = SL >= 4 && S % 4 == 0;
+        const bool off32 = (int64_t)std::max(plan->P, plan->Q) * S * 4 < ((int64_t)1 << 32);
+        const size_t lds = ((((size_t)2 * plan->rmax * SL + 3) & ~(size_t)3) + plan->recmax) * 4;
+        RSK_CHECK(lds <= 160 * 1024, "tile image needs %zu B of LDS", lds);
+        const int64_t blocks = ceil_div(S, SL) * plan->T;
+        RSK_CHECK(blocks < INT32_MAX, "tile grid too large");
+        using TileKern = void (*)(TileArgs);
+#define RSK_TK(NT) {&car_tile_kernel<false, false, false, NT>, &car_tile_kernel<false, false, true, NT>, \
+                    &car_tile_kernel<false, true, false, NT>,  &car_tile_kernel<false, true, true, NT>,  \
+                    &car_tile_kernel<true, false, false, NT>,  &car_tile_kernel<true, false, true, NT>,  \
+                    &car_tile_kernel<true, true, false, NT>,   &car_tile_kernel<true, true, true, NT>}
+        static const TileKern kerns[2][8] = {RSK_TK(128), RSK_TK(256)};
+#undef RSK_TK
+        static const int nt_env = env_int("RSK_TILE_NT", 0);
+        int nt = nt_env == 128 || nt_env == 256 ? nt_env : (plan->owners_cap >= 64 ? 256 : 128);
+        if (nt * 8 < plan->recmax) nt = 256;
+        RSK_CHECK(nt * 8 >= plan->recmax, "tile records (%d ints) exceed the copy width", plan->recmax);
+        const TileKern kern = kerns[nt == 256][(vec ? 4 : 0) + (d_score ? 2 : 0) + (off32 ? 1 : 0)];
+        if (lds > 64 * 1024)
+            RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        static const int pipe_env = env_int("RSK_TILE_PIPE", 0);
+        if (pipe_env && vec && SL == kPipeSL) {
+            PipeArgs pa;
+            pa.t = a;
+            pa.items = (int)blocks;
+            int cus = 0;
+            RSK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+            const size_t plds = (size_t)2 * kBufInts * 4;
+            using PipeKern = void (*)(PipeArgs);
+            static const PipeKern pk[4] = {&car_tile_pipe_kernel<false, false>, &car_tile_pipe_kernel<false, true>,
+                                           &car_tile_pipe_kernel<true, false>, &car_tile_pipe_kernel<true, true>};
+            const PipeKern pkern = pk[(d_score ? 2 : 0) + (off32 ? 1 : 0)];
+            RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(pkern),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds));
+            const int grid = (int)std::min<int64_t>(blocks, (int64_t)cus * std::max(1, env_int("RSK_PIPE_PER_CU", 1)));
+            ScopedTimer tm(ctx, "car_tile");
+            pkern<<<dim3((unsigned)grid), dim3(kPipeThreads), plds, ctx->stream>>>(pa);
+            RSK_HIP(hipGetLastError());
+        } else {
+            ScopedTimer tm(ctx, "car_tile");
+            kern<<<dim3((unsigned)blocks), dim3(nt), lds, ctx->stream>>>(a);
+            RSK_HIP(hipGetLastError());
+        }
+    }
     ScoreCtx sc;
     sc.nodekey = d_key;
     sc.zc_cnt = d_zcnt;
@@ -1111,57 +1525,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     const int SL = std::min(S, 64);
     sc.PS = 64 / SL;
     const int64_t chunks = ceil_div(S, SL);
-    if (plan->T > 0) {   // K1b tiles
-        TileArgs a;
-        std::memset(&a, 0, sizeof(a));
-        a.sc = sc;
-        a.members = plan->members.as<int>();
-        a.nrows = plan->nrows.as<int>();
-        a.blob = plan->blob.as<int>();
-        a.blob_off = plan->blob_off.as<int>();
-        a.assign = d_assign;
-        a.SL = SL;
-        a.RS = plan->RS;
-        a.T = plan->T;
-        a.blob_max = plan->blob_max;
-        static const int ablate = [] { const char *e = getenv("RSK_ABLATE_TILE"); return e ? atoi(e) : 0; }();
-        a.ablate = ablate;
-        const size_t lds = (size_t)plan->RS * SL * 4 + (size_t)plan->blob_max * 4;
-        RSK_CHECK(lds <= 160 * 1024, "tile image needs %zu B of LDS", lds);
-        const int64_t blocks = chunks * plan->T;
-        RSK_CHECK(blocks < INT32_MAX, "tile grid too large");
-        if (lds > 64 * 1024)
-            RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&car_tile_kernel),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        ScopedTimer tm(ctx, "car_tile");
-        car_tile_kernel<<<dim3((unsigned)blocks), dim3(kTileWaves * 64), lds, ctx->stream>>>(a);
-        RSK_HIP(hipGetLastError());
-    }
-    {   // K1a direct light rows
-        LightArgs a;
-        std::memset(&a, 0, sizeof(a));
-        a.sc = sc;
-        a.SL = SL;
-        const int iters = 2;
-        a.task_prefix[0] = 0;
-        for (int b = 0; b < kNumLight; ++b) {
-            a.ell[b] = plan->ell[b].as<int>();
-            a.n_items[b] = plan->n_light[b];
-            a.task_items[b] = kLightPK[b] * sc.PS * iters;
-            a.task_prefix[b + 1] = a.task_prefix[b] + (int)ceil_div(plan->n_light[b], a.task_items[b]);
-        }
-        const int tasks = a.task_prefix[kNumLight];
-        if (tasks > 0) {
-            a.assign = d_assign;
-            a.blocks_per_chunk = (int)ceil_div(tasks, 4);
-            const int64_t blocks = chunks * a.blocks_per_chunk;
-            RSK_CHECK(blocks < INT32_MAX, "light grid too large");
-            ScopedTimer tm(ctx, "car_light");
-            car_light_kernel<<<dim3((unsigned)blocks), dim3(256), 0, ctx->stream>>>(a);
-            RSK_HIP(hipGetLastError());
-        }
-    }
-    {   // K1c mid rows
+    {   // K2 mid rows
         MidArgs a;
         std::memset(&a, 0, sizeof(a));
         a.sc = sc;
@@ -1173,35 +1537,43 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
             a.prefix[b + 1] = a.prefix[b] + (int)ceil_div(plan->n_mid[b], sc.PS);
         }
         a.assign = d_assign;
-        for (int wide = 0; wide < 2; ++wide) {
-            const int waves = wide ? a.prefix[3] - a.prefix[2] : a.prefix[2] - a.prefix[0];
-            if (waves <= 0) continue;
+        const int waves = a.prefix[kNumMid];
+        if (waves > 0) {
             a.blocks_per_chunk = (int)ceil_div(waves, 4);
             const int64_t blocks = chunks * a.blocks_per_chunk;
             RSK_CHECK(blocks < INT32_MAX, "mid grid too large");
             ScopedTimer tm(ctx, "car_mid");
-            if (wide) car_mid_kernel<true><<<dim3((unsigned)blocks), dim3(256), 0, ctx->stream>>>(a);
-            else car_mid_kernel<false><<<dim3((unsigned)blocks), dim3(256), 0, ctx->stream>>>(a);
+            car_mid_kernel<<<dim3((unsigned)blocks), dim3(256), 0, ctx->stream>>>(a);
             RSK_HIP(hipGetLastError());
         }
     }
-    for (int c = 0; c < kNumHeavy; ++c) {   // K2
+    for (int c = 0; c < kNumHeavy; ++c) {   // K3 hub rows
         const int n = plan->n_heavy[c];
         if (!n) continue;
         const HeavyGeom g = heavy_geometry(plan->heavy_dmax[c], S, N);
-        RSK_CHECK(g.lds <= 160 * 1024, "heavy class %d needs %zu B of LDS", c, g.lds);
-        const int64_t groups = ceil_div(S, g.G);
-        RSK_CHECK(groups * n < INT32_MAX, "heavy grid too large");
-        auto kern = g.direct ? &car_heavy_kernel<true> : &car_heavy_kernel<false>;
+        RSK_CHECK(g.lds <= 160 * 1024, "hub class %d needs %zu B of LDS", c, g.lds);
+        const int64_t groups = ceil_div(S, 1 << g.lg);
+        RSK_CHECK(groups * n < INT32_MAX, "hub grid too large");
+        auto kern = g.direct ? &car_hub_kernel<true> : &car_hub_kernel<false>;
         if (g.lds > 64 * 1024)
             RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds));
         ScopedTimer tm(ctx, "car_heavy");
         kern<<<dim3((unsigned)(groups * n)), dim3(256), g.lds, ctx->stream>>>(
-            plan->heavy_items[c].as<HeavyItem>(), n, plan->hcol.as<int>(), d_assign, d_key, S, N, g.G, g.dpad,
-            g.H, g.NT, d_zcnt, d_zkey, d_target, d_score);
+            plan->heavy_items[c].as<HeavyItem>(), n, plan->hcol.as<int>(), d_assign, d_key, S, N, g.lg, g.dpad,
+            g.H, d_zcnt, d_zkey, d_target, d_score);
         RSK_HIP(hipGetLastError());
     }
+#ifdef RSK_DEBUG_BOUNDS
+    {
+        unsigned flags_h = 0, zero = 0;
+        RSK_HIP(hipStreamSynchronize(ctx->stream));
+        RSK_HIP(hipMemcpyFromSymbol(&flags_h, HIP_SYMBOL(rsk_dbg_flags), 4));
+        RSK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(rsk_dbg_flags), &zero, 4));
+        RSK_CHECK(flags_h == 0, "debug bounds violation flags=0x%x (1 out, 2 pods, 4 assign, 8 nodekey, 16 recs)",
+                  flags_h);
+    }
+#endif
     if (!dev) {
         RSK_TRY(copy_back(ctx, out_target, d_target, QS * 4, false));
         if (out_score) RSK_TRY(copy_back(ctx, out_score, d_score, QS * 4, false));
