@@ -61,6 +61,8 @@ struct rsk_ctx {
     bool profiling = false;
     std::map<std::string, std::vector<rsk::EventPair>> pending;
     std::map<std::string, std::pair<double, int64_t>> totals;
+    hipStream_t aux = nullptr;   // side stream: CAR mid/hub rows overlap the tile kernel
+    hipEvent_t fork = nullptr, join = nullptr;
     rsk::DevBuf host_stage[12];  // device staging for host-pointer calls
     rsk::DevBuf work[6];         // per-call device workspace
     std::vector<uint8_t> pinned;  // host scratch
@@ -72,10 +74,17 @@ namespace rsk {
 struct ScopedTimer {
     rsk_ctx *ctx;
     const char *name;
+    hipStream_t stream;
     hipEvent_t a = nullptr, b = nullptr;
-    ScopedTimer(rsk_ctx *c, const char *n);
+    ScopedTimer(rsk_ctx *c, const char *n, hipStream_t s = nullptr);
     ~ScopedTimer();
 };
+
+// Fork / join of the context's side stream around work that may overlap the
+// main stream: fork() makes aux wait for everything queued on ctx->stream so
+// far; join() makes ctx->stream wait for everything queued on aux.
+int aux_fork(rsk_ctx *ctx);
+int aux_join(rsk_ctx *ctx);
 
 int activate(rsk_ctx *ctx);
 

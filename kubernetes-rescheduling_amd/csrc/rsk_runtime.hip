@@ -39,16 +39,33 @@ int activate(rsk_ctx *ctx) {
     return RSK_OK;
 }
 
-ScopedTimer::ScopedTimer(rsk_ctx *c, const char *n) : ctx(c), name(n) {
+ScopedTimer::ScopedTimer(rsk_ctx *c, const char *n, hipStream_t s) : ctx(c), name(n), stream(s ? s : c->stream) {
     if (!ctx->profiling) return;
     if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) { a = b = nullptr; return; }
-    (void)hipEventRecord(a, ctx->stream);
+    (void)hipEventRecord(a, stream);
 }
 
 ScopedTimer::~ScopedTimer() {
     if (!a) return;
-    (void)hipEventRecord(b, ctx->stream);
+    (void)hipEventRecord(b, stream);
     ctx->pending[name].push_back({a, b});
+}
+
+int aux_fork(rsk_ctx *ctx) {
+    if (!ctx->aux) {
+        RSK_HIP(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+        RSK_HIP(hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming));
+        RSK_HIP(hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming));
+    }
+    RSK_HIP(hipEventRecord(ctx->fork, ctx->stream));
+    RSK_HIP(hipStreamWaitEvent(ctx->aux, ctx->fork, 0));
+    return RSK_OK;
+}
+
+int aux_join(rsk_ctx *ctx) {
+    RSK_HIP(hipEventRecord(ctx->join, ctx->aux));
+    RSK_HIP(hipStreamWaitEvent(ctx->stream, ctx->join, 0));
+    return RSK_OK;
 }
 
 int stage_in(rsk_ctx *ctx, int slot, const void *src, size_t bytes, bool device, const void **out) {
@@ -114,6 +131,12 @@ int rsk_ctx_destroy(rsk_ctx *ctx) {
         for (auto &e : kv.second) { (void)hipEventDestroy(e.start); (void)hipEventDestroy(e.stop); }
     for (auto &b : ctx->host_stage) b.release();
     for (auto &b : ctx->work) b.release();
+    if (ctx->aux) {
+        (void)hipStreamSynchronize(ctx->aux);
+        (void)hipStreamDestroy(ctx->aux);
+        (void)hipEventDestroy(ctx->fork);
+        (void)hipEventDestroy(ctx->join);
+    }
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
     return RSK_OK;

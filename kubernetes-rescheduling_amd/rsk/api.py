@@ -47,7 +47,7 @@ class CarPlan:
 
     INFO_FIELDS = ("tile_rows", "direct_rows", "mid_rows", "heavy_rows", "tiles", "tile_image_rows",
                    "tile_pods", "tile_bytes", "direct_bytes", "mid_bytes", "heavy_bytes", "max_degree",
-                   "image_rows_total", "image_pods_distinct")
+                   "image_rows_total", "image_pods_distinct", "sorted_rows")
 
     def info(self) -> dict:
         """How the plan routed its rows (rsk_car_plan_info)."""

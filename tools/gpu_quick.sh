@@ -19,4 +19,4 @@ bench() {  # bench <name> [env...]
     return 0
 }
 bench base
-for v in "$@"; do bench "$v" $(echo "$v" | tr "," " "); done
+for v in "$@"; do bench "$(echo "$v" | tr "/" "_" | cut -c1-80)" $(echo "$v" | tr "," " "); done
