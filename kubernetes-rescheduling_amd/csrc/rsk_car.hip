@@ -59,7 +59,7 @@ constexpr int kHeavyMax[kNumHeavy] = {128, 256, 512, 1024, 2048, 4096};
 // record ints = 40 KiB: four workgroups (16 waves) per CU.
 constexpr int kTileOwners = 128;                   // max rows scored per tile
 constexpr int kTileRows = 144;                     // max image rows (distinct neighbours) per tile (< 256)
-constexpr int kTileRecInts = 1024;                 // max record ints per tile (one int4 copy per thread)
+constexpr int kTileRecInts = 1020;                 // max record ints per tile (+4: unit counter; 40 KiB total)
 constexpr int kTileThreads = 256;
 constexpr int kTileWaves = kTileThreads / 64;
 constexpr int kNumCls = 6;                         // degree classes d = 1, 2, {0,3,4}, 5-8, 9-16, 17-32
@@ -304,6 +304,7 @@ struct TileArgs {
     int *out_target;
     int *out_score;
     int S, N, T, lsl, rmax;  // SL = 1 << lsl scenarios per workgroup
+    int rec_cap;             // record ints reserved in LDS (largest tile, x4); the unit counter follows
     int ablate;              // profiling only (RSK_ABLATE_TILE): 1 skip image load, 2 skip scoring
     int order;               // 0 chunk-major, 1 tile-major grid (RSK_TILE_ORDER)
     unsigned n_assign, n_out, n_pods, n_recs, n_key;  // element counts (debug bounds build)
@@ -339,20 +340,37 @@ __device__ __forceinline__ void tile_emit(const TileArgs &a, int oi, const TileL
     if (kScore) st_cell<kOff32>(a.out_score, (unsigned)oi, (unsigned)a.S, (unsigned)L.s, sc);
 }
 
-__device__ __forceinline__ int2 img_at(const int2 *img, int row, int lsl, int col) { return img[(row << lsl) + col]; }
+// The tile image in LDS: {node, key} per (image row, scenario column).  With
+// N <= 65535 (kN16) nodes are u16 next to the int32 keys (6 B per entry, five
+// workgroups per CU); otherwise int2 pairs (8 B, four per CU).
+template <bool kN16>
+struct TileImg {
+    int2 *w;                // !kN16: {node, key}
+    int *key;               // kN16
+    unsigned short *node;   // kN16
+    int lsl;
+    __device__ __forceinline__ int2 at(int row, int col) const {
+        const int i = (row << lsl) + col;
+        if (kN16) return make_int2((int)node[i], key[i]);
+        return w[i];
+    }
+    __device__ __forceinline__ void put(int i, int n, int k) const {
+        if (kN16) { node[i] = (unsigned short)n; key[i] = k; }
+        else w[i] = make_int2(n, k);
+    }
+};
 
 // d == 1: the neighbour's node is the single best unless hazard (zero case).
-template <int U, bool kScore, bool kOff32>
-__device__ __forceinline__ void tile_d1(const TileArgs &a, const int2 *img, const int *rec, int n, const TileLane &L,
-                                        int wave) {
-    const int step = kTileWaves * L.PS;
+template <int U, bool kScore, bool kOff32, class Img>
+__device__ __forceinline__ void tile_d1(const TileArgs &a, const Img &img, const int *rec, int n, const TileLane &L,
+                                        int p0) {
     const int2 *r2 = reinterpret_cast<const int2 *>(rec);
-    for (int b0 = wave * L.PS; b0 < n; b0 += step * U) {
+    {
         int2 r[U], e[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) r[u] = r2[min(b0 + u * step + L.slot, n - 1)];
+        for (int u = 0; u < U; ++u) r[u] = r2[min((p0 + u) * L.PS + L.slot, n - 1)];
 #pragma unroll
-        for (int u = 0; u < U; ++u) e[u] = img_at(img, r[u].y, a.lsl, L.col);
+        for (int u = 0; u < U; ++u) e[u] = img.at(r[u].y, L.col);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const bool h = e[u].y == kKeyHaz;
@@ -363,19 +381,18 @@ __device__ __forceinline__ void tile_d1(const TileArgs &a, const int2 *img, cons
 
 // d == 2: same node -> score 2; one hazard -> the other; two distinct
 // candidates -> tie of two: larger remaining CPU (then lower index), None if < 0.
-template <int U, bool kScore, bool kOff32>
-__device__ __forceinline__ void tile_d2(const TileArgs &a, const int2 *img, const int *rec, int n, const TileLane &L,
-                                        int wave) {
-    const int step = kTileWaves * L.PS;
+template <int U, bool kScore, bool kOff32, class Img>
+__device__ __forceinline__ void tile_d2(const TileArgs &a, const Img &img, const int *rec, int n, const TileLane &L,
+                                        int p0) {
     const int2 *r2 = reinterpret_cast<const int2 *>(rec);
-    for (int b0 = wave * L.PS; b0 < n; b0 += step * U) {
+    {
         int2 r[U], e0[U], e1[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) r[u] = r2[min(b0 + u * step + L.slot, n - 1)];
+        for (int u = 0; u < U; ++u) r[u] = r2[min((p0 + u) * L.PS + L.slot, n - 1)];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            e0[u] = img_at(img, r[u].y & 0xffff, a.lsl, L.col);
-            e1[u] = img_at(img, (int)((unsigned)r[u].y >> 16), a.lsl, L.col);
+            e0[u] = img.at(r[u].y & 0xffff, L.col);
+            e1[u] = img.at((int)((unsigned)r[u].y >> 16), L.col);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -408,18 +425,17 @@ __device__ __forceinline__ int rec_row(const int (&r)[W], int j) {
 
 // 0 or 3 <= d <= D (D = 4, 8, 16): pairwise equality counts in registers, then
 // the lexicographic (count, key, -node) maximum over the candidates in 32-bit steps.
-template <int D, int W, bool kScore, bool kOff32>
-__device__ __forceinline__ void tile_dn(const TileArgs &a, const int2 *img, const int *rec, int n, const TileLane &L,
-                                        int wave) {
-    const int step = kTileWaves * L.PS;
-    for (int b0 = wave * L.PS; b0 < n; b0 += step) {
+template <int D, int W, bool kScore, bool kOff32, class Img>
+__device__ __forceinline__ void tile_dn(const TileArgs &a, const Img &img, const int *rec, int n, const TileLane &L,
+                                        int p0) {
+    {
         int r[W];
-        load_rec<W>(rec + min(b0 + L.slot, n - 1) * W, r);
+        load_rec<W>(rec + min(p0 * L.PS + L.slot, n - 1) * W, r);
         const int d = r[1];
         int nd[D], ky[D], c[D];
 #pragma unroll
         for (int j = 0; j < D; ++j) {
-            const int2 e = img_at(img, rec_row<W>(r, j), a.lsl, L.col);
+            const int2 e = img.at(rec_row<W>(r, j), L.col);
             // padding entries (j >= d) read row 0: masked out of the counts
             // (a node id no real entry can hold) and of the candidates
             nd[j] = j < d ? e.x : -1 - j;
@@ -461,16 +477,15 @@ __device__ __forceinline__ void tile_dn(const TileArgs &a, const int2 *img, cons
 // with a register bitonic network (min/max only), then walks the sorted runs
 // once: a run's key comes from the LDS image of its entry's row; it keeps the
 // lexicographic (count, key, -node) maximum and the number of runs at the max.
-template <int D, int W, bool kScore, bool kOff32>
-__device__ __forceinline__ void tile_ds(const TileArgs &a, const int2 *img, const int *rec, int n, const TileLane &L,
-                                        int wave) {
-    const int step = kTileWaves * L.PS;
+template <int D, int W, bool kScore, bool kOff32, class Img>
+__device__ __forceinline__ void tile_ds(const TileArgs &a, const Img &img, const int *rec, int n, const TileLane &L,
+                                        int p0) {
     const unsigned lim = (unsigned)a.N << 8;
     constexpr unsigned kSentinel = 0xffffff00u;  // row 0, node 2^24 - 1 >= N
-    for (int b0 = wave * L.PS; b0 < n; b0 += step) {
+    {
         // the record stays in LDS: rows are read 8 at a time (one int4), so only
         // the D sort words are live across the network
-        const int *rc = rec + min(b0 + L.slot, n - 1) * W;
+        const int *rc = rec + min(p0 * L.PS + L.slot, n - 1) * W;
         const int2 hd = *reinterpret_cast<const int2 *>(rc);
         const int d = hd.y;
         unsigned v[D];
@@ -483,7 +498,7 @@ __device__ __forceinline__ void tile_ds(const TileArgs &a, const int2 *img, cons
             for (int t = 0; t < 8; ++t) {
                 const int j = j0 + t;
                 const int row = (t & 1) ? (int)(pw[t >> 1] >> 16) : (int)(pw[t >> 1] & 0xffffu);
-                const int2 e = img_at(img, row, a.lsl, L.col);
+                const int2 e = img.at(row, L.col);
                 v[j] = (j < d && e.y != kKeyHaz) ? (((unsigned)e.x << 8) | (unsigned)row) : kSentinel;
             }
         }
@@ -499,7 +514,7 @@ __device__ __forceinline__ void tile_ds(const TileArgs &a, const int2 *img, cons
             c = (j > 0 && nd == (v[j > 0 ? j - 1 : 0] >> 8)) ? c + 1 : 1;
             const bool end = j == D - 1 || (v[j < D - 1 ? j + 1 : j] >> 8) != nd;
             const bool cand = end && v[j] < lim;
-            const int k = img_at(img, (int)(v[j] & 0xffu), a.lsl, L.col).y;
+            const int k = img.at((int)(v[j] & 0xffu), L.col).y;
             const unsigned long long key = cand ? pack_cand(c, k, (int)nd) : 0ull;
             best = key > best ? key : best;
             const bool gt = cand && c > M, eq = cand && c == M;
@@ -516,8 +531,8 @@ __device__ __forceinline__ void tile_ds(const TileArgs &a, const int2 *img, cons
 // wave-instruction reads SL contiguous words of 64/SL rows (assign and nodekey
 // alike), i.e. whole 128-B lines.  Elements past the end redo the last element
 // (identical LDS writes), so nothing is guarded.
-template <bool kOff32>
-__device__ __forceinline__ void tile_load_image(const TileArgs &a, int2 *img, int img_off, int nrows, int s0) {
+template <bool kOff32, class Img>
+__device__ __forceinline__ void tile_load_image(const TileArgs &a, const Img &img, int img_off, int nrows, int s0) {
     const unsigned S = (unsigned)a.S, N = (unsigned)a.N;
     const int *__restrict__ pods = a.img_pods + img_off;
     const char *__restrict__ asg = reinterpret_cast<const char *>(a.assign);
@@ -544,12 +559,25 @@ __device__ __forceinline__ void tile_load_image(const TileArgs &a, int2 *img, in
             const int s = s0 + (e[u] & msk);
             const bool ok = (unsigned)v[u] < N && s < (int)S;
             const int key = ld32(a.nodekey, RSK_BOUND(ok ? (unsigned)v[u] * S + (unsigned)s : 0u, a.n_key, 8u));
-            img[e[u]] = make_int2(v[u], ok ? key : kKeyHaz);
+            img.put(e[u], v[u], ok ? key : kKeyHaz);
         }
     }
 }
 
-template <bool kScore, bool kOff32>
+// LDS ints taken by the image of `cells` entries (rounded up to 16 B).
+template <bool kN16>
+__host__ __device__ constexpr int tile_img_ints(int cells) {
+    return kN16 ? ((cells + (cells + 1) / 2 + 3) & ~3) : ((2 * cells + 3) & ~3);
+}
+
+// Next work unit of the wave: lane 0 bumps the workgroup's LDS counter.
+__device__ __forceinline__ int grab(int *ctr, int lane) {
+    int k = 0;
+    if (lane == 0) k = atomicAdd(ctr, 1);
+    return __builtin_amdgcn_readfirstlane(k);
+}
+
+template <bool kScore, bool kOff32, bool kN16>
 __global__ __launch_bounds__(kTileThreads, 4) void car_tile_kernel(TileArgs a) {
     extern __shared__ __attribute__((aligned(16))) int lds[];  // img {node,key} [rmax][SL], then records
     // chunk-major (default: concurrent workgroups share a chunk's nodekey
@@ -560,8 +588,13 @@ __global__ __launch_bounds__(kTileThreads, 4) void car_tile_kernel(TileArgs a) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int SL = 1 << a.lsl;
     const int s0 = chunk * SL;
-    int2 *img = reinterpret_cast<int2 *>(lds);
-    int *rec = lds + ((2 * a.rmax * SL + 3) & ~3);  // 16-B aligned for the int4 record reads
+    const int cells = a.rmax * SL;
+    TileImg<kN16> img;
+    img.lsl = a.lsl;
+    img.w = reinterpret_cast<int2 *>(lds);
+    img.key = lds;
+    img.node = reinterpret_cast<unsigned short *>(lds + cells);
+    int *rec = lds + tile_img_ints<kN16>(cells);  // 16-B aligned for the int4 record reads
     const cint_ptr m = const_ptr(a.meta) + (size_t)tile * kMetaW;
     const int img_off = m[0], nrows = m[1], rec_off = m[2], rec_ints = m[3];
 
@@ -582,15 +615,38 @@ __global__ __launch_bounds__(kTileThreads, 4) void car_tile_kernel(TileArgs a) {
         L.zt = zero_target(load_zc(a.zc_cnt, a.zc_key, L.s), zs);
         L.zs = zs;
     }
+    if (threadIdx.x == 0) rec[a.rec_cap] = 0;  // work-unit counter
     __syncthreads();
     if (a.ablate & 2) return;  // profiling ablation: no scoring (results are wrong)
+    // Scoring work units (pairs of PS records: d1 4 pairs, d2 2, the rest 1),
+    // most expensive class first, handed out by an LDS counter so the few
+    // costly high-degree records do not all land on one wave.
     const int n0 = m[4], n1 = m[5], n2 = m[6], n3 = m[7], n4 = m[8], n5 = m[9];
-    if (n0) tile_d1<4, kScore, kOff32>(a, img, rec + m[10], n0, L, wave);
-    if (n1) tile_d2<2, kScore, kOff32>(a, img, rec + m[11], n1, L, wave);
-    if (n2) tile_dn<4, 4, kScore, kOff32>(a, img, rec + m[12], n2, L, wave);
-    if (n3) tile_dn<8, 8, kScore, kOff32>(a, img, rec + m[13], n3, L, wave);
-    if (n4) tile_dn<16, 12, kScore, kOff32>(a, img, rec + m[14], n4, L, wave);
-    if (n5) tile_ds<32, 20, kScore, kOff32>(a, img, rec + m[15], n5, L, wave);
+    const int lp = 6 - a.lsl;  // log2(PS), PS = 64 / SL
+    const int u5 = (n5 + L.PS - 1) >> lp, u4 = (n4 + L.PS - 1) >> lp, u3 = (n3 + L.PS - 1) >> lp;
+    const int u2 = (n2 + L.PS - 1) >> lp, u1 = (((n1 + L.PS - 1) >> lp) + 1) >> 1;
+    const int u0 = (((n0 + L.PS - 1) >> lp) + 3) >> 2;
+    const int total = u5 + u4 + u3 + u2 + u1 + u0;
+    int *ctr = rec + a.rec_cap;
+    int k = grab(ctr, lane);
+    while (k < total) {
+        const int kn = grab(ctr, lane);
+        int u = k;
+        if (u < u5) {
+            tile_ds<32, 20, kScore, kOff32>(a, img, rec + m[15], n5, L, u);
+        } else if ((u -= u5) < u4) {
+            tile_dn<16, 12, kScore, kOff32>(a, img, rec + m[14], n4, L, u);
+        } else if ((u -= u4) < u3) {
+            tile_dn<8, 8, kScore, kOff32>(a, img, rec + m[13], n3, L, u);
+        } else if ((u -= u3) < u2) {
+            tile_dn<4, 4, kScore, kOff32>(a, img, rec + m[12], n2, L, u);
+        } else if ((u -= u2) < u1) {
+            tile_d2<2, kScore, kOff32>(a, img, rec + m[11], n1, L, 2 * u);
+        } else {
+            tile_d1<4, kScore, kOff32>(a, img, rec + m[10], n0, L, 4 * (u - u1));
+        }
+        k = kn;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1424,14 +1480,20 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         a.order = order;
         a.ablate = ablate;
         const bool off32 = (int64_t)std::max(plan->P, plan->Q) * S * 4 < ((int64_t)1 << 32);
-        const size_t lds = ((((size_t)2 * plan->rmax * SL + 3) & ~(size_t)3) + plan->recmax) * 4;
+        a.rec_cap = (plan->recmax + 3) & ~3;
+        const bool n16 = N <= 65535 && env_int("RSK_TILE_N16", 1) != 0;
+        const int cells = plan->rmax * SL;
+        const size_t lds = ((size_t)(n16 ? tile_img_ints<true>(cells) : tile_img_ints<false>(cells)) + a.rec_cap + 4) * 4;
         RSK_CHECK(lds <= 160 * 1024 && plan->recmax <= kTileRecInts, "tile image needs %zu B of LDS", lds);
         const int64_t blocks = ceil_div(S, SL) * plan->T;
         RSK_CHECK(blocks < INT32_MAX, "tile grid too large");
         using TileKern = void (*)(TileArgs);
-        static const TileKern kerns[4] = {&car_tile_kernel<false, false>, &car_tile_kernel<false, true>,
-                                          &car_tile_kernel<true, false>, &car_tile_kernel<true, true>};
-        const TileKern kern = kerns[(d_score ? 2 : 0) + (off32 ? 1 : 0)];
+        static const TileKern kerns[8] = {
+            &car_tile_kernel<false, false, false>, &car_tile_kernel<false, true, false>,
+            &car_tile_kernel<true, false, false>,  &car_tile_kernel<true, true, false>,
+            &car_tile_kernel<false, false, true>,  &car_tile_kernel<false, true, true>,
+            &car_tile_kernel<true, false, true>,   &car_tile_kernel<true, true, true>};
+        const TileKern kern = kerns[(n16 ? 4 : 0) + (d_score ? 2 : 0) + (off32 ? 1 : 0)];
         if (lds > 64 * 1024)
             RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

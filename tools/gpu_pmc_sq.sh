@@ -1,13 +1,14 @@
 #!/bin/bash
 # SQ / TA counter passes on the headline bench (one rocprofv3 --pmc run per group).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
-mkdir -p gpurun_out/sq
+mkdir -p gpurun_out/sq gpurun_out/sq_abl
 export TMPDIR=/tmp RSK_OVERLAP=0
+OUT=${SQ_OUT:-gpurun_out/sq}
 B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline"
 pass() {  # pass <name> <counters...>
     local name=$1; shift
-    timeout -s KILL 120 rocprofv3 --pmc "$@" -d gpurun_out/sq -o "$name" -f csv -- $B > "gpurun_out/sq/$name.log" 2>&1
-    local rc=$?; echo "== $name rc=$rc"; [ $rc -ne 0 ] && { tail -3 "gpurun_out/sq/$name.log"; exit $rc; }
+    timeout -s KILL 120 rocprofv3 --pmc "$@" -d $OUT -o "$name" -f csv -- $B > "$OUT/$name.log" 2>&1
+    local rc=$?; echo "== $name rc=$rc"; [ $rc -ne 0 ] && { tail -3 "$OUT/$name.log"; exit $rc; }
     return 0
 }
 pass p1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES
