@@ -115,7 +115,8 @@ def main():
         elapsed = float(e.item())
 
     kernels = {}
-    for name in ("car_prep", "car_tile", "car_light", "car_mid", "car_heavy"):
+    for name in ("car_prep", "car_tile", "car_mid", "car_heavy", "car_hub128", "car_hub256", "car_hub512",
+                 "car_hub1024", "car_hub2048", "car_hub4096"):
         ms, n = ctx.kernel_time(name)
         if n:
             kernels[name] = {"avg_ms": ms / n, "launches": n, "per_step_ms": ms / args.steps}
@@ -164,7 +165,8 @@ def main():
         except (OSError, ValueError):
             pass
     for k, v in kernels.items():
-        v["algorithmic_GBps"] = round(alg[k] / (v["per_step_ms"] / 1e3) / 1e9, 1)
+        if k in alg:
+            v["algorithmic_GBps"] = round(alg[k] / (v["per_step_ms"] / 1e3) / 1e9, 1)
     step_ach = B / (ms_step / 1e3) / 1e9
     roof_step = {"bound": "hbm", "achieved": round(step_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                  "frac": round(step_ach / HBM_PEAK_GBS, 4), "algorithmic_bytes": B,

@@ -53,7 +53,8 @@ constexpr int kMidMax = 64;                        // mid kernel: 33..64 (17..64
 constexpr int kNumMid = 2;                         // buckets D = 32, 64
 constexpr int kMidW[kNumMid] = {36, 68};           // record ints: oi, d, nb[D], pad to x4
 constexpr int kNumHeavy = 6;                       // hub classes: (64,128] (128,256] ... (2048,4096]
-constexpr int kHeavyMax[kNumHeavy] = {128, 256, 512, 1024, 2048, 4096};
+constexpr int kHeavyMax[kNumHeavy] = {128, 255, 512, 1024, 2048, 4096};  // <= 255: u8 counters
+constexpr int kHeavyNJ[kNumHeavy] = {2, 4, 8, 16, 0, 0};  // register entries per lane (0: LDS re-reads)
 
 // Light-row tiles.  LDS per workgroup <= 144 rows x 32 scenarios x 8 B + 1024
 // record ints = 40 KiB: four workgroups (16 waves) per CU.
@@ -203,76 +204,78 @@ __device__ __forceinline__ void bitonic_sort(T (&v)[D]) {
 }
 
 // ---------------------------------------------------------------------------
-// K0: packed node key + per-scenario zero case.  Thread t -> (4 consecutive
-// scenarios, node chunk): 16-B loads of use and 4-B loads of hazard per node,
-// four zero-case accumulators per thread, one atomic each at the end.
-// Requires S % 4 == 0; car_prep1_kernel is the one-scenario-per-thread form.
+// K0: packed node key + per-scenario zero case.  Thread t -> (V consecutive
+// scenarios, node chunk): V-wide loads of use / hazard per node.  The zero
+// case (non-hazard count, packed max) is reduced in LDS per workgroup first —
+// threads of one workgroup that share a scenario meet in one LDS slot — so a
+// scenario receives one global atomic per workgroup, not one per thread (with
+// few scenarios, e.g. S = 64, thousands of threads would otherwise contend for
+// the same address).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void car_prep4_kernel(const int *__restrict__ cap, const int4 *__restrict__ use,
-                                                        const uchar4 *__restrict__ haz, int N, int S4, int npb,
-                                                        unsigned total, int4 *__restrict__ nodekey,
-                                                        int *__restrict__ zc_cnt,
-                                                        unsigned long long *__restrict__ zc_key) {
-    const unsigned t = blockIdx.x * 256u + threadIdx.x;
-    if (t >= total) return;
-    const int s4 = (int)(t % (unsigned)S4);
-    const int n0 = (int)(t / (unsigned)S4) * npb;
-    const int n1 = min(N, n0 + npb);
-    int cnt[4] = {0, 0, 0, 0};
-    unsigned long long best[4] = {0, 0, 0, 0};
-#pragma unroll 4
-    for (int n = n0; n < n1; ++n) {
-        const size_t idx = (size_t)n * S4 + s4;
-        const int4 u = use[idx];
-        const uchar4 h = haz[idx];
-        const int c = cap[n];
-        const int uu[4] = {u.x, u.y, u.z, u.w};
-        const int hh[4] = {h.x, h.y, h.z, h.w};
-        int k[4];
-#pragma unroll
-        for (int x = 0; x < 4; ++x) {
-            k[x] = hh[x] ? kKeyHaz : c - uu[x];
-            cnt[x] += hh[x] ? 0 : 1;
-            const unsigned long long pk = hh[x] ? 0ull : zc_pack(k[x], n);
-            best[x] = pk > best[x] ? pk : best[x];
-        }
-        nodekey[idx] = make_int4(k[0], k[1], k[2], k[3]);
-    }
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-        if (cnt[x]) {
-            atomicAdd(&zc_cnt[4 * s4 + x], cnt[x]);
-            atomicMax(&zc_key[4 * s4 + x], best[x]);
-        }
-}
+template <int V>
+struct VecT;
+template <> struct VecT<1> { typedef int I; typedef uint8_t H; };
+template <> struct VecT<4> { typedef int4 I; typedef uchar4 H; };
 
-__global__ __launch_bounds__(256) void car_prep1_kernel(const int *__restrict__ cap, const int *__restrict__ use,
-                                                        const uint8_t *__restrict__ haz, int N, int S, int npb,
-                                                        unsigned total, int *__restrict__ nodekey,
-                                                        int *__restrict__ zc_cnt,
-                                                        unsigned long long *__restrict__ zc_key) {
+__device__ __forceinline__ void vec_get(const int &v, int (&o)[1]) { o[0] = v; }
+__device__ __forceinline__ void vec_get(const int4 &v, int (&o)[4]) { o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w; }
+__device__ __forceinline__ void vec_get(const uint8_t &v, int (&o)[1]) { o[0] = v; }
+__device__ __forceinline__ void vec_get(const uchar4 &v, int (&o)[4]) { o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w; }
+__device__ __forceinline__ int vec_make(const int (&k)[1]) { return k[0]; }
+__device__ __forceinline__ int4 vec_make(const int (&k)[4]) { return make_int4(k[0], k[1], k[2], k[3]); }
+
+template <int V>
+__global__ __launch_bounds__(256) void car_prep_kernel(const int *__restrict__ cap, const typename VecT<V>::I *__restrict__ use,
+                                                       const typename VecT<V>::H *__restrict__ haz, int N, int SV,
+                                                       int npb, unsigned total, typename VecT<V>::I *__restrict__ nodekey,
+                                                       int *__restrict__ zc_cnt,
+                                                       unsigned long long *__restrict__ zc_key) {
+    __shared__ int lcnt[256 * V];
+    __shared__ unsigned long long lkey[256 * V];
     const unsigned t = blockIdx.x * 256u + threadIdx.x;
-    if (t >= total) return;
-    const int s = (int)(t % (unsigned)S);
-    const int n0 = (int)(t / (unsigned)S) * npb;
-    const int n1 = min(N, n0 + npb);
-    int cnt = 0;
-    unsigned long long best = 0;
-    for (int n = n0; n < n1; ++n) {
-        const size_t idx = (size_t)n * S + s;
-        const int h = haz[idx];
-        const int key = h ? kKeyHaz : cap[n] - use[idx];
-        nodekey[idx] = key;
-        if (!h) {
-            ++cnt;
-            const unsigned long long pk = zc_pack(key, n);
-            best = pk > best ? pk : best;
+    const unsigned base = (blockIdx.x * 256u) % (unsigned)SV;  // vector slot of thread 0
+    const int nslot = min(256, SV);
+    for (int i = threadIdx.x; i < nslot * V; i += 256) { lcnt[i] = 0; lkey[i] = 0ull; }
+    __syncthreads();
+    if (t < total) {
+        const int sv = (int)(t % (unsigned)SV);
+        const int n0 = (int)(t / (unsigned)SV) * npb;
+        const int n1 = min(N, n0 + npb);
+        int cnt[V];
+        unsigned long long best[V];
+#pragma unroll
+        for (int x = 0; x < V; ++x) { cnt[x] = 0; best[x] = 0ull; }
+#pragma unroll 4
+        for (int n = n0; n < n1; ++n) {
+            const size_t idx = (size_t)n * SV + sv;
+            int uu[V], hh[V], k[V];
+            vec_get(use[idx], uu);
+            vec_get(haz[idx], hh);
+            const int c = cap[n];
+#pragma unroll
+            for (int x = 0; x < V; ++x) {
+                k[x] = hh[x] ? kKeyHaz : c - uu[x];
+                cnt[x] += hh[x] ? 0 : 1;
+                const unsigned long long pk = hh[x] ? 0ull : zc_pack(k[x], n);
+                best[x] = pk > best[x] ? pk : best[x];
+            }
+            nodekey[idx] = vec_make(k);
         }
+        const int slot = (int)(((unsigned)sv + (unsigned)SV - base) % (unsigned)SV);  // < nslot
+#pragma unroll
+        for (int x = 0; x < V; ++x)
+            if (cnt[x]) {
+                atomicAdd(&lcnt[slot * V + x], cnt[x]);
+                atomicMax(&lkey[slot * V + x], best[x]);
+            }
     }
-    if (cnt) {
-        atomicAdd(&zc_cnt[s], cnt);
-        atomicMax(&zc_key[s], best);
-    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nslot * V; i += 256)
+        if (lcnt[i]) {
+            const int s = (int)(((base + (unsigned)(i / V)) % (unsigned)SV) * V + (unsigned)(i % V));
+            atomicAdd(&zc_cnt[s], lcnt[i]);
+            atomicMax(&zc_key[s], lkey[i]);
+        }
 }
 
 // ---------------------------------------------------------------------------
@@ -784,19 +787,27 @@ __device__ __forceinline__ unsigned long long dpp_max_u64(unsigned long long v) 
     return ((unsigned long long)hi << 32) | lo;
 }
 
-template <bool kDirect>
+// Per-wave count table of one scenario's neighbour nodes: direct u8 / u16
+// counters packed 4 / 2 per word (node < kDirectMaxN; u8 only when the class
+// degree is <= 255, so a counter never carries into its neighbour), or an
+// open-addressing hash keyed by node+1 (keys[H] then cnts[H]).
+enum { kHubHash = 0, kHubU8 = 8, kHubU16 = 16 };
+
+template <int kCnt>
 struct HubTable {
-    unsigned *keys, *cnts;  // direct: cnts only (2 x u16 per word); hash: keys[H] + cnts[H]
+    unsigned *keys, *cnts;
     unsigned mask;
+    static constexpr int kSh = kCnt == kHubU8 ? 2 : 1;  // log2(counters per word)
     __device__ __forceinline__ unsigned slot(int n) const {  // hash: the slot holding n (inserted)
         const unsigned k = (unsigned)n + 1u;
         unsigned h = (k * 2654435761u) & mask;
         while (keys[h] != k) h = (h + 1u) & mask;
         return h;
     }
+    __device__ __forceinline__ unsigned shift(int n) const { return ((unsigned)n & ((1u << kSh) - 1u)) * (unsigned)kCnt; }
     __device__ __forceinline__ void add(int n) const {
-        if (kDirect) {
-            atomicAdd(&cnts[n >> 1], 1u << ((n & 1) << 4));
+        if (kCnt != kHubHash) {
+            atomicAdd(&cnts[n >> kSh], 1u << shift(n));
         } else {
             const unsigned k = (unsigned)n + 1u;
             unsigned h = (k * 2654435761u) & mask;
@@ -809,19 +820,28 @@ struct HubTable {
         }
     }
     __device__ __forceinline__ int get(int n) const {
-        if (kDirect) return (int)((cnts[n >> 1] >> ((n & 1) << 4)) & 0xffffu);
+        if (kCnt != kHubHash) return (int)((cnts[n >> kSh] >> shift(n)) & ((1u << kCnt) - 1u));
         return (int)cnts[slot(n)];
     }
+    __device__ __forceinline__ void clear(int n) const { cnts[n >> kSh] = 0u; }  // direct only
 };
 
-template <bool kDirect>
-__global__ __launch_bounds__(256) void car_hub_kernel(const HeavyItem *__restrict__ items, int n_items,
-                                                      const int *__restrict__ hcol, const int *__restrict__ assign,
-                                                      const int *__restrict__ nodekey, int S, int N, int lg, int dpad,
-                                                      int H, const int *__restrict__ zc_cnt,
-                                                      const unsigned long long *__restrict__ zc_key,
-                                                      int *__restrict__ out_target, int *__restrict__ out_score) {
+// K3 hub rows (deg > 64): one workgroup per (row, group of G = 2^lg
+// scenarios), kW waves.  The row's {node, key} columns for the G scenarios
+// are staged in LDS (3 dependent rounds of loads: hcol -> assign -> nodekey),
+// then each wave takes scenarios wave, wave+kW, ...: lanes = neighbours (NJ
+// per lane, kept in registers; NJ = 0: any degree, re-read from LDS), counts
+// into the wave's table (A), max count by DPP (B), best (count, rem, -node)
+// and the number of maximal entries by DPP/ballot (C), table cleared (D).
+template <int kCnt, int NJ, int kW>
+__global__ __launch_bounds__(64 * kW) void car_hub_kernel(const HeavyItem *__restrict__ items, int n_items,
+                                                          const int *__restrict__ hcol, const int *__restrict__ assign,
+                                                          const int *__restrict__ nodekey, int S, int N, int lg, int dpad,
+                                                          int H, const int *__restrict__ zc_cnt,
+                                                          const unsigned long long *__restrict__ zc_key,
+                                                          int *__restrict__ out_target, int *__restrict__ out_score) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
+    constexpr int kT = 64 * kW;
     const int G = 1 << lg;
     const int grp = blockIdx.x / n_items;
     const HeavyItem it = items[blockIdx.x % n_items];
@@ -829,17 +849,17 @@ __global__ __launch_bounds__(256) void car_hub_kernel(const HeavyItem *__restric
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int2 *col = reinterpret_cast<int2 *>(lds);                       // [G][dpad]
-    unsigned *tabs = reinterpret_cast<unsigned *>(col + G * dpad);   // [4][H] (x2 for the hash)
+    unsigned *tabs = reinterpret_cast<unsigned *>(col + G * dpad);   // [kW][Hw]
     const int d = it.d;
     const int total = d << lg;
     // stage: element e -> (neighbour j = e >> lg, scenario si = e & (G-1)); loads
     // unconditional (clamped), duplicates rewrite identical values
-    constexpr int kB = 16;  // d * G <= 4096 staged in one batch of loads (3 dependent round trips)
-    for (int e0 = 0; e0 < total; e0 += 256 * kB) {
+    constexpr int kB = 4096 / kT;
+    for (int e0 = 0; e0 < total; e0 += kT * kB) {
         int e[kB], q[kB], n[kB];
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
-            e[u] = min(e0 + u * 256 + tid, total - 1);
+            e[u] = min(e0 + u * kT + tid, total - 1);
             q[u] = hcol[it.rb + (e[u] >> lg)];
         }
 #pragma unroll
@@ -852,52 +872,86 @@ __global__ __launch_bounds__(256) void car_hub_kernel(const HeavyItem *__restric
             col[si * dpad + (e[u] >> lg)] = make_int2(n[u], ok ? key : kKeyHaz);
         }
     }
-    const int Hw = kDirect ? H : 2 * H;  // words per wave table
-    for (int k = tid; k < 4 * Hw; k += 256) tabs[k] = 0u;
+    const int Hw = kCnt == kHubHash ? 2 * H : H;  // words per wave table
+    for (int k = tid; k < kW * Hw; k += kT) tabs[k] = 0u;
     __syncthreads();
-    HubTable<kDirect> tb;
-    tb.cnts = tabs + wave * Hw + (kDirect ? 0 : H);
+    HubTable<kCnt> tb;
     tb.keys = tabs + wave * Hw;
+    tb.cnts = tb.keys + (kCnt == kHubHash ? H : 0);
     tb.mask = (unsigned)H - 1u;
-    const int nj = (d + 63) >> 6;  // entry slots per lane
-    for (int si = wave; si < G && s0 + si < S; si += 4) {
+    constexpr int R = NJ > 0 ? NJ : 1;
+    const int nj = NJ > 0 ? NJ : (d + 63) >> 6;  // entry slots per lane
+    for (int si = wave; si < G && s0 + si < S; si += kW) {
         const int2 *c = col + si * dpad;
-        for (int i = 0; i < nj; ++i) {  // A
-            const int j = i * 64 + lane;
-            const int2 x = c[min(j, d - 1)];
-            if (j < d && x.y != kKeyHaz) tb.add(x.x);
-        }
         int M = 0;
-        for (int i = 0; i < nj; ++i) {  // B
-            const int j = i * 64 + lane;
-            const int2 x = c[min(j, d - 1)];
-            if (j < d && x.y != kKeyHaz) M = max(M, tb.get(x.x));
-        }
-        M = dpp_max(M);
         unsigned long long best = 0;
         int nm = 0;
-        if (M > 0) {
-            for (int i = 0; i < nj; ++i) {  // C
+        if (NJ > 0) {
+            int xn[R], xk[R], cn[R];
+#pragma unroll
+            for (int i = 0; i < R; ++i) {
                 const int j = i * 64 + lane;
                 const int2 x = c[min(j, d - 1)];
-                const bool m = j < d && x.y != kKeyHaz && tb.get(x.x) == M;
+                xn[i] = x.x;
+                xk[i] = j < d ? x.y : kKeyHaz;
+            }
+#pragma unroll
+            for (int i = 0; i < R; ++i)  // A
+                if (xk[i] != kKeyHaz) tb.add(xn[i]);
+#pragma unroll
+            for (int i = 0; i < R; ++i) {  // B
+                cn[i] = xk[i] != kKeyHaz ? tb.get(xn[i]) : 0;
+                M = max(M, cn[i]);
+            }
+            M = dpp_max(M);
+#pragma unroll
+            for (int i = 0; i < R; ++i) {  // C
+                const bool m = cn[i] == M;
                 nm += __builtin_popcountll(__builtin_amdgcn_ballot_w64(m));
-                const unsigned long long k = m ? pack_rn(x.y, x.x) : 0ull;
+                const unsigned long long k = m ? pack_rn(xk[i], xn[i]) : 0ull;
                 best = k > best ? k : best;
             }
-            best = dpp_max_u64(best);
-        }
-        const int rb = (int)((unsigned)(best >> kNodeBits) ^ 0x80000000u);
-        const int nb = (int)(kNodeMask - (unsigned)(best & kNodeMask));
-        if (kDirect) {  // D
-            for (int i = 0; i < nj; ++i) {
+            if (M > 0) best = dpp_max_u64(best);
+            if (kCnt != kHubHash) {  // D
+#pragma unroll
+                for (int i = 0; i < R; ++i)
+                    if (xk[i] != kKeyHaz) tb.clear(xn[i]);
+            }
+        } else {
+            for (int i = 0; i < nj; ++i) {  // A
                 const int j = i * 64 + lane;
                 const int2 x = c[min(j, d - 1)];
-                if (j < d && x.y != kKeyHaz) tb.cnts[x.x >> 1] = 0u;
+                if (j < d && x.y != kKeyHaz) tb.add(x.x);
             }
-        } else {  // a probe may still need a slot another lane cleared: wipe the whole table
-            for (int k = lane; k < Hw; k += 64) tb.keys[k] = 0u;
+            for (int i = 0; i < nj; ++i) {  // B
+                const int j = i * 64 + lane;
+                const int2 x = c[min(j, d - 1)];
+                if (j < d && x.y != kKeyHaz) M = max(M, tb.get(x.x));
+            }
+            M = dpp_max(M);
+            if (M > 0) {
+                for (int i = 0; i < nj; ++i) {  // C
+                    const int j = i * 64 + lane;
+                    const int2 x = c[min(j, d - 1)];
+                    const bool m = j < d && x.y != kKeyHaz && tb.get(x.x) == M;
+                    nm += __builtin_popcountll(__builtin_amdgcn_ballot_w64(m));
+                    const unsigned long long k = m ? pack_rn(x.y, x.x) : 0ull;
+                    best = k > best ? k : best;
+                }
+                best = dpp_max_u64(best);
+            }
+            if (kCnt != kHubHash) {  // D
+                for (int i = 0; i < nj; ++i) {
+                    const int j = i * 64 + lane;
+                    const int2 x = c[min(j, d - 1)];
+                    if (j < d && x.y != kKeyHaz) tb.clear(x.x);
+                }
+            }
         }
+        if (kCnt == kHubHash)  // a probe may still need a slot another lane cleared: wipe the whole table
+            for (int k = lane; k < Hw; k += 64) tb.keys[k] = 0u;
+        const int rb = (int)((unsigned)(best >> kNodeBits) ^ 0x80000000u);
+        const int nb = (int)(kNodeMask - (unsigned)(best & kNodeMask));
         if (lane == 0) {
             const int s = s0 + si;
             int sc, t;
@@ -975,30 +1029,66 @@ int env_int(const char *name, int dflt) {
 }
 
 struct HeavyGeom {
-    int lg, dpad, H;
-    bool direct;
+    int lg, dpad, H, mode, waves;
     size_t lds;
 };
 
 constexpr int kDirectMaxN = 16384;  // direct count tables up to 32 KiB per wave
 
 HeavyGeom heavy_geometry(int dmax, int S, int N) {
-    // Largest scenario group G = 2^lg (<= 64, <= next_pow2(S)) whose staged
-    // columns + 4 wave tables fit 80 KiB (2 workgroups per CU), else 160 KiB.
+    // Count table per wave: u8 / u16 direct counters (N <= kDirectMaxN), else a
+    // hash of 2 * next_pow2(2 * dmax) words.  Then the widest (waves, G = 2^lg
+    // scenario group) whose staged columns + tables fit 80 KiB (2 workgroups
+    // per CU), preferring 8 waves, then 4; else the same within 160 KiB.
     HeavyGeom g;
     g.dpad = dmax | 1;
-    g.direct = N <= kDirectMaxN;
-    g.H = g.direct ? (N + 1) / 2 : next_pow2(2 * dmax);
-    const size_t tab = (size_t)4 * (g.direct ? g.H : 2 * g.H) * 4;
+    if (N <= kDirectMaxN) {
+        g.mode = dmax <= 255 ? kHubU8 : kHubU16;
+        g.H = g.mode == kHubU8 ? (N + 3) / 4 : (N + 1) / 2;
+    } else {
+        g.mode = kHubHash;
+        g.H = next_pow2(2 * dmax);
+    }
+    const size_t words = g.mode == kHubHash ? 2 * (size_t)g.H : (size_t)g.H;
     const int gmax = std::min(64, next_pow2(S));
     for (size_t lim : {(size_t)80 * 1024, (size_t)160 * 1024})
-        for (int G = gmax; G >= 1; G >>= 1) {
-            g.lds = (size_t)G * g.dpad * 8 + tab;
-            g.lg = 0;
-            while ((1 << g.lg) < G) ++g.lg;
-            if (g.lds <= lim) return g;
-        }
+        for (int w : {8, 4})
+            for (int G = gmax; G >= std::min(gmax, 8); G >>= 1) {
+                g.waves = w;
+                g.lds = (size_t)G * g.dpad * 8 + (size_t)w * words * 4;
+                g.lg = 0;
+                while ((1 << g.lg) < G) ++g.lg;
+                if (g.lds <= lim) return g;
+            }
+    for (int G = gmax; G >= 1; G >>= 1) {  // last resort: 4 waves, small groups
+        g.waves = 4;
+        g.lds = (size_t)G * g.dpad * 8 + 4 * words * 4;
+        g.lg = 0;
+        while ((1 << g.lg) < G) ++g.lg;
+        if (g.lds <= (size_t)160 * 1024) return g;
+    }
     return g;
+}
+
+typedef void (*HubKern)(const HeavyItem *, int, const int *, const int *, const int *, int, int, int, int, int,
+                        const int *, const unsigned long long *, int *, int *);
+
+template <int kCnt, int kW>
+HubKern hub_kern_nj(int nj) {
+    switch (nj) {
+        case 2: return &car_hub_kernel<kCnt, 2, kW>;
+        case 4: return &car_hub_kernel<kCnt, 4, kW>;
+        case 8: return &car_hub_kernel<kCnt, 8, kW>;
+        case 16: return &car_hub_kernel<kCnt, 16, kW>;
+        default: return &car_hub_kernel<kCnt, 0, kW>;
+    }
+}
+
+template <int kW>
+HubKern hub_kern_mode(int mode, int nj) {
+    if (mode == kHubU8) return hub_kern_nj<kHubU8, kW>(nj);
+    if (mode == kHubU16) return hub_kern_nj<kHubU16, kW>(nj);
+    return hub_kern_nj<kHubHash, kW>(nj);
 }
 
 // Locality order of the pods: DFS over the (deduplicated) relation graph, each
@@ -1315,12 +1405,15 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, const int 
         RSK_CHECK(g.lds <= 160 * 1024, "hub class %d needs %zu B of LDS", c, g.lds);
         const int64_t groups = ceil_div(S, 1 << g.lg);
         RSK_CHECK(groups * n < INT32_MAX, "hub grid too large");
-        auto kern = g.direct ? &car_hub_kernel<true> : &car_hub_kernel<false>;
+        const HubKern kern = g.waves == 8 ? hub_kern_mode<8>(g.mode, kHeavyNJ[c]) : hub_kern_mode<4>(g.mode, kHeavyNJ[c]);
         if (g.lds > 64 * 1024)
             RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds));
-        ScopedTimer tm(ctx, "car_heavy", stream);
-        kern<<<dim3((unsigned)(groups * n)), dim3(256), g.lds, stream>>>(
+        static const char *const kHubNames[kNumHeavy] = {"car_hub128", "car_hub256", "car_hub512",
+                                                         "car_hub1024", "car_hub2048", "car_hub4096"};
+        static const bool per_class = env_int("RSK_HUB_TIMERS", 0) != 0;
+        ScopedTimer tm(ctx, per_class ? kHubNames[c] : "car_heavy", stream);
+        kern<<<dim3((unsigned)(groups * n)), dim3(64 * g.waves), g.lds, stream>>>(
             plan->heavy_items[c].as<HeavyItem>(), n, plan->hcol.as<int>(), d_assign, d_key, S, N, g.lg, g.dpad,
             g.H, d_zcnt, d_zkey, d_target, d_score);
         RSK_HIP(hipGetLastError());
@@ -1428,18 +1521,18 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     {   // K0: 4 scenarios per thread when S % 4 == 0 (16-B use / nodekey words)
         const bool v4 = S % 4 == 0 && ((uintptr_t)d_use % 16) == 0 && ((uintptr_t)d_haz % 4) == 0;
         const int SV = v4 ? S / 4 : S;
-        const int target_threads = v4 ? 256 * 512 : 256 * 2048;  // 4 zero-case atomics per 4-wide thread
+        const int target_threads = 256 * 1024;
         const int npb = (int)std::max<int64_t>(1, ceil_div((int64_t)N * SV, target_threads));
         const int64_t chunks = ceil_div(N, npb);
         const unsigned total = (unsigned)(chunks * SV);
         ScopedTimer tm(ctx, "car_prep");
         if (v4)
-            car_prep4_kernel<<<dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, ctx->stream>>>(
+            car_prep_kernel<4><<<dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, ctx->stream>>>(
                 d_cap, reinterpret_cast<const int4 *>(d_use), reinterpret_cast<const uchar4 *>(d_haz), N, SV, npb,
                 total, reinterpret_cast<int4 *>(d_key), d_zcnt, d_zkey);
         else
-            car_prep1_kernel<<<dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, ctx->stream>>>(
-                d_cap, d_use, d_haz, N, S, npb, total, d_key, d_zcnt, d_zkey);
+            car_prep_kernel<1><<<dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, ctx->stream>>>(
+                d_cap, d_use, d_haz, N, SV, npb, total, d_key, d_zcnt, d_zkey);
         RSK_HIP(hipGetLastError());
     }
     // mid and hub rows run on the side stream, overlapping the tile kernel

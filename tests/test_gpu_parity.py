@@ -144,6 +144,34 @@ def test_car_degree_bucket_boundaries(ctx, S):
     assert info["sorted_rows"] >= 3 and info["mid_rows"] >= 3 and info["heavy_rows"] >= 5 and info["tile_rows"] > 0, info
 
 
+@pytest.mark.parametrize("S", [1, 40])
+def test_car_hub_exact_degrees_and_counter_limits(ctx, S):
+    """Hub rows of exact degree at the hub class edges (u8 counters up to 255,
+    u16 from 256, register entries up to 1024, LDS re-reads beyond), with
+    scenarios that pile every neighbour onto one node (count == degree)."""
+    rng = np.random.default_rng(400 + S)
+    degs = [65, 127, 128, 129, 254, 255, 256, 257, 511, 512, 513, 1023, 1024, 1025, 2049]
+    P, N = 2200, 30
+    rows = [rng.choice(P, d, replace=False).tolist() for d in degs]
+    rows = [[q for q in r if q != k] for k, r in enumerate(rows)]
+    rows += [rng.integers(0, P, int(rng.integers(0, 4))).tolist() for _ in range(P - len(degs))]
+    rp = np.zeros(P + 1, np.int32)
+    rp[1:] = np.cumsum([len(r) for r in rows])
+    ci = np.array([q for r in rows for q in r], np.int32)
+    a = rng.integers(-1, N, (P, S)).astype(np.int32)
+    a[:, 0] = 7                      # scenario 0: every pod on node 7 -> count == degree
+    if S > 1:
+        a[:, 1] = rng.integers(0, 2, P)  # two nodes, near-ties
+    a = a.reshape(-1)
+    cap = rng.choice([4000, 8000], N).astype(np.int32)
+    use = rng.integers(0, 8000, N * S).astype(np.int32)
+    haz = (rng.random(N * S) < 0.1).astype(np.uint8)
+    haz.reshape(N, S)[7, 0] = 0
+    qrows = np.arange(0, len(degs) + 20, dtype=np.int32)
+    tgt = _check_car(ctx, rp, ci, a, S, cap, use, haz, N, rows=qrows, label=f"hub degrees S={S}")
+    assert (tgt.reshape(len(qrows), S)[:len(degs), 0] == 7).all()
+
+
 def test_car_heavy_hash_path_large_n(ctx):
     """N > 16384 switches heavy rows from direct LDS count tables to the LDS hash."""
     rng = np.random.default_rng(21)
