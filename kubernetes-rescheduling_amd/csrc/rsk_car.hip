@@ -309,7 +309,8 @@ struct TileArgs {
     int S, N, T, lsl, rmax;  // SL = 1 << lsl scenarios per workgroup
     int rec_cap;             // record ints reserved in LDS (largest tile, x4); the unit counter follows
     int ablate;              // profiling only (RSK_ABLATE_TILE): 1 skip image load, 2 skip scoring
-    int order;               // 0 chunk-major, 1 tile-major grid (RSK_TILE_ORDER)
+    int order;               // grid order (RSK_TILE_ORDER): 0 chunk-major, 1 tile-major, 2 XCD-contiguous
+    int xcd_per;             // order 2: (tile, chunk) units per XCD
     unsigned n_assign, n_out, n_pods, n_recs, n_key;  // element counts (debug bounds build)
 };
 
@@ -426,8 +427,10 @@ __device__ __forceinline__ int rec_row(const int (&r)[W], int j) {
     return (j & 1) ? (int)(pr >> 16) : (int)(pr & 0xffffu);
 }
 
-// 0 or 3 <= d <= D (D = 4, 8, 16): pairwise equality counts in registers, then
-// the lexicographic (count, key, -node) maximum over the candidates in 32-bit steps.
+// 0 or 3 <= d <= D (D = 4, 8, 16): pairwise equality counts in registers,
+// c[j] = #{i < j : node i == node j}, so a node's last entry holds its count
+// - 1 and the entries at the maximum are exactly one per maximal node; then
+// the lexicographic (count, key, -node) maximum over them in 32-bit steps.
 template <int D, int W, bool kScore, bool kOff32, class Img>
 __device__ __forceinline__ void tile_dn(const TileArgs &a, const Img &img, const int *rec, int n, const TileLane &L,
                                         int p0) {
@@ -443,34 +446,31 @@ __device__ __forceinline__ void tile_dn(const TileArgs &a, const Img &img, const
             // (a node id no real entry can hold) and of the candidates
             nd[j] = j < d ? e.x : -1 - j;
             ky[j] = j < d ? e.y : kKeyHaz;
-            c[j] = 1;
+            c[j] = 0;
         }
 #pragma unroll
         for (int j = 1; j < D; ++j)
 #pragma unroll
-            for (int i2 = 0; i2 < j; ++i2) {
-                const int eq = nd[j] == nd[i2];
-                c[j] += eq;
-                c[i2] += eq;
-            }
-        int M = 0;
+            for (int i2 = 0; i2 < j; ++i2) c[j] += nd[j] == nd[i2];
+        // hazard nodes (all their entries carry KEY_HAZ) leave the count
+        int M1 = -1;
 #pragma unroll
         for (int j = 0; j < D; ++j) {
-            c[j] = ky[j] == kKeyHaz ? 0 : c[j];
-            M = max(M, c[j]);
+            c[j] = ky[j] == kKeyHaz ? -1 : c[j];
+            M1 = max(M1, c[j]);
         }
         int kb = INT_MIN;
 #pragma unroll
-        for (int j = 0; j < D; ++j) kb = max(kb, c[j] == M ? ky[j] : INT_MIN);
+        for (int j = 0; j < D; ++j) kb = max(kb, c[j] == M1 ? ky[j] : INT_MIN);
         int nb = INT_MAX, nm = 0;
 #pragma unroll
         for (int j = 0; j < D; ++j) {
-            const bool m = c[j] == M;
+            const bool m = c[j] == M1;
             nb = min(nb, (m && ky[j] == kb) ? nd[j] : INT_MAX);
             nm += m;
         }
-        const int tt = nm == M ? nb : (kb >= 0 ? nb : RSK_TARGET_NONE);
-        tile_emit<kScore, kOff32>(a, r[0], L, M == 0 ? L.zt : tt, M == 0 ? L.zs : M);
+        const int tt = nm == 1 ? nb : (kb >= 0 ? nb : RSK_TARGET_NONE);
+        tile_emit<kScore, kOff32>(a, r[0], L, M1 < 0 ? L.zt : tt, M1 < 0 ? L.zs : M1 + 1);
     }
 }
 
@@ -585,9 +585,17 @@ __global__ __launch_bounds__(kTileThreads, 4) void car_tile_kernel(TileArgs a) {
     extern __shared__ __attribute__((aligned(16))) int lds[];  // img {node,key} [rmax][SL], then records
     // chunk-major (default: concurrent workgroups share a chunk's nodekey
     // slice in L2) or tile-major (a tile's chunks back to back)
+    // or XCD-contiguous (blocks b and b + 8 share an XCD: each XCD walks its own
+    // run of chunk-major units, so a chunk's nodekey slice is fetched into one
+    // L2 instead of all eight)
     const int nchunk = (a.S + (1 << a.lsl) - 1) >> a.lsl;
-    const int tile = a.order ? blockIdx.x / nchunk : blockIdx.x % a.T;
-    const int chunk = a.order ? blockIdx.x % nchunk : blockIdx.x / a.T;
+    int unit = blockIdx.x;
+    if (a.order == 2) {
+        unit = (int)(blockIdx.x & 7u) * a.xcd_per + (int)(blockIdx.x >> 3);
+        if (unit >= nchunk * a.T) return;  // whole workgroup, before any barrier
+    }
+    const int tile = a.order == 1 ? unit / nchunk : unit % a.T;
+    const int chunk = a.order == 1 ? unit % nchunk : unit / a.T;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int SL = 1 << a.lsl;
     const int s0 = chunk * SL;
@@ -697,7 +705,7 @@ __device__ __forceinline__ void mid_row(const MidArgs &a, const int *__restrict_
 #pragma unroll
     for (int j = 0; j < D; ++j) v[j] = (j < d && (unsigned)v[j] < (unsigned)a.sc.N) ? v[j] : INT_MAX;
     bitonic_sort<D, int>(v);
-    constexpr int kC = 32;
+    constexpr int kC = D > 32 ? 16 : 32;  // key gathers in flight (D = 64: keeps 3 waves per SIMD)
     unsigned long long best = 0;
     int M = 0, R = 0, c = 0;
 #pragma unroll
@@ -746,18 +754,7 @@ __global__ __launch_bounds__(256) void car_mid_kernel(MidArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// K3: hub rows (deg > 64).  Workgroup (4 waves) = (row, group of G scenarios).
-//   stage  col[si][j] = {node, key} of neighbour j in scenario s0+si: each
-//          neighbour row's G consecutive scenarios in one coalesced segment, its
-//          node keys gathered right away (hazard / unscheduled -> KEY_HAZ);
-//   score  wave w takes scenarios si = w, w+4, ...; lanes = neighbours:
-//          A count every candidate entry into the wave's own LDS table
-//          B max count M                                  (DPP wave max)
-//          C max (remaining CPU, -node) among entries at count M  (DPP wave max)
-//            and their number nm = M * |best|             (ballot popcount)
-//          D clear the table for the next scenario.
-// Tables: two u16 counters per word indexed by node id when N <= 16384, else
-// an open-addressing hash (keys + counts) of next_pow2(2 * deg) slots.
+// K3: hub rows (deg > 64), see car_hub_kernel below.
 // ---------------------------------------------------------------------------
 struct HeavyItem {
     int oi, rb, d, pad;
@@ -1363,7 +1360,9 @@ int plan_create(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, in
 }
 
 // Mid (17..64, N >= kPackMaxN variant only) and hub (> 64) rows, queued on `stream`.
-int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, const int *d_assign, const int *d_key,
+// side[0]: mid rows and the hub classes <= 255; side[1]: the larger hub classes
+// (few rows, latency-bound: they overlap the others best on their own queue).
+int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t side[2], const int *d_assign, const int *d_key,
                 const int *d_zcnt, const unsigned long long *d_zkey, int *d_target, int *d_score, int S, int N) {
     ScoreCtx sc;
     sc.nodekey = d_key;
@@ -1393,14 +1392,15 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, const int 
             a.blocks_per_chunk = (int)ceil_div(waves, 4);
             const int64_t blocks = chunks * a.blocks_per_chunk;
             RSK_CHECK(blocks < INT32_MAX, "mid grid too large");
-            ScopedTimer tm(ctx, "car_mid", stream);
-            car_mid_kernel<<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(a);
+            ScopedTimer tm(ctx, "car_mid", side[0]);
+            car_mid_kernel<<<dim3((unsigned)blocks), dim3(256), 0, side[0]>>>(a);
             RSK_HIP(hipGetLastError());
         }
     }
     for (int c = 0; c < kNumHeavy; ++c) {   // K3 hub rows
         const int n = plan->n_heavy[c];
         if (!n) continue;
+        const hipStream_t stream = kHeavyMax[c] <= 255 ? side[0] : side[1];
         const HeavyGeom g = heavy_geometry(plan->heavy_dmax[c], S, N);
         RSK_CHECK(g.lds <= 160 * 1024, "hub class %d needs %zu B of LDS", c, g.lds);
         const int64_t groups = ceil_div(S, 1 << g.lg);
@@ -1535,12 +1535,15 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
                 d_cap, d_use, d_haz, N, SV, npb, total, d_key, d_zcnt, d_zkey);
         RSK_HIP(hipGetLastError());
     }
-    // mid and hub rows run on the side stream, overlapping the tile kernel
-    static const bool overlap = env_int("RSK_OVERLAP", 1) != 0;
-    hipStream_t side = ctx->stream;
-    if (overlap && plan_has_side(plan) && plan->T > 0) {
-        RSK_TRY(aux_fork(ctx));
-        side = ctx->aux;
+    // mid and hub rows run on side streams (RSK_OVERLAP = how many, 0..2),
+    // overlapping the tile kernel and each other
+    static const int overlap = std::max(0, std::min(2, env_int("RSK_OVERLAP", 2)));
+    hipStream_t side[2] = {ctx->stream, ctx->stream};
+    const int nside = plan_has_side(plan) && plan->T > 0 ? overlap : 0;
+    if (nside) {
+        RSK_TRY(aux_fork(ctx, nside));
+        side[0] = ctx->aux[0];
+        side[1] = ctx->aux[nside - 1];
     }
     RSK_TRY(launch_side(plan, ctx, side, d_assign, d_key, d_zcnt, d_zkey, d_target, d_score, S, N));
     if (plan->T > 0) {   // K1 tiles
@@ -1569,7 +1572,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         a.lsl = 0;
         while ((1 << a.lsl) < SL) ++a.lsl;
         static const int ablate = env_int("RSK_ABLATE_TILE", 0);
-        static const int order = env_int("RSK_TILE_ORDER", 0);
+        static const int order = env_int("RSK_TILE_ORDER", 2);
         a.order = order;
         a.ablate = ablate;
         const bool off32 = (int64_t)std::max(plan->P, plan->Q) * S * 4 < ((int64_t)1 << 32);
@@ -1578,7 +1581,9 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         const int cells = plan->rmax * SL;
         const size_t lds = ((size_t)(n16 ? tile_img_ints<true>(cells) : tile_img_ints<false>(cells)) + a.rec_cap + 4) * 4;
         RSK_CHECK(lds <= 160 * 1024 && plan->recmax <= kTileRecInts, "tile image needs %zu B of LDS", lds);
-        const int64_t blocks = ceil_div(S, SL) * plan->T;
+        const int64_t units = ceil_div(S, SL) * plan->T;
+        a.xcd_per = (int)ceil_div(units, 8);
+        const int64_t blocks = order == 2 ? 8 * (int64_t)a.xcd_per : units;
         RSK_CHECK(blocks < INT32_MAX, "tile grid too large");
         using TileKern = void (*)(TileArgs);
         static const TileKern kerns[8] = {
@@ -1594,7 +1599,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         kern<<<dim3((unsigned)blocks), dim3(kTileThreads), lds, ctx->stream>>>(a);
         RSK_HIP(hipGetLastError());
     }
-    if (side != ctx->stream) RSK_TRY(aux_join(ctx));
+    if (nside) RSK_TRY(aux_join(ctx, nside));
 #ifdef RSK_DEBUG_BOUNDS
     {
         unsigned flags_h = 0, zero = 0;

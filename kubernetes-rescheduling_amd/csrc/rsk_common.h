@@ -61,8 +61,8 @@ struct rsk_ctx {
     bool profiling = false;
     std::map<std::string, std::vector<rsk::EventPair>> pending;
     std::map<std::string, std::pair<double, int64_t>> totals;
-    hipStream_t aux = nullptr;   // side stream: CAR mid/hub rows overlap the tile kernel
-    hipEvent_t fork = nullptr, join = nullptr;
+    hipStream_t aux[2] = {};     // side streams: CAR mid/hub rows overlap the tile kernel
+    hipEvent_t fork = nullptr, join[2] = {};
     rsk::DevBuf host_stage[12];  // device staging for host-pointer calls
     rsk::DevBuf work[6];         // per-call device workspace
     std::vector<uint8_t> pinned;  // host scratch
@@ -80,11 +80,11 @@ struct ScopedTimer {
     ~ScopedTimer();
 };
 
-// Fork / join of the context's side stream around work that may overlap the
-// main stream: fork() makes aux wait for everything queued on ctx->stream so
-// far; join() makes ctx->stream wait for everything queued on aux.
-int aux_fork(rsk_ctx *ctx);
-int aux_join(rsk_ctx *ctx);
+// Fork / join of the context's first k side streams around work that may
+// overlap the main stream: fork() makes aux[0..k) wait for everything queued on
+// ctx->stream so far; join() makes ctx->stream wait for everything queued on them.
+int aux_fork(rsk_ctx *ctx, int k);
+int aux_join(rsk_ctx *ctx, int k);
 
 int activate(rsk_ctx *ctx);
 

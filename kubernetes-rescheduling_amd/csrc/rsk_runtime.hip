@@ -51,20 +51,24 @@ ScopedTimer::~ScopedTimer() {
     ctx->pending[name].push_back({a, b});
 }
 
-int aux_fork(rsk_ctx *ctx) {
-    if (!ctx->aux) {
-        RSK_HIP(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
-        RSK_HIP(hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming));
-        RSK_HIP(hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming));
-    }
+int aux_fork(rsk_ctx *ctx, int k) {
+    if (!ctx->fork) RSK_HIP(hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming));
     RSK_HIP(hipEventRecord(ctx->fork, ctx->stream));
-    RSK_HIP(hipStreamWaitEvent(ctx->aux, ctx->fork, 0));
+    for (int i = 0; i < k; ++i) {
+        if (!ctx->aux[i]) {
+            RSK_HIP(hipStreamCreateWithFlags(&ctx->aux[i], hipStreamNonBlocking));
+            RSK_HIP(hipEventCreateWithFlags(&ctx->join[i], hipEventDisableTiming));
+        }
+        RSK_HIP(hipStreamWaitEvent(ctx->aux[i], ctx->fork, 0));
+    }
     return RSK_OK;
 }
 
-int aux_join(rsk_ctx *ctx) {
-    RSK_HIP(hipEventRecord(ctx->join, ctx->aux));
-    RSK_HIP(hipStreamWaitEvent(ctx->stream, ctx->join, 0));
+int aux_join(rsk_ctx *ctx, int k) {
+    for (int i = 0; i < k; ++i) {
+        RSK_HIP(hipEventRecord(ctx->join[i], ctx->aux[i]));
+        RSK_HIP(hipStreamWaitEvent(ctx->stream, ctx->join[i], 0));
+    }
     return RSK_OK;
 }
 
@@ -131,12 +135,13 @@ int rsk_ctx_destroy(rsk_ctx *ctx) {
         for (auto &e : kv.second) { (void)hipEventDestroy(e.start); (void)hipEventDestroy(e.stop); }
     for (auto &b : ctx->host_stage) b.release();
     for (auto &b : ctx->work) b.release();
-    if (ctx->aux) {
-        (void)hipStreamSynchronize(ctx->aux);
-        (void)hipStreamDestroy(ctx->aux);
-        (void)hipEventDestroy(ctx->fork);
-        (void)hipEventDestroy(ctx->join);
-    }
+    for (int i = 0; i < 2; ++i)
+        if (ctx->aux[i]) {
+            (void)hipStreamSynchronize(ctx->aux[i]);
+            (void)hipStreamDestroy(ctx->aux[i]);
+            (void)hipEventDestroy(ctx->join[i]);
+        }
+    if (ctx->fork) (void)hipEventDestroy(ctx->fork);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
     return RSK_OK;
