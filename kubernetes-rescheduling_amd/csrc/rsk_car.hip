@@ -320,9 +320,14 @@ __device__ __forceinline__ size_t cell(unsigned i, unsigned S, unsigned s) {
     if (kOff32) return (size_t)((i * S + s) << 2);
     return ((size_t)i * S + s) << 2;
 }
+#ifndef RSK_TILE_NT
+#define RSK_TILE_NT 3  // streamed tile loads / stores non-temporal (nodekey lines stay in L2)
+#endif
 template <bool kOff32>
 __device__ __forceinline__ void st_cell(int *base, unsigned i, unsigned S, unsigned s, int v) {
-    *reinterpret_cast<int *>(reinterpret_cast<char *>(base) + cell<kOff32>(i, S, s)) = v;
+    int *p = reinterpret_cast<int *>(reinterpret_cast<char *>(base) + cell<kOff32>(i, S, s));
+    if (RSK_TILE_NT & 2) __builtin_nontemporal_store(v, p);
+    else *p = v;
 }
 
 // Per-lane constants of the scoring phase.  Lanes past the last scenario (a
@@ -555,7 +560,8 @@ __device__ __forceinline__ void tile_load_image(const TileArgs &a, const Img &im
 #ifdef RSK_DEBUG_BOUNDS
             if ((size_t)(unsigned)pod[u] * S + s >= a.n_assign) { atomicOr(&rsk_dbg_flags, 4u); pod[u] = 0; }
 #endif
-            v[u] = *reinterpret_cast<const int *>(asg + cell<kOff32>((unsigned)pod[u], S, s));
+            const int *pa = reinterpret_cast<const int *>(asg + cell<kOff32>((unsigned)pod[u], S, s));
+            v[u] = (RSK_TILE_NT & 1) ? __builtin_nontemporal_load(pa) : *pa;
         }
 #pragma unroll
         for (int u = 0; u < kE; ++u) {
@@ -596,7 +602,7 @@ __global__ __launch_bounds__(kTileThreads, 4) void car_tile_kernel(TileArgs a) {
     }
     const int tile = a.order == 1 ? unit / nchunk : unit % a.T;
     const int chunk = a.order == 1 ? unit % nchunk : unit / a.T;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
     const int SL = 1 << a.lsl;
     const int s0 = chunk * SL;
     const int cells = a.rmax * SL;

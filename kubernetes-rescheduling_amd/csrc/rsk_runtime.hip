@@ -56,7 +56,12 @@ int aux_fork(rsk_ctx *ctx, int k) {
     RSK_HIP(hipEventRecord(ctx->fork, ctx->stream));
     for (int i = 0; i < k; ++i) {
         if (!ctx->aux[i]) {
-            RSK_HIP(hipStreamCreateWithFlags(&ctx->aux[i], hipStreamNonBlocking));
+            // side work is short and latency-bound: with RSK_SIDE_PRIO=1 its
+            // workgroups are dispatched ahead of the tile kernel's as CUs free up
+            static const bool prio = getenv("RSK_SIDE_PRIO") && atoi(getenv("RSK_SIDE_PRIO")) != 0;
+            int lo = 0, hi = 0;
+            if (prio) RSK_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            RSK_HIP(hipStreamCreateWithPriority(&ctx->aux[i], hipStreamNonBlocking, prio ? hi : lo));
             RSK_HIP(hipEventCreateWithFlags(&ctx->join[i], hipEventDisableTiming));
         }
         RSK_HIP(hipStreamWaitEvent(ctx->aux[i], ctx->fork, 0));
