@@ -59,6 +59,9 @@ int rsk_ctx_synchronize(rsk_ctx *ctx);
 /* Kernel timing with HIP events recorded on the context's stream around every
  * launch of the named kernel ("car_light", "car_heavy", "car_prep", ...). */
 int rsk_ctx_set_profiling(rsk_ctx *ctx, int on);
+/* Restrict the timing events to launches of one kernel name (NULL or "" = all):
+ * fewer events inside a timed region. */
+int rsk_ctx_set_profile_only(rsk_ctx *ctx, const char *kernel);
 int rsk_ctx_kernel_time(rsk_ctx *ctx, const char *kernel, double *total_ms, int64_t *launches);
 int rsk_ctx_reset_profiling(rsk_ctx *ctx);
 

@@ -1543,7 +1543,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     }
     // mid and hub rows run on side streams (RSK_OVERLAP = how many, 0..2),
     // overlapping the tile kernel and each other
-    static const int overlap = std::max(0, std::min(2, env_int("RSK_OVERLAP", 2)));
+    static const int overlap = std::max(0, std::min(2, env_int("RSK_OVERLAP", 1)));
     hipStream_t side[2] = {ctx->stream, ctx->stream};
     const int nside = plan_has_side(plan) && plan->T > 0 ? overlap : 0;
     if (nside) {

@@ -59,6 +59,8 @@ struct rsk_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     bool profiling = false;
+    std::string profile_only;            // time only this kernel name (empty: all)
+    std::vector<hipEvent_t> event_pool;  // recycled timing events
     std::map<std::string, std::vector<rsk::EventPair>> pending;
     std::map<std::string, std::pair<double, int64_t>> totals;
     hipStream_t aux[2] = {};     // side streams: CAR mid/hub rows overlap the tile kernel

@@ -39,9 +39,27 @@ int activate(rsk_ctx *ctx) {
     return RSK_OK;
 }
 
+static hipEvent_t pooled_event(rsk_ctx *ctx) {
+    if (!ctx->event_pool.empty()) {
+        hipEvent_t e = ctx->event_pool.back();
+        ctx->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    return hipEventCreate(&e) == hipSuccess ? e : nullptr;
+}
+
 ScopedTimer::ScopedTimer(rsk_ctx *c, const char *n, hipStream_t s) : ctx(c), name(n), stream(s ? s : c->stream) {
     if (!ctx->profiling) return;
-    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) { a = b = nullptr; return; }
+    if (!ctx->profile_only.empty() && ctx->profile_only != name) return;
+    a = pooled_event(ctx);
+    b = pooled_event(ctx);
+    if (!a || !b) {
+        if (a) ctx->event_pool.push_back(a);
+        if (b) ctx->event_pool.push_back(b);
+        a = b = nullptr;
+        return;
+    }
     (void)hipEventRecord(a, stream);
 }
 
@@ -138,6 +156,7 @@ int rsk_ctx_destroy(rsk_ctx *ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     for (auto &kv : ctx->pending)
         for (auto &e : kv.second) { (void)hipEventDestroy(e.start); (void)hipEventDestroy(e.stop); }
+    for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     for (auto &b : ctx->host_stage) b.release();
     for (auto &b : ctx->work) b.release();
     for (int i = 0; i < 2; ++i)
@@ -182,8 +201,8 @@ int rsk_ctx_kernel_time(rsk_ctx *ctx, const char *kernel, double *total_ms, int6
             RSK_HIP(hipEventElapsedTime(&ms, e.start, e.stop));
             acc.first += ms;
             acc.second += 1;
-            (void)hipEventDestroy(e.start);
-            (void)hipEventDestroy(e.stop);
+            ctx->event_pool.push_back(e.start);
+            ctx->event_pool.push_back(e.stop);
         }
         it->second.clear();
     }
@@ -197,9 +216,15 @@ int rsk_ctx_reset_profiling(rsk_ctx *ctx) {
     RSK_TRY(activate(ctx));
     RSK_HIP(hipStreamSynchronize(ctx->stream));
     for (auto &kv : ctx->pending)
-        for (auto &e : kv.second) { (void)hipEventDestroy(e.start); (void)hipEventDestroy(e.stop); }
+        for (auto &e : kv.second) { ctx->event_pool.push_back(e.start); ctx->event_pool.push_back(e.stop); }
     ctx->pending.clear();
     ctx->totals.clear();
+    return RSK_OK;
+}
+
+int rsk_ctx_set_profile_only(rsk_ctx *ctx, const char *kernel) {
+    RSK_CHECK(ctx, "null context");
+    ctx->profile_only = kernel ? kernel : "";
     return RSK_OK;
 }
 

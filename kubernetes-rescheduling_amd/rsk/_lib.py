@@ -40,6 +40,7 @@ SIGNATURES = {
     "rsk_ctx_set_profiling": (C.c_int, [_vp, C.c_int]),
     "rsk_ctx_kernel_time": (C.c_int, [_vp, C.c_char_p, _f64p, _i64p]),
     "rsk_ctx_reset_profiling": (C.c_int, [_vp]),
+    "rsk_ctx_set_profile_only": (C.c_int, [_vp, C.c_char_p]),
     "rsk_car_plan_create": (C.c_int, [_vp, _vp, _vp, C.c_int32, _vp, C.c_int32, C.POINTER(_vp)]),
     "rsk_car_plan_destroy": (C.c_int, [_vp]),
     "rsk_car_plan_info": (C.c_int, [_vp, _vp, C.c_int]),
@@ -165,6 +166,10 @@ class Context:
 
     def set_profiling(self, on: bool):
         check(self.lib.rsk_ctx_set_profiling(self.handle, int(on)))
+
+    def set_profile_only(self, kernel: str | None):
+        """Time only launches of `kernel` (None: every kernel)."""
+        check(self.lib.rsk_ctx_set_profile_only(self.handle, kernel.encode() if kernel else None))
 
     def reset_profiling(self):
         check(self.lib.rsk_ctx_reset_profiling(self.handle))

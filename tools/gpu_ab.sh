@@ -11,7 +11,7 @@ for r in $(seq 1 "$reps"); do
         k=$((k + 1))
         name=v$k
         envs=$(echo "$v" | tr "," " "); [ "$v" = base ] && envs=""
-        env $envs timeout -k 10 300 python -u bench.py --steps 30 --warmup 3 --no-cpu-baseline > gpurun_out/ab/$name.$r.log 2>&1
+        env $envs timeout -k 10 300 python -u bench.py --steps 30 --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/ab/$name.$r.log 2>&1
         rc=$?
         echo "$r $name [$(echo "$v" | sed 's#.*/##' | cut -c1-60)] rc=$rc $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab/$name.$r.log) $(grep -o '"car_tile": {"avg_ms": [0-9.]*' gpurun_out/ab/$name.$r.log | cut -c24-30) $(grep -o '"parity_sample_ok": [a-z]*' gpurun_out/ab/$name.$r.log)"
         [ $rc -ne 0 ] && { tail -5 gpurun_out/ab/$name.$r.log; exit $rc; }
