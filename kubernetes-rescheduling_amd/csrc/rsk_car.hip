@@ -840,15 +840,16 @@ template <int kCnt, int NJ, int kW>
 __global__ __launch_bounds__(64 * kW) void car_hub_kernel(const HeavyItem *__restrict__ items, int n_items,
                                                           const int *__restrict__ hcol, const int *__restrict__ assign,
                                                           const int *__restrict__ nodekey, int S, int N, int lg, int dpad,
-                                                          int H, const int *__restrict__ zc_cnt,
+                                                          int H, int gpw, const int *__restrict__ zc_cnt,
                                                           const unsigned long long *__restrict__ zc_key,
                                                           int *__restrict__ out_target, int *__restrict__ out_score) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
     constexpr int kT = 64 * kW;
     const int G = 1 << lg;
-    const int grp = blockIdx.x / n_items;
+    const int ngroups = (S + G - 1) >> lg;
+    const int g0 = (blockIdx.x / n_items) * gpw;
+    const int g1 = min(g0 + gpw, ngroups);
     const HeavyItem it = items[blockIdx.x % n_items];
-    const int s0 = grp * G;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int2 *col = reinterpret_cast<int2 *>(lds);                       // [G][dpad]
@@ -856,118 +857,155 @@ __global__ __launch_bounds__(64 * kW) void car_hub_kernel(const HeavyItem *__res
     const int d = it.d;
     const int total = d << lg;
     // stage: element e -> (neighbour j = e >> lg, scenario si = e & (G-1)); loads
-    // unconditional (clamped), duplicates rewrite identical values
+    // unconditional (clamped), duplicates rewrite identical values.  When one
+    // batch covers the row (single), the neighbour ids stay in registers across
+    // the workgroup's groups and the next group's assign words load beside the
+    // current group's key gathers.
     constexpr int kB = 4096 / kT;
-    for (int e0 = 0; e0 < total; e0 += kT * kB) {
-        int e[kB], q[kB], n[kB];
+    const bool single = total <= kT * kB;
+    int e[kB], q[kB], n[kB];
+    if (single) {
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
-            e[u] = min(e0 + u * kT + tid, total - 1);
+            e[u] = min(u * kT + tid, total - 1);
             q[u] = hcol[it.rb + (e[u] >> lg)];
         }
 #pragma unroll
-        for (int u = 0; u < kB; ++u) n[u] = assign[(size_t)q[u] * S + min(s0 + (e[u] & (G - 1)), S - 1)];
-#pragma unroll
-        for (int u = 0; u < kB; ++u) {
-            const int si = e[u] & (G - 1), s = s0 + si;
-            const bool ok = (unsigned)n[u] < (unsigned)N && s < S;
-            const int key = ld32(nodekey, ok ? (unsigned)n[u] * (unsigned)S + (unsigned)s : 0u);
-            col[si * dpad + (e[u] >> lg)] = make_int2(n[u], ok ? key : kKeyHaz);
-        }
+        for (int u = 0; u < kB; ++u) n[u] = assign[(size_t)q[u] * S + min(g0 * G + (e[u] & (G - 1)), S - 1)];
     }
     const int Hw = kCnt == kHubHash ? 2 * H : H;  // words per wave table
     for (int k = tid; k < kW * Hw; k += kT) tabs[k] = 0u;
-    __syncthreads();
     HubTable<kCnt> tb;
     tb.keys = tabs + wave * Hw;
     tb.cnts = tb.keys + (kCnt == kHubHash ? H : 0);
     tb.mask = (unsigned)H - 1u;
     constexpr int R = NJ > 0 ? NJ : 1;
     const int nj = NJ > 0 ? NJ : (d + 63) >> 6;  // entry slots per lane
-    for (int si = wave; si < G && s0 + si < S; si += kW) {
-        const int2 *c = col + si * dpad;
-        int M = 0;
-        unsigned long long best = 0;
-        int nm = 0;
-        if (NJ > 0) {
-            int xn[R], xk[R], cn[R];
-#pragma unroll
-            for (int i = 0; i < R; ++i) {
-                const int j = i * 64 + lane;
-                const int2 x = c[min(j, d - 1)];
-                xn[i] = x.x;
-                xk[i] = j < d ? x.y : kKeyHaz;
+    for (int g = g0; g < g1; ++g) {
+        const int s0 = g * G;
+        if (single) {
+            int k[kB], nn[kB];
+    #pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                const int s = s0 + (e[u] & (G - 1));
+                const bool ok = (unsigned)n[u] < (unsigned)N && s < S;
+                k[u] = ld32(nodekey, ok ? (unsigned)n[u] * (unsigned)S + (unsigned)s : 0u);
             }
-#pragma unroll
-            for (int i = 0; i < R; ++i)  // A
-                if (xk[i] != kKeyHaz) tb.add(xn[i]);
-#pragma unroll
-            for (int i = 0; i < R; ++i) {  // B
-                cn[i] = xk[i] != kKeyHaz ? tb.get(xn[i]) : 0;
-                M = max(M, cn[i]);
-            }
-            M = dpp_max(M);
-#pragma unroll
-            for (int i = 0; i < R; ++i) {  // C
-                const bool m = cn[i] == M;
-                nm += __builtin_popcountll(__builtin_amdgcn_ballot_w64(m));
-                const unsigned long long k = m ? pack_rn(xk[i], xn[i]) : 0ull;
-                best = k > best ? k : best;
-            }
-            if (M > 0) best = dpp_max_u64(best);
-            if (kCnt != kHubHash) {  // D
-#pragma unroll
-                for (int i = 0; i < R; ++i)
-                    if (xk[i] != kKeyHaz) tb.clear(xn[i]);
+    #pragma unroll
+            for (int u = 0; u < kB; ++u) nn[u] = assign[(size_t)q[u] * S + min(s0 + G + (e[u] & (G - 1)), S - 1)];
+    #pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                const int si = e[u] & (G - 1), s = s0 + si;
+                const bool ok = (unsigned)n[u] < (unsigned)N && s < S;
+                col[si * dpad + (e[u] >> lg)] = make_int2(n[u], ok ? k[u] : kKeyHaz);
+                n[u] = nn[u];
             }
         } else {
-            for (int i = 0; i < nj; ++i) {  // A
-                const int j = i * 64 + lane;
-                const int2 x = c[min(j, d - 1)];
-                if (j < d && x.y != kKeyHaz) tb.add(x.x);
+            for (int e0 = 0; e0 < total; e0 += kT * kB) {
+                int eb[kB], qb[kB], nb[kB];
+    #pragma unroll
+                for (int u = 0; u < kB; ++u) {
+                    eb[u] = min(e0 + u * kT + tid, total - 1);
+                    qb[u] = hcol[it.rb + (eb[u] >> lg)];
+                }
+    #pragma unroll
+                for (int u = 0; u < kB; ++u) nb[u] = assign[(size_t)qb[u] * S + min(s0 + (eb[u] & (G - 1)), S - 1)];
+    #pragma unroll
+                for (int u = 0; u < kB; ++u) {
+                    const int si = eb[u] & (G - 1), s = s0 + si;
+                    const bool ok = (unsigned)nb[u] < (unsigned)N && s < S;
+                    const int key = ld32(nodekey, ok ? (unsigned)nb[u] * (unsigned)S + (unsigned)s : 0u);
+                    col[si * dpad + (eb[u] >> lg)] = make_int2(nb[u], ok ? key : kKeyHaz);
+                }
             }
-            for (int i = 0; i < nj; ++i) {  // B
-                const int j = i * 64 + lane;
-                const int2 x = c[min(j, d - 1)];
-                if (j < d && x.y != kKeyHaz) M = max(M, tb.get(x.x));
-            }
-            M = dpp_max(M);
-            if (M > 0) {
-                for (int i = 0; i < nj; ++i) {  // C
+        }
+        __syncthreads();
+        for (int si = wave; si < G && s0 + si < S; si += kW) {
+            const int2 *c = col + si * dpad;
+            int M = 0;
+            unsigned long long best = 0;
+            int nm = 0;
+            if (NJ > 0) {
+                int xn[R], xk[R], cn[R];
+    #pragma unroll
+                for (int i = 0; i < R; ++i) {
                     const int j = i * 64 + lane;
                     const int2 x = c[min(j, d - 1)];
-                    const bool m = j < d && x.y != kKeyHaz && tb.get(x.x) == M;
+                    xn[i] = x.x;
+                    xk[i] = j < d ? x.y : kKeyHaz;
+                }
+    #pragma unroll
+                for (int i = 0; i < R; ++i)  // A
+                    if (xk[i] != kKeyHaz) tb.add(xn[i]);
+    #pragma unroll
+                for (int i = 0; i < R; ++i) {  // B
+                    cn[i] = xk[i] != kKeyHaz ? tb.get(xn[i]) : 0;
+                    M = max(M, cn[i]);
+                }
+                M = dpp_max(M);
+    #pragma unroll
+                for (int i = 0; i < R; ++i) {  // C
+                    const bool m = cn[i] == M;
                     nm += __builtin_popcountll(__builtin_amdgcn_ballot_w64(m));
-                    const unsigned long long k = m ? pack_rn(x.y, x.x) : 0ull;
+                    const unsigned long long k = m ? pack_rn(xk[i], xn[i]) : 0ull;
                     best = k > best ? k : best;
                 }
-                best = dpp_max_u64(best);
-            }
-            if (kCnt != kHubHash) {  // D
-                for (int i = 0; i < nj; ++i) {
+                if (M > 0) best = dpp_max_u64(best);
+                if (kCnt != kHubHash) {  // D
+    #pragma unroll
+                    for (int i = 0; i < R; ++i)
+                        if (xk[i] != kKeyHaz) tb.clear(xn[i]);
+                }
+            } else {
+                for (int i = 0; i < nj; ++i) {  // A
                     const int j = i * 64 + lane;
                     const int2 x = c[min(j, d - 1)];
-                    if (j < d && x.y != kKeyHaz) tb.clear(x.x);
+                    if (j < d && x.y != kKeyHaz) tb.add(x.x);
+                }
+                for (int i = 0; i < nj; ++i) {  // B
+                    const int j = i * 64 + lane;
+                    const int2 x = c[min(j, d - 1)];
+                    if (j < d && x.y != kKeyHaz) M = max(M, tb.get(x.x));
+                }
+                M = dpp_max(M);
+                if (M > 0) {
+                    for (int i = 0; i < nj; ++i) {  // C
+                        const int j = i * 64 + lane;
+                        const int2 x = c[min(j, d - 1)];
+                        const bool m = j < d && x.y != kKeyHaz && tb.get(x.x) == M;
+                        nm += __builtin_popcountll(__builtin_amdgcn_ballot_w64(m));
+                        const unsigned long long k = m ? pack_rn(x.y, x.x) : 0ull;
+                        best = k > best ? k : best;
+                    }
+                    best = dpp_max_u64(best);
+                }
+                if (kCnt != kHubHash) {  // D
+                    for (int i = 0; i < nj; ++i) {
+                        const int j = i * 64 + lane;
+                        const int2 x = c[min(j, d - 1)];
+                        if (j < d && x.y != kKeyHaz) tb.clear(x.x);
+                    }
                 }
             }
-        }
-        if (kCnt == kHubHash)  // a probe may still need a slot another lane cleared: wipe the whole table
-            for (int k = lane; k < Hw; k += 64) tb.keys[k] = 0u;
-        const int rb = (int)((unsigned)(best >> kNodeBits) ^ 0x80000000u);
-        const int nb = (int)(kNodeMask - (unsigned)(best & kNodeMask));
-        if (lane == 0) {
-            const int s = s0 + si;
-            int sc, t;
-            if (M == 0) {
-                t = zero_target(load_zc(zc_cnt, zc_key, s), sc);
-            } else {
-                sc = M;
-                t = nm == M ? nb : (rb >= 0 ? nb : RSK_TARGET_NONE);
+            if (kCnt == kHubHash)  // a probe may still need a slot another lane cleared: wipe the whole table
+                for (int k = lane; k < Hw; k += 64) tb.keys[k] = 0u;
+            const int rb = (int)((unsigned)(best >> kNodeBits) ^ 0x80000000u);
+            const int nb = (int)(kNodeMask - (unsigned)(best & kNodeMask));
+            if (lane == 0) {
+                const int s = s0 + si;
+                int sc, t;
+                if (M == 0) {
+                    t = zero_target(load_zc(zc_cnt, zc_key, s), sc);
+                } else {
+                    sc = M;
+                    t = nm == M ? nb : (rb >= 0 ? nb : RSK_TARGET_NONE);
+                }
+                const size_t o = (size_t)it.oi * S + s;
+                out_target[o] = t;
+                if (out_score) out_score[o] = sc;
             }
-            const size_t o = (size_t)it.oi * S + s;
-            out_target[o] = t;
-            if (out_score) out_score[o] = sc;
         }
+        __syncthreads();  // the next group restages the columns
     }
 }
 
@@ -1073,7 +1111,7 @@ HeavyGeom heavy_geometry(int dmax, int S, int N) {
     return g;
 }
 
-typedef void (*HubKern)(const HeavyItem *, int, const int *, const int *, const int *, int, int, int, int, int,
+typedef void (*HubKern)(const HeavyItem *, int, const int *, const int *, const int *, int, int, int, int, int, int,
                         const int *, const unsigned long long *, int *, int *);
 
 template <int kCnt, int kW>
@@ -1366,10 +1404,14 @@ int plan_create(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, in
 }
 
 // Mid (17..64, N >= kPackMaxN variant only) and hub (> 64) rows, queued on `stream`.
-// side[0]: mid rows and the hub classes <= 255; side[1]: the larger hub classes
-// (few rows, latency-bound: they overlap the others best on their own queue).
-int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t side[2], const int *d_assign, const int *d_key,
-                const int *d_zcnt, const unsigned long long *d_zkey, int *d_target, int *d_score, int S, int N) {
+// Mid and hub launches go round-robin over the `nside` streams in `side`
+// (mid, hub classes in degree order), so the few-row latency-bound hub classes
+// do not queue behind each other.
+int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t *side, int nside, const int *d_assign,
+                const int *d_key, const int *d_zcnt, const unsigned long long *d_zkey, int *d_target, int *d_score,
+                int S, int N) {
+    int next = 0;
+    auto pick = [&]() { return side[next++ % nside]; };
     ScoreCtx sc;
     sc.nodekey = d_key;
     sc.zc_cnt = d_zcnt;
@@ -1398,19 +1440,24 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t side[2], con
             a.blocks_per_chunk = (int)ceil_div(waves, 4);
             const int64_t blocks = chunks * a.blocks_per_chunk;
             RSK_CHECK(blocks < INT32_MAX, "mid grid too large");
-            ScopedTimer tm(ctx, "car_mid", side[0]);
-            car_mid_kernel<<<dim3((unsigned)blocks), dim3(256), 0, side[0]>>>(a);
+            const hipStream_t stream = pick();
+            ScopedTimer tm(ctx, "car_mid", stream);
+            car_mid_kernel<<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(a);
             RSK_HIP(hipGetLastError());
         }
     }
     for (int c = 0; c < kNumHeavy; ++c) {   // K3 hub rows
         const int n = plan->n_heavy[c];
         if (!n) continue;
-        const hipStream_t stream = kHeavyMax[c] <= 255 ? side[0] : side[1];
+        const hipStream_t stream = pick();
         const HeavyGeom g = heavy_geometry(plan->heavy_dmax[c], S, N);
         RSK_CHECK(g.lds <= 160 * 1024, "hub class %d needs %zu B of LDS", c, g.lds);
         const int64_t groups = ceil_div(S, 1 << g.lg);
-        RSK_CHECK(groups * n < INT32_MAX, "hub grid too large");
+        // scenario groups per workgroup: enough workgroups to fill the GPU twice over
+        static const int gpw_env = env_int("RSK_HUB_GPW", 0);
+        const int gpw = gpw_env > 0 ? gpw_env : (int)std::max<int64_t>(1, std::min<int64_t>(8, groups * n / 1024));
+        const int64_t gblocks = ceil_div(groups, gpw);
+        RSK_CHECK(gblocks * n < INT32_MAX, "hub grid too large");
         const HubKern kern = g.waves == 8 ? hub_kern_mode<8>(g.mode, kHeavyNJ[c]) : hub_kern_mode<4>(g.mode, kHeavyNJ[c]);
         if (g.lds > 64 * 1024)
             RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -1419,9 +1466,9 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t side[2], con
                                                          "car_hub1024", "car_hub2048", "car_hub4096"};
         static const bool per_class = env_int("RSK_HUB_TIMERS", 0) != 0;
         ScopedTimer tm(ctx, per_class ? kHubNames[c] : "car_heavy", stream);
-        kern<<<dim3((unsigned)(groups * n)), dim3(64 * g.waves), g.lds, stream>>>(
+        kern<<<dim3((unsigned)(gblocks * n)), dim3(64 * g.waves), g.lds, stream>>>(
             plan->heavy_items[c].as<HeavyItem>(), n, plan->hcol.as<int>(), d_assign, d_key, S, N, g.lg, g.dpad,
-            g.H, d_zcnt, d_zkey, d_target, d_score);
+            g.H, gpw, d_zcnt, d_zkey, d_target, d_score);
         RSK_HIP(hipGetLastError());
     }
     return RSK_OK;
@@ -1541,17 +1588,19 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
                 d_cap, d_use, d_haz, N, SV, npb, total, d_key, d_zcnt, d_zkey);
         RSK_HIP(hipGetLastError());
     }
-    // mid and hub rows run on side streams (RSK_OVERLAP = how many, 0..2),
-    // overlapping the tile kernel and each other
-    static const int overlap = std::max(0, std::min(2, env_int("RSK_OVERLAP", 1)));
-    hipStream_t side[2] = {ctx->stream, ctx->stream};
+    // mid and hub rows run on up to kAux side streams (RSK_OVERLAP = how many),
+    // beside the tile kernel or, with RSK_SIDE_FIRST=1, ahead of it
+    static const int overlap = std::max(0, std::min(rsk_ctx::kAux, env_int("RSK_OVERLAP", 1)));
+    static const bool side_first = env_int("RSK_SIDE_FIRST", 0) != 0;
+    hipStream_t side[rsk_ctx::kAux] = {ctx->stream, ctx->stream, ctx->stream};
     const int nside = plan_has_side(plan) && plan->T > 0 ? overlap : 0;
     if (nside) {
         RSK_TRY(aux_fork(ctx, nside));
-        side[0] = ctx->aux[0];
-        side[1] = ctx->aux[nside - 1];
+        for (int i = 0; i < nside; ++i) side[i] = ctx->aux[i];
     }
-    RSK_TRY(launch_side(plan, ctx, side, d_assign, d_key, d_zcnt, d_zkey, d_target, d_score, S, N));
+    RSK_TRY(launch_side(plan, ctx, side, std::max(nside, 1), d_assign, d_key, d_zcnt, d_zkey, d_target, d_score, S,
+                        N));
+    if (nside && side_first) RSK_TRY(aux_join(ctx, nside));
     if (plan->T > 0) {   // K1 tiles
         TileArgs a;
         std::memset(&a, 0, sizeof(a));
@@ -1605,7 +1654,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         kern<<<dim3((unsigned)blocks), dim3(kTileThreads), lds, ctx->stream>>>(a);
         RSK_HIP(hipGetLastError());
     }
-    if (nside) RSK_TRY(aux_join(ctx, nside));
+    if (nside && !side_first) RSK_TRY(aux_join(ctx, nside));
 #ifdef RSK_DEBUG_BOUNDS
     {
         unsigned flags_h = 0, zero = 0;

@@ -63,8 +63,9 @@ struct rsk_ctx {
     std::vector<hipEvent_t> event_pool;  // recycled timing events
     std::map<std::string, std::vector<rsk::EventPair>> pending;
     std::map<std::string, std::pair<double, int64_t>> totals;
-    hipStream_t aux[2] = {};     // side streams: CAR mid/hub rows overlap the tile kernel
-    hipEvent_t fork = nullptr, join[2] = {};
+    static constexpr int kAux = 3;  // side streams (with ctx->stream: 4 hardware queues)
+    hipStream_t aux[kAux] = {};     // CAR mid/hub rows, beside the tile kernel or ahead of it
+    hipEvent_t fork = nullptr, join[kAux] = {};
     rsk::DevBuf host_stage[12];  // device staging for host-pointer calls
     rsk::DevBuf work[6];         // per-call device workspace
     std::vector<uint8_t> pinned;  // host scratch

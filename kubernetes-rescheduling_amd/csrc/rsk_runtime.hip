@@ -159,7 +159,7 @@ int rsk_ctx_destroy(rsk_ctx *ctx) {
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     for (auto &b : ctx->host_stage) b.release();
     for (auto &b : ctx->work) b.release();
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < rsk_ctx::kAux; ++i)
         if (ctx->aux[i]) {
             (void)hipStreamSynchronize(ctx->aux[i]);
             (void)hipStreamDestroy(ctx->aux[i]);
