@@ -200,15 +200,18 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
-        probe = np.arange(0, P, max(1, P // 8), dtype=np.int32)[:8]
-        t1 = time.perf_counter()
-        orc.car(c.row_ptr, c.col_idx, c.assign, S, c.cap_cpu, c.use_cpu, c.hazard, N, rows=probe, threads=threads)
-        per_row = (time.perf_counter() - t1) / len(probe)
-        nrows = int(max(8, min(P, args.cpu_seconds / max(per_row, 1e-9))))
-        sample = np.linspace(0, P - 1, nrows).astype(np.int32)
-        t1 = time.perf_counter()
-        orc.car(c.row_ptr, c.col_idx, c.assign, S, c.cap_cpu, c.use_cpu, c.hazard, N, rows=sample, threads=threads)
-        dt = time.perf_counter() - t1
+        # grow an evenly spaced pod sample until one timed pass takes >= 60 % of
+        # --cpu-seconds (about 10-30 s of CPU work at the default)
+        nrows = 64
+        while True:
+            sample = np.linspace(0, P - 1, nrows).astype(np.int32)
+            t1 = time.perf_counter()
+            orc.car(c.row_ptr, c.col_idx, c.assign, S, c.cap_cpu, c.use_cpu, c.hazard, N, rows=sample,
+                    threads=threads)
+            dt = time.perf_counter() - t1
+            if dt >= 0.6 * args.cpu_seconds or nrows >= P:
+                break
+            nrows = int(min(P, max(nrows + 1, nrows * args.cpu_seconds / max(dt, 1e-3))))
         cpu = {"value": round(nrows * S * N / dt, 1), "unit": "pod×node evals/s", "cores": threads, "kind": "port",
                "sample": f"{nrows} evenly spaced pods x {S} scenarios x {N} nodes ({dt:.1f}s), oracle/rsk_oracle.c "
                          f"literal CAR restatement, OpenMP {threads} threads",

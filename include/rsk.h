@@ -57,7 +57,7 @@ int rsk_ctx_destroy(rsk_ctx *ctx);
 int rsk_ctx_set_stream(rsk_ctx *ctx, void *hip_stream);
 int rsk_ctx_synchronize(rsk_ctx *ctx);
 /* Kernel timing with HIP events recorded on the context's stream around every
- * launch of the named kernel ("car_light", "car_heavy", "car_prep", ...). */
+ * launch of the named kernel ("car_prep", "car_tile", "car_mid", "car_heavy" = the hub rows). */
 int rsk_ctx_set_profiling(rsk_ctx *ctx, int on);
 /* Restrict the timing events to launches of one kernel name (NULL or "" = all):
  * fewer events inside a timed region. */
