@@ -182,6 +182,21 @@ def test_car_heavy_hash_path_large_n(ctx):
         _check_car(ctx, rp, ci, a, S, cap, use, haz, N, rows=np.arange(0, 60, dtype=np.int32), label=f"hash S={S}")
 
 
+def test_car_huge_n_alt_plan(ctx):
+    """N >= 2^24 - 1: node ids no longer fit the tiles' packed (node << 8 | row)
+    sort words, so the plan's N >= kPackMaxN variant sends rows 17..64 to the
+    mid kernel.  Neighbours crowd onto node ids around 2^24 for real counts."""
+    rng = np.random.default_rng(31)
+    N, S, P = (1 << 24) + 5, 2, 500
+    hubs = [17, 20, 31, 32, 33, 40, 63, 64, 65, 100]
+    rp, ci, a, cap, use, haz = _random_case(rng, P, N, S, max_deg=12, hub_deg=hubs, p_haz=0.2)
+    pool = np.array([0, 5, (1 << 24) - 2, (1 << 24) - 1, 1 << 24, N - 1], np.int32)
+    a[:] = rng.choice(pool, P * S)
+    a[rng.random(P * S) < 0.05] = -1
+    haz.reshape(N, S)[pool] = 0
+    _check_car(ctx, rp, ci, a, S, cap, use, haz, N, label="N >= 2^24")
+
+
 def test_car_all_hazard_and_rows_subset(ctx):
     rng = np.random.default_rng(7)
     P, N, S = 300, 12, 70
