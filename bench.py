@@ -32,7 +32,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 CONFIGS = {
     "headline": dict(P=100_000, N=5_000, S=4096, name="100k pods x 5k nodes, PA tree, 4096 scenarios/GPU (config 3)"),
     "2k64": dict(P=2_000, N=64, S=1, name="2k pods x 64 nodes, single CAR round (config 2)"),
-    "1m50k": dict(P=1_000_000, N=50_000, S=64, name="1M pods x 50k nodes, 64 scenarios/GPU (config 4 sizes)"),
+    "1m50k": dict(P=1_000_000, N=50_000, S=64, shard="rows",
+                  name="1M pods x 50k nodes x 64 scenarios, pod-row sharded (config 4)"),
 }
 
 
@@ -66,6 +67,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="headline", choices=sorted(CONFIGS))
     ap.add_argument("--scenarios", type=int, default=0, help="override S per GPU")
+    ap.add_argument("--shard", choices=("scenarios", "rows"), default=None,
+                    help="multi-GPU layout (SURVEY §8e): scenario sharding (default; 1m50k: rows)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-events", action="store_true", default=os.environ.get("RSK_BENCH_NO_EVENTS") == "1",
@@ -91,17 +94,24 @@ def main():
     if args.scenarios:
         cfg["S"] = args.scenarios
     P, N, S = cfg["P"], cfg["N"], cfg["S"]
+    by_rows = (args.shard or cfg.get("shard", "scenarios")) == "rows"
     t0 = time.time()
-    shard = rdist.shard_for(rank, world, S)
-    c = synth.make_cluster(P, N, S=S, seed=0, s0=shard.s0)
+    if by_rows:  # pod-row sharding: full assign replica, a contiguous row range per rank
+        c = synth.make_cluster(P, N, S=S, seed=0)
+        rshard = rdist.row_shard_for(rank, world, c.row_ptr)
+        my_rows, Q = rshard.rows, rshard.q
+    else:        # scenario sharding: this rank's scenario range, every row
+        shard = rdist.shard_for(rank, world, S)
+        c = synth.make_cluster(P, N, S=S, seed=0, s0=shard.s0)
+        my_rows, Q = None, P
     log(f"[bench] rank {rank}: generated {P}x{N}x{S} in {time.time() - t0:.1f}s")
 
     ctx = _lib.Context(local)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
-    plan = api.CarPlan(c.row_ptr, c.col_idx, ctx=ctx)
+    plan = api.CarPlan(c.row_ptr, c.col_idx, rows=my_rows, ctx=ctx)
     T = {k: torch.from_numpy(getattr(c, k)).to(dev) for k in ("assign", "cap_cpu", "use_cpu", "hazard")}
-    out_t = torch.empty(P * S, dtype=torch.int32, device=dev)
+    out_t = torch.empty(max(Q, 1) * S, dtype=torch.int32, device=dev)
     torch.cuda.synchronize(dev)
 
     def step():
@@ -157,15 +167,32 @@ def main():
         kernels[dom] = dict(timed[dom], breakdown_pass_avg_ms=kernels[dom]["avg_ms"])
     ms_step = elapsed * 1e3 / args.steps
     evals = P * N * S
-    value = world * evals / (ms_step / 1e3)
+    # scenario sharding: every rank scores P x N x S of its own (weak scaling);
+    # row sharding: the ranks split one P x N x S batch (strong scaling)
+    value = (1 if by_rows else world) * evals / (ms_step / 1e3)
     info = plan.info()
+    gather_ms = None
+    if by_rows and world > 1:  # the round's only data-path exchange, timed on its own
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            full = rdist.gather_rows(out_t[: Q * S], rshard, S)
+        torch.cuda.synchronize(dev)
+        g = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+        dist.all_reduce(g, op=dist.ReduceOp.MAX)
+        gather_ms = float(g.item()) * 1e3 / args.steps
+        del full
 
     # parity spot check against the oracle on sampled rows of this rank's batch
     from oracle import oracle as orc
     deg = np.diff(c.row_ptr)
     rng = np.random.default_rng(rank)
-    rows = np.unique(np.concatenate([np.argsort(deg)[-4:], rng.choice(P, 28, replace=False)])).astype(np.int32)
-    got = out_t.view(P, S)[torch.from_numpy(rows).to(dev).long()].cpu().numpy().reshape(-1)
+    r0 = rshard.r0 if by_rows else 0
+    mine = deg[r0:r0 + Q]
+    rows = np.unique(np.concatenate([np.argsort(mine)[-4:], rng.choice(Q, min(Q, 28), replace=False)]))
+    rows = (rows + r0).astype(np.int32)
+    got = out_t.view(Q, S)[torch.from_numpy(rows - r0).to(dev).long()].cpu().numpy().reshape(-1)
     exp, _ = orc.car(c.row_ptr, c.col_idx, c.assign, S, c.cap_cpu, c.use_cpu, c.hazard, N, rows=rows,
                      threads=min(16, os.cpu_count() or 1))
     parity_ok = bool(np.array_equal(got, exp))
@@ -221,12 +248,17 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "pod×node evals/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
+            "scaling": "strong" if by_rows else "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
             "config": {"workload": cfg["name"], "pods": P, "nodes": N, "scenarios_per_gpu": S, "nnz": c.nnz,
-                       "max_degree": int(deg.max()), "parallelism": f"scenario-sharded x{world}"},
+                       "max_degree": int(deg.max()),
+                       "parallelism": f"{'pod-row' if by_rows else 'scenario'}-sharded x{world}"},
             "roofline": roof, "roofline_step": roof_step, "cpu_baseline": cpu, "kernels": kernels,
             "parity_sample_ok": parity_ok, "hbm_bytes_algorithmic_per_step": B, "plan": info,
         }
+        if by_rows:
+            line["rows_per_rank"] = Q
+            line["allgather_ms_per_step"] = None if gather_ms is None else round(gather_ms, 4)
+            line["end_to_end_ms_per_step"] = round(ms_step + (gather_ms or 0.0), 4)
         print(json.dumps(line), flush=True)
     plan.close()
     ctx.close()
