@@ -47,6 +47,7 @@ extern "C" {
 
 typedef struct rsk_ctx rsk_ctx;
 typedef struct rsk_car_plan rsk_car_plan;
+typedef struct rsk_rounds rsk_rounds;
 
 /* ---- library / context ---------------------------------------------------- */
 int rsk_version(void);                                /* 100*major + minor */
@@ -86,11 +87,14 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
                          const int32_t *use_cpu, const uint8_t *hazard, int32_t N,
                          int32_t *out_target, int32_t *out_score, uint32_t flags);
 /* Plan layout statistics (host, no GPU work): how the rows were routed.
- * out[0] rows on the LDS-tiled path (deg <= 16)   out[1] direct light rows (deg <= 16)
- * out[2] mid rows (17..64)    out[3] heavy rows (> 64)    out[4] tiles
- * out[5] rows per tile image  out[6] pods per tile        out[7] tile plan bytes
- * out[8] direct record bytes  out[9] mid record bytes     out[10] heavy item + CSR bytes
- * out[11] max row degree.  Returns the number of fields written (<= n).     */
+ * out[0] rows scored in tiles (deg <= 32)   out[1] (unused, 0)
+ * out[2] mid rows (33..64)   out[3] hub rows (> 64)   out[4] tiles
+ * out[5] max image rows per tile   out[6] max owner rows per tile
+ * out[7] tile plan bytes   out[8] (unused, 0)   out[9] mid record bytes
+ * out[10] hub item + CSR bytes   out[11] max row degree
+ * out[12] image rows over all tiles   out[13] distinct pods in the images
+ * out[14] rows on the sorted tile class (17..32).
+ * Returns the number of fields written (<= n).                             */
 int rsk_car_plan_info(const rsk_car_plan *plan, int64_t *out, int n);
 /* One-shot convenience: plan_create + execute + destroy. */
 int rsk_car_place(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, int32_t P,
@@ -151,6 +155,29 @@ int rsk_cut_cost(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, i
                  uint32_t flags);
 int rsk_pick_max_pod(rsk_ctx *ctx, const int32_t *assign, const int32_t *pod_cpu, int32_t P, int32_t S,
                      const int32_t *most, int32_t *out_pod, uint32_t flags);
+
+/* ---- multi-round loop --------------------
+ * The reference's control loop (main.py:55-110) for S independent scenarios,
+ * R rounds, all on the device.  Round r, scenario s:
+ *   pct = cpu_pct(use, cap) (a9); hazard = pct >= threshold and most = first
+ *   max hazard node (a8); p = pick_max_pod(assign, pod_cpu, most) (a10);
+ *   t = the CAR target of p (a1/a2) against the round's assign / use / hazard;
+ *   then the build-defined update (the reference re-measures the live cluster
+ *   instead): when t >= 0 the pod's CPU moves with it, use[old] -= pod_cpu[p],
+ *   use[t] += pod_cpu[p], assign[p] = t.  Otherwise the state stays.
+ *   out_evict[r*S+s]  = p, -1 when there is no hazard node or no pod on it
+ *   out_target[r*S+s] = t: node, RSK_TARGET_NONE, RSK_TARGET_NO_CANDIDATE, or
+ *                       RSK_TARGET_NO_EVICT (-3) when nothing was evicted.
+ * assign[P*S] and use_cpu[N*S] are updated in place.  Row degree <= 4096.
+ * rsk_rounds_create deduplicates the CSR (self edges dropped, main.py:73) and
+ * uploads it with pod_cpu[P] (millicores).                                   */
+#define RSK_TARGET_NO_EVICT (-3)
+int rsk_rounds_create(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, int32_t P,
+                      const int32_t *pod_cpu, rsk_rounds **out);
+int rsk_rounds_destroy(rsk_rounds *r);
+int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap_cpu, int32_t *use_cpu,
+                   int32_t N, int32_t threshold, int32_t R, int32_t *out_evict, int32_t *out_target,
+                   uint32_t flags);
 
 #ifdef __cplusplus
 }

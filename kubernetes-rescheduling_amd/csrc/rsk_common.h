@@ -99,6 +99,15 @@ int copy_back(rsk_ctx *ctx, void *host_dst, const void *dev_src, size_t bytes, b
 
 constexpr int kBlock = 256;
 
+// Device-pointer launches of the per-node reductions (rsk_metrics.hip), shared
+// by the public entry points and the multi-round loop (rsk_rounds.hip).
+// `key_ws` is S u64 of scratch; every call queues on `stream` only.
+int launch_cpu_pct(hipStream_t stream, const int *use, const int *cap, int N, int S, int *pct);
+int launch_detect(hipStream_t stream, const int *pct, int N, int S, int threshold, uint8_t *hazard,
+                  unsigned long long *key_ws, int *most);
+int launch_pick_max_pod(hipStream_t stream, const int *assign, const int *pod_cpu, int P, int S, const int *most,
+                        unsigned long long *key_ws, int *out_pod);
+
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 }  // namespace rsk

@@ -349,6 +349,40 @@ __global__ __launch_bounds__(256) void pick_pod_kernel(const int *__restrict__ a
     if (b) atomicMax(&best[s], b);
 }
 
+int launch_cpu_pct(hipStream_t stream, const int *use, const int *cap, int N, int S, int *pct) {
+    const size_t NS = (size_t)N * S;
+    cpu_pct_kernel<<<(unsigned)ceil_div(NS, 256), 256, 0, stream>>>(use, cap, N, S, pct);
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
+}
+
+int launch_detect(hipStream_t stream, const int *pct, int N, int S, int threshold, uint8_t *hazard,
+                  unsigned long long *key_ws, int *most) {
+    RSK_HIP(hipMemsetAsync(key_ws, 0, (size_t)S * 8, stream));
+    const int npb = chunk_for(N, S);
+    const unsigned total = (unsigned)(ceil_div(N, npb) * S);
+    detect_kernel<<<(unsigned)ceil_div(total, 256), 256, 0, stream>>>(pct, N, S, threshold, npb, total, hazard,
+                                                                       key_ws);
+    decode_first_max<<<(unsigned)ceil_div(S, 256), 256, 0, stream>>>(key_ws, S, most);
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
+}
+
+int launch_pick_max_pod(hipStream_t stream, const int *assign, const int *pod_cpu, int P, int S, const int *most,
+                        unsigned long long *key_ws, int *out_pod) {
+    RSK_HIP(hipMemsetAsync(key_ws, 0, (size_t)S * 8, stream));
+    if (P > 0) {
+        const int ppt = chunk_for(P, S);
+        const int64_t tot = ceil_div(P, ppt) * S;
+        RSK_CHECK(tot < INT32_MAX, "grid too large");
+        pick_pod_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, stream>>>(assign, pod_cpu, P, S, most, ppt,
+                                                                          (unsigned)tot, key_ws);
+    }
+    decode_first_max<<<(unsigned)ceil_div(S, 256), 256, 0, stream>>>(key_ws, S, out_pod);
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
+}
+
 }  // namespace rsk
 
 using namespace rsk;
@@ -539,8 +573,7 @@ int rsk_cpu_pct(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *cap_cpu, in
     RSK_TRY(stage_out(ctx, 2, out_pct, NS * 4, dev, reinterpret_cast<void **>(&d_out)));
     {
         ScopedTimer tm(ctx, "cpu_pct");
-        cpu_pct_kernel<<<(unsigned)ceil_div(NS, 256), 256, 0, ctx->stream>>>(d_use, d_cap, N, S, d_out);
-        RSK_HIP(hipGetLastError());
+        RSK_TRY(launch_cpu_pct(ctx->stream, d_use, d_cap, N, S, d_out));
     }
     if (!dev) {
         RSK_TRY(copy_back(ctx, out_pct, d_out, NS * 4, false));
@@ -562,16 +595,10 @@ int rsk_detect(rsk_ctx *ctx, const int32_t *cpu_pct, int32_t N, int32_t S, int32
     RSK_TRY(stage_out(ctx, 1, out_hazard, NS, dev, reinterpret_cast<void **>(&d_haz)));
     RSK_TRY(stage_out(ctx, 2, out_most, (size_t)S * 4, dev, reinterpret_cast<void **>(&d_most)));
     RSK_TRY(ctx->work[0].reserve((size_t)S * 8));
-    auto *key = ctx->work[0].as<unsigned long long>();
-    RSK_HIP(hipMemsetAsync(key, 0, (size_t)S * 8, ctx->stream));
-    const int npb = chunk_for(N, S);
-    const unsigned total = (unsigned)(ceil_div(N, npb) * S);
     {
         ScopedTimer tm(ctx, "detect");
-        detect_kernel<<<(unsigned)ceil_div(total, 256), 256, 0, ctx->stream>>>(d_pct, N, S, threshold, npb, total,
-                                                                               d_haz, key);
-        decode_first_max<<<(unsigned)ceil_div(S, 256), 256, 0, ctx->stream>>>(key, S, d_most);
-        RSK_HIP(hipGetLastError());
+        RSK_TRY(launch_detect(ctx->stream, d_pct, N, S, threshold, d_haz, ctx->work[0].as<unsigned long long>(),
+                              d_most));
     }
     if (!dev) {
         RSK_TRY(copy_back(ctx, out_hazard, d_haz, NS, false));
@@ -664,19 +691,11 @@ int rsk_pick_max_pod(rsk_ctx *ctx, const int32_t *assign, const int32_t *pod_cpu
     RSK_TRY(stage_in(ctx, 2, most, (size_t)S * 4, dev, reinterpret_cast<const void **>(&d_most)));
     RSK_TRY(stage_out(ctx, 3, out_pod, (size_t)S * 4, dev, reinterpret_cast<void **>(&d_out)));
     RSK_TRY(ctx->work[0].reserve((size_t)S * 8));
-    auto *key = ctx->work[0].as<unsigned long long>();
-    RSK_HIP(hipMemsetAsync(key, 0, (size_t)S * 8, ctx->stream));
-    if (P > 0) {
-        const int ppt = chunk_for(P, S);
-        const int64_t tot = ceil_div(P, ppt) * S;
-        RSK_CHECK(tot < INT32_MAX, "grid too large");
+    {
         ScopedTimer tm(ctx, "pick_max_pod");
-        pick_pod_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, ctx->stream>>>(d_assign, d_cpu, P, S, d_most, ppt,
-                                                                               (unsigned)tot, key);
-        RSK_HIP(hipGetLastError());
+        RSK_TRY(launch_pick_max_pod(ctx->stream, d_assign, d_cpu, P, S, d_most, ctx->work[0].as<unsigned long long>(),
+                                    d_out));
     }
-    decode_first_max<<<(unsigned)ceil_div(S, 256), 256, 0, ctx->stream>>>(key, S, d_out);
-    RSK_HIP(hipGetLastError());
     if (!dev) {
         RSK_TRY(copy_back(ctx, out_pod, d_out, (size_t)S * 4, false));
         RSK_HIP(hipStreamSynchronize(ctx->stream));

@@ -1,0 +1,269 @@
+// Multi-round rescheduling loop on the device.
+//
+// The reference's control loop (main.py:55-110) runs, per round: monitor ->
+// detection (harzard_detect.py:3-27) -> pod_delete / pick_max_pod
+// (delete_replaced_pod.py:41-61) -> edit_cluster (main.py:10-19) -> the
+// placement algorithm (here CAR, rescheduling.py:174-218).  It re-measures the
+// live cluster every round, so what happens to the state after a move is
+// build-defined: the pod's CPU moves with it.  This file runs R
+// such rounds for S independent scenarios without a host round trip:
+//
+//   cpu_pct (a9) -> detect (a8) -> pick_max_pod (a10)   [rsk_metrics.hip]
+//   car_move_kernel: CAR of the one evicted pod per scenario (a1/a2), then the
+//   update use[old] -= cpu, use[t] += cpu, assign[p] = t when t >= 0.
+//
+// car_move_kernel: one workgroup per scenario, lanes = the evicted pod's
+// neighbours; their nodes counted in an LDS open-addressing hash (node+1
+// keys), the max count and the best (rem, -node) reduced with LDS atomics.
+// With no neighbour on a candidate node (max score 0) every non-hazard node
+// ties: the workgroup scans the N nodes of its scenario.
+#include <algorithm>
+#include <climits>
+#include <vector>
+
+#include "rsk_common.h"
+
+struct rsk_rounds {
+    rsk_ctx *ctx = nullptr;
+    int P = 0, dmax = 0;
+    rsk::DevBuf row_ptr, col, pod_cpu;
+    rsk::DevBuf pct, haz, most, evict, key_ws;
+    ~rsk_rounds() {
+        row_ptr.release();
+        col.release();
+        pod_cpu.release();
+        pct.release();
+        haz.release();
+        most.release();
+        evict.release();
+        key_ws.release();
+    }
+};
+
+namespace rsk {
+namespace {
+
+constexpr int kMoveThreads = 256;
+constexpr int kMoveMaxDeg = 4096;
+constexpr int kNoEvict = -3;
+
+__device__ __forceinline__ unsigned long long move_pack(int rem, int n) {  // (rem, -node), 0 = none
+    return ((unsigned long long)((unsigned)rem ^ 0x80000000u) << 32) | (unsigned long long)(0x7fffffffu - (unsigned)n);
+}
+
+__global__ __launch_bounds__(kMoveThreads) void car_move_kernel(const int *__restrict__ row_ptr,
+                                                                const int *__restrict__ col,
+                                                                const int *__restrict__ pod_cpu, int *assign,
+                                                                int *use, const int *__restrict__ cap,
+                                                                const uint8_t *__restrict__ haz,
+                                                                const int *__restrict__ evict, int S, int N, int H,
+                                                                int *__restrict__ out_target) {
+    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
+    unsigned *keys = lds, *cnts = lds + H;
+    unsigned long long *red64 = reinterpret_cast<unsigned long long *>(lds + 2 * H);  // best
+    unsigned *red = lds + 2 * H + 2;                                                   // M, n_at_M, n_free
+    const int s = blockIdx.x, tid = threadIdx.x;
+    const int p = evict[s];
+    if (p < 0) {
+        if (tid == 0) out_target[s] = kNoEvict;
+        return;
+    }
+    const int b = row_ptr[p], d = row_ptr[p + 1] - b;
+    for (int k = tid; k < 2 * H; k += kMoveThreads) lds[k] = 0u;
+    if (tid < 8) lds[2 * H + tid] = 0u;
+    __syncthreads();
+    const unsigned mask = (unsigned)H - 1u;
+    // A: count every neighbour on a non-hazard node
+    for (int j = tid; j < d; j += kMoveThreads) {
+        const int x = assign[(size_t)col[b + j] * S + s];
+        if ((unsigned)x >= (unsigned)N || haz[(size_t)x * S + s]) continue;
+        const unsigned k = (unsigned)x + 1u;
+        unsigned h = (k * 2654435761u) & mask;
+        while (true) {
+            const unsigned prev = atomicCAS(&keys[h], 0u, k);
+            if (prev == 0u || prev == k) break;
+            h = (h + 1u) & mask;
+        }
+        atomicAdd(&cnts[h], 1u);
+    }
+    __syncthreads();
+    // B: max count over the slots
+    unsigned m = 0;
+    for (int h = tid; h < H; h += kMoveThreads) m = max(m, cnts[h]);
+    if (m) atomicMax(&red[0], m);
+    __syncthreads();
+    const unsigned M = red[0];
+    if (M > 0) {  // C: nodes at the max count -> |best| and the best (rem, -node)
+        unsigned long long best = 0;
+        unsigned nb = 0;
+        for (int h = tid; h < H; h += kMoveThreads) {
+            if (cnts[h] != M) continue;
+            const int n = (int)keys[h] - 1;
+            ++nb;
+            const unsigned long long k = move_pack(cap[n] - use[(size_t)n * S + s], n);
+            best = k > best ? k : best;
+        }
+        if (nb) {
+            atomicAdd(&red[1], nb);
+            atomicMax(red64, best);
+        }
+    } else {  // max score 0: every non-hazard node ties
+        unsigned long long best = 0;
+        unsigned nb = 0;
+        for (int n = tid; n < N; n += kMoveThreads) {
+            if (haz[(size_t)n * S + s]) continue;
+            ++nb;
+            const unsigned long long k = move_pack(cap[n] - use[(size_t)n * S + s], n);
+            best = k > best ? k : best;
+        }
+        if (nb) {
+            atomicAdd(&red[1], nb);
+            atomicMax(red64, best);
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned nbest = red[1];
+        const unsigned long long best = *red64;
+        const int rem = (int)((unsigned)(best >> 32) ^ 0x80000000u);
+        const int node = (int)(0x7fffffffu - (unsigned)(best & 0xffffffffu));
+        int t;
+        if (nbest == 0) t = RSK_TARGET_NO_CANDIDATE;  // max() of an empty sequence
+        else if (nbest == 1) t = node;                // the single best, even if overloaded
+        else t = rem >= 0 ? node : RSK_TARGET_NONE;   // largest remaining CPU, None if < 0
+        out_target[s] = t;
+        if (t >= 0) {  // build-defined update: the pod's CPU moves with it
+            const size_t pc = (size_t)p * S + s;
+            const int old = assign[pc], c = pod_cpu[p];
+            if ((unsigned)old < (unsigned)N) use[(size_t)old * S + s] -= c;
+            use[(size_t)t * S + s] += c;
+            assign[pc] = t;
+        }
+    }
+}
+
+int next_pow2(int x) {
+    int p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+}  // namespace
+}  // namespace rsk
+
+using namespace rsk;
+
+extern "C" {
+
+int rsk_rounds_create(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, int32_t P, const int32_t *pod_cpu,
+                      rsk_rounds **out) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK(out && row_ptr && pod_cpu && P >= 0 && (P == 0 || col_idx || row_ptr[P] == 0), "bad arguments");
+    // deduplicated rows without the self edge (the evicted pod is off the cluster, main.py:73)
+    std::vector<int32_t> rp(1, 0), ci;
+    ci.reserve(P ? (size_t)row_ptr[P] : 0);
+    int dmax = 0;
+    for (int p = 0; p < P; ++p) {
+        RSK_CHECK(row_ptr[p + 1] >= row_ptr[p], "row_ptr not monotone at %d", p);
+        const size_t r0 = ci.size();
+        for (int k = row_ptr[p]; k < row_ptr[p + 1]; ++k) {
+            RSK_CHECK(col_idx[k] >= 0 && col_idx[k] < P, "col_idx[%d] = %d out of range", k, col_idx[k]);
+            if (col_idx[k] != p) ci.push_back(col_idx[k]);
+        }
+        std::sort(ci.begin() + r0, ci.end());
+        ci.erase(std::unique(ci.begin() + r0, ci.end()), ci.end());
+        dmax = std::max(dmax, (int)(ci.size() - r0));
+        rp.push_back((int32_t)ci.size());
+    }
+    RSK_CHECK(dmax <= kMoveMaxDeg, "row degree %d above %d", dmax, kMoveMaxDeg);
+    auto *r = new rsk_rounds();
+    r->ctx = ctx;
+    r->P = P;
+    r->dmax = dmax;
+    int rc = r->row_ptr.reserve(rp.size() * 4);
+    if (rc == RSK_OK) rc = r->col.reserve(std::max<size_t>(1, ci.size()) * 4);
+    if (rc == RSK_OK) rc = r->pod_cpu.reserve(std::max<size_t>(1, (size_t)P) * 4);
+    if (rc != RSK_OK) { delete r; return rc; }
+    RSK_HIP(hipMemcpy(r->row_ptr.ptr, rp.data(), rp.size() * 4, hipMemcpyHostToDevice));
+    if (!ci.empty()) RSK_HIP(hipMemcpy(r->col.ptr, ci.data(), ci.size() * 4, hipMemcpyHostToDevice));
+    if (P) RSK_HIP(hipMemcpy(r->pod_cpu.ptr, pod_cpu, (size_t)P * 4, hipMemcpyHostToDevice));
+    *out = r;
+    return RSK_OK;
+}
+
+int rsk_rounds_destroy(rsk_rounds *r) {
+    if (!r) return RSK_OK;
+    (void)hipSetDevice(r->ctx->device);
+    (void)hipStreamSynchronize(r->ctx->stream);
+    delete r;
+    return RSK_OK;
+}
+
+int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap_cpu, int32_t *use_cpu, int32_t N,
+                   int32_t threshold, int32_t R, int32_t *out_evict, int32_t *out_target, uint32_t flags) {
+    RSK_CHECK(r, "null rounds object");
+    rsk_ctx *ctx = r->ctx;
+    RSK_TRY(activate(ctx));
+    RSK_CHECK(assign && cap_cpu && use_cpu && out_evict && out_target, "null argument");
+    RSK_CHECK(S > 0 && N > 0 && R >= 0 && (int64_t)N * S < INT32_MAX && (int64_t)r->P * S < INT32_MAX &&
+                  (int64_t)R * S < INT32_MAX,
+              "bad sizes S=%d N=%d R=%d", S, N, R);
+    const bool dev = flags & RSK_F_DEVICE;
+    const size_t NS = (size_t)N * S, PS = (size_t)r->P * S, RS = (size_t)R * S;
+    hipStream_t st = ctx->stream;
+    // in-out state: host callers' arrays are staged and copied back at the end
+    int *d_assign, *d_use, *d_evict, *d_target;
+    const int *d_cap;
+    RSK_TRY(stage_out(ctx, 0, assign, std::max<size_t>(PS, 1) * 4, dev, reinterpret_cast<void **>(&d_assign)));
+    RSK_TRY(stage_out(ctx, 1, use_cpu, NS * 4, dev, reinterpret_cast<void **>(&d_use)));
+    RSK_TRY(stage_in(ctx, 2, cap_cpu, (size_t)N * 4, dev, reinterpret_cast<const void **>(&d_cap)));
+    RSK_TRY(stage_out(ctx, 3, out_evict, std::max<size_t>(RS, 1) * 4, dev, reinterpret_cast<void **>(&d_evict)));
+    RSK_TRY(stage_out(ctx, 4, out_target, std::max<size_t>(RS, 1) * 4, dev, reinterpret_cast<void **>(&d_target)));
+    if (!dev) {
+        if (PS) RSK_HIP(hipMemcpyAsync(d_assign, assign, PS * 4, hipMemcpyHostToDevice, st));
+        RSK_HIP(hipMemcpyAsync(d_use, use_cpu, NS * 4, hipMemcpyHostToDevice, st));
+    }
+    RSK_TRY(r->pct.reserve(NS * 4));
+    RSK_TRY(r->haz.reserve(NS));
+    RSK_TRY(r->most.reserve((size_t)S * 4));
+    RSK_TRY(r->key_ws.reserve((size_t)S * 8));
+    const int H = next_pow2(std::max(2, 2 * r->dmax));
+    const size_t lds = ((size_t)2 * H + 8) * 4;
+    RSK_CHECK(lds <= 160 * 1024, "rounds hash needs %zu B of LDS", lds);
+    if (lds > 64 * 1024)
+        RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&car_move_kernel),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    for (int round = 0; round < R; ++round) {
+        int *ev = d_evict + (size_t)round * S;
+        {
+            ScopedTimer tm(ctx, "rounds_detect");
+            RSK_TRY(launch_cpu_pct(st, d_use, d_cap, N, S, r->pct.as<int>()));
+            RSK_TRY(launch_detect(st, r->pct.as<int>(), N, S, threshold, r->haz.as<uint8_t>(),
+                                  r->key_ws.as<unsigned long long>(), r->most.as<int>()));
+        }
+        {
+            ScopedTimer tm(ctx, "rounds_pick");
+            RSK_TRY(launch_pick_max_pod(st, d_assign, r->pod_cpu.as<int>(), r->P, S, r->most.as<int>(),
+                                        r->key_ws.as<unsigned long long>(), ev));
+        }
+        {
+            ScopedTimer tm(ctx, "rounds_move");
+            car_move_kernel<<<dim3((unsigned)S), dim3(kMoveThreads), lds, st>>>(
+                r->row_ptr.as<int>(), r->col.as<int>(), r->pod_cpu.as<int>(), d_assign, d_use, d_cap,
+                r->haz.as<uint8_t>(), ev, S, N, H, d_target + (size_t)round * S);
+            RSK_HIP(hipGetLastError());
+        }
+    }
+    if (!dev) {
+        if (PS) RSK_TRY(copy_back(ctx, assign, d_assign, PS * 4, false));
+        RSK_TRY(copy_back(ctx, use_cpu, d_use, NS * 4, false));
+        if (RS) {
+            RSK_TRY(copy_back(ctx, out_evict, d_evict, RS * 4, false));
+            RSK_TRY(copy_back(ctx, out_target, d_target, RS * 4, false));
+        }
+        RSK_HIP(hipStreamSynchronize(st));
+    }
+    return RSK_OK;
+}
+
+}  // extern "C"

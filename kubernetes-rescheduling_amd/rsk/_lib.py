@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("RSK_LIB", os.path.join(HERE, "librsk.so"))
 
 RSK_OK, RSK_NO_CANDIDATE, RSK_EINVAL, RSK_EHIP, RSK_ERCCL = 0, 1, 2, 3, 4
 RSK_F_DEVICE = 1
-TARGET_NONE, TARGET_NO_CANDIDATE = -1, -2
+TARGET_NONE, TARGET_NO_CANDIDATE, TARGET_NO_EVICT = -1, -2, -3
 
 _i32p = C.POINTER(C.c_int32)
 _i64p = C.POINTER(C.c_int64)
@@ -58,6 +58,10 @@ SIGNATURES = {
     "rsk_detect": (C.c_int, [_vp, _vp, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, C.c_uint32]),
     "rsk_load_std": (C.c_int, [_vp, _vp, _vp, C.c_int32, C.c_int32, _vp, C.c_uint32]),
     "rsk_cut_cost": (C.c_int, [_vp, _vp, _vp, C.c_int32, _vp, C.c_int32, _vp, _vp, C.c_uint32]),
+    "rsk_rounds_create": (C.c_int, [_vp, _vp, _vp, C.c_int32, _vp, C.POINTER(_vp)]),
+    "rsk_rounds_destroy": (C.c_int, [_vp]),
+    "rsk_rounds_run": (C.c_int, [_vp, _vp, C.c_int32, _vp, _vp, C.c_int32, C.c_int32, C.c_int32, _vp, _vp,
+                                 C.c_uint32]),
     "rsk_pick_max_pod": (C.c_int, [_vp, _vp, _vp, C.c_int32, C.c_int32, _vp, _vp, C.c_uint32]),
 }
 

@@ -93,6 +93,53 @@ def car_place(row_ptr, col_idx, assign, S, cap_cpu, use_cpu, hazard, N, rows=Non
         plan.close()
 
 
+class Rounds:
+    """The multi-round detect -> evict -> CAR -> update loop (rsk_rounds_*,
+    SURVEY §8f item 1; main.py:55-110 per scenario, the pod's CPU moving with
+    it).  ``run`` updates ``assign`` / ``use_cpu`` in place and returns
+    (evict[R*S], target[R*S])."""
+
+    def __init__(self, row_ptr, col_idx, pod_cpu, ctx: Optional[Context] = None):
+        self.ctx = ctx or default_context()
+        rp, pc = _c(row_ptr, _I32), _c(pod_cpu, _I32)
+        ci = _c(col_idx, _I32) if len(col_idx) else np.zeros(1, _I32)
+        self.P = int(rp.shape[0]) - 1
+        if pc.size != self.P:
+            raise ValueError("pod_cpu must have P entries")
+        import ctypes as C
+        h = C.c_void_p()
+        check(self.ctx.lib.rsk_rounds_create(self.ctx.handle, ptr(rp), ptr(ci), self.P, ptr(pc), C.byref(h)))
+        self.handle = h
+
+    def run(self, assign, S, cap_cpu, use_cpu, N, R, threshold=30, out_evict=None, out_target=None,
+            device: bool = False):
+        if device:
+            check(self.ctx.lib.rsk_rounds_run(self.handle, ptr(assign), S, ptr(cap_cpu), ptr(use_cpu), N, threshold,
+                                              R, ptr(out_evict), ptr(out_target), RSK_F_DEVICE))
+            return out_evict, out_target
+        for a, dt in ((assign, _I32), (use_cpu, _I32)):
+            if not (isinstance(a, np.ndarray) and a.dtype == dt and a.flags.c_contiguous):
+                raise TypeError("assign and use_cpu are updated in place: pass contiguous int32 numpy arrays")
+        cap = _c(cap_cpu, _I32)
+        if assign.size != self.P * S or cap.size != N or use_cpu.size != N * S:
+            raise ValueError("array sizes do not match P, N, S")
+        ev, tg = np.empty(max(R * S, 1), _I32), np.empty(max(R * S, 1), _I32)
+        check(self.ctx.lib.rsk_rounds_run(self.handle, ptr(assign), S, ptr(cap), ptr(use_cpu), N, threshold, R,
+                                          ptr(ev), ptr(tg), 0))
+        return ev[:R * S], tg[:R * S]
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.ctx.lib.rsk_rounds_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
 def spread_place(pod_count, name_rank, hazard, N, S, ctx=None, out=None, device=False):
     ctx = ctx or default_context()
     if device:

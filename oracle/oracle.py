@@ -51,6 +51,8 @@ def lib():
         L.oracle_load_std.restype = None
         L.oracle_cut_cost.argtypes = [vp, vp, i32, vp, i32, vp, vp]
         L.oracle_cut_cost.restype = None
+        L.oracle_rounds.argtypes = [vp, vp, i32, vp, vp, i32, vp, vp, i32, i32, i32, vp, vp]
+        L.oracle_rounds.restype = None
         _lib = L
     return _lib
 
@@ -147,3 +149,25 @@ def cut_cost(row_ptr, col_idx, assign, P, S, missing=None):
     a, m = _c(assign, np.int32), (None if missing is None else _c(missing, np.int32))
     lib().oracle_cut_cost(_p(rp), _p(ci), P, _p(a), S, _p(m), _p(out))
     return out
+
+
+def dedup_csr(row_ptr, col_idx):
+    """Rows as sets without the self edge (relation lists never double count,
+    rescheduling.py:193; the evicted pod is off the cluster, main.py:73)."""
+    rp, ci = [0], []
+    for p in range(len(row_ptr) - 1):
+        nb = sorted(set(int(q) for q in col_idx[row_ptr[p]:row_ptr[p + 1]]) - {p})
+        ci += nb
+        rp.append(len(ci))
+    return np.array(rp, np.int32), np.array(ci if ci else [0], np.int32)
+
+
+def rounds(row_ptr, col_idx, pod_cpu, assign, S, cap, use, N, R, threshold=30):
+    """The multi-round loop (oracle_rounds); returns (assign', use', evict[R*S], target[R*S])."""
+    rp, ci = dedup_csr(row_ptr, col_idx)
+    P = len(rp) - 1
+    a, u = np.array(assign, np.int32).copy(), np.array(use, np.int32).copy()
+    pc, c = _c(pod_cpu, np.int32), _c(cap, np.int32)
+    ev, tg = np.empty(max(R * S, 1), np.int32), np.empty(max(R * S, 1), np.int32)
+    lib().oracle_rounds(_p(rp), _p(ci), P, _p(pc), _p(a), S, _p(c), _p(u), N, threshold, R, _p(ev), _p(tg))
+    return a, u, ev[:R * S], tg[:R * S]

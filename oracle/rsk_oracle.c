@@ -346,3 +346,48 @@ void oracle_cut_cost(const int32_t *row_ptr, const int32_t *col_idx, int32_t P,
         out_directed[s] = c;
     }
 }
+
+/* ------------------------------------------------------------------------
+ * rounds — the control loop of main.py:55-110 for S independent scenarios,
+ * R rounds, with the build-defined state update of SURVEY.md §8f item 1 (the
+ * reference re-measures the live cluster each round instead):
+ *   pct = cpu_pct(use, cap)                     get_resource_usage.py:37
+ *   hazard, most = detection(pct >= threshold)  harzard_detect.py:3-27
+ *   if most: p = pick_max_pod(most)             delete_replaced_pod.py:41-61
+ *     if p: t = communication(p)                rescheduling.py:174-218
+ *           (p off the cluster, main.py:73: its own entry never counts)
+ *           t >= 0: use[old] -= cpu[p]; use[t] += cpu[p]; assign[p] = t
+ * out_evict[r*S+s] = p (-1 none); out_target[r*S+s] = t, or -3 when nothing
+ * was evicted.  Expects a deduplicated CSR (car_one counts every entry).
+ * ---------------------------------------------------------------------- */
+void oracle_rounds(const int32_t *row_ptr, const int32_t *col_idx, int32_t P, const int32_t *pod_cpu,
+                   int32_t *assign, int32_t S, const int32_t *cap, int32_t *use, int32_t N,
+                   int32_t threshold, int32_t R, int32_t *out_evict, int32_t *out_target)
+{
+    int32_t *pct = (int32_t *)malloc(sizeof(int32_t) * (size_t)N * S);
+    uint8_t *haz = (uint8_t *)malloc((size_t)N * S);
+    int32_t *most = (int32_t *)malloc(sizeof(int32_t) * (size_t)S);
+    int32_t *score = (int32_t *)malloc(sizeof(int32_t) * (size_t)N);
+    for (int32_t r = 0; r < R; ++r) {
+        int32_t *ev = out_evict + (int64_t)r * S, *tg = out_target + (int64_t)r * S;
+        oracle_cpu_pct(use, cap, N, S, pct);
+        oracle_detect(pct, N, S, threshold, haz, most);
+        oracle_pick_max_pod(assign, pod_cpu, P, S, most, ev);
+        for (int32_t s = 0; s < S; ++s) {
+            int32_t p = ev[s], t, m;
+            if (p < 0) { tg[s] = -3; continue; }
+            car_one(row_ptr, col_idx, p, assign, S, s, cap, use, haz, N, score, &t, &m);
+            tg[s] = t;
+            if (t >= 0) {
+                int32_t old = assign[(int64_t)p * S + s];
+                if (old >= 0 && old < N) use[(int64_t)old * S + s] -= pod_cpu[p];
+                use[(int64_t)t * S + s] += pod_cpu[p];
+                assign[(int64_t)p * S + s] = t;
+            }
+        }
+    }
+    free(pct);
+    free(haz);
+    free(most);
+    free(score);
+}

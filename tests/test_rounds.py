@@ -1,0 +1,118 @@
+"""The multi-round loop: detect -> evict -> CAR -> update.
+
+CPU: the oracle's C loop (oracle_rounds) equals a round-by-round composition
+of the single-step oracle functions, which tests/test_oracle_golden.py pins
+against the reference's own fixtures.  The update rule (the pod's CPU moves
+with it) is build-defined: the reference re-measures the live cluster each
+round, so beyond one round the loop is "parity unpinned" against the
+reference and pinned against this restatement only.
+GPU: librsk's rsk_rounds_run against oracle_rounds, bit-exact.
+"""
+import numpy as np
+import pytest
+
+
+def _case(seed, P=400, N=12, S=6):
+    """A synthetic cluster whose hottest nodes sit around the threshold."""
+    from rsk import synth
+    rng = np.random.default_rng(seed)
+    c = synth.make_cluster(P, N, S=S, seed=seed)
+    pod_cpu = c.pod_cpu.astype(np.int32).copy()
+    pod_cpu[rng.random(P) < 0.05] = -1  # never picked (strict '>' from -1)
+    a = c.assign.reshape(P, S)
+    load = np.stack([np.bincount(a[:, s][a[:, s] >= 0], weights=np.maximum(pod_cpu[a[:, s] >= 0], 0),
+                                 minlength=N) for s in range(S)], axis=1)
+    cap = np.full(N, int(load.mean() * 100 / 30) + 1, np.int32)  # mean node at ~30 %
+    use = (load + rng.integers(0, cap[0] // 10, (N, 1))).astype(np.int32).reshape(-1)
+    return c, pod_cpu, cap, use
+
+
+def _compose(c, pod_cpu, cap, use, N, S, R, thr):
+    """Round by round from the pinned single-step oracles."""
+    from oracle import oracle as orc
+    rp, ci = orc.dedup_csr(c.row_ptr, c.col_idx)
+    a, u = c.assign.copy(), use.copy()
+    evs, tgs = [], []
+    for _ in range(R):
+        pct = orc.cpu_pct(u, cap, N, S)
+        haz, most = orc.detect(pct, N, S, thr)
+        ev = orc.pick_max_pod(a, pod_cpu, c.P, S, most)
+        tg = np.full(S, -3, np.int32)
+        for s in range(S):
+            p = int(ev[s])
+            if p < 0:
+                continue
+            t, _ = orc.car(rp, ci, a, S, cap, u, haz, N, rows=np.array([p], np.int32))
+            tg[s] = t.reshape(S)[s]
+            if tg[s] >= 0:
+                old = a[p * S + s]
+                if 0 <= old < N:
+                    u[old * S + s] -= pod_cpu[p]
+                u[tg[s] * S + s] += pod_cpu[p]
+                a[p * S + s] = tg[s]
+        evs.append(ev)
+        tgs.append(tg)
+    return a, u, np.concatenate(evs), np.concatenate(tgs)
+
+
+@pytest.mark.parametrize("seed,thr,moves", [(1, 30, True), (2, 34, True), (3, 10, False)])
+def test_oracle_rounds_equals_composition(seed, thr, moves):
+    """thr 10: every node is hazard, every move raises (target -2)."""
+    from oracle import oracle as orc
+    c, pod_cpu, cap, use = _case(seed)
+    R = 12
+    got = orc.rounds(c.row_ptr, c.col_idx, pod_cpu, c.assign, c.S, cap, use, c.N, R, thr)
+    exp = _compose(c, pod_cpu, cap, use, c.N, c.S, R, thr)
+    for g, e, name in zip(got, exp, ("assign", "use", "evict", "target")):
+        assert np.array_equal(g, e), name
+    if moves:
+        assert (got[2] >= 0).any() and (got[3] >= 0).any()  # the loop really moved pods
+    else:
+        assert (got[3][got[2] >= 0] == -2).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,thr,S", [(1, 30, 6), (2, 45, 64), (3, 10, 65), (4, 30, 1)])
+def test_gpu_rounds_match_oracle(seed, thr, S):
+    from oracle import oracle as orc
+    from rsk import _lib, api
+    c, pod_cpu, cap, use = _case(seed, S=S)
+    R = 16
+    exp = orc.rounds(c.row_ptr, c.col_idx, pod_cpu, c.assign, c.S, cap, use, c.N, R, thr)
+    rounds = api.Rounds(c.row_ptr, c.col_idx, pod_cpu, ctx=_lib.default_context())
+    a, u = c.assign.copy(), use.copy()
+    ev, tg = rounds.run(a, c.S, cap, u, c.N, R, threshold=thr)
+    rounds.close()
+    for g, e, name in zip((a, u, ev, tg), exp, ("assign", "use", "evict", "target")):
+        bad = np.nonzero(g != e)[0]
+        assert bad.size == 0, f"{name}: {bad.size} differ, first {bad[0]}: gpu {g[bad[0]]} oracle {e[bad[0]]}"
+
+
+@pytest.mark.gpu
+def test_gpu_rounds_hub_rows_and_hash():
+    """An evicted hub pod (degree up to 700) and N = 20000 (large hash spread)."""
+    from oracle import oracle as orc
+    from rsk import _lib, api
+    rng = np.random.default_rng(9)
+    P, N, S, R = 1500, 20000, 8, 6
+    rows = [rng.integers(0, P, int(rng.integers(0, 4))).tolist() for _ in range(P)]
+    for k, d in enumerate([700, 300, 90]):
+        rows[k] = rng.choice(P, d, replace=False).tolist()
+    rp = np.zeros(P + 1, np.int32)
+    rp[1:] = np.cumsum([len(r) for r in rows])
+    ci = np.array([q for r in rows for q in r], np.int32)
+    assign = rng.integers(0, 40, P * S).astype(np.int32)  # crowded: real counts and ties
+    assign.reshape(P, S)[:3] = 0                           # the hubs sit on node 0, the hottest
+    pod_cpu = rng.integers(1, 500, P).astype(np.int32)
+    pod_cpu[:3] = 100000
+    cap = np.full(N, 50000, np.int32)
+    use = rng.integers(0, 20000, N * S).astype(np.int32)
+    use.reshape(N, S)[0] = 49000
+    exp = orc.rounds(rp, ci, pod_cpu, assign, S, cap, use, N, R)
+    rounds = api.Rounds(rp, ci, pod_cpu, ctx=_lib.default_context())
+    a, u = assign.copy(), use.copy()
+    ev, tg = rounds.run(a, S, cap, u, N, R)
+    rounds.close()
+    assert (exp[2][:S] <= 2).all()  # the first round evicts a hub pod
+    for g, e, name in zip((a, u, ev, tg), exp, ("assign", "use", "evict", "target")):
+        assert np.array_equal(g, e), name
