@@ -32,6 +32,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 CONFIGS = {
     "headline": dict(P=100_000, N=5_000, S=4096, name="100k pods x 5k nodes, PA tree, 4096 scenarios/GPU (config 3)"),
     "2k64": dict(P=2_000, N=64, S=1, name="2k pods x 64 nodes, single CAR round (config 2)"),
+    "rounds": dict(P=100_000, N=5_000, S=1024, rounds=True,
+                   name="100k pods x 5k nodes x 1024 scenarios/GPU, detect -> evict -> CAR -> update rounds (config 5)"),
     "1m50k": dict(P=1_000_000, N=50_000, S=64, shard="rows",
                   name="1M pods x 50k nodes x 64 scenarios, pod-row sharded (config 4)"),
 }
@@ -58,6 +60,85 @@ def alg_bytes(kernel, P, N, S, info):
             "car_mid": 4 * S * info["mid_rows"] + info["mid_bytes"],
             "car_heavy": 4 * S * info["heavy_rows"] + info["heavy_bytes"],
             "car_prep": 9 * N * S + 4 * N}.get(kernel, 0)
+
+
+def bench_rounds(args, cfg, world, rank, local, dev):
+    """Config 5: one step = one round of detect -> evict -> CAR -> update over
+    this rank's S scenarios (rsk_rounds_run with R = 1 per step, state carried
+    across steps on the device).  Scenario sharded, no data-path collective."""
+    import torch
+    import torch.distributed as dist
+    from rsk import _lib, api, synth
+    from rsk import dist as rdist
+    P, N, S = cfg["P"], cfg["N"], cfg["S"]
+    shard = rdist.shard_for(rank, world, S)
+    c = synth.make_cluster(P, N, S=S, seed=0, s0=shard.s0)
+    ctx = _lib.Context(local)
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_stream(stream.cuda_stream)
+    rounds = api.Rounds(c.row_ptr, c.col_idx, c.pod_cpu, ctx=ctx)
+    T = {k: torch.from_numpy(np.ascontiguousarray(getattr(c, k), dtype=np.int32)).to(dev)
+         for k in ("assign", "cap_cpu", "use_cpu")}
+    R = args.warmup + args.steps
+    ev = torch.empty(R * S, dtype=torch.int32, device=dev)
+    tg = torch.empty(R * S, dtype=torch.int32, device=dev)
+
+    def step(i):
+        rounds.run(T["assign"], S, T["cap_cpu"], T["use_cpu"], N, 1, 30, ev[i * S:], tg[i * S:], device=True)
+
+    for i in range(args.warmup):
+        step(i)
+    ctx.reset_profiling()
+    ctx.set_profiling(not args.no_kernel_events)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    for i in range(args.warmup, R):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t1
+    ctx.set_profiling(False)
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    kernels = {}
+    for name in ("rounds_detect", "rounds_pick", "rounds_move"):
+        ms, n = ctx.kernel_time(name)
+        if n:
+            kernels[name] = {"avg_ms": ms / n, "launches": n, "per_step_ms": ms / args.steps}
+    tgt = tg.cpu().numpy()[args.warmup * S:]
+    # parity: 4 scenarios, 6 rounds from the initial state, GPU loop vs oracle_rounds
+    from oracle import oracle as orc
+    k = min(S, 4)
+    a0 = c.assign.reshape(P, S)[:, :k].copy().reshape(-1)
+    u0 = c.use_cpu.reshape(N, S)[:, :k].copy().reshape(-1)
+    exp = orc.rounds(c.row_ptr, c.col_idx, c.pod_cpu, a0, k, c.cap_cpu, u0, N, 6)
+    a1, u1 = a0.copy(), u0.copy()
+    e1, t1_ = rounds.run(a1, k, c.cap_cpu, u1, N, 6)
+    parity_ok = all(np.array_equal(g, e) for g, e in zip((a1, u1, e1, t1_), exp))
+    ms_step = elapsed * 1e3 / args.steps
+    if rank == 0:
+        line = {
+            "metric": "rescheduling rounds x scenarios per second (detect -> evict -> CAR -> update)",
+            "value": round(world * S / (ms_step / 1e3), 1), "unit": "scenario-rounds/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32",
+            "data": "synthetic",
+            "config": {"workload": cfg["name"], "pods": P, "nodes": N, "scenarios_per_gpu": S, "threshold": 30,
+                       "parallelism": f"scenario-sharded x{world}"},
+            "kernels": kernels, "moves": int((tgt >= 0).sum()), "none": int((tgt == -1).sum()),
+            "no_candidate": int((tgt == -2).sum()), "no_evict": int((tgt == -3).sum()),
+            "parity_sample_ok": bool(parity_ok),
+        }
+        print(json.dumps(line), flush=True)
+    rounds.close()
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
@@ -94,6 +175,8 @@ def main():
     if args.scenarios:
         cfg["S"] = args.scenarios
     P, N, S = cfg["P"], cfg["N"], cfg["S"]
+    if cfg.get("rounds"):
+        return bench_rounds(args, cfg, world, rank, local, dev)
     by_rows = (args.shard or cfg.get("shard", "scenarios")) == "rows"
     t0 = time.time()
     if by_rows:  # pod-row sharding: full assign replica, a contiguous row range per rank
