@@ -179,6 +179,24 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
                    int32_t N, int32_t threshold, int32_t R, int32_t *out_evict, int32_t *out_target,
                    uint32_t flags);
 
+/* ---- µBench workmodel -> relation CSR (host only, no device) -----------------
+ * The caller's on-disk format (workmodelC.json).  One
+ * streaming pass over the JSON (mmap for _load): every service key and every
+ * name under external_services[*].services is interned, nothing else is
+ * materialised.  The relation is the one the reference hard-codes
+ * (main.py:31-52, communicationcost.py:69-88): rel(s) = callees(s) ∪
+ * callers(s), self calls dropped, deduplicated, columns ascending.  Rows are
+ * the defined services in file order, then callees never defined, in order of
+ * first mention (json.load's dict order; rsk/workmodel.py restates it).
+ * _names writes the P names NUL-separated (name_bytes from _sizes).          */
+typedef struct rsk_workmodel rsk_workmodel;
+int rsk_workmodel_parse(const char *json, int64_t len, rsk_workmodel **out);
+int rsk_workmodel_load(const char *path, rsk_workmodel **out);
+int rsk_workmodel_sizes(const rsk_workmodel *wm, int32_t *P, int64_t *nnz, int64_t *name_bytes);
+int rsk_workmodel_csr(const rsk_workmodel *wm, int32_t *row_ptr, int32_t *col_idx);
+int rsk_workmodel_names(const rsk_workmodel *wm, char *buf);
+int rsk_workmodel_destroy(rsk_workmodel *wm);
+
 #ifdef __cplusplus
 }
 #endif

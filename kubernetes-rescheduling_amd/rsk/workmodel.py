@@ -84,3 +84,73 @@ def relation_csr(relations: Dict[str, List[str]], names: List[str], dedup: bool 
         missing.append(miss)
     return (np.asarray(row_ptr, dtype=np.int32), np.asarray(cols, dtype=np.int32),
             np.asarray(missing, dtype=np.int32))
+
+
+# ---------------------------------------------------------------------------
+# Native streaming reader (librsk.so, csrc/rsk_workmodel.cpp) and a synthetic
+# µBench workmodel writer for 100k-1M services.
+# ---------------------------------------------------------------------------
+def read_workmodel(src):
+    """Parse a µBench workmodel with the native one-pass reader.
+
+    ``src``: a path, or the JSON text as ``bytes``/``str``.  Returns
+    ``(names, row_ptr int32[P+1], col_idx int32[nnz])``: the symmetrised relation
+    of ``relation_from_workmodel`` over ``names`` (defined services in file order,
+    then never-defined callees in order of first mention), self calls dropped,
+    deduplicated, columns ascending.  Malformed JSON raises ``RskError``.
+    Host-only: needs librsk.so, not a GPU."""
+    import ctypes as C
+
+    from . import _lib
+
+    lib = _lib.load_library()
+    h = C.c_void_p()
+    text = isinstance(src, (bytes, bytearray)) or (isinstance(src, str) and src.lstrip().startswith("{"))
+    if text:
+        buf = src.encode() if isinstance(src, str) else bytes(src)
+        _lib.check(lib.rsk_workmodel_parse(buf, len(buf), C.byref(h)))
+    else:
+        _lib.check(lib.rsk_workmodel_load(str(src).encode(), C.byref(h)))
+    try:
+        P, nnz, nb = C.c_int32(), C.c_int64(), C.c_int64()
+        _lib.check(lib.rsk_workmodel_sizes(h, C.byref(P), C.byref(nnz), C.byref(nb)))
+        row_ptr = np.empty(P.value + 1, dtype=np.int32)
+        col_idx = np.empty(max(nnz.value, 1), dtype=np.int32)
+        _lib.check(lib.rsk_workmodel_csr(h, row_ptr.ctypes.data, col_idx.ctypes.data))
+        raw = C.create_string_buffer(max(nb.value, 1))
+        _lib.check(lib.rsk_workmodel_names(h, raw))
+        names = raw.raw[: nb.value].decode("utf-8").split("\0")[:-1] if nb.value else []
+    finally:
+        lib.rsk_workmodel_destroy(h)
+    return names, row_ptr, col_idx[: nnz.value]
+
+
+_LOADER = ('{"loader": {"cpu_stress": {"run": true, "range_complexity": [100, 100], "thread_pool_size": 1, '
+           '"trials": 10}, "mean_response_size": 11, "function_id": "f2"}}')
+
+
+def write_synth_workmodel(path: str, P: int, seed: int = 0, chunk: int = 65536) -> None:
+    """Write a µBench-style workmodel of ``P`` services ``s0..s{P-1}`` whose call
+    graph is the preferential-attachment tree of ``synth.pa_tree_parents`` (each
+    parent calls its children, as workmodelC.json's tree does), streamed to
+    ``path`` in chunks so 1M services never build a dict.  Its relation CSR
+    equals ``synth.tree_csr`` of the same parents."""
+    from .synth import pa_tree_parents
+
+    parent = pa_tree_parents(P, np.random.default_rng(seed))
+    order = np.argsort(parent[1:], kind="stable") + 1          # children grouped by parent
+    starts = np.searchsorted(parent[order], np.arange(P + 1))
+    with open(path, "w", encoding="utf-8") as f:
+        f.write("{\n")
+        buf = []
+        for i in range(P):
+            kids = order[starts[i]:starts[i + 1]]
+            ext = ('[{"seq_len": 100, "services": [' + ", ".join(f'"s{k}"' for k in kids) + "]}]") if len(kids) else "[]"
+            buf.append(f'  "s{i}": {{"external_services": {ext}, "internal_service": {_LOADER}, '
+                       f'"request_method": "rest", "workers": 8, "threads": 128, "cpu-requests": "100m"}}'
+                       + (",\n" if i + 1 < P else "\n"))
+            if len(buf) >= chunk:
+                f.write("".join(buf))
+                buf.clear()
+        f.write("".join(buf))
+        f.write("}\n")
