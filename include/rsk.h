@@ -197,6 +197,20 @@ int rsk_workmodel_csr(const rsk_workmodel *wm, int32_t *row_ptr, int32_t *col_id
 int rsk_workmodel_names(const rsk_workmodel *wm, char *buf);
 int rsk_workmodel_destroy(rsk_workmodel *wm);
 
+/* ---- Kubernetes quantity strings -> integers (host only, no device) --------
+ * The snapshot replay of cluster_monitoring.  Replaces the
+ * per-value calls of unit_convertion.py:1-32 (cpu_conversion -> millicores,
+ * mem_conversion -> bytes) made by get_resource_usage.py:11-12,33-34,63-64.
+ * Element i is buf[offs[i] .. offs[i+1]) (n+1 offsets).  status[i] = 0: out[i]
+ * holds the reference's value; 1: outside the plain decimal grammar or int64
+ * (underscores, inf/nan, non-ASCII, malformed) -- the caller converts it with
+ * the Python restatement (rsk/snapshot.py), which also raises the reference's
+ * exception for malformed text.                                              */
+#define RSK_QTY_CPU 0
+#define RSK_QTY_MEM 1
+int rsk_parse_quantities(const char *buf, const int64_t *offs, int64_t n, int32_t kind, int64_t *out,
+                         uint8_t *status);
+
 #ifdef __cplusplus
 }
 #endif

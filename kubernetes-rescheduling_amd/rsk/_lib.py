@@ -69,6 +69,7 @@ SIGNATURES = {
     "rsk_workmodel_csr": (C.c_int, [_vp, _vp, _vp]),
     "rsk_workmodel_names": (C.c_int, [_vp, _vp]),
     "rsk_workmodel_destroy": (C.c_int, [_vp]),
+    "rsk_parse_quantities": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, _vp, _vp]),
 }
 
 
