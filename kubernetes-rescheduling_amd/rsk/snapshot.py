@@ -28,7 +28,6 @@ returns follow the reference function by function; each cites its lines.
 """
 from __future__ import annotations
 
-import ctypes as C
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -75,10 +74,16 @@ def parse_quantities(values: Sequence, kind: int) -> np.ndarray:
     out = np.zeros(n, np.int64)
     if n == 0:
         return out
-    enc = [str(v).encode("utf-8") for v in values]
+    strs = [v if type(v) is str else str(v) for v in values]
+    joined = "".join(strs)
+    buf = joined.encode("utf-8")
+    if len(buf) == len(joined):  # ASCII: byte offsets are character offsets
+        lens = np.fromiter(map(len, strs), np.int64, n)
+    else:
+        lens = np.fromiter((len(x.encode("utf-8")) for x in strs), np.int64, n)
     offs = np.zeros(n + 1, np.int64)
-    np.cumsum([len(b) for b in enc], out=offs[1:])
-    buf = b"".join(enc) or b"\0"
+    np.cumsum(lens, out=offs[1:])
+    buf = buf or b"\0"
     status = np.zeros(n, np.uint8)
     lib = _lib.load_library()
     _lib.check(lib.rsk_parse_quantities(buf, offs.ctypes.data, n, kind, out.ctypes.data, status.ctypes.data))
