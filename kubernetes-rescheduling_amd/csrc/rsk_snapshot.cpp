@@ -17,6 +17,8 @@
 // outside int64, malformed text that must raise the reference's exception) is
 // flagged status 1 and converted by the Python restatement, so the whole
 // function is exact by construction.
+#include <locale.h>
+
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -62,8 +64,10 @@ bool parse_decimal(const char *b, const char *e, double *v) {
     char tmp[128];
     std::memcpy(tmp, b, (size_t)(e - b));
     tmp[e - b] = '\0';
+    // the C locale whatever the host process set (Python's float() ignores LC_NUMERIC)
+    static const locale_t c_loc = newlocale(LC_NUMERIC_MASK, "C", (locale_t)0);
     char *end = nullptr;
-    double d = std::strtod(tmp, &end);
+    double d = c_loc ? strtod_l(tmp, &end, c_loc) : std::strtod(tmp, &end);
     if (end != tmp + (e - b) || !std::isfinite(d)) return false;
     *v = d;
     return true;
