@@ -1,0 +1,265 @@
+// rsk_car.h — internals shared by the CAR sources of librsk.so:
+//   rsk_car.hip    plan building, execute, the wide tile path (N > 65535),
+//                  mid / hub rows for the wide path;
+//   rsk_car16.hip  the compact path (N <= 65535): node-state prep, tiles with
+//                  32-bit {code, node} cells, pivot-delta mid / hub rows.
+// Reference semantics: rescheduling.py:183-214 (see rsk_car.hip's header).
+#pragma once
+
+#include <climits>
+#include <cstdint>
+
+#include "rsk_common.h"
+
+namespace rsk {
+
+constexpr int kKeyHaz = INT_MIN;  // cap - use never reaches INT_MIN (both in [0, 2^31))
+constexpr int kMaxDegree = 1 << 20;                // rows above kHubMax go through the chunked hub path
+constexpr int kLightMax = 32;                      // LDS-tile rows: deg <= 32
+constexpr int kPairMax = 16;                       // pairwise-count classes: deg <= 16
+constexpr int kPackMaxN = (1 << 24) - 1;           // wide sorted classes pack node << 8 | image row: N < kPackMaxN
+constexpr int kMidMax = 64;                        // mid rows: 33..64 (17..64 when N >= kPackMaxN)
+constexpr int kNumMid = 2;                         // buckets D = 32, 64
+constexpr int kMidW[kNumMid] = {36, 68};           // record ints: oi, d, nb[D], pad to x4
+constexpr int kNumHeavy = 6;                       // hub classes: (64,128] (128,256] ... (2048,4096]
+constexpr int kHeavyMax[kNumHeavy] = {128, 255, 512, 1024, 2048, 4096};  // <= 255: u8 counters
+constexpr int kHeavyNJ[kNumHeavy] = {2, 4, 8, 16, 0, 0};  // register entries per lane (0: LDS re-reads)
+constexpr int kHubMax = 4096;                      // wide hub kernel: rows up to this degree
+
+// Light-row tiles.
+constexpr int kTileOwners = 128;                   // max rows scored per tile
+constexpr int kTileRows = 144;                     // max image rows (distinct neighbours) per tile (< 256)
+constexpr int kTileRecInts = 1020;                 // max record ints per tile (+4: unit counter)
+constexpr int kTileThreads = 256;
+constexpr int kNumCls = 6;                         // degree classes d = 1, 2, {0,3,4}, 5-8, 9-16, 17-32
+constexpr int kClsW[kNumCls] = {2, 2, 4, 8, 12, 20};  // record ints
+constexpr int kMetaW = 16;                         // tile meta ints: img_off, nrows, rec_off, rec_ints, n[6], off[6]
+static_assert(kTileRecInts <= kTileThreads * 4, "records are copied to LDS as one int4 per thread");
+
+struct HeavyItem {
+    int oi, rb, d, pad;
+};
+
+struct CarState {
+    int bc;  // best count (max score); 0 = no non-hazard neighbour node
+    int br;  // remaining CPU of the best node
+    int bn;  // best node index
+    int nm;  // neighbour entries whose count == bc  (= bc * |best|)
+};
+
+// Candidate key of the sorted scorers: lexicographic (count, remaining CPU,
+// -node) as one u64 — count 7 bits (<= 64), remaining CPU 32 bits (sign
+// flipped), 0x1ffffff - node 25 bits (N < 2^25).  0 = no candidate.
+constexpr int kNodeBits = 25;
+constexpr unsigned kNodeMask = (1u << kNodeBits) - 1u;
+__device__ __forceinline__ unsigned long long pack_cand(int c, int rem, int n) {
+    return ((unsigned long long)c << (32 + kNodeBits)) |
+           ((unsigned long long)((unsigned)rem ^ 0x80000000u) << kNodeBits) |
+           (unsigned long long)(kNodeMask - (unsigned)n);
+}
+__device__ __forceinline__ int cand_count(unsigned long long k) { return (int)(k >> (32 + kNodeBits)); }
+__device__ __forceinline__ CarState cand_state(unsigned long long best, int nm) {
+    CarState st;
+    st.bc = cand_count(best);
+    st.nm = nm;
+    st.br = (int)((unsigned)(best >> kNodeBits) ^ 0x80000000u);
+    st.bn = (int)(kNodeMask - (unsigned)(best & kNodeMask));
+    return st;
+}
+
+// (remaining CPU, -node) as one u64, 0 = none (node < 2^25)
+__device__ __forceinline__ unsigned long long pack_rn(int rem, int n) {
+    return ((unsigned long long)((unsigned)rem ^ 0x80000000u) << kNodeBits) | (unsigned long long)(kNodeMask - (unsigned)n);
+}
+
+__device__ __forceinline__ unsigned long long zc_pack(int rem, int n) {
+    return ((unsigned long long)((unsigned)rem ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)n);
+}
+
+// The per-scenario zero case (car_prep_kernel), loaded once per lane.
+struct ZeroCase {
+    int cnt;                  // non-hazard nodes in the scenario
+    unsigned long long key;   // packed (cap-use, ~node) max over them
+};
+
+__device__ __forceinline__ ZeroCase load_zc(const int *__restrict__ zc_cnt, const unsigned long long *__restrict__ zc_key,
+                                            int s) {
+    ZeroCase z;
+    z.cnt = zc_cnt[s];
+    z.key = zc_key[s];
+    return z;
+}
+
+// rescheduling.py:199-214 when no neighbour node is a candidate (max score 0):
+// every non-hazard node ties; `max` raises on an empty candidate list.
+__device__ __forceinline__ int zero_target(const ZeroCase &z, int &score) {
+    if (z.cnt == 0) { score = -1; return RSK_TARGET_NO_CANDIDATE; }
+    const int n = (int)(~(unsigned)(z.key & 0xffffffffull));
+    const int rem = (int)((unsigned)(z.key >> 32) ^ 0x80000000u);
+    score = 0;
+    if (z.cnt == 1) return n;
+    return rem >= 0 ? n : RSK_TARGET_NONE;
+}
+
+// rescheduling.py:199-214 applied to the reduced state.
+__device__ __forceinline__ int car_finalize(const CarState &st, const ZeroCase &z, int &score) {
+    if (st.bc == 0) return zero_target(z, score);
+    score = st.bc;
+    if (st.nm == st.bc) return st.bn;
+    return st.br >= 0 ? st.bn : RSK_TARGET_NONE;
+}
+
+// Load with a 32-bit element index: the base stays in SGPRs and the offset is
+// one VGPR (global_load saddr form) instead of a 64-bit address pair per
+// in-flight load.  Callers guarantee index * sizeof(T) < 2^32.
+__device__ __forceinline__ int ld32(const int *__restrict__ base, unsigned idx) {
+    return *reinterpret_cast<const int *>(reinterpret_cast<const char *>(base) + (idx << 2));
+}
+__device__ __forceinline__ unsigned ld16(const unsigned short *__restrict__ base, unsigned idx) {
+    return *reinterpret_cast<const unsigned short *>(reinterpret_cast<const char *>(base) + (idx << 1));
+}
+
+// Plan data read through the constant address space: it never changes during a
+// launch, so wave-uniform reads become scalar loads (lgkmcnt) instead of vector
+// loads queued behind in-flight gathers.
+typedef const __attribute__((address_space(4))) int *cint_ptr;
+__device__ __forceinline__ cint_ptr const_ptr(const int *p) { return (cint_ptr)(uintptr_t)p; }
+
+// Wave-wide reductions through DPP row shifts and row broadcasts (VALU only,
+// no LDS round trips).  Every lane must be active; the result is lane 63's.
+__device__ __forceinline__ int dpp_max(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ int dpp_min(int v) {
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x111, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x112, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x114, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x118, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x142, 0xa, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x143, 0xc, 0xf, false));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long v) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)v, kCtrl, kRowMask, 0xf, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(v >> 32), kCtrl, kRowMask, 0xf, false);
+    return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ unsigned long long dpp_max_u64(unsigned long long v) {  // identity 0
+    unsigned long long w;
+    w = dpp_u64<0x111, 0xf>(v); v = w > v ? w : v;
+    w = dpp_u64<0x112, 0xf>(v); v = w > v ? w : v;
+    w = dpp_u64<0x114, 0xf>(v); v = w > v ? w : v;
+    w = dpp_u64<0x118, 0xf>(v); v = w > v ? w : v;
+    w = dpp_u64<0x142, 0xa>(v); v = w > v ? w : v;
+    w = dpp_u64<0x143, 0xc>(v); v = w > v ? w : v;
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, 63);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), 63);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+template <int D, class T>
+__device__ __forceinline__ void bitonic_sort(T (&v)[D]) {
+#pragma unroll
+    for (int k = 2; k <= D; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const T lo = min(v[i], v[l]), hi = max(v[i], v[l]);
+                    if ((i & k) == 0) { v[i] = lo; v[l] = hi; }
+                    else { v[i] = hi; v[l] = lo; }
+                }
+            }
+            // one network stage at a time: the scheduler would otherwise
+            // interleave stages and hold both halves of every exchange
+            if (D >= 32) __builtin_amdgcn_sched_barrier(0);
+        }
+}
+
+// Next work unit of the wave: lane 0 bumps the workgroup's LDS counter.
+__device__ __forceinline__ int grab(int *ctr, int lane) {
+    int k = 0;
+    if (lane == 0) k = atomicAdd(ctr, 1);
+    return __builtin_amdgcn_readfirstlane(k);
+}
+
+// ---------------------------------------------------------------------------
+// Compact path (rsk_car16.hip), N <= 65535.
+//
+// Node state per (node, scenario) as a 16-bit code, monotone in the remaining
+// CPU rem = cap - use:
+//   0            hazard (never a candidate)
+//   1            rem < 0 (any negative value: a tie whose best rem is < 0 is
+//                None whichever node wins it, rescheduling.py:203-212)
+//   2 + f(rem)   rem >= 0, f non-decreasing: exact below 2^14, then 13
+//                mantissa bits per power of two up to 2^19, one bucket above.
+// A code comparison decides every tie except between distinct nodes with the
+// same code >= 2; those few are resolved exactly from cap / use.
+// ---------------------------------------------------------------------------
+constexpr unsigned kCodeHaz = 0u;
+constexpr unsigned kCodeNeg = 1u;
+constexpr int kMaxNodes16 = 65535;  // node ids fit 16 bits, 0xffff stays free as the pad node
+
+struct Prep16Args {
+    const int *cap, *use;
+    const uint8_t *haz;
+    int N, S;
+    unsigned short *code;        // [N*S] or null
+    int *nodekey;                // [N*S] (hazard ? KEY_HAZ : cap - use) or null
+    int *zc_cnt;                 // [S]
+    unsigned long long *zc_key;  // [S]
+};
+
+struct Tile16Args {
+    const int *img_pods;   // concatenated per-tile image pod lists
+    const int *meta;       // [T][kMetaW]
+    const int *recs;       // concatenated per-tile record blobs (16-B aligned)
+    const int *assign;
+    const unsigned short *code;
+    const int *cap, *use;  // exact tie resolution between equal codes
+    const int *zc_cnt;
+    const unsigned long long *zc_key;
+    int *out_target;
+    int *out_score;
+    int S, N, T, lsl;      // SL = 1 << lsl scenarios per workgroup (64 when S >= 64)
+    int img_cells;         // LDS cells of the largest image (rmax * SL); the records follow
+    int rec_cap;           // record ints reserved in LDS; the unit counter follows
+    int order, xcd_per;    // grid order (RSK_TILE_ORDER) as in the wide kernel
+    int ablate;            // profiling only (RSK_ABLATE_TILE): 1 skip image load, 2 skip scoring
+    unsigned n_assign, n_out, n_pods, n_recs, n_key;  // element counts (debug bounds build)
+};
+
+// Pivot-delta rows (mid and hub rows of the compact path).
+struct PivotArgs {
+    const HeavyItem *items;   // {out_row, col offset, deg}
+    int n_items;
+    const int *hcol;          // neighbour lists
+    const int *assign;
+    const unsigned short *code;
+    const int *cap, *use;
+    const int *zc_cnt;
+    const unsigned long long *zc_key;
+    int *out_target;
+    int *out_score;
+    int S, N;
+    int H;                    // pivot count table: N (direct u16) or hash slots
+    int hash;                 // 1: hash table of 2*H words (N too large for a direct table)
+};
+
+int launch_prep(hipStream_t stream, const Prep16Args &a);
+int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off32, unsigned blocks, size_t lds);
+size_t tile16_lds_bytes(int rmax, int lsl, int rec_cap);
+int launch_pivot(hipStream_t stream, const PivotArgs &a, int dmax, unsigned groups_per_item);
+unsigned tile16_debug_take();  // debug bounds build: violation flags of the compact kernels (cleared)
+
+}  // namespace rsk

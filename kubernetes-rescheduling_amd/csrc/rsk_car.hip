@@ -40,110 +40,9 @@
 #include <unordered_map>
 #include <vector>
 
-#include "rsk_common.h"
+#include "rsk_car.h"
 
 namespace rsk {
-
-constexpr int kKeyHaz = INT_MIN;  // cap - use never reaches INT_MIN (both in [0, 2^31))
-constexpr int kMaxDegree = 4096;
-constexpr int kLightMax = 32;                      // LDS-tile rows: deg <= 32
-constexpr int kPairMax = 16;                       // pairwise-count classes: deg <= 16
-constexpr int kPackMaxN = (1 << 24) - 1;           // sorted classes pack node << 8 | image row: N < kPackMaxN
-constexpr int kMidMax = 64;                        // mid kernel: 33..64 (17..64 when N >= kPackMaxN)
-constexpr int kNumMid = 2;                         // buckets D = 32, 64
-constexpr int kMidW[kNumMid] = {36, 68};           // record ints: oi, d, nb[D], pad to x4
-constexpr int kNumHeavy = 6;                       // hub classes: (64,128] (128,256] ... (2048,4096]
-constexpr int kHeavyMax[kNumHeavy] = {128, 255, 512, 1024, 2048, 4096};  // <= 255: u8 counters
-constexpr int kHeavyNJ[kNumHeavy] = {2, 4, 8, 16, 0, 0};  // register entries per lane (0: LDS re-reads)
-
-// Light-row tiles.  LDS per workgroup <= 144 rows x 32 scenarios x 8 B + 1024
-// record ints = 40 KiB: four workgroups (16 waves) per CU.
-constexpr int kTileOwners = 128;                   // max rows scored per tile
-constexpr int kTileRows = 144;                     // max image rows (distinct neighbours) per tile (< 256)
-constexpr int kTileRecInts = 1020;                 // max record ints per tile (+4: unit counter; 40 KiB total)
-constexpr int kTileThreads = 256;
-constexpr int kTileWaves = kTileThreads / 64;
-constexpr int kNumCls = 6;                         // degree classes d = 1, 2, {0,3,4}, 5-8, 9-16, 17-32
-constexpr int kClsW[kNumCls] = {2, 2, 4, 8, 12, 20};  // record ints
-constexpr int kMetaW = 16;                         // tile meta ints: img_off, nrows, rec_off, rec_ints, n[6], off[6]
-static_assert(kTileRecInts <= kTileThreads * 4, "records are copied to LDS as one int4 per thread");
-
-struct CarState {
-    int bc;  // best count (max score); 0 = no non-hazard neighbour node
-    int br;  // remaining CPU of the best node
-    int bn;  // best node index
-    int nm;  // neighbour entries whose count == bc  (= bc * |best|)
-};
-
-// Candidate key of the sorted scorers: lexicographic (count, remaining CPU,
-// -node) as one u64 — count 7 bits (<= 64), remaining CPU 32 bits (sign
-// flipped), 0x1ffffff - node 25 bits (N < 2^25).  0 = no candidate.
-constexpr int kNodeBits = 25;
-constexpr unsigned kNodeMask = (1u << kNodeBits) - 1u;
-__device__ __forceinline__ unsigned long long pack_cand(int c, int rem, int n) {
-    return ((unsigned long long)c << (32 + kNodeBits)) |
-           ((unsigned long long)((unsigned)rem ^ 0x80000000u) << kNodeBits) |
-           (unsigned long long)(kNodeMask - (unsigned)n);
-}
-__device__ __forceinline__ int cand_count(unsigned long long k) { return (int)(k >> (32 + kNodeBits)); }
-__device__ __forceinline__ CarState cand_state(unsigned long long best, int nm) {
-    CarState st;
-    st.bc = cand_count(best);
-    st.nm = nm;
-    st.br = (int)((unsigned)(best >> kNodeBits) ^ 0x80000000u);
-    st.bn = (int)(kNodeMask - (unsigned)(best & kNodeMask));
-    return st;
-}
-
-__device__ __forceinline__ unsigned long long zc_pack(int rem, int n) {
-    return ((unsigned long long)((unsigned)rem ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)n);
-}
-
-// The per-scenario zero case (car_prep_kernel), loaded once per lane.
-struct ZeroCase {
-    int cnt;                  // non-hazard nodes in the scenario
-    unsigned long long key;   // packed (cap-use, ~node) max over them
-};
-
-__device__ __forceinline__ ZeroCase load_zc(const int *__restrict__ zc_cnt, const unsigned long long *__restrict__ zc_key,
-                                            int s) {
-    ZeroCase z;
-    z.cnt = zc_cnt[s];
-    z.key = zc_key[s];
-    return z;
-}
-
-// rescheduling.py:199-214 when no neighbour node is a candidate (max score 0):
-// every non-hazard node ties; `max` raises on an empty candidate list.
-__device__ __forceinline__ int zero_target(const ZeroCase &z, int &score) {
-    if (z.cnt == 0) { score = -1; return RSK_TARGET_NO_CANDIDATE; }
-    const int n = (int)(~(unsigned)(z.key & 0xffffffffull));
-    const int rem = (int)((unsigned)(z.key >> 32) ^ 0x80000000u);
-    score = 0;
-    if (z.cnt == 1) return n;
-    return rem >= 0 ? n : RSK_TARGET_NONE;
-}
-
-// rescheduling.py:199-214 applied to the reduced state.
-__device__ __forceinline__ int car_finalize(const CarState &st, const ZeroCase &z, int &score) {
-    if (st.bc == 0) return zero_target(z, score);
-    score = st.bc;
-    if (st.nm == st.bc) return st.bn;
-    return st.br >= 0 ? st.bn : RSK_TARGET_NONE;
-}
-
-// Load with a 32-bit element index: the base stays in SGPRs and the offset is
-// one VGPR (global_load saddr form) instead of a 64-bit address pair per
-// in-flight load.  Callers guarantee index * 4 < 2^32.
-__device__ __forceinline__ int ld32(const int *__restrict__ base, unsigned idx) {
-    return *reinterpret_cast<const int *>(reinterpret_cast<const char *>(base) + (idx << 2));
-}
-
-// Plan data read through the constant address space: it never changes during a
-// launch, so wave-uniform reads become scalar loads (lgkmcnt) instead of vector
-// loads queued behind in-flight gathers.
-typedef const __attribute__((address_space(4))) int *cint_ptr;
-__device__ __forceinline__ cint_ptr const_ptr(const int *p) { return (cint_ptr)(uintptr_t)p; }
 
 // Bounds-checked debug build (make debug -> librsk_dbg.so, -DRSK_DEBUG_BOUNDS):
 // tile-kernel global accesses check their element index against the buffer
@@ -160,123 +59,6 @@ __device__ __forceinline__ unsigned dbg_bound(unsigned idx, unsigned lim, unsign
 #else
 #define RSK_BOUND(idx, lim, code) (idx)
 #endif
-
-// Wave-wide reductions through DPP row shifts and row broadcasts (VALU only,
-// no LDS round trips).  Every lane must be active; the result is lane 63's.
-__device__ __forceinline__ int dpp_max(int v) {
-    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x111, 0xf, 0xf, false));  // row_shr:1
-    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x112, 0xf, 0xf, false));  // row_shr:2
-    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x114, 0xf, 0xf, false));  // row_shr:4
-    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x118, 0xf, 0xf, false));  // row_shr:8
-    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
-    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
-    return __builtin_amdgcn_readlane(v, 63);
-}
-__device__ __forceinline__ int dpp_min(int v) {
-    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x111, 0xf, 0xf, false));
-    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x112, 0xf, 0xf, false));
-    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x114, 0xf, 0xf, false));
-    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x118, 0xf, 0xf, false));
-    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x142, 0xa, 0xf, false));
-    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x143, 0xc, 0xf, false));
-    return __builtin_amdgcn_readlane(v, 63);
-}
-
-template <int D, class T>
-__device__ __forceinline__ void bitonic_sort(T (&v)[D]) {
-#pragma unroll
-    for (int k = 2; k <= D; k <<= 1)
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-#pragma unroll
-            for (int i = 0; i < D; ++i) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const T lo = min(v[i], v[l]), hi = max(v[i], v[l]);
-                    if ((i & k) == 0) { v[i] = lo; v[l] = hi; }
-                    else { v[i] = hi; v[l] = lo; }
-                }
-            }
-            // one network stage at a time: the scheduler would otherwise
-            // interleave stages and hold both halves of every exchange
-            if (D > 32) __builtin_amdgcn_sched_barrier(0);
-        }
-}
-
-// ---------------------------------------------------------------------------
-// K0: packed node key + per-scenario zero case.  Thread t -> (V consecutive
-// scenarios, node chunk): V-wide loads of use / hazard per node.  The zero
-// case (non-hazard count, packed max) is reduced in LDS per workgroup first —
-// threads of one workgroup that share a scenario meet in one LDS slot — so a
-// scenario receives one global atomic per workgroup, not one per thread (with
-// few scenarios, e.g. S = 64, thousands of threads would otherwise contend for
-// the same address).
-// ---------------------------------------------------------------------------
-template <int V>
-struct VecT;
-template <> struct VecT<1> { typedef int I; typedef uint8_t H; };
-template <> struct VecT<4> { typedef int4 I; typedef uchar4 H; };
-
-__device__ __forceinline__ void vec_get(const int &v, int (&o)[1]) { o[0] = v; }
-__device__ __forceinline__ void vec_get(const int4 &v, int (&o)[4]) { o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w; }
-__device__ __forceinline__ void vec_get(const uint8_t &v, int (&o)[1]) { o[0] = v; }
-__device__ __forceinline__ void vec_get(const uchar4 &v, int (&o)[4]) { o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w; }
-__device__ __forceinline__ int vec_make(const int (&k)[1]) { return k[0]; }
-__device__ __forceinline__ int4 vec_make(const int (&k)[4]) { return make_int4(k[0], k[1], k[2], k[3]); }
-
-template <int V>
-__global__ __launch_bounds__(256) void car_prep_kernel(const int *__restrict__ cap, const typename VecT<V>::I *__restrict__ use,
-                                                       const typename VecT<V>::H *__restrict__ haz, int N, int SV,
-                                                       int npb, unsigned total, typename VecT<V>::I *__restrict__ nodekey,
-                                                       int *__restrict__ zc_cnt,
-                                                       unsigned long long *__restrict__ zc_key) {
-    __shared__ int lcnt[256 * V];
-    __shared__ unsigned long long lkey[256 * V];
-    const unsigned t = blockIdx.x * 256u + threadIdx.x;
-    const unsigned base = (blockIdx.x * 256u) % (unsigned)SV;  // vector slot of thread 0
-    const int nslot = min(256, SV);
-    for (int i = threadIdx.x; i < nslot * V; i += 256) { lcnt[i] = 0; lkey[i] = 0ull; }
-    __syncthreads();
-    if (t < total) {
-        const int sv = (int)(t % (unsigned)SV);
-        const int n0 = (int)(t / (unsigned)SV) * npb;
-        const int n1 = min(N, n0 + npb);
-        int cnt[V];
-        unsigned long long best[V];
-#pragma unroll
-        for (int x = 0; x < V; ++x) { cnt[x] = 0; best[x] = 0ull; }
-#pragma unroll 4
-        for (int n = n0; n < n1; ++n) {
-            const size_t idx = (size_t)n * SV + sv;
-            int uu[V], hh[V], k[V];
-            vec_get(use[idx], uu);
-            vec_get(haz[idx], hh);
-            const int c = cap[n];
-#pragma unroll
-            for (int x = 0; x < V; ++x) {
-                k[x] = hh[x] ? kKeyHaz : c - uu[x];
-                cnt[x] += hh[x] ? 0 : 1;
-                const unsigned long long pk = hh[x] ? 0ull : zc_pack(k[x], n);
-                best[x] = pk > best[x] ? pk : best[x];
-            }
-            nodekey[idx] = vec_make(k);
-        }
-        const int slot = (int)(((unsigned)sv + (unsigned)SV - base) % (unsigned)SV);  // < nslot
-#pragma unroll
-        for (int x = 0; x < V; ++x)
-            if (cnt[x]) {
-                atomicAdd(&lcnt[slot * V + x], cnt[x]);
-                atomicMax(&lkey[slot * V + x], best[x]);
-            }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < nslot * V; i += 256)
-        if (lcnt[i]) {
-            const int s = (int)(((base + (unsigned)(i / V)) % (unsigned)SV) * V + (unsigned)(i % V));
-            atomicAdd(&zc_cnt[s], lcnt[i]);
-            atomicMax(&zc_key[s], lkey[i]);
-        }
-}
 
 // ---------------------------------------------------------------------------
 // K1: rows with deg <= 32 in LDS tiles.
@@ -349,24 +131,15 @@ __device__ __forceinline__ void tile_emit(const TileArgs &a, int oi, const TileL
     if (kScore) st_cell<kOff32>(a.out_score, (unsigned)oi, (unsigned)a.S, (unsigned)L.s, sc);
 }
 
-// The tile image in LDS: {node, key} per (image row, scenario column).  With
-// N <= 65535 (kN16) nodes are u16 next to the int32 keys (6 B per entry, five
-// workgroups per CU); otherwise int2 pairs (8 B, four per CU).
-template <bool kN16>
+// The tile image in LDS: {node, key} int2 per (image row, scenario column).
+// This kernel serves N > 65535 only (rsk_car16.hip's 32-bit cells cover the
+// rest), so node ids are full ints and an assignment outside [0, N) can never
+// alias a real node.
 struct TileImg {
-    int2 *w;                // !kN16: {node, key}
-    int *key;               // kN16
-    unsigned short *node;   // kN16
+    int2 *w;
     int lsl;
-    __device__ __forceinline__ int2 at(int row, int col) const {
-        const int i = (row << lsl) + col;
-        if (kN16) return make_int2((int)node[i], key[i]);
-        return w[i];
-    }
-    __device__ __forceinline__ void put(int i, int n, int k) const {
-        if (kN16) { node[i] = (unsigned short)n; key[i] = k; }
-        else w[i] = make_int2(n, k);
-    }
+    __device__ __forceinline__ int2 at(int row, int col) const { return w[(row << lsl) + col]; }
+    __device__ __forceinline__ void put(int i, int n, int k) const { w[i] = make_int2(n, k); }
 };
 
 // d == 1: the neighbour's node is the single best unless hazard (zero case).
@@ -573,20 +346,7 @@ __device__ __forceinline__ void tile_load_image(const TileArgs &a, const Img &im
     }
 }
 
-// LDS ints taken by the image of `cells` entries (rounded up to 16 B).
-template <bool kN16>
-__host__ __device__ constexpr int tile_img_ints(int cells) {
-    return kN16 ? ((cells + (cells + 1) / 2 + 3) & ~3) : ((2 * cells + 3) & ~3);
-}
-
-// Next work unit of the wave: lane 0 bumps the workgroup's LDS counter.
-__device__ __forceinline__ int grab(int *ctr, int lane) {
-    int k = 0;
-    if (lane == 0) k = atomicAdd(ctr, 1);
-    return __builtin_amdgcn_readfirstlane(k);
-}
-
-template <bool kScore, bool kOff32, bool kN16>
+template <bool kScore, bool kOff32>
 __global__ __launch_bounds__(kTileThreads, 4) void car_tile_kernel(TileArgs a) {
     extern __shared__ __attribute__((aligned(16))) int lds[];  // img {node,key} [rmax][SL], then records
     // chunk-major (default: concurrent workgroups share a chunk's nodekey
@@ -606,12 +366,10 @@ __global__ __launch_bounds__(kTileThreads, 4) void car_tile_kernel(TileArgs a) {
     const int SL = 1 << a.lsl;
     const int s0 = chunk * SL;
     const int cells = a.rmax * SL;
-    TileImg<kN16> img;
+    TileImg img;
     img.lsl = a.lsl;
     img.w = reinterpret_cast<int2 *>(lds);
-    img.key = lds;
-    img.node = reinterpret_cast<unsigned short *>(lds + cells);
-    int *rec = lds + tile_img_ints<kN16>(cells);  // 16-B aligned for the int4 record reads
+    int *rec = lds + ((2 * cells + 3) & ~3);  // 16-B aligned for the int4 record reads
     const cint_ptr m = const_ptr(a.meta) + (size_t)tile * kMetaW;
     const int img_off = m[0], nrows = m[1], rec_off = m[2], rec_ints = m[3];
 
@@ -762,34 +520,6 @@ __global__ __launch_bounds__(256) void car_mid_kernel(MidArgs a) {
 // ---------------------------------------------------------------------------
 // K3: hub rows (deg > 64), see car_hub_kernel below.
 // ---------------------------------------------------------------------------
-struct HeavyItem {
-    int oi, rb, d, pad;
-};
-
-// (remaining CPU, -node) as one u64, 0 = none (node < 2^25)
-__device__ __forceinline__ unsigned long long pack_rn(int rem, int n) {
-    return ((unsigned long long)((unsigned)rem ^ 0x80000000u) << kNodeBits) | (unsigned long long)(kNodeMask - (unsigned)n);
-}
-
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long v) {
-    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)v, kCtrl, kRowMask, 0xf, false);
-    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(v >> 32), kCtrl, kRowMask, 0xf, false);
-    return ((unsigned long long)hi << 32) | lo;
-}
-__device__ __forceinline__ unsigned long long dpp_max_u64(unsigned long long v) {  // identity 0
-    unsigned long long w;
-    w = dpp_u64<0x111, 0xf>(v); v = w > v ? w : v;
-    w = dpp_u64<0x112, 0xf>(v); v = w > v ? w : v;
-    w = dpp_u64<0x114, 0xf>(v); v = w > v ? w : v;
-    w = dpp_u64<0x118, 0xf>(v); v = w > v ? w : v;
-    w = dpp_u64<0x142, 0xa>(v); v = w > v ? w : v;
-    w = dpp_u64<0x143, 0xc>(v); v = w > v ? w : v;
-    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, 63);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), 63);
-    return ((unsigned long long)hi << 32) | lo;
-}
-
 // Per-wave count table of one scenario's neighbour nodes: direct u8 / u16
 // counters packed 4 / 2 per word (node < kDirectMaxN; u8 only when the class
 // degree is <= 255, so a counter never carries into its neighbour), or an
@@ -1032,7 +762,7 @@ struct rsk_car_plan {
     DevBuf heavy_items[kNumHeavy];
     DevBuf hcol;
     // per-execute workspace
-    DevBuf nodekey, zc;
+    DevBuf nodekey, code, zc;
     // the inputs, kept for the N >= kPackMaxN variant (built on first use)
     std::vector<int32_t> h_row_ptr, h_col_idx, h_rows;
     bool has_rows = false;
@@ -1046,6 +776,7 @@ struct rsk_car_plan {
         for (auto &b : heavy_items) b.release();
         hcol.release();
         nodekey.release();
+        code.release();
         zc.release();
     }
 };
@@ -1407,9 +1138,24 @@ int plan_create(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, in
 // Mid and hub launches go round-robin over the `nside` streams in `side`
 // (mid, hub classes in degree order), so the few-row latency-bound hub classes
 // do not queue behind each other.
-int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t *side, int nside, const int *d_assign,
-                const int *d_key, const int *d_zcnt, const unsigned long long *d_zkey, int *d_target, int *d_score,
-                int S, int N) {
+struct SideBufs {
+    const int *assign, *key, *cap, *use, *zcnt;
+    const unsigned short *code;
+    const unsigned long long *zkey;
+    int *target, *score;
+};
+
+// Mid and hub rows of the compact path go through the pivot-delta kernel
+// (rsk_car16.hip) once it covers them; until then the wide kernels read the
+// exact node keys.
+bool plan_side_compact(const rsk_car_plan *) { return false; }
+
+int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t *side, int nside, const SideBufs &b, int S, int N,
+                bool compact) {
+    (void)compact;
+    const int *d_assign = b.assign, *d_key = b.key, *d_zcnt = b.zcnt;
+    const unsigned long long *d_zkey = b.zkey;
+    int *d_target = b.target, *d_score = b.score;
     int next = 0;
     auto pick = [&]() { return side[next++ % nside]; };
     ScoreCtx sc;
@@ -1543,14 +1289,19 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     RSK_CHECK((int64_t)N * S < ((int64_t)1 << 30) && N < (1 << kNodeBits) && (int64_t)plan->P * S < ((int64_t)1 << 40),
               "N*S too large (N=%d S=%d; need N*S < 2^30, N < 2^25)", N, S);
     RSK_CHECK(out_target, "null out_target");
-    if (N >= kPackMaxN && plan->n_sorted_rows > 0) {
-        // the sorted tile classes pack node << 8 | row into 32 bits: route
+    // compact path (rsk_car16.hip) whenever node ids fit 16 bits
+    static const bool compact_ok = env_int("RSK_COMPACT", 1) != 0;
+    const bool compact = N <= kMaxNodes16 && compact_ok;
+    if (!compact && N >= kPackMaxN && plan->n_sorted_rows > 0) {
+        // the wide sorted tile classes pack node << 8 | row into 32 bits: route
         // 17..64 rows through the mid kernel instead (variant built once)
         if (!plan->alt)
             RSK_TRY(plan_create(ctx, plan->h_row_ptr.data(), plan->h_col_idx.data(), plan->P,
                                 plan->has_rows ? plan->h_rows.data() : nullptr, plan->Q, kPairMax, &plan->alt));
         return rsk_car_plan_execute(plan->alt, assign, S, cap_cpu, use_cpu, hazard, N, out_target, out_score, flags);
     }
+    RSK_CHECK(compact || plan->max_deg <= kHubMax, "a row has degree %d > %d: supported for N <= %d only",
+              plan->max_deg, kHubMax, kMaxNodes16);
     const bool dev = (flags & RSK_F_DEVICE) != 0;
     const size_t PS_ = (size_t)plan->P * S, NS = (size_t)N * S, QS = (size_t)plan->Q * S;
 
@@ -1564,44 +1315,100 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     RSK_TRY(stage_out(ctx, 4, out_target, QS * 4, dev, reinterpret_cast<void **>(&d_target)));
     if (out_score) RSK_TRY(stage_out(ctx, 5, out_score, QS * 4, dev, reinterpret_cast<void **>(&d_score)));
 
-    RSK_TRY(plan->nodekey.reserve(NS * 4));
+    const bool side_rows = plan_has_side(plan);
+    int *d_key = nullptr;
+    unsigned short *d_code = nullptr;
+    if (!compact || (side_rows && !plan_side_compact(plan))) {
+        RSK_TRY(plan->nodekey.reserve(NS * 4));
+        d_key = plan->nodekey.as<int>();
+    }
+    if (compact) {
+        RSK_TRY(plan->code.reserve(NS * 2));
+        d_code = plan->code.as<unsigned short>();
+    }
     RSK_TRY(plan->zc.reserve((size_t)S * 12 + 16));
-    int *d_key = plan->nodekey.as<int>();
     unsigned long long *d_zkey = plan->zc.as<unsigned long long>();
     int *d_zcnt = reinterpret_cast<int *>(d_zkey + S);
     RSK_HIP(hipMemsetAsync(plan->zc.ptr, 0, (size_t)S * 12, ctx->stream));
 
-    {   // K0: 4 scenarios per thread when S % 4 == 0 (16-B use / nodekey words)
-        const bool v4 = S % 4 == 0 && ((uintptr_t)d_use % 16) == 0 && ((uintptr_t)d_haz % 4) == 0;
-        const int SV = v4 ? S / 4 : S;
-        const int target_threads = 256 * 1024;
-        const int npb = (int)std::max<int64_t>(1, ceil_div((int64_t)N * SV, target_threads));
-        const int64_t chunks = ceil_div(N, npb);
-        const unsigned total = (unsigned)(chunks * SV);
+    {   // K0: node state (codes and / or exact keys) + the zero case
+        Prep16Args pa;
+        pa.cap = d_cap;
+        pa.use = d_use;
+        pa.haz = d_haz;
+        pa.N = N;
+        pa.S = S;
+        pa.code = d_code;
+        pa.nodekey = d_key;
+        pa.zc_cnt = d_zcnt;
+        pa.zc_key = d_zkey;
         ScopedTimer tm(ctx, "car_prep");
-        if (v4)
-            car_prep_kernel<4><<<dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, ctx->stream>>>(
-                d_cap, reinterpret_cast<const int4 *>(d_use), reinterpret_cast<const uchar4 *>(d_haz), N, SV, npb,
-                total, reinterpret_cast<int4 *>(d_key), d_zcnt, d_zkey);
-        else
-            car_prep_kernel<1><<<dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, ctx->stream>>>(
-                d_cap, d_use, d_haz, N, SV, npb, total, d_key, d_zcnt, d_zkey);
-        RSK_HIP(hipGetLastError());
+        RSK_TRY(launch_prep(ctx->stream, pa));
     }
     // mid and hub rows run on up to kAux side streams (RSK_OVERLAP = how many),
     // beside the tile kernel or, with RSK_SIDE_FIRST=1, ahead of it
     static const int overlap = std::max(0, std::min(rsk_ctx::kAux, env_int("RSK_OVERLAP", 1)));
     static const bool side_first = env_int("RSK_SIDE_FIRST", 0) != 0;
     hipStream_t side[rsk_ctx::kAux] = {ctx->stream, ctx->stream, ctx->stream};
-    const int nside = plan_has_side(plan) && plan->T > 0 ? overlap : 0;
+    const int nside = side_rows && plan->T > 0 ? overlap : 0;
     if (nside) {
         RSK_TRY(aux_fork(ctx, nside));
         for (int i = 0; i < nside; ++i) side[i] = ctx->aux[i];
     }
-    RSK_TRY(launch_side(plan, ctx, side, std::max(nside, 1), d_assign, d_key, d_zcnt, d_zkey, d_target, d_score, S,
-                        N));
+    SideBufs sb;
+    sb.assign = d_assign;
+    sb.key = d_key;
+    sb.code = d_code;
+    sb.cap = d_cap;
+    sb.use = d_use;
+    sb.zcnt = d_zcnt;
+    sb.zkey = d_zkey;
+    sb.target = d_target;
+    sb.score = d_score;
+    RSK_TRY(launch_side(plan, ctx, side, std::max(nside, 1), sb, S, N, compact));
     if (nside && side_first) RSK_TRY(aux_join(ctx, nside));
-    if (plan->T > 0) {   // K1 tiles
+    static const int ablate = env_int("RSK_ABLATE_TILE", 0);
+    static const int order = env_int("RSK_TILE_ORDER", 2);
+    const bool off32 = (int64_t)std::max(plan->P, plan->Q) * S * 4 < ((int64_t)1 << 32);
+    if (plan->T > 0 && compact) {   // K1 tiles, 32-bit {code, node} cells
+        Tile16Args a;
+        std::memset(&a, 0, sizeof(a));
+        a.img_pods = plan->img_pods.as<int>();
+        a.meta = plan->meta.as<int>();
+        a.recs = plan->recs.as<int>();
+        a.assign = d_assign;
+        a.code = d_code;
+        a.cap = d_cap;
+        a.use = d_use;
+        a.zc_cnt = d_zcnt;
+        a.zc_key = d_zkey;
+        a.out_target = d_target;
+        a.out_score = d_score;
+        a.S = S;
+        a.N = N;
+        a.T = plan->T;
+        a.n_assign = (unsigned)std::min<size_t>(PS_, UINT32_MAX);
+        a.n_out = (unsigned)std::min<size_t>(QS, UINT32_MAX);
+        a.n_pods = (unsigned)plan->n_img_pods;
+        a.n_recs = (unsigned)plan->n_recs;
+        a.n_key = (unsigned)NS;
+        static const int sl_max = [] { int v = env_int("RSK_TILE_SL", 64); return v >= 1 && v <= 64 ? v : 64; }();
+        const int SL = std::min(next_pow2(S), next_pow2(sl_max));
+        a.lsl = 0;
+        while ((1 << a.lsl) < SL) ++a.lsl;
+        a.order = order;
+        a.ablate = ablate;
+        a.rec_cap = (plan->recmax + 3) & ~3;
+        a.img_cells = (plan->rmax * SL + 3) & ~3;
+        const size_t lds = tile16_lds_bytes(plan->rmax, a.lsl, a.rec_cap);
+        RSK_CHECK(plan->recmax <= kTileRecInts, "tile records exceed %d ints", kTileRecInts);
+        const int64_t units = ceil_div(S, SL) * plan->T;
+        a.xcd_per = (int)ceil_div(units, 8);
+        const int64_t blocks = order == 2 ? 8 * (int64_t)a.xcd_per : units;
+        RSK_CHECK(blocks < INT32_MAX, "tile grid too large");
+        ScopedTimer tm(ctx, "car_tile");
+        RSK_TRY(launch_tile16(ctx->stream, a, d_score != nullptr, off32, (unsigned)blocks, lds));
+    } else if (plan->T > 0) {   // K1 tiles, wide {node, key} pairs
         TileArgs a;
         std::memset(&a, 0, sizeof(a));
         a.img_pods = plan->img_pods.as<int>();
@@ -1622,31 +1429,23 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         a.n_pods = (unsigned)plan->n_img_pods;
         a.n_recs = (unsigned)plan->n_recs;
         a.n_key = (unsigned)NS;
-        static const int sl_max = [] { int v = env_int("RSK_TILE_SL", 32); return v >= 1 && v <= 32 ? v : 32; }();
-        const int SL = std::min(next_pow2(S), next_pow2(sl_max));
+        const int SL = std::min(next_pow2(S), 32);
         a.lsl = 0;
         while ((1 << a.lsl) < SL) ++a.lsl;
-        static const int ablate = env_int("RSK_ABLATE_TILE", 0);
-        static const int order = env_int("RSK_TILE_ORDER", 2);
         a.order = order;
         a.ablate = ablate;
-        const bool off32 = (int64_t)std::max(plan->P, plan->Q) * S * 4 < ((int64_t)1 << 32);
         a.rec_cap = (plan->recmax + 3) & ~3;
-        const bool n16 = N <= 65535 && env_int("RSK_TILE_N16", 1) != 0;
         const int cells = plan->rmax * SL;
-        const size_t lds = ((size_t)(n16 ? tile_img_ints<true>(cells) : tile_img_ints<false>(cells)) + a.rec_cap + 4) * 4;
+        const size_t lds = ((size_t)((2 * cells + 3) & ~3) + a.rec_cap + 4) * 4;
         RSK_CHECK(lds <= 160 * 1024 && plan->recmax <= kTileRecInts, "tile image needs %zu B of LDS", lds);
         const int64_t units = ceil_div(S, SL) * plan->T;
         a.xcd_per = (int)ceil_div(units, 8);
         const int64_t blocks = order == 2 ? 8 * (int64_t)a.xcd_per : units;
         RSK_CHECK(blocks < INT32_MAX, "tile grid too large");
         using TileKern = void (*)(TileArgs);
-        static const TileKern kerns[8] = {
-            &car_tile_kernel<false, false, false>, &car_tile_kernel<false, true, false>,
-            &car_tile_kernel<true, false, false>,  &car_tile_kernel<true, true, false>,
-            &car_tile_kernel<false, false, true>,  &car_tile_kernel<false, true, true>,
-            &car_tile_kernel<true, false, true>,   &car_tile_kernel<true, true, true>};
-        const TileKern kern = kerns[(n16 ? 4 : 0) + (d_score ? 2 : 0) + (off32 ? 1 : 0)];
+        static const TileKern kerns[4] = {&car_tile_kernel<false, false>, &car_tile_kernel<false, true>,
+                                          &car_tile_kernel<true, false>, &car_tile_kernel<true, true>};
+        const TileKern kern = kerns[(d_score ? 2 : 0) + (off32 ? 1 : 0)];
         if (lds > 64 * 1024)
             RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -1661,6 +1460,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         RSK_HIP(hipStreamSynchronize(ctx->stream));
         RSK_HIP(hipMemcpyFromSymbol(&flags_h, HIP_SYMBOL(rsk_dbg_flags), 4));
         RSK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(rsk_dbg_flags), &zero, 4));
+        flags_h |= tile16_debug_take();
         RSK_CHECK(flags_h == 0, "debug bounds violation flags=0x%x (1 out, 2 pods, 4 assign, 8 nodekey, 16 recs)",
                   flags_h);
     }

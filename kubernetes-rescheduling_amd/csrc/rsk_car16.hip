@@ -1,0 +1,633 @@
+// rsk_car16.hip — the compact CAR path for N <= 65535 nodes (gfx950).
+//
+// Reference: the score loop + argmax of `communication`,
+// rescheduling.py:183-214 (see rsk_car.hip for the full statement).
+//
+// car_prep_kernel  one pass over the node state per (node, scenario):
+//                  code16[n*S+s] (rsk_car.h: 0 hazard, 1 rem < 0, 2+f(rem)
+//                  monotone), optionally the exact nodekey[n*S+s] for the wide
+//                  kernels, and the per-scenario zero case.
+// car_tile16       rows of degree <= 32 in LDS tiles, like the wide tile
+//                  kernel, but the image cell is ONE 32-bit word
+//                  (code << 16 | node) and a workgroup covers 64 scenarios:
+//                  per image row a wave-instruction reads 256 contiguous
+//                  bytes of assign and gathers 128 contiguous bytes of codes
+//                  (the wide kernel: 128 B + 128 B of 32-bit keys per 32
+//                  scenarios) — a third fewer cache lines through the vector
+//                  memory path, which bounds the kernel.  Ties decided by
+//                  codes alone except equal codes >= 2 on distinct nodes,
+//                  resolved exactly from cap / use (rare: the code spacing is
+//                  1 below 16384 millicores and 2..32 up to 2^19).
+#include <algorithm>
+#include <climits>
+
+#include "rsk_car.h"
+
+namespace rsk {
+
+#ifdef RSK_DEBUG_BOUNDS
+static __device__ unsigned rsk_dbg16;
+__device__ __forceinline__ unsigned dbg16(unsigned idx, unsigned lim, unsigned code) {
+    if (idx < lim) return idx;
+    atomicOr(&rsk_dbg16, code);
+    return 0u;
+}
+#define RSK_B16(idx, lim, code) dbg16((unsigned)(idx), (unsigned)(lim), (code))
+#else
+#define RSK_B16(idx, lim, code) (idx)
+#endif
+
+// ---------------------------------------------------------------------------
+// node state
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned code16(int rem, bool haz) {
+    if (haz) return kCodeHaz;
+    if (rem < 0) return kCodeNeg;
+    const unsigned x = (unsigned)rem;
+    if (x < (1u << 14)) return 2u + x;
+    const int e = 31 - __clz((int)x);  // 14..30
+    if (e > 18) return 2u + (1u << 14) + 5u * 8192u;  // one bucket from 2^19 up (exact ties resolve it)
+    return 2u + (1u << 14) + (unsigned)(e - 14) * 8192u + ((x >> (e - 13)) & 0x1fffu);
+}
+
+template <int V>
+struct VecT;
+template <> struct VecT<1> { typedef int I; typedef uint8_t H; typedef unsigned short C; };
+template <> struct VecT<4> { typedef int4 I; typedef uchar4 H; typedef ushort4 C; };
+
+__device__ __forceinline__ void vec_get(const int &v, int (&o)[1]) { o[0] = v; }
+__device__ __forceinline__ void vec_get(const int4 &v, int (&o)[4]) { o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w; }
+__device__ __forceinline__ void vec_get(const uint8_t &v, int (&o)[1]) { o[0] = v; }
+__device__ __forceinline__ void vec_get(const uchar4 &v, int (&o)[4]) { o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w; }
+__device__ __forceinline__ int vec_make(const int (&k)[1]) { return k[0]; }
+__device__ __forceinline__ int4 vec_make(const int (&k)[4]) { return make_int4(k[0], k[1], k[2], k[3]); }
+__device__ __forceinline__ unsigned short cvec_make(const unsigned (&k)[1]) { return (unsigned short)k[0]; }
+__device__ __forceinline__ ushort4 cvec_make(const unsigned (&k)[4]) {
+    return make_ushort4((unsigned short)k[0], (unsigned short)k[1], (unsigned short)k[2], (unsigned short)k[3]);
+}
+
+// Thread t -> (V consecutive scenarios, node chunk): V-wide loads of use /
+// hazard per node.  The zero case (non-hazard count, packed max of (rem,
+// ~node)) is reduced in LDS per workgroup first — threads of one workgroup
+// that share a scenario meet in one LDS slot — so a scenario receives one
+// global atomic per workgroup, not one per thread.
+template <int V, bool kCode, bool kKey>
+__global__ __launch_bounds__(256) void car_prep_kernel(const int *__restrict__ cap, const typename VecT<V>::I *__restrict__ use,
+                                                       const typename VecT<V>::H *__restrict__ haz, int N, int SV,
+                                                       int npb, unsigned total, typename VecT<V>::C *__restrict__ code,
+                                                       typename VecT<V>::I *__restrict__ nodekey,
+                                                       int *__restrict__ zc_cnt, unsigned long long *__restrict__ zc_key) {
+    __shared__ int lcnt[256 * V];
+    __shared__ unsigned long long lkey[256 * V];
+    const unsigned t = blockIdx.x * 256u + threadIdx.x;
+    const unsigned base = (blockIdx.x * 256u) % (unsigned)SV;  // vector slot of thread 0
+    const int nslot = min(256, SV);
+    for (int i = threadIdx.x; i < nslot * V; i += 256) { lcnt[i] = 0; lkey[i] = 0ull; }
+    __syncthreads();
+    if (t < total) {
+        const int sv = (int)(t % (unsigned)SV);
+        const int n0 = (int)(t / (unsigned)SV) * npb;
+        const int n1 = min(N, n0 + npb);
+        int cnt[V];
+        unsigned long long best[V];
+#pragma unroll
+        for (int x = 0; x < V; ++x) { cnt[x] = 0; best[x] = 0ull; }
+#pragma unroll 4
+        for (int n = n0; n < n1; ++n) {
+            const size_t idx = (size_t)n * SV + sv;
+            int uu[V], hh[V], k[V];
+            unsigned cd[V];
+            vec_get(use[idx], uu);
+            vec_get(haz[idx], hh);
+            const int c = cap[n];
+#pragma unroll
+            for (int x = 0; x < V; ++x) {
+                const int rem = c - uu[x];
+                k[x] = hh[x] ? kKeyHaz : rem;
+                cd[x] = code16(rem, hh[x] != 0);
+                cnt[x] += hh[x] ? 0 : 1;
+                const unsigned long long pk = hh[x] ? 0ull : zc_pack(rem, n);
+                best[x] = pk > best[x] ? pk : best[x];
+            }
+            if (kKey) nodekey[idx] = vec_make(k);
+            if (kCode) code[idx] = cvec_make(cd);
+        }
+        const int slot = (int)(((unsigned)sv + (unsigned)SV - base) % (unsigned)SV);  // < nslot
+#pragma unroll
+        for (int x = 0; x < V; ++x)
+            if (cnt[x]) {
+                atomicAdd(&lcnt[slot * V + x], cnt[x]);
+                atomicMax(&lkey[slot * V + x], best[x]);
+            }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nslot * V; i += 256)
+        if (lcnt[i]) {
+            const int s = (int)(((base + (unsigned)(i / V)) % (unsigned)SV) * V + (unsigned)(i % V));
+            atomicAdd(&zc_cnt[s], lcnt[i]);
+            atomicMax(&zc_key[s], lkey[i]);
+        }
+}
+
+template <int V>
+static int prep_launch(hipStream_t stream, const Prep16Args &a, int SV, int npb, unsigned total) {
+    typedef typename VecT<V>::I I;
+    typedef typename VecT<V>::H H;
+    typedef typename VecT<V>::C C;
+    const dim3 grid((unsigned)ceil_div(total, 256)), block(256);
+    const I *use = reinterpret_cast<const I *>(a.use);
+    const H *haz = reinterpret_cast<const H *>(a.haz);
+    C *code = reinterpret_cast<C *>(a.code);
+    I *key = reinterpret_cast<I *>(a.nodekey);
+    if (a.code && a.nodekey)
+        car_prep_kernel<V, true, true><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key);
+    else if (a.code)
+        car_prep_kernel<V, true, false><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key);
+    else
+        car_prep_kernel<V, false, true><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key);
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
+}
+
+int launch_prep(hipStream_t stream, const Prep16Args &a) {
+    RSK_CHECK(a.code || a.nodekey, "prep: nothing to write");
+    // 4 scenarios per thread when S % 4 == 0 (16-B use / key words, 8-B codes)
+    const bool v4 = a.S % 4 == 0 && ((uintptr_t)a.use % 16) == 0 && ((uintptr_t)a.haz % 4) == 0;
+    const int SV = v4 ? a.S / 4 : a.S;
+    const int target_threads = 256 * 1024;
+    const int npb = (int)std::max<int64_t>(1, ceil_div((int64_t)a.N * SV, target_threads));
+    const int64_t chunks = ceil_div(a.N, npb);
+    const unsigned total = (unsigned)(chunks * SV);
+    return v4 ? prep_launch<4>(stream, a, SV, npb, total) : prep_launch<1>(stream, a, SV, npb, total);
+}
+
+// ---------------------------------------------------------------------------
+// car_tile16: rows with deg <= 32 in LDS tiles (plan: rsk_car.hip TileBuilder).
+//
+// Workgroup = (tile, chunk of SL = 2^lsl scenarios), 4 waves; SL = 64 when
+// S >= 64 (kL64: lane = scenario throughout, every record wave-uniform).
+//   phase 1  image row r, scenario column c -> LDS cell
+//              (code16[node, s] << 16) | node        node = assign[pod_r, s]
+//            or kCellPad (code 0 = no candidate, node 0xffff = no real node)
+//            when the assignment is outside [0, N).
+//   phase 2  per record the degree-class scorer reads its cells from LDS,
+//            stores one target word per lane.
+// Every global access is issued from a clamped, always-valid index and never
+// guarded by a lane-divergent branch (hipcc otherwise waits vmcnt(0) per
+// element), except the exact tie resolution, which is rare.
+// ---------------------------------------------------------------------------
+constexpr unsigned kCellPad = 0x0000ffffu;
+
+__device__ __forceinline__ unsigned cell_code(unsigned c) { return c >> 16; }
+__device__ __forceinline__ int cell_node(unsigned c) { return (int)(c & 0xffffu); }
+// candidate word: larger code first, then the lower node (the reference's
+// `rem > r` keeps the first node in nodes_name order on equal rem)
+__device__ __forceinline__ unsigned cell_cand(unsigned c) { return c ^ 0xffffu; }
+__device__ __forceinline__ int cand_node(unsigned w) { return (int)((w & 0xffffu) ^ 0xffffu); }
+
+#ifndef RSK_TILE_NT
+#define RSK_TILE_NT 3  // streamed image loads / target stores non-temporal (codes stay in L2)
+#endif
+
+struct Lane16 {
+    int col;    // image column of the lane's (clamped) scenario
+    int s;      // clamped scenario
+    int slot, PS;
+    int zt, zs; // zero-case target / score
+};
+
+template <bool kOff32>
+__device__ __forceinline__ size_t cell_off(unsigned i, unsigned S, unsigned s) {
+    if (kOff32) return (size_t)((i * S + s) << 2);
+    return ((size_t)i * S + s) << 2;
+}
+
+template <bool kScore, bool kOff32>
+__device__ __forceinline__ void emit16(const Tile16Args &a, int oi, const Lane16 &L, int t, int sc) {
+#ifdef RSK_DEBUG_BOUNDS
+    if ((size_t)(unsigned)oi * a.S + L.s >= a.n_out || oi < 0) { atomicOr(&rsk_dbg16, 1u); return; }
+#endif
+    int *p = reinterpret_cast<int *>(reinterpret_cast<char *>(a.out_target) + cell_off<kOff32>((unsigned)oi, a.S, L.s));
+    if (RSK_TILE_NT & 2) __builtin_nontemporal_store(t, p);
+    else *p = t;
+    if (kScore) {
+        int *q = reinterpret_cast<int *>(reinterpret_cast<char *>(a.out_score) + cell_off<kOff32>((unsigned)oi, a.S, L.s));
+        if (RSK_TILE_NT & 2) __builtin_nontemporal_store(sc, q);
+        else *q = sc;
+    }
+}
+
+// Exact remaining CPU of node n in scenario s (a code >= 2: not hazard).
+__device__ __forceinline__ int exact_rem(const Tile16Args &a, int n, int s) {
+    return a.cap[n] - ld32(a.use, (unsigned)n * (unsigned)a.S + (unsigned)s);
+}
+
+struct Img16 {
+    const unsigned *w;
+    int lsl;
+    __device__ __forceinline__ unsigned at(int row, int col) const { return w[(row << lsl) + col]; }
+};
+
+// d == 1: the neighbour's node unless it is no candidate (zero case).
+template <int U, bool kScore, bool kOff32>
+__device__ __forceinline__ void t16_d1(const Tile16Args &a, const Img16 &img, const int *rec, int n, const Lane16 &L,
+                                       int p0) {
+    const int2 *r2 = reinterpret_cast<const int2 *>(rec);
+    int2 r[U];
+    unsigned c[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) r[u] = r2[min((p0 + u) * L.PS + L.slot, n - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) c[u] = img.at(r[u].y, L.col);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const bool z = cell_code(c[u]) == kCodeHaz;
+        emit16<kScore, kOff32>(a, r[u].x, L, z ? L.zt : cell_node(c[u]), z ? L.zs : 1);
+    }
+}
+
+// d == 2: same node -> score 2; one no-candidate -> the other; two distinct
+// candidates -> a tie of two: larger remaining CPU, then lower index, None
+// when that remaining CPU is < 0.
+template <int U, bool kScore, bool kOff32>
+__device__ __forceinline__ void t16_d2(const Tile16Args &a, const Img16 &img, const int *rec, int n, const Lane16 &L,
+                                       int p0) {
+    const int2 *r2 = reinterpret_cast<const int2 *>(rec);
+    int2 r[U];
+    unsigned c0[U], c1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) r[u] = r2[min((p0 + u) * L.PS + L.slot, n - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        c0[u] = img.at(r[u].y & 0xffff, L.col);
+        c1[u] = img.at((int)((unsigned)r[u].y >> 16), L.col);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const unsigned k0 = cell_code(c0[u]), k1 = cell_code(c1[u]);
+        const unsigned w0 = k0 ? cell_cand(c0[u]) : 0u, w1 = k1 ? cell_cand(c1[u]) : 0u;
+        const unsigned best = max(w0, w1);
+        const bool same = c0[u] == c1[u];
+        const bool single = w0 == 0u || w1 == 0u || same;
+        int t = cand_node(best);
+        if (!single && cell_code(best) < 2u) t = RSK_TARGET_NONE;
+        if (!single && k0 == k1 && k0 >= 2u) {  // equal codes: exact remaining CPU (rare)
+            const int n0 = cell_node(c0[u]), n1 = cell_node(c1[u]);
+            const int e0 = exact_rem(a, n0, L.s), e1 = exact_rem(a, n1, L.s);
+            t = (e0 > e1 || (e0 == e1 && n0 < n1)) ? n0 : n1;
+        }
+        const bool zero = best == 0u;
+        emit16<kScore, kOff32>(a, r[u].x, L, zero ? L.zt : t, zero ? L.zs : (same ? 2 : 1));
+    }
+}
+
+template <int W>
+__device__ __forceinline__ void load_rec16(const int *rec, int (&r)[W]) {
+    const int4 *r4 = reinterpret_cast<const int4 *>(rec);
+#pragma unroll
+    for (int w = 0; w < W / 4; ++w) {
+        const int4 x = r4[w];
+        r[4 * w] = x.x; r[4 * w + 1] = x.y; r[4 * w + 2] = x.z; r[4 * w + 3] = x.w;
+    }
+}
+
+// Exact resolution among candidates whose word's code equals `bk`: max exact
+// remaining CPU, then the lower node.
+template <int D>
+__device__ __forceinline__ int exact_among(const Tile16Args &a, const unsigned (&w)[D], unsigned bk, int s) {
+    int br = INT_MIN, bn = INT_MAX;
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+        if (cell_code(w[j]) == bk) {
+            const int nd = cand_node(w[j]);
+            const int e = exact_rem(a, nd, s);
+            if (e > br || (e == br && nd < bn)) { br = e; bn = nd; }
+        }
+    return bn;
+}
+
+// 0 or 3 <= d <= D (D = 4, 8, 16): pairwise equality counts of the cells in
+// registers — equal cells are the same node (in one scenario a node has one
+// code) — c[j] = #{i < j : cell i == cell j}, so a node's last entry holds its
+// count - 1 and the entries at the maximum are exactly one per maximal node.
+template <int D, int W, bool kScore, bool kOff32>
+__device__ __forceinline__ void t16_dn(const Tile16Args &a, const Img16 &img, const int *rec, int n, const Lane16 &L,
+                                       int p0) {
+    int r[W];
+    load_rec16<W>(rec + min(p0 * L.PS + L.slot, n - 1) * W, r);
+    const int d = r[1];
+    unsigned x[D];
+    int c[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        const unsigned pr = (unsigned)r[2 + j / 2];
+        const int row = (j & 1) ? (int)(pr >> 16) : (int)(pr & 0xffffu);
+        const unsigned e = img.at(row, L.col);  // padding entries read row 0
+        x[j] = j < d ? e : kCellPad;
+        c[j] = 0;
+    }
+#pragma unroll
+    for (int j = 1; j < D; ++j)
+#pragma unroll
+        for (int i = 0; i < j; ++i) c[j] += x[j] == x[i];
+    int M1 = -1;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        c[j] = cell_code(x[j]) == kCodeHaz ? -1 : c[j];
+        M1 = max(M1, c[j]);
+    }
+    unsigned w[D], best = 0u;
+    int nm = 0;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        const bool m = c[j] == M1;
+        w[j] = m ? cell_cand(x[j]) : 0u;
+        best = max(best, w[j]);
+        nm += m;
+    }
+    const unsigned bk = cell_code(best);
+    int t = nm == 1 ? cand_node(best) : (bk >= 2u ? cand_node(best) : RSK_TARGET_NONE);
+    if (nm > 1 && bk >= 2u) {
+        int namb = 0;
+#pragma unroll
+        for (int j = 0; j < D; ++j) namb += cell_code(w[j]) == bk;
+        if (namb > 1) t = exact_among<D>(a, w, bk, L.s);
+    }
+    emit16<kScore, kOff32>(a, r[0], L, M1 < 0 ? L.zt : t, M1 < 0 ? L.zs : M1 + 1);
+}
+
+// The 17..32 class row's cells in registers, sorted (equal nodes form runs).
+template <int D>
+__device__ __forceinline__ void t16_ds_cells(const Img16 &img, const int *rc, int d, int col, unsigned (&x)[D]) {
+#pragma unroll
+    for (int j0 = 0; j0 < D; j0 += 8) {
+        if (j0 % 16 == 0) __builtin_amdgcn_sched_barrier(0);
+        const int4 pk = *reinterpret_cast<const int4 *>(rc + 4 + (j0 >> 1));
+        const unsigned pw[4] = {(unsigned)pk.x, (unsigned)pk.y, (unsigned)pk.z, (unsigned)pk.w};
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const int j = j0 + t;
+            const int row = (t & 1) ? (int)(pw[t >> 1] >> 16) : (int)(pw[t >> 1] & 0xffffu);
+            const unsigned e = img.at(row, col);
+            x[j] = j < d ? e : kCellPad;
+        }
+    }
+    bitonic_sort<D, unsigned>(x);
+}
+
+// Exact tie resolution straight from the LDS image (rare path, kept free of
+// register arrays): among the row's distinct nodes with code bk and count M,
+// the largest exact remaining CPU, then the lower node.
+__device__ __forceinline__ int t16_exact_scan(const Tile16Args &a, const Img16 &img, const int *rows, int d, int col, int M,
+                                           unsigned bk, int s) {
+    int br = INT_MIN, bn = INT_MAX;
+#pragma unroll 1
+    for (int j = 0; j < d; ++j) {
+        const unsigned cj = img.at((int)(((unsigned)rows[j >> 1] >> ((j & 1) * 16)) & 0xffffu), col);
+        if (cell_code(cj) != bk) continue;
+        int cnt = 0;
+#pragma unroll 1
+        for (int i = 0; i < d; ++i)
+            cnt += img.at((int)(((unsigned)rows[i >> 1] >> ((i & 1) * 16)) & 0xffffu), col) == cj;
+        if (cnt != M) continue;
+        const int nd = cell_node(cj);
+        const int e = exact_rem(a, nd, s);
+        if (e > br || (e == br && nd < bn)) { br = e; bn = nd; }
+    }
+    return bn;
+}
+
+// 17 <= d <= 32, record [oi, d, -, -, rows from int 4]: sort the 32 cells with
+// a register bitonic network (equal nodes become runs), then walk the runs
+// once keeping the lexicographic (count, code, -node) maximum, the number of
+// runs at the maximal count and the number of runs sharing the best
+// (count, code).  The rare exact tie (equal codes >= 2) rescans the LDS image
+// (t16_exact_scan) rather than keeping the cells live across the walk.
+template <bool kScore, bool kOff32>
+__device__ __forceinline__ void t16_ds(const Tile16Args &a, const Img16 &img, const int *rec, int n, const Lane16 &L,
+                                       int p0) {
+    constexpr int D = 32, W = 20;
+    const int *rc = rec + min(p0 * L.PS + L.slot, n - 1) * W;
+    const int2 hd = *reinterpret_cast<const int2 *>(rc);
+    const int d = hd.y;
+    unsigned bw = 0u;
+    int M = 0, R = 0, namb = 0;
+    {
+        unsigned x[D];
+        t16_ds_cells<D>(img, rc, d, L.col, x);
+        // walk 1: the maximal run length over candidate nodes and how many runs reach it
+        int c = 0;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            c = (j > 0 && x[j] == x[j > 0 ? j - 1 : 0]) ? c + 1 : 1;
+            const bool end = j == D - 1 || x[j < D - 1 ? j + 1 : j] != x[j];
+            const bool cand = end && cell_code(x[j]) != kCodeHaz;
+            const bool gt = cand && c > M, eq = cand && c == M;
+            R = gt ? 1 : (eq ? R + 1 : R);
+            M = gt ? c : M;
+        }
+        // walk 2: among runs of length M, the best (code, -node) word and how
+        // many of them share its code
+        c = 0;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            c = (j > 0 && x[j] == x[j > 0 ? j - 1 : 0]) ? c + 1 : 1;
+            const bool end = j == D - 1 || x[j < D - 1 ? j + 1 : j] != x[j];
+            const bool cand = end && c == M && cell_code(x[j]) != kCodeHaz;
+            const unsigned w = cand ? cell_cand(x[j]) : 0u;
+            const unsigned kw = cell_code(w), kb = cell_code(bw);
+            namb = kw > kb ? 1 : (cand && kw == kb ? namb + 1 : namb);
+            bw = max(bw, w);
+        }
+    }
+    const unsigned bk = cell_code(bw);
+    int t = R == 1 ? cand_node(bw) : (bk >= 2u ? cand_node(bw) : RSK_TARGET_NONE);
+    const bool need = R > 1 && bk >= 2u && namb > 1;
+    if (__builtin_amdgcn_ballot_w64(need)) {  // rare: wave-uniform branch
+        const int te = t16_exact_scan(a, img, rc + 4, d, L.col, M, bk, L.s);
+        t = need ? te : t;
+    }
+    emit16<kScore, kOff32>(a, rc[0], L, M == 0 ? L.zt : t, M == 0 ? L.zs : M);
+}
+
+// Phase 1.  kL64: wave w loads image rows w, w+4, ... — the pod index is
+// wave-uniform (scalar load), the assign slice one 256-B row, the code gather
+// one 128-B line whenever the row's pod sits on one node in all 64 scenarios.
+// Generic (SL < 64): lanes = (row, scenario) pairs as in the wide kernel.
+template <bool kL64, bool kOff32>
+__device__ __forceinline__ void t16_load_image(const Tile16Args &a, unsigned *img, int img_off, int nrows, int s0) {
+    const unsigned S = (unsigned)a.S, N = (unsigned)a.N;
+    const char *__restrict__ asg = reinterpret_cast<const char *>(a.assign);
+    if (kL64) {
+        const int lane = threadIdx.x & 63;
+        const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+        const int s = s0 + lane;
+        const unsigned sl = (unsigned)min(s, (int)S - 1);
+        const bool s_ok = s < (int)S;
+        const cint_ptr pods = const_ptr(a.img_pods) + img_off;
+        constexpr int kB = kTileRows / 8;  // rows per wave per batch: two batches cover 144 rows
+        for (int r0 = 0; r0 < nrows; r0 += 4 * kB) {
+            int v[kB];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                const int row = min(r0 + u * 4 + wave, nrows - 1);
+                const unsigned q = (unsigned)pods[RSK_B16(row, a.n_pods - img_off, 2u)];
+#ifdef RSK_DEBUG_BOUNDS
+                if ((size_t)q * S + sl >= a.n_assign) atomicOr(&rsk_dbg16, 4u);
+#endif
+                const int *pa = reinterpret_cast<const int *>(asg + cell_off<kOff32>(RSK_B16(q, a.n_assign / S, 4u), S, sl));
+                v[u] = (RSK_TILE_NT & 1) ? __builtin_nontemporal_load(pa) : *pa;
+            }
+            unsigned cd[kB];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                const bool ok = (unsigned)v[u] < N && s_ok;
+                cd[u] = ld16(a.code, RSK_B16(ok ? (unsigned)v[u] * S + sl : 0u, a.n_key, 8u));
+            }
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                const int row = min(r0 + u * 4 + wave, nrows - 1);
+                const bool ok = (unsigned)v[u] < N && s_ok;
+                img[(row << 6) + lane] = ok ? ((cd[u] << 16) | (unsigned)v[u]) : kCellPad;
+            }
+        }
+    } else {
+        const int *__restrict__ pods = a.img_pods + img_off;
+        constexpr int kE = kTileRows * 32 / kTileThreads;
+        const int total = nrows << a.lsl;
+        const int msk = (1 << a.lsl) - 1;
+        for (int b = 0; b < total; b += kTileThreads * kE) {
+            int e[kE], v[kE];
+#pragma unroll
+            for (int u = 0; u < kE; ++u) {
+                e[u] = min(b + u * kTileThreads + (int)threadIdx.x, total - 1);
+                const unsigned q = (unsigned)pods[RSK_B16(e[u] >> a.lsl, a.n_pods - img_off, 2u)];
+                const unsigned s = (unsigned)min(s0 + (e[u] & msk), (int)S - 1);
+                const int *pa = reinterpret_cast<const int *>(asg + cell_off<kOff32>(RSK_B16(q, a.n_assign / S, 4u), S, s));
+                v[u] = *pa;
+            }
+            unsigned cd[kE];
+#pragma unroll
+            for (int u = 0; u < kE; ++u) {
+                const int s = s0 + (e[u] & msk);
+                const bool ok = (unsigned)v[u] < N && s < (int)S;
+                cd[u] = ld16(a.code, RSK_B16(ok ? (unsigned)v[u] * S + (unsigned)s : 0u, a.n_key, 8u));
+            }
+#pragma unroll
+            for (int u = 0; u < kE; ++u) {
+                const int s = s0 + (e[u] & msk);
+                const bool ok = (unsigned)v[u] < N && s < (int)S;
+                img[e[u]] = ok ? ((cd[u] << 16) | (unsigned)v[u]) : kCellPad;
+            }
+        }
+    }
+}
+
+size_t tile16_lds_bytes(int rmax, int lsl, int rec_cap) {
+    return ((size_t)rmax * ((size_t)1 << lsl) + (size_t)rec_cap + 4) * 4;
+}
+
+template <bool kScore, bool kOff32, bool kL64>
+__global__ __launch_bounds__(kTileThreads, 4) void car_tile16_kernel(Tile16Args a) {
+    extern __shared__ __attribute__((aligned(16))) int lds[];  // img cells [rmax][SL], records, unit counter
+    const int lsl = kL64 ? 6 : a.lsl;
+    const int SL = 1 << lsl;
+    const int nchunk = (a.S + SL - 1) >> lsl;
+    int unit = blockIdx.x;
+    if (a.order == 2) {  // XCD-contiguous: blocks b and b + 8 share an XCD
+        unit = (int)(blockIdx.x & 7u) * a.xcd_per + (int)(blockIdx.x >> 3);
+        if (unit >= nchunk * a.T) return;  // whole workgroup, before any barrier
+    }
+    const int tile = a.order == 1 ? unit / nchunk : unit % a.T;
+    const int chunk = a.order == 1 ? unit % nchunk : unit / a.T;
+    const int lane = threadIdx.x & 63;
+    const int s0 = chunk * SL;
+    unsigned *img = reinterpret_cast<unsigned *>(lds);
+    int *rec = lds + a.img_cells;  // 16-B aligned (img_cells % 4 == 0) for the int4 record reads
+    const cint_ptr m = const_ptr(a.meta) + (size_t)tile * kMetaW;
+    const int img_off = m[0], nrows = m[1], rec_off = m[2], rec_ints = m[3];
+
+    {   // records -> LDS: one int4 per thread, clamped
+        const int i = min((int)threadIdx.x * 4, rec_ints - 4);
+        *reinterpret_cast<int4 *>(rec + i) =
+            *reinterpret_cast<const int4 *>(a.recs + RSK_B16(rec_off + i + 3, a.n_recs, 16u) - 3);
+    }
+    if (!(a.ablate & 1)) t16_load_image<kL64, kOff32>(a, img, img_off, nrows, s0);
+
+    Lane16 L;
+    L.PS = 64 >> lsl;
+    L.slot = lane >> lsl;
+    L.s = min(s0 + (lane & (SL - 1)), a.S - 1);
+    L.col = L.s - s0;
+    {
+        int zs;
+        L.zt = zero_target(load_zc(a.zc_cnt, a.zc_key, L.s), zs);
+        L.zs = zs;
+    }
+    if (threadIdx.x == 0) rec[a.rec_cap] = 0;  // work-unit counter
+    __syncthreads();
+    if (a.ablate & 2) return;  // profiling ablation: no scoring (results are wrong)
+    Img16 im;
+    im.w = img;
+    im.lsl = lsl;
+    // Work units (PS records each: d1 4 x PS, d2 2 x PS, the rest PS), most
+    // expensive class first, handed out by an LDS counter.
+    const int n0 = m[4], n1 = m[5], n2 = m[6], n3 = m[7], n4 = m[8], n5 = m[9];
+    const int lp = 6 - lsl;  // log2(PS)
+    const int u5 = (n5 + L.PS - 1) >> lp, u4 = (n4 + L.PS - 1) >> lp, u3 = (n3 + L.PS - 1) >> lp;
+    const int u2 = (n2 + L.PS - 1) >> lp, u1 = (((n1 + L.PS - 1) >> lp) + 1) >> 1;
+    const int u0 = (((n0 + L.PS - 1) >> lp) + 3) >> 2;
+    const int total = u5 + u4 + u3 + u2 + u1 + u0;
+    int *ctr = rec + a.rec_cap;
+    int k = grab(ctr, lane);
+    while (k < total) {
+        const int kn = grab(ctr, lane);
+        int u = k;
+        if (u < u5) {
+            t16_ds<kScore, kOff32>(a, im, rec + m[15], n5, L, u);
+        } else if ((u -= u5) < u4) {
+            t16_dn<16, 12, kScore, kOff32>(a, im, rec + m[14], n4, L, u);
+        } else if ((u -= u4) < u3) {
+            t16_dn<8, 8, kScore, kOff32>(a, im, rec + m[13], n3, L, u);
+        } else if ((u -= u3) < u2) {
+            t16_dn<4, 4, kScore, kOff32>(a, im, rec + m[12], n2, L, u);
+        } else if ((u -= u2) < u1) {
+            t16_d2<2, kScore, kOff32>(a, im, rec + m[11], n1, L, 2 * u);
+        } else {
+            t16_d1<4, kScore, kOff32>(a, im, rec + m[10], n0, L, 4 * (u - u1));
+        }
+        k = kn;
+    }
+}
+
+int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off32, unsigned blocks, size_t lds) {
+    using K = void (*)(Tile16Args);
+    static const K kerns[8] = {
+        &car_tile16_kernel<false, false, false>, &car_tile16_kernel<false, true, false>,
+        &car_tile16_kernel<true, false, false>,  &car_tile16_kernel<true, true, false>,
+        &car_tile16_kernel<false, false, true>,  &car_tile16_kernel<false, true, true>,
+        &car_tile16_kernel<true, false, true>,   &car_tile16_kernel<true, true, true>};
+    const bool l64 = a.lsl == 6;
+    const K kern = kerns[(l64 ? 4 : 0) + (score ? 2 : 0) + (off32 ? 1 : 0)];
+    RSK_CHECK(lds <= 160 * 1024, "tile image needs %zu B of LDS", lds);
+    if (lds > 64 * 1024)
+        RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds));
+    kern<<<dim3(blocks), dim3(kTileThreads), lds, stream>>>(a);
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
+}
+
+unsigned tile16_debug_take() {
+#ifdef RSK_DEBUG_BOUNDS
+    unsigned f = 0, zero = 0;
+    if (hipDeviceSynchronize() != hipSuccess) return 0x80000000u;
+    if (hipMemcpyFromSymbol(&f, HIP_SYMBOL(rsk_dbg16), 4) != hipSuccess) return 0x80000000u;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(rsk_dbg16), &zero, 4);
+    return f;
+#else
+    return 0u;
+#endif
+}
+
+}  // namespace rsk

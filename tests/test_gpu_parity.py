@@ -320,3 +320,69 @@ def test_cut_cost_golden(ctx, metrics_golden):
         rp, ci, miss = workmodel.relation_csr(case["relation"], names, dedup=False)
         d = int(api.cut_cost(rp, ci, assign, len(names), 1, miss, ctx=ctx)[0])
         assert d / 2 == case["cost"]
+
+
+# ---------------------------------------------------------------------------
+# compact path (N <= 65535): 16-bit node codes + exact resolution of equal codes
+# ---------------------------------------------------------------------------
+
+def _crowded_rem_case(rng, P, N, S, hubs, neg_frac=0.1):
+    """Remaining CPU crowded into single 16-bit code buckets (spacing 1 below
+    2^14, 2..32 up to 2^19, one bucket above): ties between distinct nodes that
+    only the exact cap - use comparison can order."""
+    rp, ci, a, _, _, haz = _random_case(rng, P, N, S, max_deg=int(rng.choice([4, 12, 30])), hub_deg=hubs, p_haz=0.1)
+    a[:] = rng.integers(-1, min(N, 24), P * S)  # neighbours on few nodes: real counts and many-way ties
+    base = rng.choice([3000, 20000, 100000, 300000, 600000, 1 << 29], N).astype(np.int64)
+    cap = (base + 5000).astype(np.int32)
+    rem = base[:, None] + rng.integers(0, 4, (N, S))         # within one code bucket above 2^14
+    neg = rng.random((N, S)) < neg_frac
+    rem[neg] = -rng.integers(1, 5, neg.sum())                  # rem < 0: all one code
+    use = (cap.astype(np.int64)[:, None] - rem).astype(np.int32).reshape(-1)
+    return rp, ci, a, cap, use, haz
+
+
+@pytest.mark.parametrize("S", [1, 7, 64, 100])
+def test_car_code_collisions_exact(ctx, S):
+    rng = np.random.default_rng(500 + S)
+    hubs = [3, 5, 9, 16, 17, 20, 31, 32, 33, 40, 64, 65, 130, 300]
+    for N in (7, 300, 5000):
+        rp, ci, a, cap, use, haz = _crowded_rem_case(rng, 900, N, S, hubs)
+        _check_car(ctx, rp, ci, a, S, cap, use, haz, N, label=f"collisions S={S} N={N}")
+
+
+@pytest.mark.parametrize("S", [1, 64, 70])
+def test_car_invalid_assign_values_never_alias(ctx, S):
+    """Assignments outside [0, N) mean "on no node" (include/rsk.h): values that
+    truncate to a real 16-bit node id (65536 + x, -2 = 0xfffe) must not add to
+    that node's score."""
+    rng = np.random.default_rng(600 + S)
+    P, N = 1200, 300
+    rp, ci, a, cap, use, haz = _random_case(rng, P, N, S, max_deg=16, hub_deg=[20, 40, 70], p_haz=0.1)
+    x = rng.integers(0, 8, P * S)
+    bad = rng.random(P * S) < 0.4
+    pool = np.array([-2, -1, -65536, 65536, 65536 + 3, 131072 + 5, N, N + 5, 2 ** 31 - 1], np.int64)
+    a = np.where(bad, rng.choice(pool, P * S), x).astype(np.int32)
+    _check_car(ctx, rp, ci, a, S, cap, use, haz, N, label=f"invalid S={S}")
+
+
+def test_car_wide_path_n_above_u16(ctx):
+    """65535 < N < 2^24: the wide tile kernel (int2 {node, key} image)."""
+    rng = np.random.default_rng(41)
+    N, P = 70000, 800
+    for S in (1, 33):
+        rp, ci, a, cap, use, haz = _random_case(rng, P, N, S, max_deg=12, hub_deg=[17, 33, 65, 200], p_haz=0.2)
+        pool = np.array([0, 3, 65534, 65535, 65536, 65537, N - 1], np.int32)
+        a[:] = rng.choice(pool, P * S)
+        a[rng.random(P * S) < 0.05] = -1
+        haz.reshape(N, S)[pool] = 0
+        _check_car(ctx, rp, ci, a, S, cap, use, haz, N, label=f"wide S={S}")
+
+
+def test_car_score_variant_matches(ctx):
+    """want_score=False (the bench's template instance) gives the same targets."""
+    from rsk import api, synth
+    c = synth.make_cluster(5000, 300, S=128, seed=4)
+    plan = api.CarPlan(c.row_ptr, c.col_idx, ctx=ctx)
+    t0, _ = plan.execute(c.assign, c.S, c.cap_cpu, c.use_cpu, c.hazard, c.N)
+    t1, _ = plan.execute(c.assign, c.S, c.cap_cpu, c.use_cpu, c.hazard, c.N, want_score=True)
+    assert np.array_equal(t0, t1)
