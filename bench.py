@@ -26,17 +26,76 @@ sys.path[:0] = [os.path.join(REPO, "kubernetes-rescheduling_amd"), REPO]
 
 import numpy as np  # noqa: E402
 
-METRIC = "pod×node move evaluations/sec at 100k pods×5k nodes; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
 CONFIGS = {
-    "headline": dict(P=100_000, N=5_000, S=4096, name="100k pods x 5k nodes, PA tree, 4096 scenarios/GPU (config 3)"),
-    "2k64": dict(P=2_000, N=64, S=1, name="2k pods x 64 nodes, single CAR round (config 2)"),
+    "headline": dict(P=100_000, N=5_000, S=4096, name="100k pods x 5k nodes, PA tree, 4096 scenarios/GPU (config 3)",
+                     metric="pod×node move evaluations/sec at 100k pods×5k nodes; % of HBM roofline"),
+    "2k64": dict(P=2_000, N=64, S=1, name="2k pods x 64 nodes, single CAR round (config 2)",
+                 metric="pod×node move evaluations/sec at 2k pods×64 nodes, one CAR round (latency-bound)"),
     "rounds": dict(P=100_000, N=5_000, S=1024, rounds=True,
-                   name="100k pods x 5k nodes x 1024 scenarios/GPU, detect -> evict -> CAR -> update rounds (config 5)"),
+                   name="100k pods x 5k nodes x 1024 scenarios/GPU, detect -> evict -> CAR -> update rounds (config 5)",
+                   metric="rescheduling rounds x scenarios per second (detect -> evict -> CAR -> update)"),
     "1m50k": dict(P=1_000_000, N=50_000, S=64, shard="rows",
-                  name="1M pods x 50k nodes x 64 scenarios, pod-row sharded (config 4)"),
+                  name="1M pods x 50k nodes x 64 scenarios, pod-row sharded (config 4)",
+                  metric="pod×node move evaluations/sec at 1M pods×50k nodes; % of HBM roofline"),
 }
+PMC_JSON = os.path.join(REPO, "profiles", "pmc_traffic.json")
+
+
+def cpu_model():
+    """Host CPU model name and logical CPU count (the GPU box's host cores)."""
+    name = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    name = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return name, os.cpu_count() or 1
+
+
+def python_legs(c, N, S, budget_s=6.0):
+    """SURVEY §8d CPU legs 1 and 2 (oracle/car_py.py, one core): the literal
+    pure-Python restatement of rescheduling.py:183-214 on 64 evenly spaced pods
+    of scenario 0, and the numpy vectorized one on the same pods over as many
+    scenarios as fit the budget.  One call = one (pod, scenario) = N evaluations."""
+    from oracle import car_py
+    P = c.P
+    pods = np.linspace(0, P - 1, 64).astype(np.int64)
+    nbrs = car_py.dedup_rows(c.row_ptr, c.col_idx, pods)
+    legs = []
+    a, u, h = car_py.scenario_view(c.assign, c.use_cpu, c.hazard, P, N, S, 0)
+    by_node = car_py.pods_by_node(a, N)
+    haz_list = [n for n in range(N) if h[n]]
+    t0 = time.perf_counter()
+    calls = 0
+    for nb in nbrs:
+        car_py.car_literal(nb.tolist(), by_node, haz_list, c.cap_cpu, u)
+        calls += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    legs.append({"kind": "port", "impl": "literal pure-Python restatement (oracle/car_py.car_literal)",
+                 "value": round(calls * N / dt, 1), "unit": "pod×node evals/s", "cores": 1,
+                 "sample": f"{calls} evenly spaced pods x scenario 0 x {N} nodes",
+                 "ms_per_call": round(dt * 1e3 / calls, 3)})
+    calls, s = 0, 0
+    t0 = time.perf_counter()
+    while s < S and time.perf_counter() - t0 < budget_s:
+        a, u, h = car_py.scenario_view(c.assign, c.use_cpu, c.hazard, P, N, S, s)
+        for nb in nbrs:
+            car_py.car_numpy(nb, a, c.cap_cpu, u, h, N)
+            calls += 1
+        s += 1
+    dt = time.perf_counter() - t0
+    legs.append({"kind": "port", "impl": "numpy vectorized restatement (oracle/car_py.car_numpy)",
+                 "value": round(calls * N / dt, 1), "unit": "pod×node evals/s", "cores": 1,
+                 "sample": f"64 evenly spaced pods x {s} scenarios x {N} nodes",
+                 "ms_per_call": round(dt * 1e3 / calls, 4)})
+    return legs
 
 
 def log(*a):
@@ -123,7 +182,7 @@ def bench_rounds(args, cfg, world, rank, local, dev):
     ms_step = elapsed * 1e3 / args.steps
     if rank == 0:
         line = {
-            "metric": "rescheduling rounds x scenarios per second (detect -> evict -> CAR -> update)",
+            "metric": cfg["metric"],
             "value": round(world * S / (ms_step / 1e3), 1), "unit": "scenario-rounds/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32",
@@ -154,7 +213,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-events", action="store_true", default=os.environ.get("RSK_BENCH_NO_EVENTS") == "1",
                     help="time the steps without per-kernel HIP events")
-    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_headline.json"))
+    ap.add_argument("--pmc-json", default=PMC_JSON,
+                    help="per-config PMC traffic (tools/pmc_summary.py, FETCH_SIZE x2-corrected)")
     args = ap.parse_args()
 
     import torch
@@ -192,7 +252,9 @@ def main():
     ctx = _lib.Context(local)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
+    t_plan = time.perf_counter()
     plan = api.CarPlan(c.row_ptr, c.col_idx, rows=my_rows, ctx=ctx)
+    plan_ms = (time.perf_counter() - t_plan) * 1e3  # host C++ dedup + DFS order + tiling + upload, once per graph
     T = {k: torch.from_numpy(getattr(c, k)).to(dev) for k in ("assign", "cap_cpu", "use_cpu", "hazard")}
     out_t = torch.empty(max(Q, 1) * S, dtype=torch.int32, device=dev)
     torch.cuda.synchronize(dev)
@@ -293,11 +355,11 @@ def main():
         try:
             with open(args.pmc_json) as f:
                 pmc = json.load(f)
-            entry = pmc.get(args.config, {}).get(dom)
+            entry = pmc.get("configs", {}).get(args.config, {}).get(dom)
             if entry and entry.get("S") == S:
                 roof["traffic"] = entry["hbm_bytes_per_launch"]
-                roof["traffic_source"] = os.path.relpath(args.pmc_json, REPO)
-        except (OSError, ValueError):
+                roof["traffic_source"] = f"{os.path.relpath(args.pmc_json, REPO)} ({entry['source']})"
+        except (OSError, ValueError, KeyError):
             pass
     for k, v in kernels.items():
         if k in alg:
@@ -310,6 +372,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
+        model, ncpu = cpu_model()
         # grow an evenly spaced pod sample until one timed pass takes >= 60 % of
         # --cpu-seconds (about 10-30 s of CPU work at the default)
         nrows = 64
@@ -325,11 +388,12 @@ def main():
         cpu = {"value": round(nrows * S * N / dt, 1), "unit": "pod×node evals/s", "cores": threads, "kind": "port",
                "sample": f"{nrows} evenly spaced pods x {S} scenarios x {N} nodes ({dt:.1f}s), oracle/rsk_oracle.c "
                          f"literal CAR restatement, OpenMP {threads} threads",
-               "seconds": round(dt, 2)}
+               "seconds": round(dt, 2), "cpu_model": model, "host_logical_cpus": ncpu,
+               "legs": python_legs(c, N, S)}
 
     if rank == 0:
         line = {
-            "metric": METRIC, "value": round(value, 1), "unit": "pod×node evals/s", "n_gpus": world,
+            "metric": cfg["metric"], "value": round(value, 1), "unit": "pod×node evals/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
             "scaling": "strong" if by_rows else "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
             "config": {"workload": cfg["name"], "pods": P, "nodes": N, "scenarios_per_gpu": S, "nnz": c.nnz,
@@ -337,6 +401,7 @@ def main():
                        "parallelism": f"{'pod-row' if by_rows else 'scenario'}-sharded x{world}"},
             "roofline": roof, "roofline_step": roof_step, "cpu_baseline": cpu, "kernels": kernels,
             "parity_sample_ok": parity_ok, "hbm_bytes_algorithmic_per_step": B, "plan": info,
+            "plan_create_ms": round(plan_ms, 1),
         }
         if by_rows:
             line["rows_per_rank"] = Q

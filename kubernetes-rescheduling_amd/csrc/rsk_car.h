@@ -231,7 +231,8 @@ struct Tile16Args {
     const unsigned long long *zc_key;
     int *out_target;
     int *out_score;
-    int S, N, T, lsl;      // SL = 1 << lsl scenarios per workgroup (64 when S >= 64)
+    int S, N, T, lsl;      // SL = 1 << lsl scenarios per workgroup (64 when S >= 64); T tiles from tile0
+    int tile0;
     int img_cells;         // LDS cells of the largest image (rmax * SL); the records follow
     int rec_cap;           // record ints reserved in LDS; the unit counter follows
     int order, xcd_per;    // grid order (RSK_TILE_ORDER) as in the wide kernel
@@ -256,10 +257,26 @@ struct PivotArgs {
     int hash;                 // 1: hash table of 2*H words (N too large for a direct table)
 };
 
+// Mid rows (17..64) of the compact path: buckets D = 32, 64 (records kMidW ints).
+struct Mid16Args {
+    const int *rec[2];
+    int n_items[2];
+    const int *assign;
+    const unsigned short *code;
+    const int *cap, *use;
+    const int *zc_cnt;
+    const unsigned long long *zc_key;
+    int *out_target, *out_score;
+    int S, N, SL, PS;         // SL, PS set by launch_mid16
+};
+
 int launch_prep(hipStream_t stream, const Prep16Args &a);
-int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off32, unsigned blocks, size_t lds);
+int launch_mid16(hipStream_t stream, const Mid16Args &a);
+int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off32, bool heavy, unsigned blocks,
+                  size_t lds);
 size_t tile16_lds_bytes(int rmax, int lsl, int rec_cap);
 int launch_pivot(hipStream_t stream, const PivotArgs &a, int dmax, unsigned groups_per_item);
-unsigned tile16_debug_take();  // debug bounds build: violation flags of the compact kernels (cleared)
+unsigned tile16_debug_take();
+int tile16_rows_built();       // image rows per tile the compact kernels are compiled for (RSK_TILE16_ROWS)  // debug bounds build: violation flags of the compact kernels (cleared)
 
 }  // namespace rsk

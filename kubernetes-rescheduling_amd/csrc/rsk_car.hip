@@ -749,7 +749,7 @@ struct rsk_car_plan {
     int P = 0, Q = 0, max_deg = 0;
     int light_max = kLightMax;  // rows with deg <= light_max go to the tiles
     // tiles
-    int T = 0, rmax = 0, recmax = 0, n_tile_rows = 0, n_sorted_rows = 0;
+    int T = 0, T_lean = 0, rmax = 0, recmax = 0, n_tile_rows = 0, n_sorted_rows = 0;  // tiles [T_lean, T): heavy
     int owners_cap = kTileOwners, rows_cap = kTileRows;  // tile limits (RSK_TILE_OWNERS / RSK_TILE_ROWS)
     int64_t img_rows_total = 0, img_pods_distinct = 0, n_img_pods = 0, n_recs = 0;
     DevBuf img_pods, meta, recs;
@@ -996,7 +996,8 @@ struct TileBuilder {
         const int rec_off = (int)recs.size();
         int m[kMetaW] = {};
         for (int c = 0; c < kNumCls; ++c) {
-            if (c == 2) while ((recs.size() - rec_off) % 4) recs.push_back(0);  // int4 records from here on
+            // every class starts 16-B aligned (int4 record reads, 16-B scalar block loads)
+            while ((recs.size() - rec_off) % 4) recs.push_back(0);
             m[4 + kNumCls + c] = (int)recs.size() - rec_off;
             m[4 + c] = (int)cur_rec[c].size() / kClsW[c];
             recs.insert(recs.end(), cur_rec[c].begin(), cur_rec[c].end());
@@ -1071,17 +1072,41 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
     std::stable_sort(light.begin(), light.end(), [&](int x, int y) {
         return pos[rows ? rows[x] : x] < pos[rows ? rows[y] : y];
     });
-    TileBuilder tb;
-    tb.owners_cap = plan->owners_cap;
-    tb.rows_cap = plan->rows_cap;
+    // Two tile lists: "heavy" tiles hold every row of degree 17..32 (the
+    // register-hungry class the compact kernel scores in its own, lower-occupancy
+    // instantiation) together with the rows that follow it in DFS order — its
+    // children, whose pods its record reads — and "lean" tiles everything else.
+    TileBuilder tl, th;
+    tl.owners_cap = th.owners_cap = plan->owners_cap;
+    tl.rows_cap = th.rows_cap = plan->rows_cap;
+    int heavy_left = 0;
     for (int i : light) {
         const int p = rows ? rows[i] : i;
         const int d = rp[p + 1] - rp[p];
         const int *nbp = ci.data() + rp[p];
+        if (light_class(d) == 5) heavy_left = std::max(heavy_left, d + 1);
+        TileBuilder &tb = heavy_left > 0 ? th : tl;
+        if (heavy_left > 0) --heavy_left;
         if (!tb.fits(nbp, d)) tb.close();
         tb.add(i, nbp, d);
     }
-    tb.close();
+    tl.close();
+    th.close();
+    plan->T_lean = tl.T;
+    TileBuilder &tb = tl;  // lean tiles first, then the heavy ones (offsets shifted)
+    for (int t = 0; t < th.T; ++t) {
+        int *m = th.meta.data() + (size_t)t * kMetaW;
+        m[0] += (int)tl.img_pods.size();
+        m[2] += (int)tl.recs.size();
+    }
+    tb.img_pods.insert(tb.img_pods.end(), th.img_pods.begin(), th.img_pods.end());
+    tb.meta.insert(tb.meta.end(), th.meta.begin(), th.meta.end());
+    tb.recs.insert(tb.recs.end(), th.recs.begin(), th.recs.end());
+    tb.T += th.T;
+    tb.rmax = std::max(tb.rmax, th.rmax);
+    tb.recmax = std::max(tb.recmax, th.recmax);
+    tb.n_sorted += th.n_sorted;
+    tb.img_total += th.img_total;
     plan->T = tb.T;
     plan->rmax = std::max(1, tb.rmax);
     plan->recmax = tb.recmax;
@@ -1098,7 +1123,9 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
     if (tb.T > 0) {
         RSK_TRY(upload(plan->img_pods, tb.img_pods.data(), tb.img_pods.size() * 4));
         RSK_TRY(upload(plan->meta, tb.meta.data(), tb.meta.size() * 4));
-        if (tb.recs.empty()) tb.recs.assign(4, 0);
+        // 64 zero ints past the last blob: the 64-scenario tile kernel reads
+        // record blocks through the scalar cache without clamping them
+        tb.recs.resize(tb.recs.size() + 64, 0);
         RSK_TRY(upload(plan->recs, tb.recs.data(), tb.recs.size() * 4));
     }
     for (int b = 0; b < kNumMid; ++b) RSK_TRY(upload(plan->mid[b], midr[b].data(), midr[b].size() * 4));
@@ -1113,8 +1140,11 @@ int plan_create(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, in
     auto plan = new rsk_car_plan();
     plan->ctx = ctx;
     plan->light_max = light_max;
-    plan->owners_cap = std::min(kTileOwners, std::max(8, env_int("RSK_TILE_OWNERS", kTileOwners)));
-    plan->rows_cap = std::min(kTileRows, std::max(kLightMax, env_int("RSK_TILE_ROWS", kTileRows)));  // a row fits alone
+    // tile limits: the image rows the compact kernels are built for (RSK_TILE16_ROWS), owners
+    // in the 128 : 144 ratio; RSK_TILE_ROWS / RSK_TILE_OWNERS override (experiments)
+    const int rows_built = tile16_rows_built();
+    plan->owners_cap = std::min(kTileOwners, std::max(8, env_int("RSK_TILE_OWNERS", rows_built * kTileOwners / kTileRows)));
+    plan->rows_cap = std::min(rows_built, std::max(kLightMax, env_int("RSK_TILE_ROWS", rows_built)));  // a row fits alone
     plan->P = P;
     plan->Q = Q;
     const int rc = build_plan(plan, row_ptr, col_idx, P, rows, Q);
@@ -1145,14 +1175,21 @@ struct SideBufs {
     int *target, *score;
 };
 
-// Mid and hub rows of the compact path go through the pivot-delta kernel
-// (rsk_car16.hip) once it covers them; until then the wide kernels read the
-// exact node keys.
-bool plan_side_compact(const rsk_car_plan *) { return false; }
+// Side rows of the compact path: mid rows (17..64) read codes (car_mid16);
+// hub rows (> 64) still go through the wide hub kernel, which reads exact keys.
+bool mid16_on() {
+    static const bool on = env_int("RSK_MID16", 0) != 0;  // car_mid16 (codes) instead of car_mid (exact keys)
+    return on;
+}
+
+bool plan_side_compact(const rsk_car_plan *plan) {
+    for (int c = 0; c < kNumHeavy; ++c)
+        if (plan->n_heavy[c]) return false;
+    return mid16_on() || plan->n_mid[0] + plan->n_mid[1] == 0;
+}
 
 int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t *side, int nside, const SideBufs &b, int S, int N,
                 bool compact) {
-    (void)compact;
     const int *d_assign = b.assign, *d_key = b.key, *d_zcnt = b.zcnt;
     const unsigned long long *d_zkey = b.zkey;
     int *d_target = b.target, *d_score = b.score;
@@ -1169,7 +1206,27 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t *side, int n
     const int SL = std::min(S, 64);
     sc.PS = 64 / SL;
     const int64_t chunks = ceil_div(S, SL);
-    {   // K2 mid rows
+    if (compact && mid16_on() && plan->n_mid[0] + plan->n_mid[1] > 0) {   // K2 mid rows, codes
+        Mid16Args a;
+        std::memset(&a, 0, sizeof(a));
+        for (int k = 0; k < kNumMid; ++k) {
+            a.rec[k] = plan->mid[k].as<int>();
+            a.n_items[k] = plan->n_mid[k];
+        }
+        a.assign = d_assign;
+        a.code = b.code;
+        a.cap = b.cap;
+        a.use = b.use;
+        a.zc_cnt = d_zcnt;
+        a.zc_key = d_zkey;
+        a.out_target = d_target;
+        a.out_score = d_score;
+        a.S = S;
+        a.N = N;
+        const hipStream_t stream = pick();
+        ScopedTimer tm(ctx, "car_mid", stream);
+        RSK_TRY(launch_mid16(stream, a));
+    } else {   // K2 mid rows, exact keys
         MidArgs a;
         std::memset(&a, 0, sizeof(a));
         a.sc = sc;
@@ -1402,12 +1459,19 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         a.img_cells = (plan->rmax * SL + 3) & ~3;
         const size_t lds = tile16_lds_bytes(plan->rmax, a.lsl, a.rec_cap);
         RSK_CHECK(plan->recmax <= kTileRecInts, "tile records exceed %d ints", kTileRecInts);
-        const int64_t units = ceil_div(S, SL) * plan->T;
-        a.xcd_per = (int)ceil_div(units, 8);
-        const int64_t blocks = order == 2 ? 8 * (int64_t)a.xcd_per : units;
-        RSK_CHECK(blocks < INT32_MAX, "tile grid too large");
         ScopedTimer tm(ctx, "car_tile");
-        RSK_TRY(launch_tile16(ctx->stream, a, d_score != nullptr, off32, (unsigned)blocks, lds));
+        // lean tiles [0, T_lean) at full occupancy, then the heavy tiles (17..32 rows)
+        for (int part = 0; part < 2; ++part) {
+            const int t0 = part ? plan->T_lean : 0, nt = part ? plan->T - plan->T_lean : plan->T_lean;
+            if (nt <= 0) continue;
+            a.tile0 = t0;
+            a.T = nt;
+            const int64_t units = ceil_div(S, SL) * nt;
+            a.xcd_per = (int)ceil_div(units, 8);
+            const int64_t blocks = order == 2 ? 8 * (int64_t)a.xcd_per : units;
+            RSK_CHECK(blocks < INT32_MAX, "tile grid too large");
+            RSK_TRY(launch_tile16(ctx->stream, a, d_score != nullptr, off32, part == 1, (unsigned)blocks, lds));
+        }
     } else if (plan->T > 0) {   // K1 tiles, wide {node, key} pairs
         TileArgs a;
         std::memset(&a, 0, sizeof(a));

@@ -185,6 +185,24 @@ __device__ __forceinline__ int cell_node(unsigned c) { return (int)(c & 0xffffu)
 __device__ __forceinline__ unsigned cell_cand(unsigned c) { return c ^ 0xffffu; }
 __device__ __forceinline__ int cand_node(unsigned w) { return (int)((w & 0xffffu) ^ 0xffffu); }
 
+// Image rows per tile the compact kernel is compiled for (the plan's
+// RSK_TILE_ROWS must not exceed it) and workgroups per CU it is register-sized for.
+// 80 rows x 64 scenarios x 4 B = 20 KiB of LDS and <= 64 VGPRs: eight
+// workgroups (32 waves) per CU, the occupancy that hides the load phase of one
+// workgroup behind the store phase of others (measured: 144 rows / 4 per CU
+// 0.84 ms, 96 / 6 0.75, 88 / 7 0.72, 80 / 8 0.715, 64 / 8 0.76 at config 3).
+#ifndef RSK_TILE16_ROWS
+#define RSK_TILE16_ROWS 80
+#endif
+#ifndef RSK_TILE16_WGS
+#define RSK_TILE16_WGS 8
+#endif
+#ifndef RSK_TILE16_WGS_HEAVY
+#define RSK_TILE16_WGS_HEAVY 6  // heavy tiles (17..32 rows): 32 cells in registers (<= 80 VGPRs)
+#endif
+constexpr int kT16Rows = RSK_TILE16_ROWS;
+static_assert(kT16Rows % 4 == 0 && kT16Rows <= kTileRows, "bad RSK_TILE16_ROWS");
+
 #ifndef RSK_TILE_NT
 #define RSK_TILE_NT 3  // streamed image loads / target stores non-temporal (codes stay in L2)
 #endif
@@ -310,7 +328,7 @@ __device__ __forceinline__ int exact_among(const Tile16Args &a, const unsigned (
 // registers — equal cells are the same node (in one scenario a node has one
 // code) — c[j] = #{i < j : cell i == cell j}, so a node's last entry holds its
 // count - 1 and the entries at the maximum are exactly one per maximal node.
-template <int D, int W, bool kScore, bool kOff32>
+template <int D, int W, int kR0, bool kScore, bool kOff32>
 __device__ __forceinline__ void t16_dn(const Tile16Args &a, const Img16 &img, const int *rec, int n, const Lane16 &L,
                                        int p0) {
     int r[W];
@@ -320,7 +338,7 @@ __device__ __forceinline__ void t16_dn(const Tile16Args &a, const Img16 &img, co
     int c[D];
 #pragma unroll
     for (int j = 0; j < D; ++j) {
-        const unsigned pr = (unsigned)r[2 + j / 2];
+        const unsigned pr = (unsigned)r[kR0 + j / 2];
         const int row = (j & 1) ? (int)(pr >> 16) : (int)(pr & 0xffffu);
         const unsigned e = img.at(row, L.col);  // padding entries read row 0
         x[j] = j < d ? e : kCellPad;
@@ -356,23 +374,42 @@ __device__ __forceinline__ void t16_dn(const Tile16Args &a, const Img16 &img, co
     emit16<kScore, kOff32>(a, r[0], L, M1 < 0 ? L.zt : t, M1 < 0 ? L.zs : M1 + 1);
 }
 
-// The 17..32 class row's cells in registers, sorted (equal nodes form runs).
+// Decision over sorted cells (equal nodes in runs): two walks — the maximal
+// run length M over candidate nodes and how many runs reach it, then the best
+// (code, -node) word among those runs and how many share its code.  Returns
+// INT_MIN when no neighbour node is a candidate (M = 0: the caller applies the
+// zero case); `need` when equal codes >= 2 tie (exact resolution required).
 template <int D>
-__device__ __forceinline__ void t16_ds_cells(const Img16 &img, const int *rc, int d, int col, unsigned (&x)[D]) {
+__device__ __forceinline__ int sorted_runs_decide(const unsigned (&x)[D], int &score, unsigned &bk_out, bool &need) {
+    int M = 0, Rn = 0, namb = 0;
+    unsigned bw = 0u;
+    int c = 0;
 #pragma unroll
-    for (int j0 = 0; j0 < D; j0 += 8) {
-        if (j0 % 16 == 0) __builtin_amdgcn_sched_barrier(0);
-        const int4 pk = *reinterpret_cast<const int4 *>(rc + 4 + (j0 >> 1));
-        const unsigned pw[4] = {(unsigned)pk.x, (unsigned)pk.y, (unsigned)pk.z, (unsigned)pk.w};
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            const int j = j0 + t;
-            const int row = (t & 1) ? (int)(pw[t >> 1] >> 16) : (int)(pw[t >> 1] & 0xffffu);
-            const unsigned e = img.at(row, col);
-            x[j] = j < d ? e : kCellPad;
-        }
+    for (int i = 0; i < D; ++i) {
+        c = (i > 0 && x[i] == x[i > 0 ? i - 1 : 0]) ? c + 1 : 1;
+        const bool end = i == D - 1 || x[i < D - 1 ? i + 1 : i] != x[i];
+        const bool cand = end && cell_code(x[i]) != kCodeHaz;
+        const bool gt = cand && c > M, eq = cand && c == M;
+        Rn = gt ? 1 : (eq ? Rn + 1 : Rn);
+        M = gt ? c : M;
     }
-    bitonic_sort<D, unsigned>(x);
+    c = 0;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        c = (i > 0 && x[i] == x[i > 0 ? i - 1 : 0]) ? c + 1 : 1;
+        const bool end = i == D - 1 || x[i < D - 1 ? i + 1 : i] != x[i];
+        const bool cand = end && c == M && cell_code(x[i]) != kCodeHaz;
+        const unsigned wv = cand ? cell_cand(x[i]) : 0u;
+        const unsigned kw = cell_code(wv), kb = cell_code(bw);
+        namb = kw > kb ? 1 : (cand && kw == kb ? namb + 1 : namb);
+        bw = max(bw, wv);
+    }
+    score = M;
+    const unsigned bk = cell_code(bw);
+    bk_out = bk;
+    need = M > 0 && Rn > 1 && bk >= 2u && namb > 1;
+    if (M == 0) return INT_MIN;
+    return Rn == 1 ? cand_node(bw) : (bk >= 2u ? cand_node(bw) : RSK_TARGET_NONE);
 }
 
 // Exact tie resolution straight from the LDS image (rare path, kept free of
@@ -397,100 +434,67 @@ __device__ __forceinline__ int t16_exact_scan(const Tile16Args &a, const Img16 &
     return bn;
 }
 
-// 17 <= d <= 32, record [oi, d, -, -, rows from int 4]: sort the 32 cells with
-// a register bitonic network (equal nodes become runs), then walk the runs
-// once keeping the lexicographic (count, code, -node) maximum, the number of
-// runs at the maximal count and the number of runs sharing the best
-// (count, code).  The rare exact tie (equal codes >= 2) rescans the LDS image
-// (t16_exact_scan) rather than keeping the cells live across the walk.
-template <bool kScore, bool kOff32>
-__device__ __forceinline__ void t16_ds(const Tile16Args &a, const Img16 &img, const int *rec, int n, const Lane16 &L,
-                                       int p0) {
-    constexpr int D = 32, W = 20;
-    const int *rc = rec + min(p0 * L.PS + L.slot, n - 1) * W;
-    const int2 hd = *reinterpret_cast<const int2 *>(rc);
-    const int d = hd.y;
-    unsigned bw = 0u;
-    int M = 0, R = 0, namb = 0;
-    {
-        unsigned x[D];
-        t16_ds_cells<D>(img, rc, d, L.col, x);
-        // walk 1: the maximal run length over candidate nodes and how many runs reach it
-        int c = 0;
+// kL64 phase 1 of one wave: image rows [r0, rend), at most kB of them, lane =
+// scenario.  Rows past rend re-read row rend - 1 (same lines, no LDS write).
+template <int kB, bool kOff32>
+__device__ __forceinline__ void t16_rows64(const Tile16Args &a, unsigned *img, int img_off, int r0, int rend, int s0) {
+    const unsigned S = (unsigned)a.S, N = (unsigned)a.N;
+    const char *__restrict__ asg = reinterpret_cast<const char *>(a.assign);
+    const unsigned short *__restrict__ code = a.code;
+    const int lane = threadIdx.x & 63;
+    const int s = s0 + lane;
+    const unsigned sl = (unsigned)min(s, (int)S - 1);
+    const bool s_ok = s < (int)S;
+    const cint_ptr pods = const_ptr(a.img_pods) + img_off + r0;
+    const int nr = rend - r0;  // >= 1 except for waves past the image
+    if (nr <= 0) return;
+    int v[kB];
 #pragma unroll
-        for (int j = 0; j < D; ++j) {
-            c = (j > 0 && x[j] == x[j > 0 ? j - 1 : 0]) ? c + 1 : 1;
-            const bool end = j == D - 1 || x[j < D - 1 ? j + 1 : j] != x[j];
-            const bool cand = end && cell_code(x[j]) != kCodeHaz;
-            const bool gt = cand && c > M, eq = cand && c == M;
-            R = gt ? 1 : (eq ? R + 1 : R);
-            M = gt ? c : M;
-        }
-        // walk 2: among runs of length M, the best (code, -node) word and how
-        // many of them share its code
-        c = 0;
+    for (int u = 0; u < kB; ++u) {
+        const int ur = u < nr ? u : nr - 1;
+        const unsigned qd = (unsigned)pods[ur];
+#ifdef RSK_DEBUG_BOUNDS
+        if (img_off + r0 + ur >= (int)a.n_pods) atomicOr(&rsk_dbg16, 2u);
+        if ((size_t)qd * S + sl >= a.n_assign) atomicOr(&rsk_dbg16, 4u);
+#endif
+        const int *pa = reinterpret_cast<const int *>(asg + cell_off<kOff32>(RSK_B16(qd, a.n_assign / S, 4u), S, sl));
+        v[u] = (RSK_TILE_NT & 1) ? __builtin_nontemporal_load(pa) : *pa;
+    }
+    unsigned cd[kB];
 #pragma unroll
-        for (int j = 0; j < D; ++j) {
-            c = (j > 0 && x[j] == x[j > 0 ? j - 1 : 0]) ? c + 1 : 1;
-            const bool end = j == D - 1 || x[j < D - 1 ? j + 1 : j] != x[j];
-            const bool cand = end && c == M && cell_code(x[j]) != kCodeHaz;
-            const unsigned w = cand ? cell_cand(x[j]) : 0u;
-            const unsigned kw = cell_code(w), kb = cell_code(bw);
-            namb = kw > kb ? 1 : (cand && kw == kb ? namb + 1 : namb);
-            bw = max(bw, w);
-        }
+    for (int u = 0; u < kB; ++u) {
+        const bool ok = (unsigned)v[u] < N && s_ok;
+        cd[u] = ld16(code, RSK_B16(ok ? (unsigned)v[u] * S + sl : 0u, a.n_key, 8u));
     }
-    const unsigned bk = cell_code(bw);
-    int t = R == 1 ? cand_node(bw) : (bk >= 2u ? cand_node(bw) : RSK_TARGET_NONE);
-    const bool need = R > 1 && bk >= 2u && namb > 1;
-    if (__builtin_amdgcn_ballot_w64(need)) {  // rare: wave-uniform branch
-        const int te = t16_exact_scan(a, img, rc + 4, d, L.col, M, bk, L.s);
-        t = need ? te : t;
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+        const bool ok = (unsigned)v[u] < N && s_ok;
+        if (u < nr) img[((r0 + u) << 6) + lane] = ok ? ((cd[u] << 16) | (unsigned)v[u]) : kCellPad;
     }
-    emit16<kScore, kOff32>(a, rc[0], L, M == 0 ? L.zt : t, M == 0 ? L.zs : M);
 }
 
-// Phase 1.  kL64: wave w loads image rows w, w+4, ... — the pod index is
-// wave-uniform (scalar load), the assign slice one 256-B row, the code gather
-// one 128-B line whenever the row's pod sits on one node in all 64 scenarios.
+// Phase 1.  kL64 (t16_rows64): the pod index is wave-uniform (scalar load),
+// the assign slice one 256-B row, the code gather one 128-B line whenever the
+// row's pod sits on one node in all 64 scenarios.
 // Generic (SL < 64): lanes = (row, scenario) pairs as in the wide kernel.
 template <bool kL64, bool kOff32>
 __device__ __forceinline__ void t16_load_image(const Tile16Args &a, unsigned *img, int img_off, int nrows, int s0) {
     const unsigned S = (unsigned)a.S, N = (unsigned)a.N;
     const char *__restrict__ asg = reinterpret_cast<const char *>(a.assign);
+    const unsigned short *__restrict__ code = a.code;
     if (kL64) {
-        const int lane = threadIdx.x & 63;
+        // wave w loads image rows [w*q, w*q + q), q = ceil(nrows / 4): the pod
+        // list is read with wide scalar loads, all q rows in flight at once
         const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-        const int s = s0 + lane;
-        const unsigned sl = (unsigned)min(s, (int)S - 1);
-        const bool s_ok = s < (int)S;
-        const cint_ptr pods = const_ptr(a.img_pods) + img_off;
-        constexpr int kB = kTileRows / 8;  // rows per wave per batch: two batches cover 144 rows
-        for (int r0 = 0; r0 < nrows; r0 += 4 * kB) {
-            int v[kB];
-#pragma unroll
-            for (int u = 0; u < kB; ++u) {
-                const int row = min(r0 + u * 4 + wave, nrows - 1);
-                const unsigned q = (unsigned)pods[RSK_B16(row, a.n_pods - img_off, 2u)];
-#ifdef RSK_DEBUG_BOUNDS
-                if ((size_t)q * S + sl >= a.n_assign) atomicOr(&rsk_dbg16, 4u);
-#endif
-                const int *pa = reinterpret_cast<const int *>(asg + cell_off<kOff32>(RSK_B16(q, a.n_assign / S, 4u), S, sl));
-                v[u] = (RSK_TILE_NT & 1) ? __builtin_nontemporal_load(pa) : *pa;
-            }
-            unsigned cd[kB];
-#pragma unroll
-            for (int u = 0; u < kB; ++u) {
-                const bool ok = (unsigned)v[u] < N && s_ok;
-                cd[u] = ld16(a.code, RSK_B16(ok ? (unsigned)v[u] * S + sl : 0u, a.n_key, 8u));
-            }
-#pragma unroll
-            for (int u = 0; u < kB; ++u) {
-                const int row = min(r0 + u * 4 + wave, nrows - 1);
-                const bool ok = (unsigned)v[u] < N && s_ok;
-                img[(row << 6) + lane] = ok ? ((cd[u] << 16) | (unsigned)v[u]) : kCellPad;
-            }
-        }
+        const int q = (nrows + 3) >> 2;
+        const int r0 = wave * q;
+        const int rend = min(r0 + q, nrows);
+        if (q <= 8) t16_rows64<8, kOff32>(a, img, img_off, r0, rend, s0);
+        else if (q <= 16) t16_rows64<16, kOff32>(a, img, img_off, r0, rend, s0);
+        else if (q <= 24 || kT16Rows <= 96) t16_rows64<kT16Rows <= 96 ? kT16Rows / 4 : 24, kOff32>(a, img, img_off, r0, rend, s0);
+        else if (q <= 28) t16_rows64<28, kOff32>(a, img, img_off, r0, rend, s0);
+        else if (q <= 32) t16_rows64<32, kOff32>(a, img, img_off, r0, rend, s0);
+        else t16_rows64<kT16Rows / 4, kOff32>(a, img, img_off, r0, rend, s0);
     } else {
         const int *__restrict__ pods = a.img_pods + img_off;
         constexpr int kE = kTileRows * 32 / kTileThreads;
@@ -511,7 +515,7 @@ __device__ __forceinline__ void t16_load_image(const Tile16Args &a, unsigned *im
             for (int u = 0; u < kE; ++u) {
                 const int s = s0 + (e[u] & msk);
                 const bool ok = (unsigned)v[u] < N && s < (int)S;
-                cd[u] = ld16(a.code, RSK_B16(ok ? (unsigned)v[u] * S + (unsigned)s : 0u, a.n_key, 8u));
+                cd[u] = ld16(code, RSK_B16(ok ? (unsigned)v[u] * S + (unsigned)s : 0u, a.n_key, 8u));
             }
 #pragma unroll
             for (int u = 0; u < kE; ++u) {
@@ -523,13 +527,243 @@ __device__ __forceinline__ void t16_load_image(const Tile16Args &a, unsigned *im
     }
 }
 
-size_t tile16_lds_bytes(int rmax, int lsl, int rec_cap) {
-    return ((size_t)rmax * ((size_t)1 << lsl) + (size_t)rec_cap + 4) * 4;
+// ---------------------------------------------------------------------------
+// kL64 scoring (S >= 64): lane = scenario column, every record wave-uniform.
+// Wave w takes the records of each class in blocks round-robin over the four
+// waves; records are read through the scalar cache straight from the plan
+// (no LDS copy, no work-unit atomics), so per record a wave issues its cell
+// reads (one ds_read_b32 per neighbour), the scorer's VALU and one 256-B
+// target store whose address is a scalar base + the lane's column.
+// ---------------------------------------------------------------------------
+struct W64 {
+    const char *img;  // LDS image, rows of 256 B
+    unsigned col4;    // lane's (clamped) column * 4
+    int s;            // lane's clamped scenario
+    int zt, zs;       // zero-case target / score
+    __device__ __forceinline__ unsigned cell(int row) const {
+        return *reinterpret_cast<const unsigned *>(img + ((unsigned)row << 8) + col4);
+    }
+};
+
+template <bool kScore, bool kOff32>
+__device__ __forceinline__ void emit64(const Tile16Args &a, int oi, int s0, const W64 &w, int t, int sc) {
+#ifdef RSK_DEBUG_BOUNDS
+    if ((size_t)(unsigned)oi * a.S + w.s >= a.n_out || oi < 0) { atomicOr(&rsk_dbg16, 1u); return; }
+#endif
+    const size_t row = kOff32 ? (size_t)(((unsigned)oi * (unsigned)a.S + (unsigned)s0) << 2)
+                              : ((size_t)(unsigned)oi * (unsigned)a.S + (unsigned)s0) << 2;
+    int *p = reinterpret_cast<int *>(reinterpret_cast<char *>(a.out_target) + row + w.col4);
+    if (RSK_TILE_NT & 2) __builtin_nontemporal_store(t, p);
+    else *p = t;
+    if (kScore) {
+        int *q = reinterpret_cast<int *>(reinterpret_cast<char *>(a.out_score) + row + w.col4);
+        if (RSK_TILE_NT & 2) __builtin_nontemporal_store(sc, q);
+        else *q = sc;
+    }
 }
 
-template <bool kScore, bool kOff32, bool kL64>
-__global__ __launch_bounds__(kTileThreads, 4) void car_tile16_kernel(Tile16Args a) {
-    extern __shared__ __attribute__((aligned(16))) int lds[];  // img cells [rmax][SL], records, unit counter
+// Record blocks through the scalar cache: U two-int records from index k as
+// U/2 unconditional 16-B scalar loads (the plan pads the blobs, so a block
+// may run past its class; those records are masked, never stored).
+template <int U>
+__device__ __forceinline__ void rec_pairs(cint_ptr R, int k, int (&x)[U], int (&y)[U]) {
+    const cint_ptr p = R + 2 * k;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        x[u] = p[2 * u];
+        y[u] = p[2 * u + 1];
+    }
+}
+
+// d == 1, U records from index k: {oi, row}
+template <int U, bool kScore, bool kOff32>
+__device__ __forceinline__ void w64_d1(const Tile16Args &a, const W64 &w, cint_ptr R, int n, int k, int s0) {
+    int oi[U], row[U];
+    unsigned c[U];
+    rec_pairs<U>(R, k, oi, row);
+#pragma unroll
+    for (int u = 0; u < U; ++u) c[u] = w.cell(k + u < n ? row[u] : 0);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (k + u < n) {
+            const bool z = cell_code(c[u]) == kCodeHaz;
+            emit64<kScore, kOff32>(a, oi[u], s0, w, z ? w.zt : cell_node(c[u]), z ? w.zs : 1);
+        }
+}
+
+// d == 2, U records from index k: {oi, row0 | row1 << 16}
+template <int U, bool kScore, bool kOff32>
+__device__ __forceinline__ void w64_d2(const Tile16Args &a, const W64 &w, cint_ptr R, int n, int k, int s0) {
+    int oi[U], rr[U];
+    unsigned c0[U], c1[U];
+    rec_pairs<U>(R, k, oi, rr);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const unsigned pr = k + u < n ? (unsigned)rr[u] : 0u;
+        c0[u] = w.cell((int)(pr & 0xffffu));
+        c1[u] = w.cell((int)(pr >> 16));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (k + u >= n) continue;
+        const unsigned k0 = cell_code(c0[u]), k1 = cell_code(c1[u]);
+        const unsigned w0 = k0 ? cell_cand(c0[u]) : 0u, w1 = k1 ? cell_cand(c1[u]) : 0u;
+        const unsigned best = max(w0, w1);
+        const bool same = c0[u] == c1[u];
+        const bool single = w0 == 0u || w1 == 0u || same;
+        int t = cand_node(best);
+        if (!single && cell_code(best) < 2u) t = RSK_TARGET_NONE;
+        if (!single && k0 == k1 && k0 >= 2u) {  // equal codes: exact remaining CPU (rare)
+            const int n0 = cell_node(c0[u]), n1 = cell_node(c1[u]);
+            const int e0 = exact_rem(a, n0, w.s), e1 = exact_rem(a, n1, w.s);
+            t = (e0 > e1 || (e0 == e1 && n0 < n1)) ? n0 : n1;
+        }
+        const bool zero = best == 0u;
+        emit64<kScore, kOff32>(a, oi[u], s0, w, zero ? w.zt : t, zero ? w.zs : (same ? 2 : 1));
+    }
+}
+
+// 0 or 3 <= d <= D (D = 4, 8, 16, 32), record j at R[W * j]: [oi, d, rows
+// from int kR0].  One pass over the cells, registers only for the D cells:
+// entry e's count c = #{earlier entries equal to it} (equal cells are the same
+// node: in one scenario a node has one code), so a node with k entries shows
+// c = 0 .. k-1 and the entries at the running maximum c = M are exactly one
+// per node with M + 1 entries.  Running over candidates (code != 0): M, R =
+// nodes at M, the best (code, -node) word among them and how many of them
+// share its code (> 1 with a code >= 2: the rare exact resolution).
+template <int D, int W, int kR0, bool kScore, bool kOff32>
+__device__ __forceinline__ void w64_dm(const Tile16Args &a, const W64 &w, cint_ptr R, int j, int s0) {
+    const cint_ptr r = R + W * j;
+    const int d = r[1];
+    unsigned x[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        const unsigned pr = (unsigned)r[kR0 + i / 2];
+        const int row = (i & 1) ? (int)(pr >> 16) : (int)(pr & 0xffffu);
+        x[i] = i < d ? w.cell(row) : kCellPad;
+    }
+    int M = -1, Rn = 0, namb = 0;
+    unsigned bw = 0u;
+#pragma unroll
+    for (int e = 0; e < D; ++e) {
+        if (D >= 16 && e % 8 == 0) __builtin_amdgcn_sched_barrier(0);  // bounds live registers
+        int c = 0;
+#pragma unroll
+        for (int h = 0; h < e; ++h) c += x[h] == x[e];
+        const bool cand = cell_code(x[e]) != kCodeHaz;
+        const unsigned wv = cell_cand(x[e]);
+        const bool gt = cand && c > M, eq = cand && c == M;
+        const unsigned kw = cell_code(wv), kb = cell_code(bw);
+        namb = gt ? 1 : (eq ? (kw > kb ? 1 : (kw == kb ? namb + 1 : namb)) : namb);
+        bw = gt ? wv : (eq ? max(bw, wv) : bw);
+        Rn = gt ? 1 : (eq ? Rn + 1 : Rn);
+        M = gt ? c : M;
+    }
+    const unsigned bk = cell_code(bw);
+    int t = Rn == 1 ? cand_node(bw) : (bk >= 2u ? cand_node(bw) : RSK_TARGET_NONE);
+    const bool need = Rn > 1 && bk >= 2u && namb > 1;
+    if (__builtin_amdgcn_ballot_w64(need)) {  // rare: wave-uniform branch
+        Img16 im;
+        im.w = reinterpret_cast<const unsigned *>(w.img);
+        im.lsl = 6;
+        const int te = t16_exact_scan(a, im, (const int *)(uintptr_t)(r + kR0), d, (int)(w.col4 >> 2), M + 1, bk, w.s);
+        t = need ? te : t;
+    }
+    emit64<kScore, kOff32>(a, r[0], s0, w, M < 0 ? w.zt : t, M < 0 ? w.zs : M + 1);
+}
+
+// 17 <= d <= 32, record j at R[20 * j]: [oi, d, -, -, rows from int 4].  The
+// 32 cells sorted in registers by a bitonic network (equal nodes form runs),
+// then two walks over the runs (sorted_runs_decide); the rare exact tie
+// rescans the LDS image (t16_exact_scan).
+template <bool kScore, bool kOff32>
+__device__ __forceinline__ void w64_ds(const Tile16Args &a, const W64 &w, cint_ptr R, int j, int s0) {
+    constexpr int D = 32;
+    const cint_ptr r = R + 20 * j;
+    const int d = r[1];
+    int M, t;
+    unsigned bk;
+    bool need;
+    {
+        unsigned x[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            if (i % 8 == 0) __builtin_amdgcn_sched_barrier(0);
+            const unsigned pr = (unsigned)r[4 + i / 2];
+            const int row = (i & 1) ? (int)(pr >> 16) : (int)(pr & 0xffffu);
+            x[i] = i < d ? w.cell(row) : kCellPad;
+        }
+        bitonic_sort<D, unsigned>(x);
+        t = sorted_runs_decide<D>(x, M, bk, need);
+    }
+    if (__builtin_amdgcn_ballot_w64(need)) {  // rare: wave-uniform branch
+        Img16 im;
+        im.w = reinterpret_cast<const unsigned *>(w.img);
+        im.lsl = 6;
+        const int te = t16_exact_scan(a, im, (const int *)(uintptr_t)(r + 4), d, (int)(w.col4 >> 2), M, bk, w.s);
+        t = need ? te : t;
+    }
+    emit64<kScore, kOff32>(a, r[0], s0, w, M == 0 ? w.zt : t, M == 0 ? w.zs : M);
+}
+
+// kL64 phase 2, part 1: the multi-neighbour classes (d >= 3), most expensive first.
+template <bool kScore, bool kOff32, bool kHeavy>
+__device__ __forceinline__ void w64_score_heavy(const Tile16Args &a, const W64 &w, cint_ptr m, cint_ptr R, int wave,
+                                                int s0) {
+    if (kHeavy) {  // d = 17..32: heavy tiles only (own instantiation, registers for 32 cells)
+        const cint_ptr Rc = R + m[15];
+        for (int j = wave; j < m[9]; j += 4) w64_ds<kScore, kOff32>(a, w, Rc, j, s0);
+    }
+    {
+        const cint_ptr Rc = R + m[14];
+        for (int j = wave; j < m[8]; j += 4) w64_dm<16, 12, 2, kScore, kOff32>(a, w, Rc, j, s0);
+    }
+    {
+        const cint_ptr Rc = R + m[13];
+        for (int j = wave; j < m[7]; j += 4) w64_dm<8, 8, 2, kScore, kOff32>(a, w, Rc, j, s0);
+    }
+    {
+        const cint_ptr Rc = R + m[12];
+        for (int j = wave; j < m[6]; j += 4) w64_dm<4, 4, 2, kScore, kOff32>(a, w, Rc, j, s0);
+    }
+}
+
+// kL64 phase 2, part 2: d = 2 and d = 1 records in blocks of 8.
+template <bool kScore, bool kOff32>
+__device__ __forceinline__ void w64_score_light(const Tile16Args &a, const W64 &w, cint_ptr m, cint_ptr R, int wave,
+                                                int s0) {
+    {
+        constexpr int U = 8;
+        const cint_ptr Rc = R + m[11];
+        const int n = m[5];
+        for (int k = wave * U; k < n; k += 4 * U) w64_d2<U, kScore, kOff32>(a, w, Rc, n, k, s0);
+    }
+    {
+        constexpr int U = 8;
+        const cint_ptr Rc = R + m[10];
+        const int n = m[4];
+        for (int k = wave * U; k < n; k += 4 * U) w64_d1<U, kScore, kOff32>(a, w, Rc, n, k, s0);
+    }
+}
+
+// kL64 phase 2: the records of each class, block b to wave b % 4.
+template <bool kScore, bool kOff32, bool kHeavy>
+__device__ __forceinline__ void w64_score(const Tile16Args &a, const W64 &w, cint_ptr m, cint_ptr R, int wave, int s0) {
+    if (a.ablate & 4) {  // profiling: the target stores alone (every record, zero-case value, no LDS reads)
+        for (int c = 0; c < kNumCls; ++c) {
+            const cint_ptr Rc = R + m[10 + c];
+            for (int j = wave; j < m[4 + c]; j += 4) emit64<kScore, kOff32>(a, Rc[kClsW[c] * j], s0, w, w.zt, w.zs);
+        }
+        return;
+    }
+    w64_score_heavy<kScore, kOff32, kHeavy>(a, w, m, R, wave, s0);
+    w64_score_light<kScore, kOff32>(a, w, m, R, wave, s0);
+}
+
+template <bool kScore, bool kOff32, bool kL64, bool kHeavy>
+__global__ __launch_bounds__(kTileThreads, (kHeavy || !kL64) ? RSK_TILE16_WGS_HEAVY : RSK_TILE16_WGS) void car_tile16_kernel(
+    Tile16Args a) {
+    extern __shared__ __attribute__((aligned(16))) int lds[];  // img cells [rmax][SL] (+ records, unit counter: !kL64)
     const int lsl = kL64 ? 6 : a.lsl;
     const int SL = 1 << lsl;
     const int nchunk = (a.S + SL - 1) >> lsl;
@@ -538,21 +772,37 @@ __global__ __launch_bounds__(kTileThreads, 4) void car_tile16_kernel(Tile16Args 
         unit = (int)(blockIdx.x & 7u) * a.xcd_per + (int)(blockIdx.x >> 3);
         if (unit >= nchunk * a.T) return;  // whole workgroup, before any barrier
     }
-    const int tile = a.order == 1 ? unit / nchunk : unit % a.T;
+    const int tile = a.tile0 + (a.order == 1 ? unit / nchunk : unit % a.T);
     const int chunk = a.order == 1 ? unit % nchunk : unit / a.T;
     const int lane = threadIdx.x & 63;
     const int s0 = chunk * SL;
     unsigned *img = reinterpret_cast<unsigned *>(lds);
-    int *rec = lds + a.img_cells;  // 16-B aligned (img_cells % 4 == 0) for the int4 record reads
     const cint_ptr m = const_ptr(a.meta) + (size_t)tile * kMetaW;
     const int img_off = m[0], nrows = m[1], rec_off = m[2], rec_ints = m[3];
-
+    if (kL64) {
+        if (!(a.ablate & 1)) t16_load_image<true, kOff32>(a, img, img_off, nrows, s0);
+        W64 w;
+        w.img = reinterpret_cast<const char *>(lds);
+        w.s = min(s0 + lane, a.S - 1);
+        w.col4 = (unsigned)(w.s - s0) << 2;
+        {
+            int zs;
+            w.zt = zero_target(load_zc(a.zc_cnt, a.zc_key, w.s), zs);
+            w.zs = zs;
+        }
+        __syncthreads();
+        if (a.ablate & 2) return;  // profiling ablation: no scoring (results are wrong)
+        const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+        w64_score<kScore, kOff32, kHeavy>(a, w, m, const_ptr(a.recs) + RSK_B16(rec_off, a.n_recs, 16u), wave, s0);
+        return;
+    }
+    int *rec = lds + a.img_cells;  // 16-B aligned (img_cells % 4 == 0) for the int4 record reads
     {   // records -> LDS: one int4 per thread, clamped
         const int i = min((int)threadIdx.x * 4, rec_ints - 4);
         *reinterpret_cast<int4 *>(rec + i) =
             *reinterpret_cast<const int4 *>(a.recs + RSK_B16(rec_off + i + 3, a.n_recs, 16u) - 3);
     }
-    if (!(a.ablate & 1)) t16_load_image<kL64, kOff32>(a, img, img_off, nrows, s0);
+    if (!(a.ablate & 1)) t16_load_image<false, kOff32>(a, img, img_off, nrows, s0);
 
     Lane16 L;
     L.PS = 64 >> lsl;
@@ -584,13 +834,13 @@ __global__ __launch_bounds__(kTileThreads, 4) void car_tile16_kernel(Tile16Args 
         const int kn = grab(ctr, lane);
         int u = k;
         if (u < u5) {
-            t16_ds<kScore, kOff32>(a, im, rec + m[15], n5, L, u);
+            t16_dn<32, 20, 4, kScore, kOff32>(a, im, rec + m[15], n5, L, u);
         } else if ((u -= u5) < u4) {
-            t16_dn<16, 12, kScore, kOff32>(a, im, rec + m[14], n4, L, u);
+            t16_dn<16, 12, 2, kScore, kOff32>(a, im, rec + m[14], n4, L, u);
         } else if ((u -= u4) < u3) {
-            t16_dn<8, 8, kScore, kOff32>(a, im, rec + m[13], n3, L, u);
+            t16_dn<8, 8, 2, kScore, kOff32>(a, im, rec + m[13], n3, L, u);
         } else if ((u -= u3) < u2) {
-            t16_dn<4, 4, kScore, kOff32>(a, im, rec + m[12], n2, L, u);
+            t16_dn<4, 4, 2, kScore, kOff32>(a, im, rec + m[12], n2, L, u);
         } else if ((u -= u2) < u1) {
             t16_d2<2, kScore, kOff32>(a, im, rec + m[11], n1, L, 2 * u);
         } else {
@@ -600,15 +850,134 @@ __global__ __launch_bounds__(kTileThreads, 4) void car_tile16_kernel(Tile16Args 
     }
 }
 
-int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off32, unsigned blocks, size_t lds) {
+// ---------------------------------------------------------------------------
+// car_mid16: rows of degree 17..64 (buckets D = 32, 64; records [oi, d,
+// neighbour pods...]), one wave per (row, chunk of SL scenarios), lane =
+// scenario (PS = 64 / SL rows per wave when S < 64).  Each lane gathers its
+// neighbours' cells (assign row, then the node's code), sorts the D cells in
+// registers (equal nodes become runs) and walks the runs twice: the maximal
+// run length M and the number of runs at it, then the best (code, -node)
+// among those runs and how many share its code; equal codes >= 2 on distinct
+// nodes are resolved exactly from cap / use in a third, rare walk.
+// ---------------------------------------------------------------------------
+// Exact tie resolution of a mid row (rare, kept out of registers): among the
+// row's distinct nodes with code bk and count M, the largest exact remaining
+// CPU, then the lower node — a dynamic double loop re-reading the row's
+// assignments (L2-resident) instead of the register copies.
+__device__ __forceinline__ int mid16_exact(const Mid16Args &a, const int *__restrict__ nb, int d, int s, int M,
+                                           unsigned bk) {
+    const unsigned S = (unsigned)a.S, N = (unsigned)a.N;
+    int br = INT_MIN, bn = INT_MAX;
+#pragma unroll 1
+    for (int e = 0; e < d; ++e) {
+        const int ne = ld32(a.assign, (unsigned)nb[e] * S + (unsigned)s);
+        if ((unsigned)ne >= N || ld16(a.code, (unsigned)ne * S + (unsigned)s) != bk) continue;
+        int cnt = 0;
+#pragma unroll 1
+        for (int i = 0; i < d; ++i) cnt += ld32(a.assign, (unsigned)nb[i] * S + (unsigned)s) == ne;
+        if (cnt != M) continue;
+        const int ex = a.cap[ne] - ld32(a.use, (unsigned)ne * S + (unsigned)s);
+        if (ex > br || (ex == br && ne < bn)) { br = ex; bn = ne; }
+    }
+    return bn;
+}
+
+template <int D, int W>
+__device__ __forceinline__ void mid16_row(const Mid16Args &a, const int *__restrict__ rec, int s, bool lane_ok) {
+    const unsigned S = (unsigned)a.S, N = (unsigned)a.N;
+    const int s_ld = min(s, a.S - 1);
+    const int4 *r4 = reinterpret_cast<const int4 *>(rec);
+    const int2 hd = *reinterpret_cast<const int2 *>(rec);
+    const int oi = hd.x, d = hd.y;
+    int v[D];
+#pragma unroll
+    for (int w = 0; w < W / 4; ++w) {
+        const int4 q4 = r4[w];
+        const int q[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int j = 4 * w + t - 2;
+            if (j >= 0 && j < D) v[j] = ld32(a.assign, (unsigned)(j < d ? q[t] : 0) * S + (unsigned)s_ld);
+        }
+    }
+    unsigned x[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        const bool ok = j < d && (unsigned)v[j] < N;
+        const unsigned cd = ld16(a.code, ok ? (unsigned)v[j] * S + (unsigned)s_ld : 0u);
+        x[j] = ok ? ((cd << 16) | (unsigned)v[j]) : kCellPad;
+    }
+    bitonic_sort<D, unsigned>(x);
+    int sc;
+    unsigned bk;
+    bool need;
+    int t = sorted_runs_decide<D>(x, sc, bk, need);
+    if (__builtin_amdgcn_ballot_w64(need)) {  // rare: wave-uniform branch
+        const int te = mid16_exact(a, rec + 2, d, s_ld, sc, bk);
+        t = need ? te : t;
+    }
+    if (t == INT_MIN) t = zero_target(load_zc(a.zc_cnt, a.zc_key, s_ld), sc);
+    if (lane_ok) {
+        const size_t o = (size_t)oi * S + s;
+        a.out_target[o] = t;
+        if (a.out_score) a.out_score[o] = sc;
+    }
+}
+
+// One launch per bucket (registers sized for its D): blocks of 4 waves, wave =
+// (PS rows, chunk of SL scenarios).
+template <int D, int W>
+__global__ __launch_bounds__(256) void car_mid16_kernel(Mid16Args a, const int *__restrict__ recs, int n_items,
+                                                        int blocks_per_chunk) {
+    const int chunk = blockIdx.x / blocks_per_chunk;
+    const int wave = (blockIdx.x % blocks_per_chunk) * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int slot = lane / a.SL;
+    const int s = chunk * a.SL + lane % a.SL;
+    const int item = wave * a.PS + slot;
+    if (wave * a.PS >= n_items) return;  // whole wave
+    const bool lane_ok = slot < a.PS && s < a.S && item < n_items;
+    const int it = min(item, n_items - 1);
+    mid16_row<D, W>(a, recs + (size_t)it * W, s, lane_ok);
+}
+
+int launch_mid16(hipStream_t stream, const Mid16Args &a0) {
+    Mid16Args a = a0;
+    a.SL = std::min(a.S, 64);
+    a.PS = 64 / a.SL;
+    for (int b = 0; b < 2; ++b) {
+        const int n = a.n_items[b];
+        if (n == 0) continue;
+        const int waves = (int)ceil_div(n, a.PS);
+        const int bpc = (int)ceil_div(waves, 4);
+        const int64_t blocks = ceil_div(a.S, a.SL) * bpc;
+        RSK_CHECK(blocks < INT32_MAX, "mid grid too large");
+        if (b == 0)
+            car_mid16_kernel<32, 36><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(a, a.rec[0], n, bpc);
+        else
+            car_mid16_kernel<64, 68><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(a, a.rec[1], n, bpc);
+        RSK_HIP(hipGetLastError());
+    }
+    return RSK_OK;
+}
+
+int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off32, bool heavy, unsigned blocks,
+                  size_t lds) {
     using K = void (*)(Tile16Args);
-    static const K kerns[8] = {
-        &car_tile16_kernel<false, false, false>, &car_tile16_kernel<false, true, false>,
-        &car_tile16_kernel<true, false, false>,  &car_tile16_kernel<true, true, false>,
-        &car_tile16_kernel<false, false, true>,  &car_tile16_kernel<false, true, true>,
-        &car_tile16_kernel<true, false, true>,   &car_tile16_kernel<true, true, true>};
+    // [l64][heavy][score][off32]; the generic (S < 64) kernel scores every class
+    static const K kerns[16] = {
+        &car_tile16_kernel<false, false, false, false>, &car_tile16_kernel<false, true, false, false>,
+        &car_tile16_kernel<true, false, false, false>,  &car_tile16_kernel<true, true, false, false>,
+        &car_tile16_kernel<false, false, false, false>, &car_tile16_kernel<false, true, false, false>,
+        &car_tile16_kernel<true, false, false, false>,  &car_tile16_kernel<true, true, false, false>,
+        &car_tile16_kernel<false, false, true, false>,  &car_tile16_kernel<false, true, true, false>,
+        &car_tile16_kernel<true, false, true, false>,   &car_tile16_kernel<true, true, true, false>,
+        &car_tile16_kernel<false, false, true, true>,   &car_tile16_kernel<false, true, true, true>,
+        &car_tile16_kernel<true, false, true, true>,    &car_tile16_kernel<true, true, true, true>};
     const bool l64 = a.lsl == 6;
-    const K kern = kerns[(l64 ? 4 : 0) + (score ? 2 : 0) + (off32 ? 1 : 0)];
+    RSK_CHECK(!l64 || (size_t)lds <= (size_t)kT16Rows * 256, "tile image exceeds the %d rows the kernel was built for",
+              kT16Rows);
+    const K kern = kerns[(l64 ? 8 : 0) + (heavy ? 4 : 0) + (score ? 2 : 0) + (off32 ? 1 : 0)];
     RSK_CHECK(lds <= 160 * 1024, "tile image needs %zu B of LDS", lds);
     if (lds > 64 * 1024)
         RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -617,6 +986,13 @@ int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off3
     RSK_HIP(hipGetLastError());
     return RSK_OK;
 }
+
+size_t tile16_lds_bytes(int rmax, int lsl, int rec_cap) {
+    if (lsl == 6) return (size_t)rmax * 64 * 4;  // kL64: records are read from the plan, not LDS
+    return ((((size_t)rmax << lsl) + 3) / 4 * 4 + (size_t)rec_cap + 4) * 4;
+}
+
+int tile16_rows_built() { return kT16Rows; }
 
 unsigned tile16_debug_take() {
 #ifdef RSK_DEBUG_BOUNDS

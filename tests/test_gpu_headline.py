@@ -24,7 +24,7 @@ def ctx():
 def _rows_to_check(c, n_sample, seed):
     deg = np.diff(c.row_ptr)
     rng = np.random.default_rng(seed)
-    hard = np.nonzero(deg > 32)[0]                       # every mid and hub row
+    hard = np.nonzero(deg > 16)[0]                       # every heavy-tile (17..32), mid and hub row
     sample = rng.choice(c.P, n_sample, replace=False)
     return np.unique(np.concatenate([hard, sample])).astype(np.int32), hard
 
@@ -46,7 +46,7 @@ def test_config3_headline_s4096(ctx, synth_golden):
     g = synth_golden["100k5k"]["scenarios"][0]
     assert t[g["pods"], 0].tolist() == g["car_target"]
     rows, hard = _rows_to_check(c, 1000, 7)
-    assert hard.size == info["mid_rows"] + info["heavy_rows"] == 201
+    assert hard.size == 640 and info["mid_rows"] + info["heavy_rows"] == 201 and info["sorted_rows"] == 439
     exp, _ = orc.car(c.row_ptr, c.col_idx, c.assign, S, c.cap_cpu, c.use_cpu, c.hazard, N, rows=rows,
                      threads=THREADS)
     got = t[rows].reshape(-1)

@@ -141,6 +141,7 @@ def test_car_degree_bucket_boundaries(ctx, S):
     _check_car(ctx, rp, ci, a, S, cap, use, haz, N, label=f"boundaries S={S}")
     from rsk import api
     info = api.CarPlan(rp, ci, ctx=ctx).info()
+    # 17..32 in heavy tiles, 33..64 to the mid kernel, > 64 to the hub kernel
     assert info["sorted_rows"] >= 3 and info["mid_rows"] >= 3 and info["heavy_rows"] >= 5 and info["tile_rows"] > 0, info
 
 

@@ -173,3 +173,41 @@ def test_py_randbelow_matches_cpython():
         n = int(rng.integers(1, 100000))
         assert orc.py_randbelow(seed, n) == pyrandom.Random(seed)._randbelow(n)
     assert orc.py_randbelow(0, 7) == pyrandom.Random(0)._randbelow(7)
+
+
+def test_python_restatements_match_golden_and_c_oracle(synth_golden):
+    """oracle/car_py.py's literal and numpy CAR restatements (bench.py's extra
+    CPU legs) against the reference's 2k/64 decisions and, on
+    random tie-heavy cases, against the C oracle."""
+    from oracle import car_py
+    from oracle import oracle as orc
+    from rsk import synth
+    g = synth_golden["2k64"]
+    c = synth.make_cluster(g["P"], g["N"], S=g["S"], seed=g["seed"])
+    for sc in g["scenarios"]:
+        s = sc["s"]
+        a, u, h = car_py.scenario_view(c.assign, c.use_cpu, c.hazard, c.P, c.N, c.S, s)
+        by_node = car_py.pods_by_node(a, c.N)
+        haz_list = [n for n in range(c.N) if h[n]]
+        nbrs = car_py.dedup_rows(c.row_ptr, c.col_idx, sc["pods"])
+        lit = [car_py.car_literal(nb.tolist(), by_node, haz_list, c.cap_cpu, u) for nb in nbrs]
+        vec = [car_py.car_numpy(nb, a, c.cap_cpu, u, h, c.N) for nb in nbrs]
+        assert lit == sc["car_target"] and vec == sc["car_target"], f"scenario {s}"
+    rng = np.random.default_rng(12)
+    for trial in range(40):
+        N, P = int(rng.integers(1, 9)), int(rng.integers(2, 40))
+        rows = [rng.integers(0, P, int(rng.integers(0, 6))) for _ in range(P)]
+        rp = np.zeros(P + 1, np.int32)
+        rp[1:] = np.cumsum([len(r) for r in rows])
+        ci = np.concatenate(rows + [np.zeros(0, np.int64)]).astype(np.int32)
+        a = rng.integers(-1, N, P).astype(np.int32)
+        cap = rng.choice([1000, 2000], N).astype(np.int32)
+        use = rng.choice([0, 1000, 1500, 2000, 2500], N).astype(np.int32)
+        h = (rng.random(N) < 0.3).astype(np.uint8)
+        drp, dci = orc.dedup_csr(rp, ci)  # the C oracle takes relation sets (rows deduplicated)
+        exp, _ = orc.car(drp, dci, a, 1, cap, use, h, N)
+        by_node = car_py.pods_by_node(a, N)
+        haz_list = [n for n in range(N) if h[n]]
+        for p, nb in enumerate(car_py.dedup_rows(rp, ci, range(P))):
+            assert car_py.car_literal(nb.tolist(), by_node, haz_list, cap, use) == exp[p], (trial, p)
+            assert car_py.car_numpy(nb, a, cap, use, h, N) == exp[p], (trial, p)

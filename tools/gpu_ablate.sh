@@ -1,23 +1,25 @@
 #!/bin/bash
-# Tile-kernel ablations + SQ counters (one GPU session).
+# Tile-kernel ablations on the headline bench: full, no scoring, no image load, neither
+# (RSK_ABLATE_TILE; results are wrong when ablated), side kernels serialized
+# (RSK_OVERLAP=0), plus optional env variants: gpu_ablate.sh <outdir> [VAR=val,VAR2=val ...]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
-mkdir -p gpurun_out/abl
+out=${1:-gpurun_out/ablate}; shift
+mkdir -p "$out"
 export TMPDIR=/tmp
-run() {  # run <name> <seconds> <cmd...>
-    local name=$1 secs=$2; shift 2
-    timeout -k 10 "$secs" "$@" > "gpurun_out/abl/$name.log" 2>&1
+run() {  # run <name> [env...]
+    local name=$1; shift
+    env RSK_OVERLAP=0 "$@" timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline > "$out/$name.log" 2>&1
     local rc=$?
-    echo "== $name rc=$rc"
-    grep -o '"car_tile": {[^}]*}' "gpurun_out/abl/$name.log" | head -1
-    if [ $rc -ne 0 ]; then tail -5 "gpurun_out/abl/$name.log"; exit $rc; fi
+    echo "== $name rc=$rc $(grep -o '"ms_per_step": [0-9.]*' "$out/$name.log") $(python3 -c '
+import json,sys
+for l in open(sys.argv[1]):
+    if l.startswith("{"):
+        d=json.loads(l); print({k: round(v["per_step_ms"],3) for k,v in d["kernels"].items()}, d["parity_sample_ok"])' "$out/$name.log")"
+    [ $rc -ne 0 ] && { tail -5 "$out/$name.log"; exit $rc; }
+    return 0
 }
-B="python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline"
-run full 200 $B
-RSK_ABLATE_TILE=1 run noload 200 $B
-RSK_ABLATE_TILE=2 run noscore 200 $B
-RSK_ABLATE_TILE=3 run nothing 200 $B
-RSK_TILE_SL=16 run sl16 200 $B
-RSK_TILE_SL=64 run sl64 200 $B
-timeout -k 10 60 rocprofv3 --list-avail > gpurun_out/abl/avail.txt 2>&1 || true
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES -d gpurun_out/abl/pmc -o sq -f csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/abl/pmc_sq.log 2>&1
-echo "pmc rc=$?"
+run full
+run noscore RSK_ABLATE_TILE=2
+run noload RSK_ABLATE_TILE=1
+run neither RSK_ABLATE_TILE=3
+for v in "$@"; do run "$(echo "$v" | tr ",=/" "___" | cut -c1-60)" $(echo "$v" | tr "," " "); done

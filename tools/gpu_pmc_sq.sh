@@ -1,7 +1,7 @@
 #!/bin/bash
 # SQ / TA counter passes on the headline bench (one rocprofv3 --pmc run per group).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
-mkdir -p gpurun_out/sq gpurun_out/sq_abl
+mkdir -p gpurun_out/sq gpurun_out/sq_abl "${SQ_OUT:-gpurun_out/sq}"
 export TMPDIR=/tmp RSK_OVERLAP=0
 OUT=${SQ_OUT:-gpurun_out/sq}
 B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline"

@@ -1,21 +1,21 @@
 #!/usr/bin/env python3
-"""Summarise a gpu_check.sh session (gpurun_out/) into profiles/.
+"""Summarise a tools/gpu_prof.sh session into profiles/.
 
-Reads the rocprofv3 kernel-trace stats (prof/run_kernel_stats.csv,
-prof/run_kernel_trace.csv) and the separate PMC passes (pmc/fetch_*,
-pmc/write_*, pmc/l2_*), and writes:
+Reads the rocprofv3 kernel-trace stats (<src>/prof/run_kernel_stats.csv,
+<src>/prof/run_kernel_trace.csv) and the separate PMC passes
+(<src>/pmc/fetch_*, write_*, l2_*), and writes:
 
   profiles/<tag>_kernel_stats.csv   rocprofv3 --stats summary (copied)
-  profiles/<tag>_summary.json       per-kernel: launches, avg duration (trace),
+  profiles/<tag>_summary.json       per kernel: launches, avg duration (trace),
                                     FETCH_SIZE / WRITE_SIZE / TCC hit+miss per launch
-  profiles/pmc_headline.json        hbm_bytes_per_launch per kernel for bench.py
+  profiles/pmc_traffic.json         {"configs": {config: {kernel: {S,
+                                    hbm_bytes_per_launch, ...}}}} for bench.py
 
-HBM bytes = (FETCH_SIZE + WRITE_SIZE) * 1024 per launch.  The microarch guide's
-x2 FETCH correction applies to 16-B-per-lane streaming reads; these kernels
-read 4 B per lane (dword loads / global_load_lds_dword), for which the raw
-FETCH_SIZE matched the known image bytes (391 tiles x 272 rows x 64 chunks x
-256 B = 1.74 GB vs 1.78 GB measured), so it is reported uncorrected, with the
-x2 figure alongside.
+HBM bytes per launch = (2 x FETCH_SIZE + WRITE_SIZE) x 1024: on gfx950
+FETCH_SIZE reports half the bytes of coalesced streaming reads
+(MI355X_MICROARCH.md, HBM section), and these kernels' bulk reads are
+coalesced 128-/256-B rows (lane = scenario).  Infinity-Cache hits are counted
+too (the same section), so the figure is an upper bound on DRAM bytes.
 """
 from __future__ import annotations
 
@@ -28,6 +28,10 @@ import re
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+# kernel symbol -> the timer name bench.py reports (librsk ScopedTimer names)
+BENCH_NAME = {"car_tile16": "car_tile", "car_hub": "car_heavy", "car_pivot": "car_side"}
 
 
 def short(name: str) -> str:
@@ -48,7 +52,7 @@ def read_pmc(path, counter):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", required=True)
-    ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out"))
+    ap.add_argument("--src", required=True, help="a tools/gpu_prof.sh output directory")
     ap.add_argument("--config", default="headline")
     ap.add_argument("--S", type=int, default=4096)
     args = ap.parse_args()
@@ -72,8 +76,10 @@ def main():
             if v:
                 e[c] = round(sum(v) / len(v), 1)
         if "FETCH_SIZE" in e and "WRITE_SIZE" in e:
-            e["hbm_bytes_per_launch"] = int((e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024)
-            e["hbm_bytes_per_launch_fetch_x2"] = int((2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024)
+            e["read_bytes_per_launch"] = int(2 * e["FETCH_SIZE"] * 1024)   # x2: gfx950 FETCH_SIZE correction
+            e["write_bytes_per_launch"] = int(e["WRITE_SIZE"] * 1024)
+            e["hbm_bytes_per_launch"] = e["read_bytes_per_launch"] + e["write_bytes_per_launch"]
+            e["hbm_bytes_per_launch_fetch_raw"] = int((e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024)
             e["hbm_GBps"] = round(e["hbm_bytes_per_launch"] / (e["avg_us"] * 1e3), 1)
         summary[f"{k}@{grid}"] = e
     with open(os.path.join(prof, f"{args.tag}_summary.json"), "w") as f:
@@ -82,16 +88,26 @@ def main():
     by_kernel = collections.defaultdict(lambda: [0, 0, 0.0])
     for key, e in summary.items():
         if "hbm_bytes_per_launch" in e:
-            b = by_kernel[key.split("@")[0]]
+            k = key.split("@")[0]
+            b = by_kernel[BENCH_NAME.get(k, k)]
             b[0] += e["hbm_bytes_per_launch"]
             b[1] += 1
             b[2] += e["avg_us"]
-    head = {"source": f"profiles/{args.tag}_summary.json", args.config: {}}
+    path = os.path.join(prof, "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            traffic = json.load(f)
+    except (OSError, ValueError):
+        traffic = {}
+    traffic.setdefault("note", "hbm_bytes_per_launch = (2 x FETCH_SIZE + WRITE_SIZE) x 1024, per launch "
+                               "(tools/pmc_summary.py); bench.py reads configs[config][kernel]")
+    entry = traffic.setdefault("configs", {}).setdefault(args.config, {})
+    entry.clear()
     for k, (bytes_, n, us) in by_kernel.items():
-        head[args.config][f"car_{k[4:]}" if k.startswith("car_") else k] = {
-            "S": args.S, "hbm_bytes_per_launch": bytes_ // max(n, 1), "avg_us": round(us / max(n, 1), 2)}
-    with open(os.path.join(prof, "pmc_headline.json"), "w") as f:
-        json.dump(head, f, indent=1)
+        entry[k] = {"S": args.S, "hbm_bytes_per_launch": bytes_ // max(n, 1), "avg_us": round(us / max(n, 1), 2),
+                    "source": f"profiles/{args.tag}_summary.json"}
+    with open(path, "w") as f:
+        json.dump(traffic, f, indent=1)
     print(json.dumps(summary, indent=1))
 
 
