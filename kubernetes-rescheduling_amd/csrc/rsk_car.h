@@ -25,6 +25,8 @@ constexpr int kNumHeavy = 6;                       // hub classes: (64,128] (128
 constexpr int kHeavyMax[kNumHeavy] = {128, 255, 512, 1024, 2048, 4096};  // <= 255: u8 counters
 constexpr int kHeavyNJ[kNumHeavy] = {2, 4, 8, 16, 0, 0};  // register entries per lane (0: LDS re-reads)
 constexpr int kHubMax = 4096;                      // wide hub kernel: rows up to this degree
+constexpr int kNumPiv = 5;                         // compact side rows by degree: (32,128] (128,512] (512,2048]
+constexpr int kPivMax[kNumPiv - 1] = {128, 512, 2048, kHubMax};  // (2048,4096] (4096,..): the last only here
 
 // Light-row tiles.
 constexpr int kTileOwners = 128;                   // max rows scored per tile
@@ -198,14 +200,30 @@ __device__ __forceinline__ int grab(int *ctr, int lane) {
 //
 // Node state per (node, scenario) as a 16-bit code, monotone in the remaining
 // CPU rem = cap - use:
-//   0            hazard (never a candidate)
-//   1            rem < 0 (any negative value: a tie whose best rem is < 0 is
-//                None whichever node wins it, rescheduling.py:203-212)
-//   2 + f(rem)   rem >= 0, f non-decreasing: exact below 2^14, then 13
-//                mantissa bits per power of two up to 2^19, one bucket above.
-// A code comparison decides every tie except between distinct nodes with the
-// same code >= 2; those few are resolved exactly from cap / use.
-// ---------------------------------------------------------------------------
+//   0                hazard (never a candidate)
+//   1                rem < 0 (any negative value: a tie whose best rem is < 0 is
+//                    None whichever node wins it, rescheduling.py:203-212)
+//   2 .. 8193        rem in [0, 8192) exactly, while rem < B
+//   8194 .. 32768    rem in [8192, B): 12 mantissa bits per power of two (inexact)
+//   32769 .. 65534   rem in [B, B + 32766) exactly
+//   65535            rem beyond that (inexact)
+// with B = max(0, max(cap) - 32766): every rem within 32766 millicores of the
+// largest capacity has its own code, so ties on the top nodes are decided by
+// the code word alone.  A code comparison decides every tie except between
+// distinct nodes with the same inexact code; those few are resolved exactly
+// from cap / use.
+// A cell: (code << 16) | node; kCellPad = code 0 (no candidate), node 0xffff
+// (never a node: N <= 65535) for padding and assignments outside [0, N).
+constexpr unsigned kCellPad = 0x0000ffffu;
+__device__ __forceinline__ unsigned cell_code(unsigned c) { return c >> 16; }
+__device__ __forceinline__ int cell_node(unsigned c) { return (int)(c & 0xffffu); }
+// candidate word: larger code first, then the lower node (the reference's
+// `rem > r` keeps the first node in nodes_name order on equal rem)
+__device__ __forceinline__ unsigned cell_cand(unsigned c) { return c ^ 0xffffu; }
+__device__ __forceinline__ int cand_node(unsigned w) { return (int)((w & 0xffffu) ^ 0xffffu); }
+// equal codes >= 2 that do NOT imply equal remaining CPU (exact resolution needed)
+__device__ __forceinline__ bool code_inexact(unsigned c) { return (c >= 8194u && c <= 32768u) || c == 65535u; }
+
 constexpr unsigned kCodeHaz = 0u;
 constexpr unsigned kCodeNeg = 1u;
 constexpr int kMaxNodes16 = 65535;  // node ids fit 16 bits, 0xffff stays free as the pad node
@@ -240,9 +258,9 @@ struct Tile16Args {
     unsigned n_assign, n_out, n_pods, n_recs, n_key;  // element counts (debug bounds build)
 };
 
-// Pivot-delta rows (mid and hub rows of the compact path).
+// Pivot-delta rows: every side row (deg > 32) of the compact path (rsk_pivot.hip).
 struct PivotArgs {
-    const HeavyItem *items;   // {out_row, col offset, deg}
+    const HeavyItem *items;   // {out_row, offset into hcol, deg}
     int n_items;
     const int *hcol;          // neighbour lists
     const int *assign;
@@ -253,8 +271,7 @@ struct PivotArgs {
     int *out_target;
     int *out_score;
     int S, N;
-    int H;                    // pivot count table: N (direct u16) or hash slots
-    int hash;                 // 1: hash table of 2*H words (N too large for a direct table)
+    int ablate;               // profiling only (RSK_ABLATE_PIVOT): 1 skip the slow lanes, 2 stop after pass A
 };
 
 // Mid rows (17..64) of the compact path: buckets D = 32, 64 (records kMidW ints).
@@ -275,7 +292,7 @@ int launch_mid16(hipStream_t stream, const Mid16Args &a);
 int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off32, bool heavy, unsigned blocks,
                   size_t lds);
 size_t tile16_lds_bytes(int rmax, int lsl, int rec_cap);
-int launch_pivot(hipStream_t stream, const PivotArgs &a, int dmax, unsigned groups_per_item);
+int launch_pivot(hipStream_t stream, const PivotArgs &a, int max_distinct);
 unsigned tile16_debug_take();
 int tile16_rows_built();       // image rows per tile the compact kernels are compiled for (RSK_TILE16_ROWS)  // debug bounds build: violation flags of the compact kernels (cleared)
 

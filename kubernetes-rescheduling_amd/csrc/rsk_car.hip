@@ -761,6 +761,11 @@ struct rsk_car_plan {
     int heavy_dmax[kNumHeavy] = {};
     DevBuf heavy_items[kNumHeavy];
     DevBuf hcol;
+    // every side row (deg > light_max) for the compact path's pivot kernel, by degree class
+    int n_piv[kNumPiv] = {};
+    int piv_dmax[kNumPiv] = {};
+    DevBuf piv_items[kNumPiv];
+    DevBuf pcol;
     // per-execute workspace
     DevBuf nodekey, code, zc;
     // the inputs, kept for the N >= kPackMaxN variant (built on first use)
@@ -775,6 +780,8 @@ struct rsk_car_plan {
         for (auto &b : mid) b.release();
         for (auto &b : heavy_items) b.release();
         hcol.release();
+        for (auto &b : piv_items) b.release();
+        pcol.release();
         nodekey.release();
         code.release();
         zc.release();
@@ -782,6 +789,12 @@ struct rsk_car_plan {
 };
 
 namespace {
+
+int pivot_class(int d) {
+    for (int c = 0; c < kNumPiv - 1; ++c)
+        if (d <= kPivMax[c]) return c;
+    return kNumPiv - 1;
+}
 
 int heavy_class(int d) {
     for (int c = 0; c < kNumHeavy; ++c)
@@ -1043,7 +1056,8 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
     std::vector<int> light;  // row indices i with deg <= light_max, to be tiled in DFS order
     std::vector<std::vector<int>> midr(kNumMid);
     std::vector<std::vector<HeavyItem>> hitems(kNumHeavy);
-    std::vector<int> hcol;
+    std::vector<int> hcol, pcol;
+    std::vector<std::vector<HeavyItem>> pitems(kNumPiv);
     for (int i = 0; i < Q; ++i) {
         const int p = rows ? rows[i] : i;
         const int d = rp[p + 1] - rp[p];
@@ -1061,12 +1075,18 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
             e[o + 1] = d;
             for (int j = 0; j < d; ++j) e[o + 2 + j] = nbp[j];
             plan->n_mid[b] += 1;
-        } else {
+        } else if (d <= kHubMax) {
             const int c = heavy_class(d);
             hitems[c].push_back({i, (int)hcol.size(), d, 0});
             hcol.insert(hcol.end(), nbp, nbp + d);
             plan->n_heavy[c] += 1;
             plan->heavy_dmax[c] = std::max(plan->heavy_dmax[c], d);
+        }
+        if (d > plan->light_max) {  // compact path: every side row through the pivot kernel
+            const int c = pivot_class(d);
+            pitems[c].push_back({i, (int)pcol.size(), d, 0});
+            pcol.insert(pcol.end(), nbp, nbp + d);
+            plan->piv_dmax[c] = std::max(plan->piv_dmax[c], d);
         }
     }
     std::stable_sort(light.begin(), light.end(), [&](int x, int y) {
@@ -1132,6 +1152,11 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
     for (int c = 0; c < kNumHeavy; ++c)
         RSK_TRY(upload(plan->heavy_items[c], hitems[c].data(), hitems[c].size() * sizeof(HeavyItem)));
     RSK_TRY(upload(plan->hcol, hcol.data(), hcol.size() * 4));
+    for (int c = 0; c < kNumPiv; ++c) {
+        plan->n_piv[c] = (int)pitems[c].size();
+        RSK_TRY(upload(plan->piv_items[c], pitems[c].data(), pitems[c].size() * sizeof(HeavyItem)));
+    }
+    RSK_TRY(upload(plan->pcol, pcol.data(), pcol.size() * 4));
     return RSK_OK;
 }
 
@@ -1182,7 +1207,16 @@ bool mid16_on() {
     return on;
 }
 
+// Compact side rows: car_mid (33..64) + car_hub (65..4096) by default; the
+// pivot-delta kernel for rows above kHubMax always, and for every side row
+// with RSK_PIVOT=1 (exact too, slower at the headline shapes: DESIGN.md §4).
+bool pivot_on() {
+    static const bool on = env_int("RSK_PIVOT", 0) != 0;
+    return on;
+}
+
 bool plan_side_compact(const rsk_car_plan *plan) {
+    if (pivot_on()) return true;
     for (int c = 0; c < kNumHeavy; ++c)
         if (plan->n_heavy[c]) return false;
     return mid16_on() || plan->n_mid[0] + plan->n_mid[1] == 0;
@@ -1195,6 +1229,32 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t *side, int n
     int *d_target = b.target, *d_score = b.score;
     int next = 0;
     auto pick = [&]() { return side[next++ % nside]; };
+    if (compact) {  // pivot-delta kernel: every side row (RSK_PIVOT=1) or the rows above kHubMax
+        for (int c = pivot_on() ? 0 : kNumPiv - 1; c < kNumPiv; ++c) {
+            if (!plan->n_piv[c]) continue;
+            PivotArgs a;
+            std::memset(&a, 0, sizeof(a));
+            a.items = plan->piv_items[c].as<HeavyItem>();
+            a.n_items = plan->n_piv[c];
+            a.hcol = plan->pcol.as<int>();
+            a.assign = d_assign;
+            a.code = b.code;
+            a.cap = b.cap;
+            a.use = b.use;
+            a.zc_cnt = d_zcnt;
+            a.zc_key = d_zkey;
+            a.out_target = d_target;
+            a.out_score = d_score;
+            a.S = S;
+            a.N = N;
+            static const int pablate = env_int("RSK_ABLATE_PIVOT", 0);
+            a.ablate = pablate;
+            const hipStream_t stream = pick();
+            ScopedTimer tm(ctx, "car_side", stream);
+            RSK_TRY(launch_pivot(stream, a, std::min(plan->piv_dmax[c], N)));
+        }
+        if (pivot_on()) return RSK_OK;
+    }
     ScoreCtx sc;
     sc.nodekey = d_key;
     sc.zc_cnt = d_zcnt;
@@ -1280,6 +1340,7 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t *side, int n
 bool plan_has_side(const rsk_car_plan *plan) {
     int n = plan->n_mid[0] + plan->n_mid[1];
     for (int c = 0; c < kNumHeavy; ++c) n += plan->n_heavy[c];
+    for (int c = 0; c < kNumPiv; ++c) n += plan->n_piv[c];
     return n > 0;
 }
 

@@ -40,14 +40,15 @@ __device__ __forceinline__ unsigned dbg16(unsigned idx, unsigned lim, unsigned c
 // ---------------------------------------------------------------------------
 // node state
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ unsigned code16(int rem, bool haz) {
+__device__ __forceinline__ unsigned code16(int rem, bool haz, int B) {
     if (haz) return kCodeHaz;
     if (rem < 0) return kCodeNeg;
+    if (rem >= B) return 32769u + (unsigned)min(rem - B, 32766);
     const unsigned x = (unsigned)rem;
-    if (x < (1u << 14)) return 2u + x;
-    const int e = 31 - __clz((int)x);  // 14..30
-    if (e > 18) return 2u + (1u << 14) + 5u * 8192u;  // one bucket from 2^19 up (exact ties resolve it)
-    return 2u + (1u << 14) + (unsigned)(e - 14) * 8192u + ((x >> (e - 13)) & 0x1fffu);
+    if (x < 8192u) return 2u + x;
+    const int e = 31 - __clz((int)x);  // 13..30
+    if (e > 18) return 32768u;          // one bucket from 2^19 to B (exact ties resolve it)
+    return 2u + 8192u + (unsigned)(e - 13) * 4096u + ((x >> (e - 12)) & 0xfffu);
 }
 
 template <int V>
@@ -79,11 +80,20 @@ __global__ __launch_bounds__(256) void car_prep_kernel(const int *__restrict__ c
                                                        int *__restrict__ zc_cnt, unsigned long long *__restrict__ zc_key) {
     __shared__ int lcnt[256 * V];
     __shared__ unsigned long long lkey[256 * V];
+    __shared__ int lcap;
     const unsigned t = blockIdx.x * 256u + threadIdx.x;
+    if (kCode) {  // B = max(0, max(cap) - 32766): the exact code window (rsk_car.h)
+        if (threadIdx.x == 0) lcap = 0;
+        __syncthreads();
+        int mc = 0;
+        for (int n = threadIdx.x; n < N; n += 256) mc = max(mc, cap[n]);
+        atomicMax(&lcap, mc);
+    }
     const unsigned base = (blockIdx.x * 256u) % (unsigned)SV;  // vector slot of thread 0
     const int nslot = min(256, SV);
     for (int i = threadIdx.x; i < nslot * V; i += 256) { lcnt[i] = 0; lkey[i] = 0ull; }
     __syncthreads();
+    const int B = kCode ? max(0, lcap - 32766) : 0;
     if (t < total) {
         const int sv = (int)(t % (unsigned)SV);
         const int n0 = (int)(t / (unsigned)SV) * npb;
@@ -104,7 +114,7 @@ __global__ __launch_bounds__(256) void car_prep_kernel(const int *__restrict__ c
             for (int x = 0; x < V; ++x) {
                 const int rem = c - uu[x];
                 k[x] = hh[x] ? kKeyHaz : rem;
-                cd[x] = code16(rem, hh[x] != 0);
+                cd[x] = code16(rem, hh[x] != 0, B);
                 cnt[x] += hh[x] ? 0 : 1;
                 const unsigned long long pk = hh[x] ? 0ull : zc_pack(rem, n);
                 best[x] = pk > best[x] ? pk : best[x];
@@ -176,14 +186,6 @@ int launch_prep(hipStream_t stream, const Prep16Args &a) {
 // guarded by a lane-divergent branch (hipcc otherwise waits vmcnt(0) per
 // element), except the exact tie resolution, which is rare.
 // ---------------------------------------------------------------------------
-constexpr unsigned kCellPad = 0x0000ffffu;
-
-__device__ __forceinline__ unsigned cell_code(unsigned c) { return c >> 16; }
-__device__ __forceinline__ int cell_node(unsigned c) { return (int)(c & 0xffffu); }
-// candidate word: larger code first, then the lower node (the reference's
-// `rem > r` keeps the first node in nodes_name order on equal rem)
-__device__ __forceinline__ unsigned cell_cand(unsigned c) { return c ^ 0xffffu; }
-__device__ __forceinline__ int cand_node(unsigned w) { return (int)((w & 0xffffu) ^ 0xffffu); }
 
 // Image rows per tile the compact kernel is compiled for (the plan's
 // RSK_TILE_ROWS must not exceed it) and workgroups per CU it is register-sized for.
@@ -289,7 +291,7 @@ __device__ __forceinline__ void t16_d2(const Tile16Args &a, const Img16 &img, co
         const bool single = w0 == 0u || w1 == 0u || same;
         int t = cand_node(best);
         if (!single && cell_code(best) < 2u) t = RSK_TARGET_NONE;
-        if (!single && k0 == k1 && k0 >= 2u) {  // equal codes: exact remaining CPU (rare)
+        if (!single && k0 == k1 && code_inexact(k0)) {  // equal inexact codes: exact remaining CPU (rare)
             const int n0 = cell_node(c0[u]), n1 = cell_node(c1[u]);
             const int e0 = exact_rem(a, n0, L.s), e1 = exact_rem(a, n1, L.s);
             t = (e0 > e1 || (e0 == e1 && n0 < n1)) ? n0 : n1;
@@ -365,7 +367,7 @@ __device__ __forceinline__ void t16_dn(const Tile16Args &a, const Img16 &img, co
     }
     const unsigned bk = cell_code(best);
     int t = nm == 1 ? cand_node(best) : (bk >= 2u ? cand_node(best) : RSK_TARGET_NONE);
-    if (nm > 1 && bk >= 2u) {
+    if (nm > 1 && code_inexact(bk)) {
         int namb = 0;
 #pragma unroll
         for (int j = 0; j < D; ++j) namb += cell_code(w[j]) == bk;
@@ -407,7 +409,7 @@ __device__ __forceinline__ int sorted_runs_decide(const unsigned (&x)[D], int &s
     score = M;
     const unsigned bk = cell_code(bw);
     bk_out = bk;
-    need = M > 0 && Rn > 1 && bk >= 2u && namb > 1;
+    need = M > 0 && Rn > 1 && code_inexact(bk) && namb > 1;
     if (M == 0) return INT_MIN;
     return Rn == 1 ? cand_node(bw) : (bk >= 2u ? cand_node(bw) : RSK_TARGET_NONE);
 }
@@ -613,7 +615,7 @@ __device__ __forceinline__ void w64_d2(const Tile16Args &a, const W64 &w, cint_p
         const bool single = w0 == 0u || w1 == 0u || same;
         int t = cand_node(best);
         if (!single && cell_code(best) < 2u) t = RSK_TARGET_NONE;
-        if (!single && k0 == k1 && k0 >= 2u) {  // equal codes: exact remaining CPU (rare)
+        if (!single && k0 == k1 && code_inexact(k0)) {  // equal inexact codes: exact remaining CPU (rare)
             const int n0 = cell_node(c0[u]), n1 = cell_node(c1[u]);
             const int e0 = exact_rem(a, n0, w.s), e1 = exact_rem(a, n1, w.s);
             t = (e0 > e1 || (e0 == e1 && n0 < n1)) ? n0 : n1;
@@ -661,7 +663,7 @@ __device__ __forceinline__ void w64_dm(const Tile16Args &a, const W64 &w, cint_p
     }
     const unsigned bk = cell_code(bw);
     int t = Rn == 1 ? cand_node(bw) : (bk >= 2u ? cand_node(bw) : RSK_TARGET_NONE);
-    const bool need = Rn > 1 && bk >= 2u && namb > 1;
+    const bool need = Rn > 1 && code_inexact(bk) && namb > 1;
     if (__builtin_amdgcn_ballot_w64(need)) {  // rare: wave-uniform branch
         Img16 im;
         im.w = reinterpret_cast<const unsigned *>(w.img);
@@ -781,6 +783,7 @@ __global__ __launch_bounds__(kTileThreads, (kHeavy || !kL64) ? RSK_TILE16_WGS_HE
     const int img_off = m[0], nrows = m[1], rec_off = m[2], rec_ints = m[3];
     if (kL64) {
         if (!(a.ablate & 1)) t16_load_image<true, kOff32>(a, img, img_off, nrows, s0);
+        else for (int i = threadIdx.x; i < nrows * 64; i += kTileThreads) img[i] = kCellPad;  // ablation: no loads, no garbage
         W64 w;
         w.img = reinterpret_cast<const char *>(lds);
         w.s = min(s0 + lane, a.S - 1);
@@ -803,6 +806,7 @@ __global__ __launch_bounds__(kTileThreads, (kHeavy || !kL64) ? RSK_TILE16_WGS_HE
             *reinterpret_cast<const int4 *>(a.recs + RSK_B16(rec_off + i + 3, a.n_recs, 16u) - 3);
     }
     if (!(a.ablate & 1)) t16_load_image<false, kOff32>(a, img, img_off, nrows, s0);
+    else for (int i = threadIdx.x; i < (nrows << lsl); i += kTileThreads) img[i] = kCellPad;
 
     Lane16 L;
     L.PS = 64 >> lsl;

@@ -387,3 +387,38 @@ def test_car_score_variant_matches(ctx):
     t0, _ = plan.execute(c.assign, c.S, c.cap_cpu, c.use_cpu, c.hazard, c.N)
     t1, _ = plan.execute(c.assign, c.S, c.cap_cpu, c.use_cpu, c.hazard, c.N, want_score=True)
     assert np.array_equal(t0, t1)
+
+
+@pytest.mark.parametrize("S", [1, 64])
+def test_car_row_above_4096_neighbours(ctx, S):
+    """A deployment related to more than 4096 others: the compact
+    path scores it with the pivot-delta kernel (any degree with min(deg, N)
+    distinct nodes within its LDS table)."""
+    rng = np.random.default_rng(700 + S)
+    P, N = 9000, 300
+    rows = [rng.integers(0, P, int(rng.integers(0, 4))).tolist() for _ in range(P)]
+    rows[0] = rng.choice(np.arange(1, P), 6000, replace=False).tolist()
+    rows[1] = rng.choice(np.arange(2, P), 4500, replace=False).tolist()
+    rp = np.zeros(P + 1, np.int32)
+    rp[1:] = np.cumsum([len(r) for r in rows])
+    ci = np.array([q for r in rows for q in r], np.int32)
+    a = rng.integers(-1, 40, (P, S)).astype(np.int32).reshape(-1)
+    cap = rng.choice([4000, 8000], N).astype(np.int32)
+    use = rng.integers(0, 8000, N * S).astype(np.int32)
+    haz = (rng.random(N * S) < 0.2).astype(np.uint8)
+    _check_car(ctx, rp, ci, a, S, cap, use, haz, N, rows=np.arange(0, 40, dtype=np.int32), label=f"deg>4096 S={S}")
+
+
+def test_car_pivot_kernel_every_side_row():
+    """RSK_PIVOT=1 routes every side row (deg > 32) of the compact path through
+    the pivot-delta kernel: the random-graph, bucket-boundary and collision
+    cases against the oracle (a subprocess: the switch is read once)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, RSK_PIVOT="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", os.path.join(here, "test_gpu_parity.py"),
+                        "-k", "random_graphs or bucket_boundaries or hub_exact or code_collisions or above_4096 or hash_path",
+                        "--timeout", "300"], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
