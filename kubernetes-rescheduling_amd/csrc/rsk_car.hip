@@ -1409,7 +1409,8 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     RSK_CHECK(out_target, "null out_target");
     // compact path (rsk_car16.hip) whenever node ids fit 16 bits
     static const bool compact_ok = env_int("RSK_COMPACT", 1) != 0;
-    const bool compact = N <= kMaxNodes16 && compact_ok;
+    // (S < 2^23: the tile kernel's 24-bit code offsets, rsk_car16.hip t16_rows64)
+    const bool compact = N <= kMaxNodes16 && S < (1 << 23) && compact_ok;
     if (!compact && N >= kPackMaxN && plan->n_sorted_rows > 0) {
         // the wide sorted tile classes pack node << 8 | row into 32 bits: route
         // 17..64 rows through the mid kernel instead (variant built once)
@@ -1441,7 +1442,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         d_key = plan->nodekey.as<int>();
     }
     if (compact) {
-        RSK_TRY(plan->code.reserve(NS * 2));
+        RSK_TRY(plan->code.reserve((NS + (size_t)S) * 2));  // + row N, zeroed by the prep kernel
         d_code = plan->code.as<unsigned short>();
     }
     RSK_TRY(plan->zc.reserve((size_t)S * 12 + 16));

@@ -94,6 +94,10 @@ __global__ __launch_bounds__(256) void car_prep_kernel(const int *__restrict__ c
     for (int i = threadIdx.x; i < nslot * V; i += 256) { lcnt[i] = 0; lkey[i] = 0ull; }
     __syncthreads();
     const int B = kCode ? max(0, lcap - 32766) : 0;
+    if (kCode && t < (unsigned)SV) {  // code row N: code 0 for every scenario (clamped invalid assignments)
+        const unsigned z[V] = {};
+        code[(size_t)N * SV + t] = cvec_make(z);
+    }
     if (t < total) {
         const int sv = (int)(t % (unsigned)SV);
         const int n0 = (int)(t / (unsigned)SV) * npb;
@@ -438,15 +442,20 @@ __device__ __forceinline__ int t16_exact_scan(const Tile16Args &a, const Img16 &
 
 // kL64 phase 1 of one wave: image rows [r0, rend), at most kB of them, lane =
 // scenario.  Rows past rend re-read row rend - 1 (same lines, no LDS write).
+// An assignment outside [0, N) is clamped to node N, whose code row the prep
+// kernel zeroes (code 0: never a candidate), so the cell needs no validity
+// select; the code offset is one 24-bit multiply-add (N <= 65535, 2S < 2^24:
+// rsk_car.hip routes larger S to the wide path).  Lanes past S load scenario
+// S - 1 into columns no scorer reads (W64 columns are clamped).
 template <int kB, bool kOff32>
 __device__ __forceinline__ void t16_rows64(const Tile16Args &a, unsigned *img, int img_off, int r0, int rend, int s0) {
     const unsigned S = (unsigned)a.S, N = (unsigned)a.N;
     const char *__restrict__ asg = reinterpret_cast<const char *>(a.assign);
-    const unsigned short *__restrict__ code = a.code;
+    const char *__restrict__ codeb = reinterpret_cast<const char *>(a.code);
     const int lane = threadIdx.x & 63;
     const int s = s0 + lane;
     const unsigned sl = (unsigned)min(s, (int)S - 1);
-    const bool s_ok = s < (int)S;
+    const unsigned S2 = 2u * S, sl2 = 2u * sl;
     const cint_ptr pods = const_ptr(a.img_pods) + img_off + r0;
     const int nr = rend - r0;  // >= 1 except for waves past the image
     if (nr <= 0) return;
@@ -465,14 +474,17 @@ __device__ __forceinline__ void t16_rows64(const Tile16Args &a, unsigned *img, i
     unsigned cd[kB];
 #pragma unroll
     for (int u = 0; u < kB; ++u) {
-        const bool ok = (unsigned)v[u] < N && s_ok;
-        cd[u] = ld16(code, RSK_B16(ok ? (unsigned)v[u] * S + sl : 0u, a.n_key, 8u));
+        v[u] = (int)min((unsigned)v[u], N);
+        const unsigned off = __umul24((unsigned)v[u], S2) + sl2;
+#ifdef RSK_DEBUG_BOUNDS
+        if (off / 2u >= a.n_key + S) atomicOr(&rsk_dbg16, 8u);
+#endif
+        cd[u] = *reinterpret_cast<const unsigned short *>(codeb + off);
     }
+    unsigned *dst = img + (r0 << 6) + lane;
 #pragma unroll
-    for (int u = 0; u < kB; ++u) {
-        const bool ok = (unsigned)v[u] < N && s_ok;
-        if (u < nr) img[((r0 + u) << 6) + lane] = ok ? ((cd[u] << 16) | (unsigned)v[u]) : kCellPad;
-    }
+    for (int u = 0; u < kB; ++u)
+        if (u < nr) dst[u << 6] = (cd[u] << 16) | (unsigned)v[u];
 }
 
 // Phase 1.  kL64 (t16_rows64): the pod index is wave-uniform (scalar load),
@@ -633,6 +645,14 @@ __device__ __forceinline__ void w64_d2(const Tile16Args &a, const W64 &w, cint_p
 // per node with M + 1 entries.  Running over candidates (code != 0): M, R =
 // nodes at M, the best (code, -node) word among them and how many of them
 // share its code (> 1 with a code >= 2: the rare exact resolution).
+//
+// Fast path first: when no lane of the wave holds two equal cells (distinct
+// pads: kCellPad - i, code 0), every candidate node has count 1, so the answer
+// is the largest candidate word, score 1; only a best code of 1 (None unless a
+// single candidate) or an inexact best code shared by another entry needs a
+// second look (rare, wave-uniform).  The pair tests cost one compare each
+// (lane masks OR-ed on the scalar unit) against compare + add + the running
+// state per entry of the counting walk below.
 template <int D, int W, int kR0, bool kScore, bool kOff32>
 __device__ __forceinline__ void w64_dm(const Tile16Args &a, const W64 &w, cint_ptr R, int j, int s0) {
     const cint_ptr r = R + W * j;
@@ -642,8 +662,41 @@ __device__ __forceinline__ void w64_dm(const Tile16Args &a, const W64 &w, cint_p
     for (int i = 0; i < D; ++i) {
         const unsigned pr = (unsigned)r[kR0 + i / 2];
         const int row = (i & 1) ? (int)(pr >> 16) : (int)(pr & 0xffffu);
-        x[i] = i < d ? w.cell(row) : kCellPad;
+        x[i] = i < d ? w.cell(row) : kCellPad - (unsigned)i;
     }
+    bool dup = false;
+#pragma unroll
+    for (int e = 1; e < D; ++e)
+#pragma unroll
+        for (int h = 0; h < e; ++h) dup |= x[h] == x[e];
+    if (!__builtin_amdgcn_ballot_w64(dup)) {
+        unsigned bw = 0u;
+#pragma unroll
+        for (int e = 0; e < D; ++e) bw = max(bw, cell_cand(x[e]));  // code 0 words stay below every candidate
+        const unsigned bk = cell_code(bw);
+        int t = cand_node(bw);
+        if (__builtin_amdgcn_ballot_w64(bk == kCodeNeg || code_inexact(bk))) {  // rare: wave-uniform branch
+            int rn = 0, nb = 0;
+#pragma unroll
+            for (int e = 0; e < D; ++e) {
+                rn += cell_code(x[e]) != kCodeHaz;
+                nb += cell_code(x[e]) == bk;
+            }
+            if (bk == kCodeNeg && rn > 1) t = RSK_TARGET_NONE;
+            const bool need = code_inexact(bk) && nb > 1;
+            if (__builtin_amdgcn_ballot_w64(need)) {
+                Img16 im;
+                im.w = reinterpret_cast<const unsigned *>(w.img);
+                im.lsl = 6;
+                const int te = t16_exact_scan(a, im, (const int *)(uintptr_t)(r + kR0), d, (int)(w.col4 >> 2), 1, bk, w.s);
+                t = need ? te : t;
+            }
+        }
+        emit64<kScore, kOff32>(a, r[0], s0, w, bk == kCodeHaz ? w.zt : t, bk == kCodeHaz ? w.zs : 1);
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < D; ++i) asm volatile("" : "+v"(x[i]));  // the walk recomputes its compares (no pair masks kept live)
     int M = -1, Rn = 0, namb = 0;
     unsigned bw = 0u;
 #pragma unroll
