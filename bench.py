@@ -262,7 +262,7 @@ def main():
     def step():
         plan.execute(T["assign"], S, T["cap_cpu"], T["use_cpu"], T["hazard"], N, out_t, None, device=True)
 
-    names = ("car_prep", "car_tile", "car_side", "car_mid", "car_heavy", "car_hub128", "car_hub256", "car_hub512",
+    names = ("car_prep", "car_tile", "car_tile_heavy", "car_side", "car_slot", "car_mid", "car_heavy", "car_hub128", "car_hub256", "car_hub512",
              "car_hub1024", "car_hub2048", "car_hub4096")
 
     def collect():

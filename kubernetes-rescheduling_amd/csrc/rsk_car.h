@@ -293,6 +293,7 @@ int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off3
                   size_t lds);
 size_t tile16_lds_bytes(int rmax, int lsl, int rec_cap);
 int launch_pivot(hipStream_t stream, const PivotArgs &a, int max_distinct);
+int launch_slot(hipStream_t stream, const PivotArgs &a, int dmax);  // rsk_slot.hip: degree 33..128, S >= 64
 unsigned tile16_debug_take();
 int tile16_rows_built();       // image rows per tile the compact kernels are compiled for (RSK_TILE16_ROWS)  // debug bounds build: violation flags of the compact kernels (cleared)
 

@@ -766,6 +766,10 @@ struct rsk_car_plan {
     int piv_dmax[kNumPiv] = {};
     DevBuf piv_items[kNumPiv];
     DevBuf pcol;
+    // pivot class 0 (degree 33..128) split for the slot kernel: 33..64, 65..128 (into pcol), degree descending
+    int n_slot[2] = {0, 0};
+    int slot_dmax[2] = {0, 0};
+    DevBuf slot_items[2];
     // per-execute workspace
     DevBuf nodekey, code, zc;
     // the inputs, kept for the N >= kPackMaxN variant (built on first use)
@@ -781,6 +785,7 @@ struct rsk_car_plan {
         for (auto &b : heavy_items) b.release();
         hcol.release();
         for (auto &b : piv_items) b.release();
+        for (auto &b : slot_items) b.release();
         pcol.release();
         nodekey.release();
         code.release();
@@ -1157,6 +1162,17 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
         RSK_TRY(upload(plan->piv_items[c], pitems[c].data(), pitems[c].size() * sizeof(HeavyItem)));
     }
     RSK_TRY(upload(plan->pcol, pcol.data(), pcol.size() * 4));
+    {
+        std::vector<HeavyItem> sl[2];
+        for (const HeavyItem &h : pitems[0])
+            if (h.d <= kPivMax[0]) sl[h.d <= 64 ? 0 : 1].push_back(h);
+        for (int k = 0; k < 2; ++k) {
+            std::stable_sort(sl[k].begin(), sl[k].end(), [](const HeavyItem &x, const HeavyItem &y) { return x.d > y.d; });
+            plan->n_slot[k] = (int)sl[k].size();
+            plan->slot_dmax[k] = sl[k].empty() ? 0 : sl[k][0].d;
+            RSK_TRY(upload(plan->slot_items[k], sl[k].data(), sl[k].size() * sizeof(HeavyItem)));
+        }
+    }
     return RSK_OK;
 }
 
@@ -1215,11 +1231,22 @@ bool pivot_on() {
     return on;
 }
 
-bool plan_side_compact(const rsk_car_plan *plan) {
+// Slot kernel (rsk_slot.hip) for the compact side rows of degree 33..128
+// (mid rows and hub class 0) when S >= 64 and RSK_SLOT=1 (32-bit assign
+// offsets: P * S * 4 < 2^32).  Opt-in: exact, but its per-entry LDS probe
+// chain measured slower than car_mid + hub class 0.
+bool slot_on(const rsk_car_plan *plan, int S) {
+    static const bool on = env_int("RSK_SLOT", 0) != 0;
+    return on && S >= 64 && !pivot_on() && (int64_t)plan->P * S * 4 < ((int64_t)1 << 32);
+}
+
+// Whether the side rows need codes only (no exact node keys from the prep kernel).
+bool plan_side_compact(const rsk_car_plan *plan, int S) {
     if (pivot_on()) return true;
-    for (int c = 0; c < kNumHeavy; ++c)
+    const bool slot = slot_on(plan, S);
+    for (int c = slot ? 1 : 0; c < kNumHeavy; ++c)
         if (plan->n_heavy[c]) return false;
-    return mid16_on() || plan->n_mid[0] + plan->n_mid[1] == 0;
+    return slot || mid16_on() || plan->n_mid[0] + plan->n_mid[1] == 0;
 }
 
 int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t *side, int nside, const SideBufs &b, int S, int N,
@@ -1255,6 +1282,30 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t *side, int n
         }
         if (pivot_on()) return RSK_OK;
     }
+    const bool slot = compact && slot_on(plan, S);
+    if (slot) {  // degree 33..128: slot tables (replaces car_mid and hub class 0)
+        for (int k = 0; k < 2; ++k) {
+            if (!plan->n_slot[k]) continue;
+            PivotArgs a;
+            std::memset(&a, 0, sizeof(a));
+            a.items = plan->slot_items[k].as<HeavyItem>();
+            a.n_items = plan->n_slot[k];
+            a.hcol = plan->pcol.as<int>();
+            a.assign = d_assign;
+            a.code = b.code;
+            a.cap = b.cap;
+            a.use = b.use;
+            a.zc_cnt = d_zcnt;
+            a.zc_key = d_zkey;
+            a.out_target = d_target;
+            a.out_score = d_score;
+            a.S = S;
+            a.N = N;
+            const hipStream_t stream = pick();
+            ScopedTimer tm(ctx, "car_slot", stream);
+            RSK_TRY(launch_slot(stream, a, plan->slot_dmax[k]));
+        }
+    }
     ScoreCtx sc;
     sc.nodekey = d_key;
     sc.zc_cnt = d_zcnt;
@@ -1266,7 +1317,9 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t *side, int n
     const int SL = std::min(S, 64);
     sc.PS = 64 / SL;
     const int64_t chunks = ceil_div(S, SL);
-    if (compact && mid16_on() && plan->n_mid[0] + plan->n_mid[1] > 0) {   // K2 mid rows, codes
+    if (slot) {
+        // mid rows done by the slot kernel
+    } else if (compact && mid16_on() && plan->n_mid[0] + plan->n_mid[1] > 0) {   // K2 mid rows, codes
         Mid16Args a;
         std::memset(&a, 0, sizeof(a));
         for (int k = 0; k < kNumMid; ++k) {
@@ -1309,7 +1362,7 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t *side, int n
             RSK_HIP(hipGetLastError());
         }
     }
-    for (int c = 0; c < kNumHeavy; ++c) {   // K3 hub rows
+    for (int c = slot ? 1 : 0; c < kNumHeavy; ++c) {   // K3 hub rows (class 0 by the slot kernel)
         const int n = plan->n_heavy[c];
         if (!n) continue;
         const hipStream_t stream = pick();
@@ -1437,7 +1490,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     const bool side_rows = plan_has_side(plan);
     int *d_key = nullptr;
     unsigned short *d_code = nullptr;
-    if (!compact || (side_rows && !plan_side_compact(plan))) {
+    if (!compact || (side_rows && !plan_side_compact(plan, S))) {
         RSK_TRY(plan->nodekey.reserve(NS * 4));
         d_key = plan->nodekey.as<int>();
     }
@@ -1521,11 +1574,14 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         a.img_cells = (plan->rmax * SL + 3) & ~3;
         const size_t lds = tile16_lds_bytes(plan->rmax, a.lsl, a.rec_cap);
         RSK_CHECK(plan->recmax <= kTileRecInts, "tile records exceed %d ints", kTileRecInts);
-        ScopedTimer tm(ctx, "car_tile");
+        // one timer over both launches; RSK_TILE_TIMERS=1: car_tile (lean) and car_tile_heavy apart
+        static const bool split = env_int("RSK_TILE_TIMERS", 0) != 0;
+        std::unique_ptr<ScopedTimer> tm(split ? nullptr : new ScopedTimer(ctx, "car_tile"));
         // lean tiles [0, T_lean) at full occupancy, then the heavy tiles (17..32 rows)
         for (int part = 0; part < 2; ++part) {
             const int t0 = part ? plan->T_lean : 0, nt = part ? plan->T - plan->T_lean : plan->T_lean;
             if (nt <= 0) continue;
+            std::unique_ptr<ScopedTimer> tp(split ? new ScopedTimer(ctx, part ? "car_tile_heavy" : "car_tile") : nullptr);
             a.tile0 = t0;
             a.T = nt;
             const int64_t units = ceil_div(S, SL) * nt;

@@ -422,3 +422,33 @@ def test_car_pivot_kernel_every_side_row():
                         "-k", "random_graphs or bucket_boundaries or hub_exact or code_collisions or above_4096 or hash_path",
                         "--timeout", "300"], env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+def test_car_slot_table_overflow(ctx):
+    """Rows of degree 33..128 at S >= 64 with every scenario drawing fresh
+    nodes out of 5000: thousands of distinct nodes per row and 64-scenario
+    chunk (with RSK_SLOT=1 the slot table fills and the lanes that could not
+    insert recount exactly; by default car_mid / hub class 0)."""
+    rng = np.random.default_rng(800)
+    P, N, S = 3000, 5000, 128
+    rp, ci, a, cap, use, haz = _random_case(rng, P, N, S, max_deg=3, hub_deg=[33, 50, 64, 65, 100, 128], p_haz=0.1)
+    _check_car(ctx, rp, ci, a, S, cap, use, haz, N, rows=np.arange(0, 40, dtype=np.int32), label="slot overflow")
+    a2 = a.reshape(P, S).copy()
+    a2[:, ::2] = a2[:, :1]            # half the scenarios share scenario 0's nodes: tables near the degree
+    _check_car(ctx, rp, ci, a2.reshape(-1), S, cap, use, haz, N, rows=np.arange(0, 40, dtype=np.int32),
+               label="slot mixed")
+
+
+def test_car_slot_kernel_side_rows():
+    """RSK_SLOT=1 routes degree 33..128 through the slot-table kernel
+    (rsk_slot.hip) instead of car_mid / hub class 0: the same oracle cases,
+    including the table overflow above (a subprocess: the switch is read once)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, RSK_SLOT="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", os.path.join(here, "test_gpu_parity.py"),
+                        "-k", "random_graphs or bucket_boundaries or code_collisions or invalid_assign or slot_table",
+                        "--timeout", "300"], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
