@@ -211,6 +211,8 @@ def main():
                     help="multi-GPU layout (SURVEY §8e): scenario sharding (default; 1m50k: rows)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--row-rounds", type=int, default=20,
+                    help="pod-row sharding: rounds of the row-sharded multi-round loop to time (0: skip)")
     ap.add_argument("--no-kernel-events", action="store_true", default=os.environ.get("RSK_BENCH_NO_EVENTS") == "1",
                     help="time the steps without per-kernel HIP events")
     ap.add_argument("--pmc-json", default=PMC_JSON,
@@ -342,6 +344,39 @@ def main():
                      threads=min(16, os.cpu_count() or 1))
     parity_ok = bool(np.array_equal(got, exp))
 
+    rounds_leg = None
+    if by_rows and args.row_rounds > 0:
+        # the pod-row-sharded multi-round loop (rsk/dist.py RowShardedRounds): per
+        # round an int64 all-reduce of the N*S CPU / mem partials, a MAX
+        # all-reduce of the eviction key, the all-gather of changed slices and
+        # the cut-cost all-reduce, around librsk's kernels on this rank's rows
+        be = rdist.LibrskRoundsBackend(c.row_ptr, c.col_idx, c.pod_cpu, ctx=ctx, device=dev)
+        rr = rdist.RowShardedRounds(rshard, be)
+        a2 = T["assign"].clone()
+        pc = torch.from_numpy(c.pod_cpu).to(dev)
+        pm = torch.full((P,), 1 << 28, dtype=torch.int64, device=dev)   # synthetic 256 MiB per pod
+        thr = 90   # the synthetic nodes run at 57-98 % CPU: only the hottest are hazards, so pods move
+        rr.run(a2, T["use_cpu"], T["cap_cpu"], pc, pm, N, S, 1, threshold=thr)   # warm-up round
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        res = rr.run(a2, T["use_cpu"], T["cap_cpu"], pc, pm, N, S, args.row_rounds, threshold=thr)
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t1
+        if world > 1:
+            e = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            el = float(e.item())
+        R = args.row_rounds
+        rounds_leg = {"rounds": R, "threshold_pct": thr, "ms_per_round": round(el * 1e3 / R, 4),
+                      "phase_ms_per_round": {k: round(v / R, 4) for k, v in res["ms"].items()},
+                      "scoring_only_ms_per_round": round(res["ms"]["place"] / R, 4),
+                      "moves": int((res["target"] >= 0).sum().item()),
+                      "collectives": "int64 all-reduce N*S cpu + mem partials, int64 MAX all-reduce S, "
+                                     "all-gather S changed slices, int64 all-reduce S cut cost"}
+        be.close()
+
     alg = {k: alg_bytes(k, P, N, S, info) for k in kernels}
     B = algorithmic_bytes(P, N, S, c.nnz)
     roof = None
@@ -405,6 +440,9 @@ def main():
         }
         if by_rows:
             line["rows_per_rank"] = Q
+            line["roofline_scope"] = ("rank 0's rows: the plan's distinct neighbour pods of its row range "
+                                      "(SURVEY §8e per-rank distinct-column roofline)")
+            line["row_sharded_rounds"] = rounds_leg
             line["allgather_ms_per_step"] = None if gather_ms is None else round(gather_ms, 4)
             line["end_to_end_ms_per_step"] = round(ms_step + (gather_ms or 0.0), 4)
         print(json.dumps(line), flush=True)

@@ -155,6 +155,12 @@ int rsk_cut_cost(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, i
                  uint32_t flags);
 int rsk_pick_max_pod(rsk_ctx *ctx, const int32_t *assign, const int32_t *pod_cpu, int32_t P, int32_t S,
                      const int32_t *most, int32_t *out_pod, uint32_t flags);
+/* rsk_cut_cost over rows [r0, r1) only (pod-row sharding, SURVEY §8e: each
+ * rank's partial of communicationcost.py:37-45; neighbours read from the full
+ * assign).  row_ptr / col_idx / assign are the full P-row arrays.            */
+int rsk_cut_cost_rows(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, int32_t P, int32_t r0,
+                      int32_t r1, const int32_t *assign, int32_t S, const int32_t *missing,
+                      int64_t *out_directed, uint32_t flags);
 
 /* ---- multi-round loop --------------------
  * The reference's control loop (main.py:55-110) for S independent scenarios,
@@ -178,6 +184,13 @@ int rsk_rounds_destroy(rsk_rounds *r);
 int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap_cpu, int32_t *use_cpu,
                    int32_t N, int32_t threshold, int32_t R, int32_t *out_evict, int32_t *out_target,
                    uint32_t flags);
+/* One round's placement step alone (the pod-row-sharded loop, rsk/dist.py
+ * RowShardedRounds): out_target[s] = the CAR target of pod evict[s] against
+ * assign / use_cpu / hazard (as rsk_rounds_run computes it), no state update;
+ * RSK_TARGET_NO_EVICT where evict[s] < 0.                                    */
+int rsk_rounds_place(rsk_rounds *r, const int32_t *assign, int32_t S, const int32_t *cap_cpu,
+                     const int32_t *use_cpu, const uint8_t *hazard, int32_t N, const int32_t *evict,
+                     int32_t *out_target, uint32_t flags);
 
 /* ---- µBench workmodel -> relation CSR (host only, no device) -----------------
  * The caller's on-disk format (workmodelC.json).  One

@@ -313,14 +313,15 @@ __global__ void std_merge_kernel(const double *__restrict__ pmean, const double 
 }
 
 // communicationcost.py:37-45: directed count of related pairs on different nodes.
+// rows [r0, r1) of the CSR; neighbours read from the full assign
 __global__ __launch_bounds__(256) void cut_cost_kernel(const int *__restrict__ row_ptr, const int *__restrict__ col,
-                                                       int P, const int *__restrict__ assign, int S,
+                                                       int r0, int r1, const int *__restrict__ assign, int S,
                                                        const int *__restrict__ missing, int ppt, unsigned total,
                                                        unsigned long long *__restrict__ out) {
     const unsigned t = blockIdx.x * 256u + threadIdx.x;
     if (t >= total) return;
     const int s = (int)(t % (unsigned)S);
-    const int p0 = (int)(t / (unsigned)S) * ppt, p1 = min(P, p0 + ppt);
+    const int p0 = r0 + (int)(t / (unsigned)S) * ppt, p1 = min(r1, p0 + ppt);
     unsigned long long c = 0;
     for (int p = p0; p < p1; ++p) {
         const int a = assign[(size_t)p * S + s];
@@ -643,18 +644,16 @@ int rsk_load_std(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *cap_cpu, i
 
 int rsk_cut_cost(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, int32_t P, const int32_t *assign,
                  int32_t S, const int32_t *missing, int64_t *out_directed, uint32_t flags) {
+    return rsk_cut_cost_rows(ctx, row_ptr, col_idx, P, 0, P, assign, S, missing, out_directed, flags);
+}
+
+int rsk_cut_cost_rows(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, int32_t P, int32_t r0,
+                      int32_t r1, const int32_t *assign, int32_t S, const int32_t *missing, int64_t *out_directed,
+                      uint32_t flags) {
     RSK_TRY(activate(ctx));
-    RSK_CHECK(P >= 0 && S > 0 && row_ptr && out_directed, "bad arguments");
+    RSK_CHECK(P >= 0 && S > 0 && row_ptr && out_directed && 0 <= r0 && r0 <= r1 && r1 <= P, "bad arguments");
     const bool dev = flags & RSK_F_DEVICE;
-    int64_t nnz = 0;
-    if (dev) {
-        int32_t last = 0;
-        RSK_HIP(hipMemcpyAsync(&last, row_ptr + P, 4, hipMemcpyDeviceToHost, ctx->stream));
-        RSK_HIP(hipStreamSynchronize(ctx->stream));
-        nnz = last;
-    } else {
-        nnz = row_ptr[P];
-    }
+    const int64_t nnz = dev ? 0 : row_ptr[P];  // device pointers pass through unstaged
     const int *d_rp, *d_col, *d_assign, *d_miss = nullptr;
     int64_t *d_out;
     RSK_TRY(stage_in(ctx, 0, row_ptr, (size_t)(P + 1) * 4, dev, reinterpret_cast<const void **>(&d_rp)));
@@ -663,13 +662,14 @@ int rsk_cut_cost(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, i
     if (missing) RSK_TRY(stage_in(ctx, 3, missing, (size_t)P * 4, dev, reinterpret_cast<const void **>(&d_miss)));
     RSK_TRY(stage_out(ctx, 4, out_directed, (size_t)S * 8, dev, reinterpret_cast<void **>(&d_out)));
     RSK_HIP(hipMemsetAsync(d_out, 0, (size_t)S * 8, ctx->stream));
-    if (P > 0) {
-        const int ppt = chunk_for(P, S);
-        const int64_t tot = ceil_div(P, ppt) * S;
+    if (r1 > r0) {
+        const int Q = r1 - r0;
+        const int ppt = chunk_for(Q, S);
+        const int64_t tot = ceil_div(Q, ppt) * S;
         RSK_CHECK(tot < INT32_MAX, "grid too large");
         ScopedTimer tm(ctx, "cut_cost");
         cut_cost_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, ctx->stream>>>(
-            d_rp, d_col, P, d_assign, S, d_miss, ppt, (unsigned)tot, reinterpret_cast<unsigned long long *>(d_out));
+            d_rp, d_col, r0, r1, d_assign, S, d_miss, ppt, (unsigned)tot, reinterpret_cast<unsigned long long *>(d_out));
         RSK_HIP(hipGetLastError());
     }
     if (!dev) {

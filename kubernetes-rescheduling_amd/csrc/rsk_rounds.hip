@@ -57,7 +57,7 @@ __global__ __launch_bounds__(kMoveThreads) void car_move_kernel(const int *__res
                                                                 int *use, const int *__restrict__ cap,
                                                                 const uint8_t *__restrict__ haz,
                                                                 const int *__restrict__ evict, int S, int N, int H,
-                                                                int *__restrict__ out_target) {
+                                                                int update, int *__restrict__ out_target) {
     extern __shared__ __attribute__((aligned(16))) unsigned lds[];
     unsigned *keys = lds, *cnts = lds + H;
     unsigned long long *red64 = reinterpret_cast<unsigned long long *>(lds + 2 * H);  // best
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(kMoveThreads) void car_move_kernel(const int *__res
         else if (nbest == 1) t = node;                // the single best, even if overloaded
         else t = rem >= 0 ? node : RSK_TARGET_NONE;   // largest remaining CPU, None if < 0
         out_target[s] = t;
-        if (t >= 0) {  // build-defined update: the pod's CPU moves with it
+        if (update && t >= 0) {  // build-defined update: the pod's CPU moves with it
             const size_t pc = (size_t)p * S + s;
             const int old = assign[pc], c = pod_cpu[p];
             if ((unsigned)old < (unsigned)N) use[(size_t)old * S + s] -= c;
@@ -146,6 +146,27 @@ int next_pow2(int x) {
     int p = 1;
     while (p < x) p <<= 1;
     return p;
+}
+
+struct MoveGeom {
+    int H;
+    size_t lds;
+    int rc;
+};
+
+MoveGeom move_geometry(const rsk_rounds *r) {
+    MoveGeom g;
+    g.H = next_pow2(std::max(2, 2 * r->dmax));
+    g.lds = ((size_t)2 * g.H + 8) * 4;
+    g.rc = RSK_OK;
+    if (g.lds > 160 * 1024) { set_error("rounds hash needs %zu B of LDS", g.lds); g.rc = RSK_EINVAL; return g; }
+    if (g.lds > 64 * 1024 &&
+        hipFuncSetAttribute(reinterpret_cast<const void *>(&car_move_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)g.lds) != hipSuccess) {
+        set_error("hipFuncSetAttribute failed");
+        g.rc = RSK_EHIP;
+    }
+    return g;
 }
 
 }  // namespace
@@ -227,12 +248,10 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
     RSK_TRY(r->haz.reserve(NS));
     RSK_TRY(r->most.reserve((size_t)S * 4));
     RSK_TRY(r->key_ws.reserve((size_t)S * 8));
-    const int H = next_pow2(std::max(2, 2 * r->dmax));
-    const size_t lds = ((size_t)2 * H + 8) * 4;
-    RSK_CHECK(lds <= 160 * 1024, "rounds hash needs %zu B of LDS", lds);
-    if (lds > 64 * 1024)
-        RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&car_move_kernel),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const MoveGeom g = move_geometry(r);
+    RSK_TRY(g.rc);
+    const int H = g.H;
+    const size_t lds = g.lds;
     for (int round = 0; round < R; ++round) {
         int *ev = d_evict + (size_t)round * S;
         {
@@ -250,7 +269,7 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
             ScopedTimer tm(ctx, "rounds_move");
             car_move_kernel<<<dim3((unsigned)S), dim3(kMoveThreads), lds, st>>>(
                 r->row_ptr.as<int>(), r->col.as<int>(), r->pod_cpu.as<int>(), d_assign, d_use, d_cap,
-                r->haz.as<uint8_t>(), ev, S, N, H, d_target + (size_t)round * S);
+                r->haz.as<uint8_t>(), ev, S, N, H, 1, d_target + (size_t)round * S);
             RSK_HIP(hipGetLastError());
         }
     }
@@ -262,6 +281,41 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
             RSK_TRY(copy_back(ctx, out_target, d_target, RS * 4, false));
         }
         RSK_HIP(hipStreamSynchronize(st));
+    }
+    return RSK_OK;
+}
+
+int rsk_rounds_place(rsk_rounds *r, const int32_t *assign, int32_t S, const int32_t *cap_cpu, const int32_t *use_cpu,
+                     const uint8_t *hazard, int32_t N, const int32_t *evict, int32_t *out_target, uint32_t flags) {
+    RSK_CHECK(r, "null rounds object");
+    rsk_ctx *ctx = r->ctx;
+    RSK_TRY(activate(ctx));
+    RSK_CHECK(assign && cap_cpu && use_cpu && hazard && evict && out_target, "null argument");
+    RSK_CHECK(S > 0 && N > 0 && (int64_t)N * S < INT32_MAX && (int64_t)r->P * S < INT32_MAX, "bad sizes S=%d N=%d", S,
+              N);
+    const bool dev = flags & RSK_F_DEVICE;
+    const size_t NS = (size_t)N * S, PS = (size_t)r->P * S;
+    const int *d_assign, *d_cap, *d_use, *d_evict;
+    const uint8_t *d_haz;
+    int *d_target;
+    RSK_TRY(stage_in(ctx, 0, assign, std::max<size_t>(PS, 1) * 4, dev, reinterpret_cast<const void **>(&d_assign)));
+    RSK_TRY(stage_in(ctx, 1, use_cpu, NS * 4, dev, reinterpret_cast<const void **>(&d_use)));
+    RSK_TRY(stage_in(ctx, 2, cap_cpu, (size_t)N * 4, dev, reinterpret_cast<const void **>(&d_cap)));
+    RSK_TRY(stage_in(ctx, 3, hazard, NS, dev, reinterpret_cast<const void **>(&d_haz)));
+    RSK_TRY(stage_in(ctx, 5, evict, (size_t)S * 4, dev, reinterpret_cast<const void **>(&d_evict)));
+    RSK_TRY(stage_out(ctx, 4, out_target, (size_t)S * 4, dev, reinterpret_cast<void **>(&d_target)));
+    const MoveGeom g = move_geometry(r);
+    RSK_TRY(g.rc);
+    {
+        ScopedTimer tm(ctx, "rounds_place");
+        car_move_kernel<<<dim3((unsigned)S), dim3(kMoveThreads), g.lds, ctx->stream>>>(
+            r->row_ptr.as<int>(), r->col.as<int>(), r->pod_cpu.as<int>(), const_cast<int *>(d_assign),
+            const_cast<int *>(d_use), d_cap, d_haz, d_evict, S, N, g.H, 0, d_target);
+        RSK_HIP(hipGetLastError());
+    }
+    if (!dev) {
+        RSK_TRY(copy_back(ctx, out_target, d_target, (size_t)S * 4, false));
+        RSK_HIP(hipStreamSynchronize(ctx->stream));
     }
     return RSK_OK;
 }

@@ -128,6 +128,22 @@ class Rounds:
                                           ptr(ev), ptr(tg), 0))
         return ev[:R * S], tg[:R * S]
 
+    def place(self, assign, S, cap_cpu, use_cpu, hazard, N, evict, out_target=None, device: bool = False):
+        """One round's placement step alone (rsk_rounds_place): the CAR target of
+        pod evict[s] per scenario, no state update; RSK_TARGET_NO_EVICT (-3)
+        where evict[s] < 0."""
+        if device:
+            check(self.ctx.lib.rsk_rounds_place(self.handle, ptr(assign), S, ptr(cap_cpu), ptr(use_cpu), ptr(hazard), N,
+                                                ptr(evict), ptr(out_target), RSK_F_DEVICE))
+            return out_target
+        a, c, u = _c(assign, _I32), _c(cap_cpu, _I32), _c(use_cpu, _I32)
+        h, e = _c(hazard, np.uint8), _c(evict, _I32)
+        if a.size != self.P * S or c.size != N or u.size != N * S or h.size != N * S or e.size != S:
+            raise ValueError("array sizes do not match P, N, S")
+        out = np.empty(S, _I32)
+        check(self.ctx.lib.rsk_rounds_place(self.handle, ptr(a), S, ptr(c), ptr(u), ptr(h), N, ptr(e), ptr(out), 0))
+        return out
+
     def close(self):
         if getattr(self, "handle", None):
             self.ctx.lib.rsk_rounds_destroy(self.handle)
@@ -239,6 +255,19 @@ def cut_cost(row_ptr, col_idx, assign, P, S, missing=None, ctx=None):
     m = None if missing is None else _c(missing, _I32)
     out = np.empty(S, np.int64)
     check(ctx.lib.rsk_cut_cost(ctx.handle, ptr(rp), ptr(col), P, ptr(a), S, ptr(m), ptr(out), 0))
+    return out
+
+
+def cut_cost_rows(row_ptr, col_idx, assign, P, S, r0, r1, missing=None, ctx=None):
+    """Directed cut count per scenario over CSR rows [r0, r1) (one rank's
+    partial under pod-row sharding); neighbours read from the full assign."""
+    ctx = ctx or default_context()
+    rp = _c(row_ptr, _I32)
+    col = _c(col_idx, _I32) if len(col_idx) else np.zeros(1, _I32)
+    a = _c(assign, _I32)
+    m = None if missing is None else _c(missing, _I32)
+    out = np.empty(S, np.int64)
+    check(ctx.lib.rsk_cut_cost_rows(ctx.handle, ptr(rp), ptr(col), P, r0, r1, ptr(a), S, ptr(m), ptr(out), 0))
     return out
 
 

@@ -118,3 +118,212 @@ def gather_rows(local, shard: RowShard, S: int, group=None):
     parts = [torch.empty_like(buf) for _ in range(shard.world)]
     dist.all_gather(parts, buf, group=group)
     return torch.cat([parts[k][: (b[k + 1] - b[k]) * S] for k in range(shard.world)])
+
+
+# ---------------------------------------------------------------------------
+# Pod-row-sharded multi-round loop (SURVEY.md §8e pod-row sharding x §8f item 1)
+# ---------------------------------------------------------------------------
+# The reference's loop, per scenario (main.py:56-101): monitor -> detection ->
+# pod_delete (pick_max_pod) -> edit_cluster -> communication (CAR) -> the next
+# round re-monitors the live cluster.  Rank r owns pod rows [r0, r1) (balanced
+# by nnz, ``row_shard_for``) and keeps the full assign[P*S] replica; per round:
+#
+#   monitor   per-node CPU / mem of the pods in its rows (rsk_node_reduce on
+#             its row slice) -> int64 all-reduce SUM of the N*S partials;
+#             use = base + CPU sums, base = the usage no pod accounts for
+#             (use0 minus the round-0 sums, fixed)
+#   detect    cpu_pct -> hazard / most hazardous node, replicated (N*S, tiny)
+#   evict     its rows' first max-CPU pod on most[s] (rsk_pick_max_pod on the
+#             slice), packed (cpu, -pod) -> int64 all-reduce MAX over S
+#   place     the CAR target of the evicted pod, by the rank owning its row
+#             (rsk_rounds_place), then an all-gather of every rank's changed
+#             slice (target per scenario, RSK_TARGET_NO_EVICT where not its
+#             pod) -> the element-wise max is the round's move
+#   update    assign[p_s, s] = t_s on every replica (the pod moves when
+#             t_s >= 0; its CPU moves with it through the next monitor)
+#   cut cost  directed cut over its rows (rsk_cut_cost_rows) -> int64
+#             all-reduce SUM over S (communicationcost.py:37-45, /2 there)
+#
+# Integer sums make the recomputed usage equal the single-process loop's
+# incremental update exactly, so the result is bit-equal to rsk_rounds_run /
+# oracle_rounds (tests/test_dist_rounds.py).  The per-rank compute goes through
+# a backend object: ``LibrskRoundsBackend`` (librsk on the rank's GPU, device
+# pointers) is the product path; tests supply a CPU backend for gloo runs on
+# machines without a GPU.
+
+NO_EVICT = -3
+
+
+def _coll_tensor(t):
+    """(tensor to hand to the collective, copy-back needed): gloo takes host tensors."""
+    import torch.distributed as dist
+    if t.is_cuda and dist.get_backend() == "gloo":
+        return t.cpu(), True
+    return t, False
+
+
+def allreduce_(t, op="sum", group=None):
+    """In-place all-reduce of t (SUM or MAX) on whatever device the backend needs."""
+    import torch.distributed as dist
+    red = dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX
+    x, back = _coll_tensor(t)
+    dist.all_reduce(x, op=red, group=group)
+    if back:
+        t.copy_(x)
+    return t
+
+
+def allgather(t, group=None):
+    """[world, *t.shape] stack of every rank's t."""
+    import torch
+    import torch.distributed as dist
+    x, back = _coll_tensor(t.contiguous())
+    parts = [torch.empty_like(x) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(parts, x, group=group)
+    out = torch.stack(parts)
+    return out.to(t.device) if back else out
+
+
+class LibrskRoundsBackend:
+    """Per-rank compute of the row-sharded loop on librsk (device pointers on the
+    rank's GPU; every call is asynchronous on the context's stream, which is the
+    current torch stream's device)."""
+
+    def __init__(self, row_ptr, col_idx, pod_cpu, ctx=None, device=None):
+        import numpy as np
+        import torch
+        from . import api
+        from ._lib import RSK_F_DEVICE, check, default_context
+        self.ctx = ctx or default_context()
+        self.dev = torch.device(device or "cuda")
+        self.rounds = api.Rounds(row_ptr, col_idx, pod_cpu, ctx=self.ctx)   # deduplicated CSR for the CAR step
+        rp = np.ascontiguousarray(row_ptr, np.int32)
+        ci = np.ascontiguousarray(col_idx if len(col_idx) else [0], np.int32)
+        self.row_ptr = torch.from_numpy(rp).to(self.dev)
+        self.col_idx = torch.from_numpy(ci).to(self.dev)
+        self.P = rp.shape[0] - 1
+        self._F, self._check = RSK_F_DEVICE, check
+
+    def _sync(self):
+        import torch
+        torch.cuda.synchronize(self.dev)
+
+    def node_partials(self, assign_rows, pod_cpu_rows, pod_mem_rows, q, N, S):
+        import torch
+        cpu = torch.empty(N * S, dtype=torch.int64, device=self.dev)
+        mem = torch.empty(N * S, dtype=torch.int64, device=self.dev)
+        self._check(self.ctx.lib.rsk_node_reduce(self.ctx.handle, assign_rows.data_ptr(), q, S,
+                                                 pod_cpu_rows.data_ptr(), pod_mem_rows.data_ptr(), N, None,
+                                                 cpu.data_ptr(), mem.data_ptr(), self._F))
+        self._sync()
+        return cpu, mem
+
+    def detect(self, use, cap, N, S, threshold):
+        import torch
+        pct = torch.empty(N * S, dtype=torch.int32, device=self.dev)
+        haz = torch.empty(N * S, dtype=torch.uint8, device=self.dev)
+        most = torch.empty(S, dtype=torch.int32, device=self.dev)
+        L, h = self.ctx.lib, self.ctx.handle
+        self._check(L.rsk_cpu_pct(h, use.data_ptr(), cap.data_ptr(), N, S, pct.data_ptr(), self._F))
+        self._check(L.rsk_detect(h, pct.data_ptr(), N, S, threshold, haz.data_ptr(), most.data_ptr(), self._F))
+        self._sync()
+        return haz, most
+
+    def pick_rows(self, assign_rows, pod_cpu_rows, q, S, most):
+        import torch
+        out = torch.empty(S, dtype=torch.int32, device=self.dev)
+        self._check(self.ctx.lib.rsk_pick_max_pod(self.ctx.handle, assign_rows.data_ptr(), pod_cpu_rows.data_ptr(), q,
+                                                  S, most.data_ptr(), out.data_ptr(), self._F))
+        self._sync()
+        return out
+
+    def place(self, assign, S, cap, use, haz, N, evict):
+        import torch
+        out = torch.empty(S, dtype=torch.int32, device=self.dev)
+        self.rounds.place(assign, S, cap, use, haz, N, evict, out, device=True)
+        self._sync()
+        return out
+
+    def cut_rows(self, assign, S, r0, r1):
+        import torch
+        out = torch.empty(S, dtype=torch.int64, device=self.dev)
+        self._check(self.ctx.lib.rsk_cut_cost_rows(self.ctx.handle, self.row_ptr.data_ptr(), self.col_idx.data_ptr(),
+                                                   self.P, r0, r1, assign.data_ptr(), S, None, out.data_ptr(),
+                                                   self._F))
+        self._sync()
+        return out
+
+    def close(self):
+        self.rounds.close()
+
+
+class RowShardedRounds:
+    """R rounds of the loop above for S scenarios over this rank's pod rows.
+
+    ``run(assign, use0, cap, pod_cpu, pod_mem, N, R)`` takes full-size tensors on
+    the backend's device (the assign replica is updated in place) and returns a
+    dict: evict / target / cut as [R, S] tensors (cut = directed count after the
+    round's move), the final use [N*S] int32, and per-phase wall times (ms,
+    summed over rounds; "place" is the scoring-only leg)."""
+
+    def __init__(self, shard: RowShard, backend, group=None):
+        self.shard, self.be, self.group = shard, backend, group
+
+    def _partials(self, assign, pod_cpu, pod_mem, N, S):
+        r0, r1 = self.shard.r0, self.shard.r1
+        q = r1 - r0
+        cpu, mem = self.be.node_partials(assign[r0 * S:r1 * S], pod_cpu[r0:r1], pod_mem[r0:r1], q, N, S)
+        allreduce_(cpu, "sum", self.group)
+        allreduce_(mem, "sum", self.group)
+        return cpu, mem
+
+    def run(self, assign, use0, cap, pod_cpu, pod_mem, N, S, R, threshold=30):
+        import time
+        import torch
+        dev = assign.device
+        r0, r1 = self.shard.r0, self.shard.r1
+        t = {"monitor": 0.0, "detect": 0.0, "evict": 0.0, "place": 0.0, "exchange": 0.0, "update": 0.0, "cut": 0.0}
+
+        def tick(name, t0):
+            t[name] += (time.perf_counter() - t0) * 1e3
+            return time.perf_counter()
+
+        cpu0, _ = self._partials(assign, pod_cpu, pod_mem, N, S)
+        base = use0.to(torch.int64) - cpu0            # usage no pod accounts for
+        evs, tgs, cuts = [], [], []
+        sidx = torch.arange(S, device=dev)
+        pc64 = pod_cpu.to(torch.int64)
+        mask32 = (1 << 32) - 1
+        for _ in range(R):
+            c = time.perf_counter()
+            cpu, mem = self._partials(assign, pod_cpu, pod_mem, N, S)
+            use = (base + cpu).to(torch.int32)
+            c = tick("monitor", c)
+            haz, most = self.be.detect(use, cap, N, S, threshold)
+            c = tick("detect", c)
+            loc = self.be.pick_rows(assign[r0 * S:r1 * S], pod_cpu[r0:r1], r1 - r0, S, most).to(torch.int64)
+            gp = torch.where(loc >= 0, loc + r0, torch.zeros_like(loc))
+            key = torch.where(loc >= 0, (pc64[gp] << 32) | (mask32 - gp), torch.full_like(loc, -1))
+            allreduce_(key, "max", self.group)
+            evict = torch.where(key >= 0, mask32 - (key & mask32), torch.full_like(key, -1)).to(torch.int32)
+            c = tick("evict", c)
+            mine = (evict >= r0) & (evict < r1)
+            tgt_local = self.be.place(assign, S, cap, use, haz, N, torch.where(mine, evict, torch.full_like(evict, -1)))
+            c = tick("place", c)
+            target = allgather(tgt_local, self.group).max(dim=0).values   # changed slices of every rank
+            c = tick("exchange", c)
+            moved = (evict >= 0) & (target >= 0)
+            av = assign.view(-1, S)
+            av[evict[moved].long(), sidx[moved]] = target[moved]
+            c = tick("update", c)
+            cut = self.be.cut_rows(assign, S, r0, r1)
+            allreduce_(cut, "sum", self.group)
+            tick("cut", c)
+            evs.append(evict)
+            tgs.append(target)
+            cuts.append(cut)
+        cpu, _ = self._partials(assign, pod_cpu, pod_mem, N, S)
+        use_final = (base + cpu).to(torch.int32)
+        empty = torch.empty(0, S, dtype=torch.int32, device=dev)
+        return {"evict": torch.stack(evs) if evs else empty, "target": torch.stack(tgs) if tgs else empty,
+                "cut": torch.stack(cuts) if cuts else empty.to(torch.int64), "use": use_final, "ms": t}

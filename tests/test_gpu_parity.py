@@ -452,3 +452,18 @@ def test_car_slot_kernel_side_rows():
                         "-k", "random_graphs or bucket_boundaries or code_collisions or invalid_assign or slot_table",
                         "--timeout", "300"], env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+def test_cut_cost_rows_partition_sums_to_full(ctx):
+    """rsk_cut_cost_rows over a partition of the rows sums to rsk_cut_cost and
+    to the oracle (the row-sharded cut-cost partials)."""
+    from oracle import oracle as orc
+    from rsk import api
+    rng = np.random.default_rng(900)
+    P, N, S = 700, 40, 9
+    rp, ci, a, _, _, _ = _random_case(rng, P, N, S, max_deg=6, hub_deg=[30, 90])
+    full = api.cut_cost(rp, ci, a, P, S, ctx=ctx)
+    assert np.array_equal(full, orc.cut_cost(rp, ci, a, P, S))
+    cuts = [0, 1, 250, 251, 699, 700]
+    parts = sum(api.cut_cost_rows(rp, ci, a, P, S, cuts[k], cuts[k + 1], ctx=ctx) for k in range(len(cuts) - 1))
+    assert np.array_equal(parts, full)
