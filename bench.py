@@ -355,7 +355,7 @@ def main():
         a2 = T["assign"].clone()
         pc = torch.from_numpy(c.pod_cpu).to(dev)
         pm = torch.full((P,), 1 << 28, dtype=torch.int64, device=dev)   # synthetic 256 MiB per pod
-        thr = 90   # the synthetic nodes run at 57-98 % CPU: only the hottest are hazards, so pods move
+        thr = 40   # the synthetic nodes run at 2-43 % CPU: only the hottest are hazards, so pods move
         rr.run(a2, T["use_cpu"], T["cap_cpu"], pc, pm, N, S, 1, threshold=thr)   # warm-up round
         torch.cuda.synchronize(dev)
         if world > 1:

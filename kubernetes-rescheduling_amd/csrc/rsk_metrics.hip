@@ -312,23 +312,47 @@ __global__ void std_merge_kernel(const double *__restrict__ pmean, const double 
     out[s] = n ? sqrt(m2 / (double)n) : 0.0;
 }
 
+constexpr int kCutBins = 64;
+
 // communicationcost.py:37-45: directed count of related pairs on different nodes.
 // rows [r0, r1) of the CSR; neighbours read from the full assign
 __global__ __launch_bounds__(256) void cut_cost_kernel(const int *__restrict__ row_ptr, const int *__restrict__ col,
                                                        int r0, int r1, const int *__restrict__ assign, int S,
                                                        const int *__restrict__ missing, int ppt, unsigned total,
                                                        unsigned long long *__restrict__ out) {
+    // thread i of the block holds scenario (b0 + i) % S: threads with equal i mod
+    // min(S, 256) share a scenario, so their counts meet in one LDS slot and the
+    // block issues at most 256 global atomics (not one per thread)
+    __shared__ unsigned long long red[256];
+    red[threadIdx.x] = 0ull;
+    __syncthreads();
     const unsigned t = blockIdx.x * 256u + threadIdx.x;
-    if (t >= total) return;
-    const int s = (int)(t % (unsigned)S);
-    const int p0 = r0 + (int)(t / (unsigned)S) * ppt, p1 = min(r1, p0 + ppt);
-    unsigned long long c = 0;
-    for (int p = p0; p < p1; ++p) {
-        const int a = assign[(size_t)p * S + s];
-        for (int k = row_ptr[p]; k < row_ptr[p + 1]; ++k) c += a != assign[(size_t)col[k] * S + s];
-        if (missing && a != -1) c += (unsigned long long)missing[p];
+    const unsigned nslot = S < 256 ? (unsigned)S : 256u;
+    if (t < total) {
+        const int s = (int)(t % (unsigned)S);
+        const int p0 = r0 + (int)(t / (unsigned)S) * ppt, p1 = min(r1, p0 + ppt);
+        unsigned long long c = 0;
+        for (int p = p0; p < p1; ++p) {
+            const int a = assign[(size_t)p * S + s];
+            for (int k = row_ptr[p]; k < row_ptr[p + 1]; ++k) c += a != assign[(size_t)col[k] * S + s];
+            if (missing && a != -1) c += (unsigned long long)missing[p];
+        }
+        if (c) atomicAdd(&red[threadIdx.x % nslot], c);
     }
-    if (c) atomicAdd(&out[s], c);
+    __syncthreads();
+    // then one of kCutBins rows of per-scenario bins (blocks spread over the
+    // rows so no address sees more than blocks / kCutBins atomics)
+    const unsigned long long v = threadIdx.x < nslot ? red[threadIdx.x] : 0ull;
+    if (v) atomicAdd(&out[(size_t)(blockIdx.x % kCutBins) * S + (blockIdx.x * 256u + threadIdx.x) % (unsigned)S], v);
+}
+
+__global__ __launch_bounds__(256) void cut_bins_sum(const unsigned long long *__restrict__ bins, int S,
+                                                    unsigned long long *__restrict__ out) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (s >= S) return;
+    unsigned long long c = 0;
+    for (int b = 0; b < kCutBins; ++b) c += bins[(size_t)b * S + s];
+    out[s] = c;
 }
 
 // delete_replaced_pod.py:41-61: first pod (list order) with the largest cpu > -1.
@@ -664,12 +688,20 @@ int rsk_cut_cost_rows(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_i
     RSK_HIP(hipMemsetAsync(d_out, 0, (size_t)S * 8, ctx->stream));
     if (r1 > r0) {
         const int Q = r1 - r0;
-        const int ppt = chunk_for(Q, S);
+        // rows per thread: each row is a dependent row_ptr -> col -> assign chain,
+        // so keep ~64k workgroups of (row chunk, scenario) pairs in flight
+        const int ppt = (int)std::max<int64_t>(1, ceil_div((int64_t)Q * S, (int64_t)256 * 65536));
         const int64_t tot = ceil_div(Q, ppt) * S;
         RSK_CHECK(tot < INT32_MAX, "grid too large");
+        RSK_TRY(ctx->work[4].reserve((size_t)kCutBins * S * 8));
+        auto *bins = ctx->work[4].as<unsigned long long>();
+        RSK_HIP(hipMemsetAsync(bins, 0, (size_t)kCutBins * S * 8, ctx->stream));
         ScopedTimer tm(ctx, "cut_cost");
-        cut_cost_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, ctx->stream>>>(
-            d_rp, d_col, r0, r1, d_assign, S, d_miss, ppt, (unsigned)tot, reinterpret_cast<unsigned long long *>(d_out));
+        cut_cost_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, ctx->stream>>>(d_rp, d_col, r0, r1, d_assign, S, d_miss,
+                                                                              ppt, (unsigned)tot, bins);
+        RSK_HIP(hipGetLastError());
+        cut_bins_sum<<<(unsigned)ceil_div(S, 256), 256, 0, ctx->stream>>>(bins, S,
+                                                                           reinterpret_cast<unsigned long long *>(d_out));
         RSK_HIP(hipGetLastError());
     }
     if (!dev) {

@@ -27,6 +27,8 @@ Pod-row sharding (config 4, 1M pods x 50k nodes x 64 scenarios):
 """
 from __future__ import annotations
 
+import os
+import sys
 from dataclasses import dataclass
 
 
@@ -163,8 +165,11 @@ def _coll_tensor(t):
 
 
 def allreduce_(t, op="sum", group=None):
-    """In-place all-reduce of t (SUM or MAX) on whatever device the backend needs."""
+    """In-place all-reduce of t (SUM or MAX) on whatever device the backend
+    needs; a no-op without a process group (one rank)."""
     import torch.distributed as dist
+    if not dist.is_initialized():
+        return t
     red = dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX
     x, back = _coll_tensor(t)
     dist.all_reduce(x, op=red, group=group)
@@ -174,9 +179,11 @@ def allreduce_(t, op="sum", group=None):
 
 
 def allgather(t, group=None):
-    """[world, *t.shape] stack of every rank's t."""
+    """[world, *t.shape] stack of every rank's t ([1, ...] without a process group)."""
     import torch
     import torch.distributed as dist
+    if not dist.is_initialized():
+        return t.unsqueeze(0)
     x, back = _coll_tensor(t.contiguous())
     parts = [torch.empty_like(x) for _ in range(dist.get_world_size(group))]
     dist.all_gather(parts, x, group=group)
@@ -206,20 +213,23 @@ class LibrskRoundsBackend:
 
     def _sync(self):
         import torch
-        torch.cuda.synchronize(self.dev)
+        torch.cuda.synchronize(self.dev)   # torch-stream inputs ready / librsk-stream outputs done
 
     def node_partials(self, assign_rows, pod_cpu_rows, pod_mem_rows, q, N, S):
         import torch
+        self._sync()
+        cnt = torch.empty(N * S, dtype=torch.int32, device=self.dev)
         cpu = torch.empty(N * S, dtype=torch.int64, device=self.dev)
         mem = torch.empty(N * S, dtype=torch.int64, device=self.dev)
         self._check(self.ctx.lib.rsk_node_reduce(self.ctx.handle, assign_rows.data_ptr(), q, S,
-                                                 pod_cpu_rows.data_ptr(), pod_mem_rows.data_ptr(), N, None,
+                                                 pod_cpu_rows.data_ptr(), pod_mem_rows.data_ptr(), N, cnt.data_ptr(),
                                                  cpu.data_ptr(), mem.data_ptr(), self._F))
         self._sync()
         return cpu, mem
 
     def detect(self, use, cap, N, S, threshold):
         import torch
+        self._sync()
         pct = torch.empty(N * S, dtype=torch.int32, device=self.dev)
         haz = torch.empty(N * S, dtype=torch.uint8, device=self.dev)
         most = torch.empty(S, dtype=torch.int32, device=self.dev)
@@ -231,6 +241,7 @@ class LibrskRoundsBackend:
 
     def pick_rows(self, assign_rows, pod_cpu_rows, q, S, most):
         import torch
+        self._sync()
         out = torch.empty(S, dtype=torch.int32, device=self.dev)
         self._check(self.ctx.lib.rsk_pick_max_pod(self.ctx.handle, assign_rows.data_ptr(), pod_cpu_rows.data_ptr(), q,
                                                   S, most.data_ptr(), out.data_ptr(), self._F))
@@ -239,6 +250,7 @@ class LibrskRoundsBackend:
 
     def place(self, assign, S, cap, use, haz, N, evict):
         import torch
+        self._sync()
         out = torch.empty(S, dtype=torch.int32, device=self.dev)
         self.rounds.place(assign, S, cap, use, haz, N, evict, out, device=True)
         self._sync()
@@ -246,6 +258,7 @@ class LibrskRoundsBackend:
 
     def cut_rows(self, assign, S, r0, r1):
         import torch
+        self._sync()
         out = torch.empty(S, dtype=torch.int64, device=self.dev)
         self._check(self.ctx.lib.rsk_cut_cost_rows(self.ctx.handle, self.row_ptr.data_ptr(), self.col_idx.data_ptr(),
                                                    self.P, r0, r1, assign.data_ptr(), S, None, out.data_ptr(),
@@ -294,7 +307,10 @@ class RowShardedRounds:
         sidx = torch.arange(S, device=dev)
         pc64 = pod_cpu.to(torch.int64)
         mask32 = (1 << 32) - 1
-        for _ in range(R):
+        trace = os.environ.get("RSK_DIST_TRACE")
+        for rnd in range(R):
+            if trace:
+                print(f"[rank {self.shard.rank}] round {rnd}", file=sys.stderr, flush=True)
             c = time.perf_counter()
             cpu, mem = self._partials(assign, pod_cpu, pod_mem, N, S)
             use = (base + cpu).to(torch.int32)

@@ -112,6 +112,11 @@ def _worker(rank, world, port, R, out_q, use_gpu, pg="gloo"):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if use_gpu:
+        import faulthandler
+        os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+        fh = open(os.path.join(REPO, "gpurun_out", f"dist_rounds_rank{rank}.txt"), "w")
+        faulthandler.enable(file=fh)
+        faulthandler.dump_traceback_later(60, exit=True, file=fh)   # a hung rank leaves its stack behind
         torch.cuda.set_device(0)
     dist.init_process_group(pg, rank=rank, world_size=world)
     try:
@@ -126,6 +131,12 @@ def _worker(rank, world, port, R, out_q, use_gpu, pg="gloo"):
                                                  R)
         out_q.put((rank, res["evict"].cpu().numpy(), res["target"].cpu().numpy(), res["cut"].cpu().numpy(),
                    assign.cpu().numpy(), res["use"].cpu().numpy()))
+    except BaseException:  # noqa: BLE001 - report to the parent instead of leaving the peer in a collective
+        import traceback
+        out_q.put(("error", rank, traceback.format_exc()))
+        out_q.close()
+        out_q.join_thread()   # flush the report before the hard exit
+        os._exit(1)
     finally:
         dist.destroy_process_group()
 
@@ -137,10 +148,21 @@ def _run(world, R, use_gpu=False, pg="gloo"):
     procs = [ctx.Process(target=_worker, args=(r, world, port, R, q, use_gpu, pg)) for r in range(world)]
     for p in procs:
         p.start()
-    outs = [q.get(timeout=300) for _ in range(world)]
-    for p in procs:
-        p.join(60)
-        assert p.exitcode == 0
+    outs = []
+    try:
+        for _ in range(world):
+            try:
+                o = q.get(timeout=100)
+            except Exception:
+                raise AssertionError(f"no result; exit codes {[p.exitcode for p in procs]}") from None
+            assert o[0] != "error", f"rank {o[1]} failed:\n{o[2]}"
+            outs.append(o)
+    finally:
+        for p in procs:
+            p.join(30)
+            if p.exitcode is None:
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs)
     return sorted(outs, key=lambda o: o[0])
 
 
