@@ -123,8 +123,10 @@ def alg_bytes(kernel, P, N, S, info):
 
 def bench_rounds(args, cfg, world, rank, local, dev):
     """Config 5: one step = one round of detect -> evict -> CAR -> update over
-    this rank's S scenarios (rsk_rounds_run with R = 1 per step, state carried
-    across steps on the device).  Scenario sharded, no data-path collective."""
+    this rank's S scenarios.  The timed region is ONE rsk_rounds_run call of R =
+    --steps rounds (default 256, config 5's R) with the state on the device; the
+    warm-up is another call of --warmup rounds from the same state.  Scenario
+    sharded, no data-path collective."""
     import torch
     import torch.distributed as dist
     from rsk import _lib, api, synth
@@ -141,20 +143,16 @@ def bench_rounds(args, cfg, world, rank, local, dev):
     R = args.warmup + args.steps
     ev = torch.empty(R * S, dtype=torch.int32, device=dev)
     tg = torch.empty(R * S, dtype=torch.int32, device=dev)
-
-    def step(i):
-        rounds.run(T["assign"], S, T["cap_cpu"], T["use_cpu"], N, 1, 30, ev[i * S:], tg[i * S:], device=True)
-
-    for i in range(args.warmup):
-        step(i)
+    if args.warmup:
+        rounds.run(T["assign"], S, T["cap_cpu"], T["use_cpu"], N, args.warmup, 30, ev, tg, device=True)
     ctx.reset_profiling()
     ctx.set_profiling(not args.no_kernel_events)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    for i in range(args.warmup, R):
-        step(i)
+    w = args.warmup * S
+    rounds.run(T["assign"], S, T["cap_cpu"], T["use_cpu"], N, args.steps, 30, ev[w:], tg[w:], device=True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -165,14 +163,15 @@ def bench_rounds(args, cfg, world, rank, local, dev):
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     kernels = {}
-    for name in ("rounds_detect", "rounds_pick", "rounds_move"):
+    for name in ("rounds_shadow", "rounds_detect", "rounds_pick", "rounds_move"):
         ms, n = ctx.kernel_time(name)
         if n:
             kernels[name] = {"avg_ms": ms / n, "launches": n, "per_step_ms": ms / args.steps}
     tgt = tg.cpu().numpy()[args.warmup * S:]
-    # parity: 4 scenarios, 6 rounds from the initial state, GPU loop vs oracle_rounds
+    # parity: 8 scenarios (the u16-shadow scan), 6 rounds from the initial state,
+    # GPU loop vs oracle_rounds
     from oracle import oracle as orc
-    k = min(S, 4)
+    k = min(S, 8)
     a0 = c.assign.reshape(P, S)[:, :k].copy().reshape(-1)
     u0 = c.use_cpu.reshape(N, S)[:, :k].copy().reshape(-1)
     exp = orc.rounds(c.row_ptr, c.col_idx, c.pod_cpu, a0, k, c.cap_cpu, u0, N, 6)
@@ -188,6 +187,7 @@ def bench_rounds(args, cfg, world, rank, local, dev):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32",
             "data": "synthetic",
             "config": {"workload": cfg["name"], "pods": P, "nodes": N, "scenarios_per_gpu": S, "threshold": 30,
+                       "rounds_per_call": args.steps,
                        "parallelism": f"scenario-sharded x{world}"},
             "kernels": kernels, "moves": int((tgt >= 0).sum()), "none": int((tgt == -1).sum()),
             "no_candidate": int((tgt == -2).sum()), "no_evict": int((tgt == -3).sum()),
@@ -203,7 +203,7 @@ def bench_rounds(args, cfg, world, rank, local, dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="headline", choices=sorted(CONFIGS))
     ap.add_argument("--scenarios", type=int, default=0, help="override S per GPU")
@@ -218,6 +218,9 @@ def main():
     ap.add_argument("--pmc-json", default=PMC_JSON,
                     help="per-config PMC traffic (tools/pmc_summary.py, FETCH_SIZE x2-corrected)")
     args = ap.parse_args()
+    args.steps_default = args.steps is None
+    if args.steps is None:
+        args.steps = 20
 
     import torch
     import torch.distributed as dist
@@ -238,6 +241,8 @@ def main():
         cfg["S"] = args.scenarios
     P, N, S = cfg["P"], cfg["N"], cfg["S"]
     if cfg.get("rounds"):
+        if args.steps_default:
+            args.steps = 256   # config 5's R: one rsk_rounds_run call of 256 rounds
         return bench_rounds(args, cfg, world, rank, local, dev)
     by_rows = (args.shard or cfg.get("shard", "scenarios")) == "rows"
     t0 = time.time()

@@ -107,6 +107,8 @@ int launch_detect(hipStream_t stream, const int *pct, int N, int S, int threshol
                   unsigned long long *key_ws, int *most);
 int launch_pick_max_pod(hipStream_t stream, const int *assign, const int *pod_cpu, int P, int S, const int *most,
                         unsigned long long *key_ws, int *out_pod);
+// key_ws[S] packed (cpu, ~pod) maxima -> pod index or -1 (the pick kernels' tail)
+int launch_decode_first_max(hipStream_t stream, const unsigned long long *key, int S, int *out_pod);
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

@@ -393,6 +393,12 @@ int launch_detect(hipStream_t stream, const int *pct, int N, int S, int threshol
     return RSK_OK;
 }
 
+int launch_decode_first_max(hipStream_t stream, const unsigned long long *key, int S, int *out_pod) {
+    decode_first_max<<<(unsigned)ceil_div(S, 256), 256, 0, stream>>>(key, S, out_pod);
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
+}
+
 int launch_pick_max_pod(hipStream_t stream, const int *assign, const int *pod_cpu, int P, int S, const int *most,
                         unsigned long long *key_ws, int *out_pod) {
     RSK_HIP(hipMemsetAsync(key_ws, 0, (size_t)S * 8, stream));

@@ -28,7 +28,9 @@ struct rsk_rounds {
     int P = 0, dmax = 0;
     rsk::DevBuf row_ptr, col, pod_cpu;
     rsk::DevBuf pct, haz, most, evict, key_ws;
+    rsk::DevBuf asg16;  // u16 shadow of assign for the eviction scan (N <= 65535, S % 8 == 0)
     ~rsk_rounds() {
+        asg16.release();
         row_ptr.release();
         col.release();
         pod_cpu.release();
@@ -57,7 +59,8 @@ __global__ __launch_bounds__(kMoveThreads) void car_move_kernel(const int *__res
                                                                 int *use, const int *__restrict__ cap,
                                                                 const uint8_t *__restrict__ haz,
                                                                 const int *__restrict__ evict, int S, int N, int H,
-                                                                int update, int *__restrict__ out_target) {
+                                                                int update, int *__restrict__ out_target,
+                                                                unsigned short *__restrict__ asg16) {
     extern __shared__ __attribute__((aligned(16))) unsigned lds[];
     unsigned *keys = lds, *cnts = lds + H;
     unsigned long long *red64 = reinterpret_cast<unsigned long long *>(lds + 2 * H);  // best
@@ -138,6 +141,7 @@ __global__ __launch_bounds__(kMoveThreads) void car_move_kernel(const int *__res
             if ((unsigned)old < (unsigned)N) use[(size_t)old * S + s] -= c;
             use[(size_t)t * S + s] += c;
             assign[pc] = t;
+            if (asg16) asg16[pc] = (unsigned short)t;
         }
     }
 }
@@ -146,6 +150,52 @@ int next_pow2(int x) {
     int p = 1;
     while (p < x) p <<= 1;
     return p;
+}
+
+// u16 shadow of assign: node ids < N <= 65535, anything outside [0, N) -> 0xffff
+// (never a hazard node)
+__global__ __launch_bounds__(256) void asg16_kernel(const int *__restrict__ assign, size_t n, int N,
+                                                     unsigned short *__restrict__ out) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = (unsigned)assign[i] < (unsigned)N ? (unsigned short)assign[i] : (unsigned short)0xffff;
+}
+
+// delete_replaced_pod.py:41-61 over the u16 shadow: thread = (chunk of ppt pods,
+// 8 consecutive scenarios), one 16-B load per pod; the first max (cpu, -pod)
+// among pods on most[s] with cpu > -1, packed as pick_pod_kernel packs it.  Half
+// the bytes of the int32 scan (rsk_metrics.hip pick_pod_kernel).
+__global__ __launch_bounds__(256) void pick16_kernel(const uint4 *__restrict__ asg, const int *__restrict__ pod_cpu,
+                                                      int P, int S8, const int *__restrict__ most, int ppt,
+                                                      unsigned total, unsigned long long *__restrict__ best) {
+    const unsigned t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= total) return;
+    const int s8 = (int)(t % (unsigned)S8);
+    const int p0 = (int)(t / (unsigned)S8) * ppt, p1 = min(P, p0 + ppt);
+    unsigned m[8];
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int v = most[s8 * 8 + j];
+        m[j] = v < 0 ? 0x10000u : (unsigned)v;  // no hazard node: matches nothing
+        any |= v >= 0;
+    }
+    if (!any) return;
+    unsigned long long b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int p = p0; p < p1; ++p) {
+        const uint4 x = asg[(size_t)p * S8 + s8];
+        const unsigned w[4] = {x.x, x.y, x.z, x.w};
+        const int c = pod_cpu[p];
+        const unsigned long long k = c >= 0 ? ((unsigned long long)((unsigned)c ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)p)
+                                            : 0ull;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const unsigned nd = (w[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
+            b[j] = (nd == m[j] && k > b[j]) ? k : b[j];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if (b[j]) atomicMax(&best[s8 * 8 + j], b[j]);
 }
 
 struct MoveGeom {
@@ -252,6 +302,17 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
     RSK_TRY(g.rc);
     const int H = g.H;
     const size_t lds = g.lds;
+    // the eviction scan reads a u16 shadow of assign when node ids fit (kept in
+    // step by the move kernel); otherwise the int32 scan
+    const bool s16 = N <= 65535 && S % 8 == 0 && PS > 0;
+    unsigned short *a16 = nullptr;
+    if (s16) {
+        RSK_TRY(r->asg16.reserve(PS * 2));
+        a16 = r->asg16.as<unsigned short>();
+        ScopedTimer tm(ctx, "rounds_shadow");
+        asg16_kernel<<<(unsigned)ceil_div((int64_t)PS, 256), 256, 0, st>>>(d_assign, PS, N, a16);
+        RSK_HIP(hipGetLastError());
+    }
     for (int round = 0; round < R; ++round) {
         int *ev = d_evict + (size_t)round * S;
         {
@@ -262,14 +323,28 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         }
         {
             ScopedTimer tm(ctx, "rounds_pick");
-            RSK_TRY(launch_pick_max_pod(st, d_assign, r->pod_cpu.as<int>(), r->P, S, r->most.as<int>(),
-                                        r->key_ws.as<unsigned long long>(), ev));
+            if (s16) {
+                unsigned long long *key = r->key_ws.as<unsigned long long>();
+                RSK_HIP(hipMemsetAsync(key, 0, (size_t)S * 8, st));
+                const int S8 = S / 8;
+                const int ppt = (int)std::max<int64_t>(1, ceil_div((int64_t)r->P * S8, (int64_t)256 * 4096));
+                const int64_t tot = ceil_div(r->P, ppt) * S8;
+                RSK_CHECK(tot < INT32_MAX, "grid too large");
+                pick16_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, st>>>(
+                    reinterpret_cast<const uint4 *>(a16), r->pod_cpu.as<int>(), r->P, S8, r->most.as<int>(), ppt,
+                    (unsigned)tot, key);
+                RSK_HIP(hipGetLastError());
+                RSK_TRY(launch_decode_first_max(st, key, S, ev));
+            } else {
+                RSK_TRY(launch_pick_max_pod(st, d_assign, r->pod_cpu.as<int>(), r->P, S, r->most.as<int>(),
+                                            r->key_ws.as<unsigned long long>(), ev));
+            }
         }
         {
             ScopedTimer tm(ctx, "rounds_move");
             car_move_kernel<<<dim3((unsigned)S), dim3(kMoveThreads), lds, st>>>(
                 r->row_ptr.as<int>(), r->col.as<int>(), r->pod_cpu.as<int>(), d_assign, d_use, d_cap,
-                r->haz.as<uint8_t>(), ev, S, N, H, 1, d_target + (size_t)round * S);
+                r->haz.as<uint8_t>(), ev, S, N, H, 1, d_target + (size_t)round * S, a16);
             RSK_HIP(hipGetLastError());
         }
     }
@@ -310,7 +385,7 @@ int rsk_rounds_place(rsk_rounds *r, const int32_t *assign, int32_t S, const int3
         ScopedTimer tm(ctx, "rounds_place");
         car_move_kernel<<<dim3((unsigned)S), dim3(kMoveThreads), g.lds, ctx->stream>>>(
             r->row_ptr.as<int>(), r->col.as<int>(), r->pod_cpu.as<int>(), const_cast<int *>(d_assign),
-            const_cast<int *>(d_use), d_cap, d_haz, d_evict, S, N, g.H, 0, d_target);
+            const_cast<int *>(d_use), d_cap, d_haz, d_evict, S, N, g.H, 0, d_target, nullptr);
         RSK_HIP(hipGetLastError());
     }
     if (!dev) {
