@@ -268,6 +268,7 @@ __global__ __launch_bounds__(256) void std_partial_kernel(const int *__restrict_
                                                           int N, int S, int npb, unsigned total,
                                                           double *__restrict__ pmean, double *__restrict__ pm2,
                                                           int *__restrict__ pcnt) {
+#pragma clang fp contract(off)  // separate multiply and add, as numpy (no FMA contraction)
     const unsigned t = blockIdx.x * 256u + threadIdx.x;
     if (t >= total) return;
     const int s = (int)(t % (unsigned)S), ch = (int)(t / (unsigned)S);
@@ -295,6 +296,7 @@ __global__ __launch_bounds__(256) void std_partial_kernel(const int *__restrict_
 
 __global__ void std_merge_kernel(const double *__restrict__ pmean, const double *__restrict__ pm2,
                                  const int *__restrict__ pcnt, int nchunks, int S, double *__restrict__ out) {
+#pragma clang fp contract(off)
     const int s = blockIdx.x * 256 + threadIdx.x;
     if (s >= S) return;
     double mean = 0.0, m2 = 0.0;

@@ -51,7 +51,7 @@ def sha(a) -> str:
 
 
 def load_reference(ref_dir):
-    sys.path.insert(1, ref_dir)
+    sys.path.insert(0, ref_dir)  # ahead of the package dir (its rescheduling.py is the drop-in)
     import rescheduling as R  # noqa: E402  (the reference module)
     import main as M
     import harzard_detect as H

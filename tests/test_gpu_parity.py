@@ -467,3 +467,21 @@ def test_cut_cost_rows_partition_sums_to_full(ctx):
     cuts = [0, 1, 250, 251, 699, 700]
     parts = sum(api.cut_cost_rows(rp, ci, a, P, S, cuts[k], cuts[k + 1], ctx=ctx) for k in range(len(cuts) - 1))
     assert np.array_equal(parts, full)
+
+
+def test_pick_max_pod_metric_edges_gpu(ctx):
+    """librsk's pick on the reference's metric-edge fixtures (pick_edges.json):
+    equal to the reference where it returns, the documented divergence where it
+    raises TypeError."""
+    import json
+    import os
+    from rsk import api
+    from test_oracle_golden import _pick_edge_arrays, pick_edge_expected
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "pick_edges.json")) as f:
+        cases = json.load(f)["cases"]
+    for case in cases:
+        pods, assign, cpu, most = _pick_edge_arrays(case)
+        if not pods:
+            continue
+        r = int(api.pick_max_pod(assign, cpu, len(pods), 1, [most], ctx=ctx)[0])
+        assert (pods[r][0] if r >= 0 else None) == pick_edge_expected(case), case

@@ -211,3 +211,44 @@ def test_python_restatements_match_golden_and_c_oracle(synth_golden):
         for p, nb in enumerate(car_py.dedup_rows(rp, ci, range(P))):
             assert car_py.car_literal(nb.tolist(), by_node, haz_list, cap, use) == exp[p], (trial, p)
             assert car_py.car_numpy(nb, a, cap, use, h, N) == exp[p], (trial, p)
+
+
+def _pick_edge_arrays(case):
+    pods = case["pods"]
+    nodes = sorted({p[1] for p in pods} | {case["most"]})
+    idx = {n: i for i, n in enumerate(nodes)}
+    assign = np.array([idx[p[1]] for p in pods], np.int32)
+    cpu = np.array([-1 if p[2] is None else p[2] for p in pods], np.int32)   # no metrics -> -1 (rsk/snapshot.py)
+    return pods, assign, cpu, idx[case["most"]]
+
+
+def pick_edge_expected(case):
+    """The build's documented answer: the reference's pick where
+    it returns; where it raises TypeError (a pod without metrics on the hazard node
+    meets the ("0", "0") default), the first max-CPU pod among those with metrics."""
+    if "picked" in case:
+        return case["picked"]
+    assert case["raises"] == "TypeError"
+    best, name = -1, None
+    for n, node, c in case["pods"]:
+        if node == case["most"] and c is not None and c > best:
+            best, name = c, n
+    return name
+
+
+def test_pick_max_pod_metric_edges_vs_reference():
+    """pick_edges.json (tests/golden/make_pick_edges.py, the reference run here):
+    0-CPU pods, ties and missing-elsewhere pods match the reference exactly; the
+    16 cases where the reference raises TypeError get the documented divergence."""
+    import json
+    import os
+    from oracle import oracle as orc
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "pick_edges.json")) as f:
+        cases = json.load(f)["cases"]
+    raised = 0
+    for case in cases:
+        pods, assign, cpu, most = _pick_edge_arrays(case)
+        r = int(orc.pick_max_pod(assign, cpu, len(pods), 1, [most])[0])
+        assert (pods[r][0] if r >= 0 else None) == pick_edge_expected(case), case
+        raised += "raises" in case
+    assert raised >= 10 and any(c.get("picked") and any(p[2] == 0 for p in c["pods"]) for c in cases)
