@@ -15,6 +15,7 @@ The resulting int32/uint8 arrays follow include/rsk.h with S = 1.
 from __future__ import annotations
 
 from dataclasses import dataclass
+from operator import itemgetter
 from typing import List
 
 import numpy as np
@@ -35,6 +36,17 @@ def _i32(v, what: str) -> int:
     if not 0 <= iv <= INT32_MAX:
         raise ValueError(f"{what}={v!r} outside the ABI range [0, 2^31-1] of librsk")
     return iv
+
+
+def _i32_array(vals, names, field: str) -> np.ndarray:
+    """int32 array of the values, _i32's range check (and message) on the first bad one."""
+    try:
+        a = np.array(vals, np.int64)
+        if a.size == 0 or (a.min() >= 0 and a.max() <= INT32_MAX):
+            return a.astype(np.int32)
+    except (OverflowError, TypeError, ValueError):
+        pass
+    return np.array([_i32(v, f"{n}.{field}") for v, n in zip(vals, names)], np.int32)
 
 
 @dataclass
@@ -61,21 +73,25 @@ def car_request(name, harzard_node, cluster_monitoring, relations, nodes_name) -
     N = len(nodes)
     member = _members(relations.get(name, []))
     is_haz = _members(harzard_node)
-    haz = np.zeros(N, np.uint8)
-    cap = np.zeros(N, np.int32)
-    use = np.zeros(N, np.int32)
-    nb: List[int] = []
+    dep = itemgetter("deploymentname")
+    hz = [1 if is_haz(n) else 0 for n in nodes]
+    cnt = [0] * N
+    capl = [0] * N
+    usel = [0] * N
     for i, n in enumerate(nodes):
-        if is_haz(n):
-            haz[i] = 1
+        if hz[i]:
             continue
         info = cluster_monitoring[n]
-        for pod in info["pods"]:
-            if member(pod["deploymentname"]):
-                nb.append(i)
-        cap[i] = _i32(info["node_cpu_capacity"], f"{n}.node_cpu_capacity")
-        use[i] = _i32(info["node_cpu_usage"], f"{n}.node_cpu_usage")
-    k = len(nb)
+        # the per-pod membership test runs in C (map over the pod list), with the
+        # reference's KeyError for a pod without "deploymentname"
+        cnt[i] = sum(map(member, map(dep, info["pods"])))
+        capl[i] = info["node_cpu_capacity"]
+        usel[i] = info["node_cpu_usage"]
+    haz = np.array(hz, np.uint8)
+    cap = _i32_array(capl, nodes, "node_cpu_capacity")
+    use = _i32_array(usel, nodes, "node_cpu_usage")
+    nb = np.repeat(np.arange(N, dtype=np.int32), cnt)   # one neighbour entry per related pod, on its node
+    k = int(nb.size)
     row_ptr = np.full(k + 2, k, np.int32)
     row_ptr[0] = 0
     col_idx = np.arange(1, k + 1, dtype=np.int32)
