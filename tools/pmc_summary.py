@@ -32,6 +32,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # kernel symbol -> the timer name bench.py reports (librsk ScopedTimer names)
 BENCH_NAME = {"car_tile16": "car_tile", "car_hub": "car_heavy", "car_pivot": "car_side"}
+# bench timers that bracket several launches of one step (car_tile: the lean and
+# the heavy tile launch, two grid sizes of car_tile16): their per-"launch"
+# traffic is the sum over the grids, not the mean
+SUM_GRIDS = {"car_tile"}
 
 
 def short(name: str) -> str:
@@ -89,9 +93,10 @@ def main():
     for key, e in summary.items():
         if "hbm_bytes_per_launch" in e:
             k = key.split("@")[0]
-            b = by_kernel[BENCH_NAME.get(k, k)]
+            name = BENCH_NAME.get(k, k)
+            b = by_kernel[name]
             b[0] += e["hbm_bytes_per_launch"]
-            b[1] += 1
+            b[1] = 1 if name in SUM_GRIDS else b[1] + 1
             b[2] += e["avg_us"]
     path = os.path.join(prof, "pmc_traffic.json")
     try:
