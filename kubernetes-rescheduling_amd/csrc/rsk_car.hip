@@ -1523,8 +1523,9 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     static const bool side_first = env_int("RSK_SIDE_FIRST", 0) != 0;
     hipStream_t side[rsk_ctx::kAux] = {ctx->stream, ctx->stream, ctx->stream};
     const int nside = side_rows && plan->T > 0 ? overlap : 0;
-    if (nside) {
-        RSK_TRY(aux_fork(ctx, nside));
+    const int nfork = nside;
+    if (nfork) {
+        RSK_TRY(aux_fork(ctx, nfork));
         for (int i = 0; i < nside; ++i) side[i] = ctx->aux[i];
     }
     SideBufs sb;
@@ -1538,7 +1539,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     sb.target = d_target;
     sb.score = d_score;
     RSK_TRY(launch_side(plan, ctx, side, std::max(nside, 1), sb, S, N, compact));
-    if (nside && side_first) RSK_TRY(aux_join(ctx, nside));
+    if (nfork && side_first) RSK_TRY(aux_join(ctx, nfork));
     static const int ablate = env_int("RSK_ABLATE_TILE", 0);
     static const int order = env_int("RSK_TILE_ORDER", 2);
     const bool off32 = (int64_t)std::max(plan->P, plan->Q) * S * 4 < ((int64_t)1 << 32);
@@ -1581,14 +1582,16 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         for (int part = 0; part < 2; ++part) {
             const int t0 = part ? plan->T_lean : 0, nt = part ? plan->T - plan->T_lean : plan->T_lean;
             if (nt <= 0) continue;
-            std::unique_ptr<ScopedTimer> tp(split ? new ScopedTimer(ctx, part ? "car_tile_heavy" : "car_tile") : nullptr);
+            const hipStream_t ts = ctx->stream;
+            std::unique_ptr<ScopedTimer> tp(split ? new ScopedTimer(ctx, part ? "car_tile_heavy" : "car_tile", ts)
+                                                  : nullptr);
             a.tile0 = t0;
             a.T = nt;
             const int64_t units = ceil_div(S, SL) * nt;
             a.xcd_per = (int)ceil_div(units, 8);
             const int64_t blocks = order == 2 ? 8 * (int64_t)a.xcd_per : units;
             RSK_CHECK(blocks < INT32_MAX, "tile grid too large");
-            RSK_TRY(launch_tile16(ctx->stream, a, d_score != nullptr, off32, part == 1, (unsigned)blocks, lds));
+            RSK_TRY(launch_tile16(ts, a, d_score != nullptr, off32, part == 1, (unsigned)blocks, lds));
         }
     } else if (plan->T > 0) {   // K1 tiles, wide {node, key} pairs
         TileArgs a;
@@ -1635,7 +1638,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         kern<<<dim3((unsigned)blocks), dim3(kTileThreads), lds, ctx->stream>>>(a);
         RSK_HIP(hipGetLastError());
     }
-    if (nside && !side_first) RSK_TRY(aux_join(ctx, nside));
+    if (nfork && !side_first) RSK_TRY(aux_join(ctx, nfork));
 #ifdef RSK_DEBUG_BOUNDS
     {
         unsigned flags_h = 0, zero = 0;

@@ -1032,8 +1032,8 @@ int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off3
         &car_tile16_kernel<false, false, true, true>,   &car_tile16_kernel<false, true, true, true>,
         &car_tile16_kernel<true, false, true, true>,    &car_tile16_kernel<true, true, true, true>};
     const bool l64 = a.lsl == 6;
-    RSK_CHECK(!l64 || (size_t)lds <= (size_t)kT16Rows * 256, "tile image exceeds the %d rows the kernel was built for",
-              kT16Rows);
+    RSK_CHECK(!l64 || (size_t)a.img_cells * 4 <= (size_t)kT16Rows * 256,
+              "tile image exceeds the %d rows the kernel was built for", kT16Rows);
     const K kern = kerns[(l64 ? 8 : 0) + (heavy ? 4 : 0) + (score ? 2 : 0) + (off32 ? 1 : 0)];
     RSK_CHECK(lds <= 160 * 1024, "tile image needs %zu B of LDS", lds);
     if (lds > 64 * 1024)
