@@ -746,10 +746,34 @@ __device__ __forceinline__ void w64_ds(const Tile16Args &a, const W64 &w, cint_p
             if (i % 8 == 0) __builtin_amdgcn_sched_barrier(0);
             const unsigned pr = (unsigned)r[4 + i / 2];
             const int row = (i & 1) ? (int)(pr >> 16) : (int)(pr & 0xffffu);
-            x[i] = i < d ? w.cell(row) : kCellPad;
+            x[i] = i < d ? w.cell(row) : kCellPad - (unsigned)i;  // distinct pads (code 0)
         }
         bitonic_sort<D, unsigned>(x);
-        t = sorted_runs_decide<D>(x, M, bk, need);
+        unsigned dup = 0u;  // equal cells sit next to each other now
+#pragma unroll
+        for (int i = 1; i < D; ++i) dup |= (unsigned)(x[i] == x[i - 1]);
+        if (!__builtin_amdgcn_ballot_w64(dup != 0u)) {
+            // no lane holds a node twice: every candidate counts 1 (as w64_dm's fast path)
+            unsigned bw = 0u;
+#pragma unroll
+            for (int i = 0; i < D; ++i) bw = max(bw, cell_cand(x[i]));
+            bk = cell_code(bw);
+            M = bk != kCodeHaz ? 1 : 0;
+            t = M == 0 ? INT_MIN : cand_node(bw);
+            need = false;
+            if (__builtin_amdgcn_ballot_w64(bk == kCodeNeg || code_inexact(bk))) {  // rare: count the ties
+                int rn = 0, nb = 0;
+#pragma unroll
+                for (int i = 0; i < D; ++i) {
+                    rn += cell_code(x[i]) != kCodeHaz;
+                    nb += cell_code(x[i]) == bk;
+                }
+                if (bk == kCodeNeg && rn > 1) t = RSK_TARGET_NONE;
+                need = code_inexact(bk) && nb > 1;
+            }
+        } else {
+            t = sorted_runs_decide<D>(x, M, bk, need);
+        }
     }
     if (__builtin_amdgcn_ballot_w64(need)) {  // rare: wave-uniform branch
         Img16 im;
