@@ -236,6 +236,7 @@ struct Prep16Args {
     int *nodekey;                // [N*S] (hazard ? KEY_HAZ : cap - use) or null
     int *zc_cnt;                 // [S]
     unsigned long long *zc_key;  // [S]
+    int *capmax;                 // [1] scratch: max(cap), written by launch_prep before the prep kernel
 };
 
 struct Tile16Args {

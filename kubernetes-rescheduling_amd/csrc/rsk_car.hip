@@ -1514,12 +1514,16 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         pa.nodekey = d_key;
         pa.zc_cnt = d_zcnt;
         pa.zc_key = d_zkey;
+        pa.capmax = d_zcnt + S;  // the zc buffer's spare words
         ScopedTimer tm(ctx, "car_prep");
         RSK_TRY(launch_prep(ctx->stream, pa));
     }
-    // mid and hub rows run on up to kAux side streams (RSK_OVERLAP = how many),
-    // beside the tile kernel or, with RSK_SIDE_FIRST=1, ahead of it
-    static const int overlap = std::max(0, std::min(rsk_ctx::kAux, env_int("RSK_OVERLAP", 1)));
+    // mid and hub rows run after the tiles on the same stream by default; with
+    // RSK_OVERLAP = k on k side streams beside the tile kernel (or, with
+    // RSK_SIDE_FIRST=1, ahead of it).  Overlap does not shorten the step (the
+    // lean tile kernel holds every CU's LDS and VGPRs) and it
+    // stretches the tile kernel, so it is off.
+    static const int overlap = std::max(0, std::min(rsk_ctx::kAux, env_int("RSK_OVERLAP", 0)));
     static const bool side_first = env_int("RSK_SIDE_FIRST", 0) != 0;
     hipStream_t side[rsk_ctx::kAux] = {ctx->stream, ctx->stream, ctx->stream};
     const int nside = side_rows && plan->T > 0 ? overlap : 0;

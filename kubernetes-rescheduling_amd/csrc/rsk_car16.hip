@@ -20,6 +20,7 @@
 //                  1 below 16384 millicores and 2..32 up to 2^19).
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 
 #include "rsk_car.h"
 
@@ -72,28 +73,33 @@ __device__ __forceinline__ ushort4 cvec_make(const unsigned (&k)[4]) {
 // ~node)) is reduced in LDS per workgroup first — threads of one workgroup
 // that share a scenario meet in one LDS slot — so a scenario receives one
 // global atomic per workgroup, not one per thread.
+// max(cap) once per execute, for the exact code window B = max(0, max(cap) - 32766)
+__global__ __launch_bounds__(1024) void car_capmax_kernel(const int *__restrict__ cap, int N, int *__restrict__ out) {
+    __shared__ int m;
+    if (threadIdx.x == 0) m = 0;
+    __syncthreads();
+    int mc = 0;
+    for (int n = threadIdx.x; n < N; n += 1024) mc = max(mc, cap[n]);
+    atomicMax(&m, mc);
+    __syncthreads();
+    if (threadIdx.x == 0) *out = m;
+}
+
 template <int V, bool kCode, bool kKey>
 __global__ __launch_bounds__(256) void car_prep_kernel(const int *__restrict__ cap, const typename VecT<V>::I *__restrict__ use,
                                                        const typename VecT<V>::H *__restrict__ haz, int N, int SV,
                                                        int npb, unsigned total, typename VecT<V>::C *__restrict__ code,
                                                        typename VecT<V>::I *__restrict__ nodekey,
-                                                       int *__restrict__ zc_cnt, unsigned long long *__restrict__ zc_key) {
+                                                       int *__restrict__ zc_cnt, unsigned long long *__restrict__ zc_key,
+                                                       const int *__restrict__ capmax) {
     __shared__ int lcnt[256 * V];
     __shared__ unsigned long long lkey[256 * V];
-    __shared__ int lcap;
     const unsigned t = blockIdx.x * 256u + threadIdx.x;
-    if (kCode) {  // B = max(0, max(cap) - 32766): the exact code window (rsk_car.h)
-        if (threadIdx.x == 0) lcap = 0;
-        __syncthreads();
-        int mc = 0;
-        for (int n = threadIdx.x; n < N; n += 256) mc = max(mc, cap[n]);
-        atomicMax(&lcap, mc);
-    }
     const unsigned base = (blockIdx.x * 256u) % (unsigned)SV;  // vector slot of thread 0
     const int nslot = min(256, SV);
     for (int i = threadIdx.x; i < nslot * V; i += 256) { lcnt[i] = 0; lkey[i] = 0ull; }
     __syncthreads();
-    const int B = kCode ? max(0, lcap - 32766) : 0;
+    const int B = kCode ? max(0, *capmax - 32766) : 0;  // the exact code window (rsk_car.h)
     if (kCode && t < (unsigned)SV) {  // code row N: code 0 for every scenario (clamped invalid assignments)
         const unsigned z[V] = {};
         code[(size_t)N * SV + t] = cvec_make(z);
@@ -154,21 +160,29 @@ static int prep_launch(hipStream_t stream, const Prep16Args &a, int SV, int npb,
     C *code = reinterpret_cast<C *>(a.code);
     I *key = reinterpret_cast<I *>(a.nodekey);
     if (a.code && a.nodekey)
-        car_prep_kernel<V, true, true><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key);
+        car_prep_kernel<V, true, true><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
+                                                                 a.capmax);
     else if (a.code)
-        car_prep_kernel<V, true, false><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key);
+        car_prep_kernel<V, true, false><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
+                                                                 a.capmax);
     else
-        car_prep_kernel<V, false, true><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key);
+        car_prep_kernel<V, false, true><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
+                                                                 a.capmax);
     RSK_HIP(hipGetLastError());
     return RSK_OK;
 }
 
 int launch_prep(hipStream_t stream, const Prep16Args &a) {
     RSK_CHECK(a.code || a.nodekey, "prep: nothing to write");
+    RSK_CHECK(!a.code || a.capmax, "prep: codes need the capmax scratch");
+    if (a.code) {
+        car_capmax_kernel<<<1, 1024, 0, stream>>>(a.cap, a.N, a.capmax);
+        RSK_HIP(hipGetLastError());
+    }
     // 4 scenarios per thread when S % 4 == 0 (16-B use / key words, 8-B codes)
     const bool v4 = a.S % 4 == 0 && ((uintptr_t)a.use % 16) == 0 && ((uintptr_t)a.haz % 4) == 0;
     const int SV = v4 ? a.S / 4 : a.S;
-    const int target_threads = 256 * 1024;
+    const int target_threads = 256 * 1024;  // 2^18 threads (1024 workgroups): more cost zero-case atomics, fewer cost bandwidth
     const int npb = (int)std::max<int64_t>(1, ceil_div((int64_t)a.N * SV, target_threads));
     const int64_t chunks = ceil_div(a.N, npb);
     const unsigned total = (unsigned)(chunks * SV);
