@@ -277,7 +277,7 @@ struct PivotArgs {
 
 // Mid rows (17..64) of the compact path: buckets D = 32, 64 (records kMidW ints).
 struct Mid16Args {
-    const int *rec[2];
+    const int *rec[2];        // buckets D = 32, 64
     int n_items[2];
     const int *assign;
     const unsigned short *code;
@@ -287,6 +287,31 @@ struct Mid16Args {
     int *out_target, *out_score;
     int S, N, SL, PS;         // SL, PS set by launch_mid16
 };
+
+// Hub rows of the compact path (rsk_hub16.hip), every degree class in one grid.
+struct Hub16Args {
+    const int *items;         // [n][4]: out row, offset into hcol, degree, s0 | lg << 24
+    const int *hcol;          // neighbour lists
+    const int *assign;
+    const unsigned short *code;
+    const int *cap, *use;
+    const int *zc_cnt;
+    const unsigned long long *zc_key;
+    int *out_target, *out_score;
+    int S, N;
+    int H, hshift;            // table words per wave, hash shift (from Hub16Geom)
+};
+struct Hub16Geom {
+    int tab, nj, ns;          // table kind (u8 / u16 direct, hash), register entries per lane (0: any
+                              // degree), scenarios per wave at once (tables per wave)
+    int dmax, H, hshift;
+    size_t lds;
+};
+constexpr int kNumHub16 = 3;                       // car_hub16 launches: degree (64,128] (128,256] (256,kHubMax]
+constexpr int kHub16Max[kNumHub16] = {128, 256, kHubMax};
+Hub16Geom hub16_geometry(int dmax, int N);
+int hub16_lg(int d, int S);
+int launch_hub16(hipStream_t stream, const Hub16Args &a, const Hub16Geom &g, int n_items);
 
 int launch_prep(hipStream_t stream, const Prep16Args &a);
 int launch_mid16(hipStream_t stream, const Mid16Args &a);

@@ -756,6 +756,12 @@ struct rsk_car_plan {
     // mid rows (17..64), only in a plan with light_max = kPairMax
     int n_mid[kNumMid] = {0, 0};
     DevBuf mid[kNumMid];
+    // compact path: the hub rows (65..kHubMax) for car_hub16, whose work items depend on S
+    std::vector<HeavyItem> h_hubrows;
+    DevBuf hub16_items;
+    int hub16_S = -1, hub16_thr = -1, hub16_N = -1;
+    int n_hub16[kNumHub16] = {}, hub16_off[kNumHub16] = {};
+    Hub16Geom hub16_geom[kNumHub16] = {};
     // hub rows (> 64)
     int n_heavy[kNumHeavy] = {};
     int heavy_dmax[kNumHeavy] = {};
@@ -782,6 +788,7 @@ struct rsk_car_plan {
         meta.release();
         recs.release();
         for (auto &b : mid) b.release();
+        hub16_items.release();
         for (auto &b : heavy_items) b.release();
         hcol.release();
         for (auto &b : piv_items) b.release();
@@ -1083,6 +1090,7 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
         } else if (d <= kHubMax) {
             const int c = heavy_class(d);
             hitems[c].push_back({i, (int)hcol.size(), d, 0});
+            plan->h_hubrows.push_back({i, (int)hcol.size(), d, 0});
             hcol.insert(hcol.end(), nbp, nbp + d);
             plan->n_heavy[c] += 1;
             plan->heavy_dmax[c] = std::max(plan->heavy_dmax[c], d);
@@ -1154,6 +1162,9 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
         RSK_TRY(upload(plan->recs, tb.recs.data(), tb.recs.size() * 4));
     }
     for (int b = 0; b < kNumMid; ++b) RSK_TRY(upload(plan->mid[b], midr[b].data(), midr[b].size() * 4));
+    // the longest hub rows first in the car_hub16 grid
+    std::stable_sort(plan->h_hubrows.begin(), plan->h_hubrows.end(),
+                     [](const HeavyItem &x, const HeavyItem &y) { return x.d > y.d; });
     for (int c = 0; c < kNumHeavy; ++c)
         RSK_TRY(upload(plan->heavy_items[c], hitems[c].data(), hitems[c].size() * sizeof(HeavyItem)));
     RSK_TRY(upload(plan->hcol, hcol.data(), hcol.size() * 4));
@@ -1240,9 +1251,49 @@ bool slot_on(const rsk_car_plan *plan, int S) {
     return on && S >= 64 && !pivot_on() && (int64_t)plan->P * S * 4 < ((int64_t)1 << 32);
 }
 
+// Compact side rows through car_mid16 + car_hub16 (codes only; default), or
+// with RSK_SIDE16=0 through the wide car_mid / car_hub kernels (exact keys).
+bool side16_on() {
+    static const bool on = env_int("RSK_SIDE16", 1) != 0;
+    return on;
+}
+
+// Rows of degree 65..128 go to car_hub16 (a D = 128 car_mid16 — lane =
+// scenario, register sort of 128 cells — does not compile in reasonable time).
+int mid16_max() { return kMidMax; }
+
+// car_hub16 work items for the hub rows of degree > thr at S scenarios:
+// (row, group of 2^lg scenarios), built on the host when S, thr or N change.
+int hub16_prepare(rsk_car_plan *plan, int S, int N, int thr) {
+    if (plan->hub16_S == S && plan->hub16_thr == thr && plan->hub16_N == N) return RSK_OK;
+    plan->hub16_S = -1;
+    std::vector<int32_t> items;
+    for (int c = 0; c < kNumHub16; ++c) {
+        const int lo = c ? kHub16Max[c - 1] : thr;
+        int dmax = 0;
+        for (const HeavyItem &h : plan->h_hubrows)
+            if (h.d > lo && h.d <= kHub16Max[c]) dmax = std::max(dmax, h.d);
+        plan->hub16_off[c] = (int)(items.size() / 4);
+        plan->n_hub16[c] = 0;
+        if (dmax == 0) continue;
+        plan->hub16_geom[c] = hub16_geometry(dmax, N);
+        for (const HeavyItem &h : plan->h_hubrows) {  // degree descending
+            if (h.d <= lo || h.d > kHub16Max[c]) continue;
+            const int lg = hub16_lg(h.d, S);
+            for (int64_t s0 = 0; s0 < S; s0 += (int64_t)1 << lg)
+                items.insert(items.end(), {h.oi, h.rb, h.d, (int)s0 | (lg << 24)});
+        }
+        plan->n_hub16[c] = (int)(items.size() / 4) - plan->hub16_off[c];
+    }
+    RSK_CHECK(items.size() / 4 < (size_t)INT32_MAX, "hub grid too large");
+    RSK_TRY(upload(plan->hub16_items, items.data(), items.size() * 4));
+    plan->hub16_S = S, plan->hub16_thr = thr, plan->hub16_N = N;
+    return RSK_OK;
+}
+
 // Whether the side rows need codes only (no exact node keys from the prep kernel).
 bool plan_side_compact(const rsk_car_plan *plan, int S) {
-    if (pivot_on()) return true;
+    if (pivot_on() || side16_on()) return true;
     const bool slot = slot_on(plan, S);
     for (int c = slot ? 1 : 0; c < kNumHeavy; ++c)
         if (plan->n_heavy[c]) return false;
@@ -1281,6 +1332,57 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t *side, int n
             RSK_TRY(launch_pivot(stream, a, std::min(plan->piv_dmax[c], N)));
         }
         if (pivot_on()) return RSK_OK;
+    }
+    if (compact && side16_on()) {
+        const int thr = mid16_max();
+        if (plan->n_mid[0] + plan->n_mid[1] > 0) {  // K2 mid rows (33..thr), codes
+            Mid16Args a;
+            std::memset(&a, 0, sizeof(a));
+            for (int k = 0; k < kNumMid; ++k) {
+                a.rec[k] = plan->mid[k].as<int>();
+                a.n_items[k] = plan->n_mid[k];
+            }
+            a.assign = d_assign;
+            a.code = b.code;
+            a.cap = b.cap;
+            a.use = b.use;
+            a.zc_cnt = d_zcnt;
+            a.zc_key = d_zkey;
+            a.out_target = d_target;
+            a.out_score = d_score;
+            a.S = S;
+            a.N = N;
+            const hipStream_t stream = pick();
+            ScopedTimer tm(ctx, "car_mid", stream);
+            RSK_TRY(launch_mid16(stream, a));
+        }
+        RSK_TRY(hub16_prepare(plan, S, N, thr));
+        for (int c = 0; c < kNumHub16; ++c) {  // K3 hub rows (thr..kHubMax), three degree classes
+            if (!plan->n_hub16[c]) continue;
+            Hub16Args a;
+            std::memset(&a, 0, sizeof(a));
+            a.items = plan->hub16_items.as<int>() + (size_t)plan->hub16_off[c] * 4;
+            a.hcol = plan->hcol.as<int>();
+            a.assign = d_assign;
+            a.code = b.code;
+            a.cap = b.cap;
+            a.use = b.use;
+            a.zc_cnt = d_zcnt;
+            a.zc_key = d_zkey;
+            a.out_target = d_target;
+            a.out_score = d_score;
+            a.S = S;
+            a.N = N;
+            const Hub16Geom &g = plan->hub16_geom[c];
+            a.H = g.H;
+            a.hshift = g.hshift;
+            const hipStream_t stream = pick();
+            static const bool per_class = env_int("RSK_HUB_TIMERS", 0) != 0;
+            static const char *const kNames[kNumHub16] = {"car_hub128", "car_hub256", "car_hub4096"};
+            ScopedTimer tm(ctx, per_class ? kNames[c] : "car_heavy", stream);
+            RSK_TRY(launch_hub16(stream, a, g, plan->n_hub16[c]));
+        }
+        return RSK_OK;
     }
     const bool slot = compact && slot_on(plan, S);
     if (slot) {  // degree 33..128: slot tables (replaces car_mid and hub class 0)

@@ -432,6 +432,43 @@ __device__ __forceinline__ int sorted_runs_decide(const unsigned (&x)[D], int &s
     return Rn == 1 ? cand_node(bw) : (bk >= 2u ? cand_node(bw) : RSK_TARGET_NONE);
 }
 
+// The same decision in one walk: the two largest (run length, code, -node)
+// keys over the runs of candidate nodes.  The second key tells whether
+// another node reaches the maximal count (a tie) and, being the best of the
+// others, whether one of them shares the best code (exact resolution).
+template <int D>
+__device__ __forceinline__ int sorted_runs_top2(const unsigned (&x)[D], int &score, unsigned &bk_out, bool &need) {
+    unsigned long long k1 = 0ull, k2 = 0ull;
+    int c = 0;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        c = (i > 0 && x[i] == x[i > 0 ? i - 1 : 0]) ? c + 1 : 1;
+        const bool end = i == D - 1 || x[i < D - 1 ? i + 1 : i] != x[i];
+        const bool cand = end && cell_code(x[i]) != kCodeHaz;
+        const unsigned long long k = cand ? ((unsigned long long)c << 32) | cell_cand(x[i]) : 0ull;
+        const bool g1 = k > k1;
+        k2 = g1 ? k1 : (k > k2 ? k : k2);
+        k1 = g1 ? k : k1;
+    }
+    const int M = (int)(k1 >> 32);
+    const unsigned bw = (unsigned)k1, bk = cell_code(bw);
+    const bool tie = (int)(k2 >> 32) == M;
+    score = M;
+    bk_out = bk;
+    need = M > 0 && tie && code_inexact(bk) && cell_code((unsigned)k2) == bk;
+    if (M == 0) return INT_MIN;
+    return !tie ? cand_node(bw) : (bk >= 2u ? cand_node(bw) : RSK_TARGET_NONE);
+}
+
+#ifndef RSK_RUNS_TOP2
+#define RSK_RUNS_TOP2 1
+#endif
+template <int D>
+__device__ __forceinline__ int sorted_runs(const unsigned (&x)[D], int &score, unsigned &bk_out, bool &need) {
+    if (RSK_RUNS_TOP2) return sorted_runs_top2<D>(x, score, bk_out, need);
+    return sorted_runs_decide<D>(x, score, bk_out, need);
+}
+
 // Exact tie resolution straight from the LDS image (rare path, kept free of
 // register arrays): among the row's distinct nodes with code bk and count M,
 // the largest exact remaining CPU, then the lower node.
@@ -763,6 +800,9 @@ __device__ __forceinline__ void w64_ds(const Tile16Args &a, const W64 &w, cint_p
             x[i] = i < d ? w.cell(row) : kCellPad - (unsigned)i;  // distinct pads (code 0)
         }
         bitonic_sort<D, unsigned>(x);
+#if RSK_RUNS_TOP2
+        t = sorted_runs<D>(x, M, bk, need);
+#else
         unsigned dup = 0u;  // equal cells sit next to each other now
 #pragma unroll
         for (int i = 1; i < D; ++i) dup |= (unsigned)(x[i] == x[i - 1]);
@@ -788,6 +828,7 @@ __device__ __forceinline__ void w64_ds(const Tile16Args &a, const W64 &w, cint_p
         } else {
             t = sorted_runs_decide<D>(x, M, bk, need);
         }
+#endif
     }
     if (__builtin_amdgcn_ballot_w64(need)) {  // rare: wave-uniform branch
         Img16 im;
@@ -965,11 +1006,11 @@ __device__ __forceinline__ int mid16_exact(const Mid16Args &a, const int *__rest
     int br = INT_MIN, bn = INT_MAX;
 #pragma unroll 1
     for (int e = 0; e < d; ++e) {
-        const int ne = ld32(a.assign, (unsigned)nb[e] * S + (unsigned)s);
+        const int ne = a.assign[(size_t)nb[e] * S + (unsigned)s];
         if ((unsigned)ne >= N || ld16(a.code, (unsigned)ne * S + (unsigned)s) != bk) continue;
         int cnt = 0;
 #pragma unroll 1
-        for (int i = 0; i < d; ++i) cnt += ld32(a.assign, (unsigned)nb[i] * S + (unsigned)s) == ne;
+        for (int i = 0; i < d; ++i) cnt += a.assign[(size_t)nb[i] * S + (unsigned)s] == ne;
         if (cnt != M) continue;
         const int ex = a.cap[ne] - ld32(a.use, (unsigned)ne * S + (unsigned)s);
         if (ex > br || (ex == br && ne < bn)) { br = ex; bn = ne; }
@@ -984,7 +1025,9 @@ __device__ __forceinline__ void mid16_row(const Mid16Args &a, const int *__restr
     const int4 *r4 = reinterpret_cast<const int4 *>(rec);
     const int2 hd = *reinterpret_cast<const int2 *>(rec);
     const int oi = hd.x, d = hd.y;
-    int v[D];
+    // assignments: pads (j >= d) and values outside [0, N) become node N, whose
+    // code row is zero (never a candidate)
+    unsigned x[D];
 #pragma unroll
     for (int w = 0; w < W / 4; ++w) {
         const int4 q4 = r4[w];
@@ -992,21 +1035,26 @@ __device__ __forceinline__ void mid16_row(const Mid16Args &a, const int *__restr
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int j = 4 * w + t - 2;
-            if (j >= 0 && j < D) v[j] = ld32(a.assign, (unsigned)(j < d ? q[t] : 0) * S + (unsigned)s_ld);
+            if (j >= 0 && j < D) x[j] = (unsigned)a.assign[(size_t)(j < d ? q[t] : 0) * S + (unsigned)s_ld];
         }
     }
-    unsigned x[D];
 #pragma unroll
-    for (int j = 0; j < D; ++j) {
-        const bool ok = j < d && (unsigned)v[j] < N;
-        const unsigned cd = ld16(a.code, ok ? (unsigned)v[j] * S + (unsigned)s_ld : 0u);
-        x[j] = ok ? ((cd << 16) | (unsigned)v[j]) : kCellPad;
+    for (int j = 0; j < D; ++j) x[j] = j < d ? min(x[j], N) : N;
+    // code gathers, all in flight
+    constexpr int kC = D;
+#pragma unroll
+    for (int j0 = 0; j0 < D; j0 += kC) {
+        unsigned cd[kC];
+#pragma unroll
+        for (int t = 0; t < kC; ++t) cd[t] = ld16(a.code, x[j0 + t] * S + (unsigned)s_ld);
+#pragma unroll
+        for (int t = 0; t < kC; ++t) x[j0 + t] |= cd[t] << 16;
     }
     bitonic_sort<D, unsigned>(x);
     int sc;
     unsigned bk;
     bool need;
-    int t = sorted_runs_decide<D>(x, sc, bk, need);
+    int t = sorted_runs<D>(x, sc, bk, need);
     if (__builtin_amdgcn_ballot_w64(need)) {  // rare: wave-uniform branch
         const int te = mid16_exact(a, rec + 2, d, s_ld, sc, bk);
         t = need ? te : t;
@@ -1040,7 +1088,7 @@ int launch_mid16(hipStream_t stream, const Mid16Args &a0) {
     Mid16Args a = a0;
     a.SL = std::min(a.S, 64);
     a.PS = 64 / a.SL;
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 1; b >= 0; --b) {  // the longest rows first
         const int n = a.n_items[b];
         if (n == 0) continue;
         const int waves = (int)ceil_div(n, a.PS);

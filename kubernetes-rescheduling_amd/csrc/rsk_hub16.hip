@@ -1,0 +1,354 @@
+// rsk_hub16.hip — CAR for the hub rows of the compact path (N <= 65535): rows
+// above the mid classes (degree 65..kHubMax), in three launches by degree
+// (65..128, 129..256, 257..kHubMax).
+//
+// Reference: the score loop + argmax of `communication`,
+// rescheduling.py:183-214 (see rsk_car.hip for the full statement).
+//
+// Work item = (row, group of G = 2^lg scenarios) with d * G <= 4096, one
+// workgroup of kHW waves:
+//   stage   the G x d cells (code << 16 | node) in LDS, every thread up to kHB
+//           (neighbour, scenario) elements with all loads in flight: neighbour
+//           id (plan) -> assign word -> 16-bit code gather (an assignment
+//           outside [0, N) reads the zero code row N: never a candidate);
+//   count   one wave per scenario, lanes = neighbours: counters in the wave's
+//           LDS table — direct and node-indexed (u8 for degree <= 255, else
+//           u16) or an open-addressing hash of (node + 1) << 16 | count words,
+//           whichever is smaller for the launch;
+//   decide  one u64 DPP max over (count, code, -node) gives the best node; a
+//           ballot tells whether another node reaches the same count (a tie:
+//           the best code decides, None when it is code 1 = rem < 0) and
+//           whether it shares an inexact code (rare: exact cap - use).
+#include <algorithm>
+#include <climits>
+#include <cstdlib>
+
+#include "rsk_car.h"
+
+namespace rsk {
+
+constexpr int kHW = 4;      // waves per workgroup
+constexpr int kHT = 64 * kHW;
+constexpr int kHB = 16;     // staging elements in flight per thread
+constexpr int kHStage = kHT * kHB;  // cells per work item (d * G <= kHStage)
+
+enum { kTabU8 = 0, kTabU16 = 1, kTabHash = 2 };
+
+template <int kTab>
+struct HubTab16 {
+    unsigned *w;
+    unsigned mask;  // hash: slots - 1
+    int shift;      // hash: 32 - log2(slots)
+    __device__ __forceinline__ void add(int n) const {
+        if (kTab == kTabU8) {
+            atomicAdd(&w[n >> 2], 1u << ((n & 3) * 8));
+        } else if (kTab == kTabU16) {
+            atomicAdd(&w[n >> 1], 1u << ((n & 1) * 16));
+        } else {
+            const unsigned k = (unsigned)n + 1u;
+            unsigned h = (k * 2654435761u) >> shift;
+            while (true) {
+                const unsigned prev = atomicCAS(&w[h], 0u, (k << 16) | 1u);
+                if (prev == 0u) return;
+                if ((prev >> 16) == k) { atomicAdd(&w[h], 1u); return; }
+                h = (h + 1u) & mask;
+            }
+        }
+    }
+    __device__ __forceinline__ int get(int n) const {  // n was added
+        if (kTab == kTabU8) return (int)((w[n >> 2] >> ((n & 3) * 8)) & 0xffu);
+        if (kTab == kTabU16) return (int)((w[n >> 1] >> ((n & 1) * 16)) & 0xffffu);
+        const unsigned k = (unsigned)n + 1u;
+        unsigned h = (k * 2654435761u) >> shift;
+        unsigned x = w[h];
+        while ((x >> 16) != k) {
+            h = (h + 1u) & mask;
+            x = w[h];
+        }
+        return (int)(x & 0xffffu);
+    }
+    // direct tables: zero the counter word of n (every other node in that
+    // word is one of this scenario's entries, cleared too); hash: see caller
+    __device__ __forceinline__ void clear(int n) const {
+        if (kTab == kTabU8) w[n >> 2] = 0u;
+        else if (kTab == kTabU16) w[n >> 1] = 0u;
+    }
+};
+
+// Running best (count, code, -node) key over a lane's entries (count 0 = not
+// a candidate).
+struct HubDecide {
+    unsigned long long best;
+    __device__ __forceinline__ void init() { best = 0ull; }
+    __device__ __forceinline__ void put(unsigned x, int cnt) {
+        const unsigned long long k = cnt ? ((unsigned long long)cnt << 32) | (unsigned long long)cell_cand(x) : 0ull;
+        best = k > best ? k : best;
+    }
+};
+
+// Rare path: among the entries at count M with the inexact code bk, the node
+// with the largest exact remaining CPU, then the lower index.  Reads counts,
+// so it runs before the table is cleared.
+template <int kTab>
+__device__ __forceinline__ int hub16_exact(const Hub16Args &a, const HubTab16<kTab> &tb, const unsigned *cs, int d,
+                                           int M, unsigned bk, int s, int lane) {
+    unsigned long long kx = 0ull;
+    for (int j = lane; j < d; j += 64) {
+        const unsigned x = cs[j];
+        if (cell_code(x) == bk && tb.get(cell_node(x)) == M) {
+            const int nd = cell_node(x);
+            const int rem = a.cap[nd] - ld32(a.use, (unsigned)nd * (unsigned)a.S + (unsigned)s);
+            const unsigned long long k = pack_rn(rem, nd);
+            kx = k > kx ? k : kx;
+        }
+    }
+    kx = dpp_max_u64(kx);
+    return (int)(kNodeMask - (unsigned)(kx & kNodeMask));
+}
+
+// Output of one scenario from its reduced state (rescheduling.py:199-214).
+__device__ __forceinline__ void hub16_emit(const Hub16Args &a, int oi, int s, int M, unsigned bw, bool any_tie,
+                                           bool any_amb, int ex) {
+    const unsigned bk = cell_code(bw);
+    int t, sc = 0;
+    if (M == 0) {
+        t = zero_target(load_zc(a.zc_cnt, a.zc_key, s), sc);
+    } else {
+        sc = M;
+        t = !any_tie ? cand_node(bw) : (bk >= 2u ? cand_node(bw) : RSK_TARGET_NONE);
+        if (any_tie && any_amb && code_inexact(bk)) t = ex;
+    }
+    const size_t o = (size_t)oi * (unsigned)a.S + (unsigned)s;
+    a.out_target[o] = t;
+    if (a.out_score) a.out_score[o] = sc;
+}
+
+template <int kTab>
+__device__ __forceinline__ void tab_wipe(const HubTab16<kTab> &tb, int H, int lane) {
+    if (kTab == kTabHash) {  // a probe may pass any slot: wipe the whole table
+        uint4 *w4 = reinterpret_cast<uint4 *>(tb.w);
+        for (int k = lane; k < (H >> 2); k += 64) w4[k] = make_uint4(0u, 0u, 0u, 0u);
+    }
+}
+
+// NS scenarios of a row of degree d <= 64 * NJ at once (independent chains
+// the scheduler interleaves): entries and their counts in registers, one
+// table per scenario.  cs[k] = the staged cells of scenario k (null: none).
+template <int kTab, int NJ, int NS>
+__device__ __forceinline__ void hub16_multi(const Hub16Args &a, const HubTab16<kTab> (&tb)[NS],
+                                            const unsigned *const (&cs)[NS], int d, int oi, int s0, int lane) {
+    unsigned x[NS][NJ];
+    int c[NS][NJ];
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+#pragma unroll
+        for (int i = 0; i < NJ; ++i) {
+            const int j = i * 64 + lane;
+            x[k][i] = cs[k] ? cs[k][min(j, d - 1)] : kCellPad;
+            if (j >= d) x[k][i] = kCellPad;
+        }
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+#pragma unroll
+        for (int i = 0; i < NJ; ++i)
+            if (cell_code(x[k][i]) != kCodeHaz) tb[k].add(cell_node(x[k][i]));
+    unsigned long long best[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        HubDecide h;
+        h.init();
+#pragma unroll
+        for (int i = 0; i < NJ; ++i) {
+            c[k][i] = cell_code(x[k][i]) != kCodeHaz ? tb[k].get(cell_node(x[k][i])) : 0;
+            h.put(x[k][i], c[k][i]);
+        }
+        best[k] = h.best;
+    }
+#pragma unroll
+    for (int k = 0; k < NS; ++k) best[k] = dpp_max_u64(best[k]);
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        const int M = (int)(best[k] >> 32);
+        const unsigned bw = (unsigned)best[k];
+        const int bn = cand_node(bw);
+        const unsigned bk = cell_code(bw);
+        bool tie = false, amb = false;
+#pragma unroll
+        for (int i = 0; i < NJ; ++i) {
+            const bool o = c[k][i] == M && M > 0 && cell_node(x[k][i]) != bn;
+            tie = tie || o;
+            amb = amb || (o && cell_code(x[k][i]) == bk);
+        }
+        const bool any_tie = __builtin_amdgcn_ballot_w64(tie) != 0ull;
+        const bool any_amb = __builtin_amdgcn_ballot_w64(amb) != 0ull;
+        int ex = -1;
+        if (any_tie && any_amb && code_inexact(bk)) ex = hub16_exact<kTab>(a, tb[k], cs[k], d, M, bk, s0 + k, lane);
+        if (lane == k && cs[k]) hub16_emit(a, oi, s0 + k, M, bw, any_tie, any_amb, ex);
+    }
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        if (kTab != kTabHash) {
+#pragma unroll
+            for (int i = 0; i < NJ; ++i)
+                if (cell_code(x[k][i]) != kCodeHaz) tb[k].clear(cell_node(x[k][i]));
+        }
+        tab_wipe<kTab>(tb[k], a.H, lane);
+    }
+}
+
+// One scenario of a row of any degree: entries re-read from the staged cells.
+template <int kTab>
+__device__ __forceinline__ void hub16_scenario(const Hub16Args &a, const HubTab16<kTab> &tb, const unsigned *cs, int d,
+                                               int oi, int s, int lane) {
+    for (int j = lane; j < d; j += 64) {
+        const unsigned x = cs[j];
+        if (cell_code(x) != kCodeHaz) tb.add(cell_node(x));
+    }
+    HubDecide h;
+    h.init();
+    for (int j = lane; j < d; j += 64) {
+        const unsigned x = cs[j];
+        h.put(x, cell_code(x) != kCodeHaz ? tb.get(cell_node(x)) : 0);
+    }
+    const unsigned long long best = dpp_max_u64(h.best);
+    const int M = (int)(best >> 32);
+    const unsigned bw = (unsigned)best;
+    const int bn = cand_node(bw);
+    const unsigned bk = cell_code(bw);
+    bool tie = false, amb = false;
+    if (M > 0) {
+        for (int j = lane; j < d; j += 64) {
+            const unsigned x = cs[j];
+            if (cell_code(x) != kCodeHaz && cell_node(x) != bn && tb.get(cell_node(x)) == M) {
+                tie = true;
+                amb = amb || cell_code(x) == bk;
+            }
+        }
+    }
+    const bool any_tie = __builtin_amdgcn_ballot_w64(tie) != 0ull;
+    const bool any_amb = __builtin_amdgcn_ballot_w64(amb) != 0ull;
+    int ex = -1;
+    if (any_tie && any_amb && code_inexact(bk)) ex = hub16_exact<kTab>(a, tb, cs, d, M, bk, s, lane);
+    if (kTab != kTabHash) {
+        for (int j = lane; j < d; j += 64) {
+            const unsigned x = cs[j];
+            if (cell_code(x) != kCodeHaz) tb.clear(cell_node(x));
+        }
+    }
+    tab_wipe<kTab>(tb, a.H, lane);
+    if (lane == 0) hub16_emit(a, oi, s, M, bw, any_tie, any_amb, ex);
+}
+
+template <int kTab, int NJ, int NS>
+__global__ __launch_bounds__(kHT) void car_hub16_kernel(Hub16Args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned hlds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const cint_ptr it = const_ptr(a.items) + (size_t)blockIdx.x * 4;
+    const int oi = it[0], rb = it[1], d = it[2], gw = it[3];
+    const int s0 = gw & 0xffffff, lg = gw >> 24;
+    const int G = 1 << lg;
+    const unsigned S = (unsigned)a.S, N = (unsigned)a.N;
+    unsigned *col = hlds;  // [G][d], d * G <= kHStage
+    HubTab16<kTab> tb[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        tb[k].w = hlds + kHStage + (wave * NS + k) * a.H;
+        tb[k].mask = (unsigned)a.H - 1u;
+        tb[k].shift = a.hshift;
+    }
+
+    {   // stage: element e -> (neighbour j = e >> lg, scenario si = e & (G - 1)),
+        // one batch, loads unconditional (clamped)
+        const int total = d << lg;
+        int e[kHB], n[kHB];
+        unsigned c[kHB];
+#pragma unroll
+        for (int u = 0; u < kHB; ++u) {
+            e[u] = min(u * kHT + tid, total - 1);
+            n[u] = a.hcol[rb + (e[u] >> lg)];
+        }
+#pragma unroll
+        for (int u = 0; u < kHB; ++u) {
+            const unsigned s = min((unsigned)(s0 + (e[u] & (G - 1))), S - 1u);
+            n[u] = a.assign[(size_t)n[u] * S + s];
+        }
+#pragma unroll
+        for (int u = 0; u < kHB; ++u) {
+            const unsigned s = min((unsigned)(s0 + (e[u] & (G - 1))), S - 1u);
+            n[u] = (int)min((unsigned)n[u], N);
+            c[u] = ld16(a.code, (unsigned)n[u] * S + s);
+        }
+#pragma unroll
+        for (int u = 0; u < kHB; ++u)
+            if (u * kHT + tid < total) col[(e[u] & (G - 1)) * d + (e[u] >> lg)] = (c[u] << 16) | (unsigned)n[u];
+        // zero the tables (each wave's clears keep them zero between scenarios)
+        uint4 *t4 = reinterpret_cast<uint4 *>(hlds + kHStage);
+        for (int k = tid; k < (kHW * NS * a.H) >> 2; k += kHT) t4[k] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    __syncthreads();
+    if constexpr (NJ > 0) {
+        for (int sb = wave * NS; sb < G && s0 + sb < a.S; sb += kHW * NS) {
+            const unsigned *cs[NS];
+#pragma unroll
+            for (int k = 0; k < NS; ++k) cs[k] = (sb + k < G && s0 + sb + k < a.S) ? col + (sb + k) * d : nullptr;
+            hub16_multi<kTab, NJ, NS>(a, tb, cs, d, oi, s0 + sb, lane);
+        }
+    } else {
+        for (int si = wave; si < G && s0 + si < a.S; si += kHW)
+            hub16_scenario<kTab>(a, tb[0], col + si * d, d, oi, s0 + si, lane);
+    }
+}
+
+Hub16Geom hub16_geometry(int dmax, int N) {
+    Hub16Geom g;
+    g.dmax = dmax;
+    const int direct = dmax <= 255 ? (N + 3) / 4 : (N + 1) / 2;  // u8 / u16 counter words
+    int H = 64;
+    while (H < 2 * dmax) H <<= 1;
+    static const int force = [] { const char *e = getenv("RSK_HUB16_TABLE"); return e ? atoi(e) : -1; }();
+    const bool use_hash = force >= 0 ? force == kTabHash : H < direct;
+    if (use_hash) {
+        g.tab = kTabHash;
+        g.H = H;
+        int l = 0;
+        while ((1 << l) < H) ++l;
+        g.hshift = 32 - l;
+    } else {
+        g.tab = dmax <= 255 ? kTabU8 : kTabU16;
+        g.H = (direct + 3) & ~3;
+        g.hshift = 0;
+    }
+    g.nj = dmax <= 128 ? 2 : (dmax <= 256 ? 4 : 0);
+    static const int ns_env = [] { const char *e = getenv("RSK_HUB16_NS"); return e ? atoi(e) : 0; }();
+    g.ns = g.nj == 0 ? 1 : (ns_env == 1 || ns_env == 2 || ns_env == 4 ? ns_env : (g.nj == 2 ? 4 : 2));
+    g.lds = ((size_t)kHStage + (size_t)kHW * g.ns * g.H) * 4;
+    return g;
+}
+
+int hub16_lg(int d, int S) {  // log2 of the scenario group of a degree-d row
+    int lg = 0;
+    while (lg < 6 && ((int64_t)d << (lg + 1)) <= kHStage && (1 << lg) < S) ++lg;
+    return lg;
+}
+
+int launch_hub16(hipStream_t stream, const Hub16Args &a, const Hub16Geom &g, int n_items) {
+    if (n_items == 0) return RSK_OK;
+    RSK_CHECK(g.dmax <= kHStage, "hub row degree %d exceeds %d", g.dmax, kHStage);
+    RSK_CHECK(g.lds <= 160 * 1024, "hub rows need %zu B of LDS", g.lds);
+    using K = void (*)(Hub16Args);
+#define RSK_HUB16_NS(T, J)                                                                           \
+    (g.ns == 4 ? &car_hub16_kernel<T, J, 4> : g.ns == 2 ? &car_hub16_kernel<T, J, 2> : &car_hub16_kernel<T, J, 1>)
+#define RSK_HUB16_NJ(T) (g.nj == 2 ? RSK_HUB16_NS(T, 2) : g.nj == 4 ? RSK_HUB16_NS(T, 4) : &car_hub16_kernel<T, 0, 1>)
+    const K kern = g.tab == kTabU8 ? RSK_HUB16_NJ(kTabU8) : g.tab == kTabU16 ? RSK_HUB16_NJ(kTabU16) : RSK_HUB16_NJ(kTabHash);
+#undef RSK_HUB16_NJ
+#undef RSK_HUB16_NS
+    if (g.lds > 64 * 1024)
+        RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)g.lds));
+    kern<<<dim3((unsigned)n_items), dim3(kHT), g.lds, stream>>>(a);
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
+}
+
+}  // namespace rsk
