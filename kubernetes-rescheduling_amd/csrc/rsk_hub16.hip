@@ -34,46 +34,81 @@ constexpr int kHStage = kHT * kHB;  // cells per work item (d * G <= kHStage)
 
 enum { kTabU8 = 0, kTabU16 = 1, kTabHash = 2 };
 
+// A wave's count table for one scenario.  Every call takes the entry's
+// candidate flag and is branch-free for the lanes without one (they touch word
+// 0 of a direct table with a zero increment, or the hash table's sink word H),
+// so the compiler emits no exec-mask branches around the LDS traffic.
 template <int kTab>
 struct HubTab16 {
     unsigned *w;
-    unsigned mask;  // hash: slots - 1
+    unsigned mask;  // hash: slots - 1 (the sink word H = mask + 1 follows)
     int shift;      // hash: 32 - log2(slots)
-    __device__ __forceinline__ void add(int n) const {
+    __device__ __forceinline__ unsigned home(unsigned k) const { return (k * 2654435761u) >> shift; }
+    __device__ __forceinline__ void add(int n, bool cand) const {
         if (kTab == kTabU8) {
-            atomicAdd(&w[n >> 2], 1u << ((n & 3) * 8));
+            atomicAdd(&w[cand ? n >> 2 : 0], cand ? 1u << ((n & 3) * 8) : 0u);
         } else if (kTab == kTabU16) {
-            atomicAdd(&w[n >> 1], 1u << ((n & 1) * 16));
+            atomicAdd(&w[cand ? n >> 1 : 0], cand ? 1u << ((n & 1) * 16) : 0u);
         } else {
+            // first probe: claim the home slot, or add 1 to it when it holds
+            // the key (0 otherwise); collided lanes walk the chain
             const unsigned k = (unsigned)n + 1u;
-            unsigned h = (k * 2654435761u) >> shift;
-            while (true) {
-                const unsigned prev = atomicCAS(&w[h], 0u, (k << 16) | 1u);
-                if (prev == 0u) return;
-                if ((prev >> 16) == k) { atomicAdd(&w[h], 1u); return; }
-                h = (h + 1u) & mask;
+            unsigned h = cand ? home(k) : mask + 1u;
+            unsigned prev = atomicCAS(&w[h], 0u, (k << 16) | 1u);
+            bool hit = cand && prev != 0u && (prev >> 16) == k;
+            atomicAdd(&w[h], hit ? 1u : 0u);
+            bool more = cand && prev != 0u && !hit;
+            if (__builtin_amdgcn_ballot_w64(more)) {
+                while (more) {
+                    h = (h + 1u) & mask;
+                    prev = atomicCAS(&w[h], 0u, (k << 16) | 1u);
+                    hit = prev != 0u && (prev >> 16) == k;
+                    if (hit) atomicAdd(&w[h], 1u);
+                    more = prev != 0u && !hit;
+                }
             }
         }
     }
-    __device__ __forceinline__ int get(int n) const {  // n was added
-        if (kTab == kTabU8) return (int)((w[n >> 2] >> ((n & 3) * 8)) & 0xffu);
-        if (kTab == kTabU16) return (int)((w[n >> 1] >> ((n & 1) * 16)) & 0xffffu);
-        const unsigned k = (unsigned)n + 1u;
-        unsigned h = (k * 2654435761u) >> shift;
-        unsigned x = w[h];
-        while ((x >> 16) != k) {
-            h = (h + 1u) & mask;
-            x = w[h];
+    __device__ __forceinline__ int get(int n, bool cand) const {  // 0 when !cand
+        unsigned v;
+        if (kTab == kTabU8) {
+            v = (w[cand ? n >> 2 : 0] >> ((n & 3) * 8)) & 0xffu;
+        } else if (kTab == kTabU16) {
+            v = (w[cand ? n >> 1 : 0] >> ((n & 1) * 16)) & 0xffffu;
+        } else {
+            const unsigned k = (unsigned)n + 1u;
+            unsigned h = cand ? home(k) : mask + 1u;
+            unsigned x = w[h];
+            bool miss = cand && (x >> 16) != k;
+            if (__builtin_amdgcn_ballot_w64(miss)) {
+                while (miss) {
+                    h = (h + 1u) & mask;
+                    x = w[h];
+                    miss = (x >> 16) != k;
+                }
+            }
+            v = x & 0xffffu;
         }
-        return (int)(x & 0xffffu);
+        return cand ? (int)v : 0;
     }
     // direct tables: zero the counter word of n (every other node in that
-    // word is one of this scenario's entries, cleared too); hash: see caller
-    __device__ __forceinline__ void clear(int n) const {
-        if (kTab == kTabU8) w[n >> 2] = 0u;
-        else if (kTab == kTabU16) w[n >> 1] = 0u;
+    // word is one of this scenario's entries, cleared too; word 0 gets zeroed
+    // by the lanes without a candidate); hash: the caller wipes the table
+    __device__ __forceinline__ void clear(int n, bool cand) const {
+        if (kTab == kTabU8) w[cand ? n >> 2 : 0] = 0u;
+        else if (kTab == kTabU16) w[cand ? n >> 1 : 0] = 0u;
     }
 };
+
+__device__ __forceinline__ unsigned dpp_max_u32(unsigned v) {  // identity 0
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+    return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+}
 
 // Running best (count, code, -node) key over a lane's entries (count 0 = not
 // a candidate).
@@ -95,7 +130,7 @@ __device__ __forceinline__ int hub16_exact(const Hub16Args &a, const HubTab16<kT
     unsigned long long kx = 0ull;
     for (int j = lane; j < d; j += 64) {
         const unsigned x = cs[j];
-        if (cell_code(x) == bk && tb.get(cell_node(x)) == M) {
+        if (cell_code(x) == bk && tb.get(cell_node(x), true) == M) {
             const int nd = cell_node(x);
             const int rem = a.cap[nd] - ld32(a.use, (unsigned)nd * (unsigned)a.S + (unsigned)s);
             const unsigned long long k = pack_rn(rem, nd);
@@ -127,7 +162,7 @@ template <int kTab>
 __device__ __forceinline__ void tab_wipe(const HubTab16<kTab> &tb, int H, int lane) {
     if (kTab == kTabHash) {  // a probe may pass any slot: wipe the whole table
         uint4 *w4 = reinterpret_cast<uint4 *>(tb.w);
-        for (int k = lane; k < (H >> 2); k += 64) w4[k] = make_uint4(0u, 0u, 0u, 0u);
+        for (int k = lane; k <= (H >> 2); k += 64) w4[k] = make_uint4(0u, 0u, 0u, 0u);  // + the sink
     }
 }
 
@@ -150,47 +185,50 @@ __device__ __forceinline__ void hub16_multi(const Hub16Args &a, const HubTab16<k
 #pragma unroll
     for (int k = 0; k < NS; ++k)
 #pragma unroll
-        for (int i = 0; i < NJ; ++i)
-            if (cell_code(x[k][i]) != kCodeHaz) tb[k].add(cell_node(x[k][i]));
-    unsigned long long best[NS];
+        for (int i = 0; i < NJ; ++i) tb[k].add(cell_node(x[k][i]), cell_code(x[k][i]) != kCodeHaz);
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+#pragma unroll
+        for (int i = 0; i < NJ; ++i) c[k][i] = tb[k].get(cell_node(x[k][i]), cell_code(x[k][i]) != kCodeHaz);
+    // the maximal count, then the best (code, -node) word at it: two 32-bit DPP maxima
+    int M[NS];
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
-        HubDecide h;
-        h.init();
+        int m = 0;
 #pragma unroll
-        for (int i = 0; i < NJ; ++i) {
-            c[k][i] = cell_code(x[k][i]) != kCodeHaz ? tb[k].get(cell_node(x[k][i])) : 0;
-            h.put(x[k][i], c[k][i]);
-        }
-        best[k] = h.best;
+        for (int i = 0; i < NJ; ++i) m = max(m, c[k][i]);
+        M[k] = dpp_max(m);
+    }
+    unsigned bw[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        unsigned v = 0u;
+#pragma unroll
+        for (int i = 0; i < NJ; ++i) v = max(v, c[k][i] == M[k] && M[k] > 0 ? cell_cand(x[k][i]) : 0u);
+        bw[k] = dpp_max_u32(v);
     }
 #pragma unroll
-    for (int k = 0; k < NS; ++k) best[k] = dpp_max_u64(best[k]);
-#pragma unroll
     for (int k = 0; k < NS; ++k) {
-        const int M = (int)(best[k] >> 32);
-        const unsigned bw = (unsigned)best[k];
-        const int bn = cand_node(bw);
-        const unsigned bk = cell_code(bw);
+        const int bn = cand_node(bw[k]);
+        const unsigned bk = cell_code(bw[k]);
         bool tie = false, amb = false;
 #pragma unroll
         for (int i = 0; i < NJ; ++i) {
-            const bool o = c[k][i] == M && M > 0 && cell_node(x[k][i]) != bn;
+            const bool o = c[k][i] == M[k] && M[k] > 0 && cell_node(x[k][i]) != bn;
             tie = tie || o;
             amb = amb || (o && cell_code(x[k][i]) == bk);
         }
         const bool any_tie = __builtin_amdgcn_ballot_w64(tie) != 0ull;
         const bool any_amb = __builtin_amdgcn_ballot_w64(amb) != 0ull;
         int ex = -1;
-        if (any_tie && any_amb && code_inexact(bk)) ex = hub16_exact<kTab>(a, tb[k], cs[k], d, M, bk, s0 + k, lane);
-        if (lane == k && cs[k]) hub16_emit(a, oi, s0 + k, M, bw, any_tie, any_amb, ex);
+        if (any_tie && any_amb && code_inexact(bk)) ex = hub16_exact<kTab>(a, tb[k], cs[k], d, M[k], bk, s0 + k, lane);
+        if (lane == k && cs[k]) hub16_emit(a, oi, s0 + k, M[k], bw[k], any_tie, any_amb, ex);
     }
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
         if (kTab != kTabHash) {
 #pragma unroll
-            for (int i = 0; i < NJ; ++i)
-                if (cell_code(x[k][i]) != kCodeHaz) tb[k].clear(cell_node(x[k][i]));
+            for (int i = 0; i < NJ; ++i) tb[k].clear(cell_node(x[k][i]), cell_code(x[k][i]) != kCodeHaz);
         }
         tab_wipe<kTab>(tb[k], a.H, lane);
     }
@@ -202,13 +240,13 @@ __device__ __forceinline__ void hub16_scenario(const Hub16Args &a, const HubTab1
                                                int oi, int s, int lane) {
     for (int j = lane; j < d; j += 64) {
         const unsigned x = cs[j];
-        if (cell_code(x) != kCodeHaz) tb.add(cell_node(x));
+        tb.add(cell_node(x), cell_code(x) != kCodeHaz);
     }
     HubDecide h;
     h.init();
     for (int j = lane; j < d; j += 64) {
         const unsigned x = cs[j];
-        h.put(x, cell_code(x) != kCodeHaz ? tb.get(cell_node(x)) : 0);
+        h.put(x, tb.get(cell_node(x), cell_code(x) != kCodeHaz));
     }
     const unsigned long long best = dpp_max_u64(h.best);
     const int M = (int)(best >> 32);
@@ -219,7 +257,7 @@ __device__ __forceinline__ void hub16_scenario(const Hub16Args &a, const HubTab1
     if (M > 0) {
         for (int j = lane; j < d; j += 64) {
             const unsigned x = cs[j];
-            if (cell_code(x) != kCodeHaz && cell_node(x) != bn && tb.get(cell_node(x)) == M) {
+            if (cell_code(x) != kCodeHaz && cell_node(x) != bn && tb.get(cell_node(x), true) == M) {
                 tie = true;
                 amb = amb || cell_code(x) == bk;
             }
@@ -232,7 +270,7 @@ __device__ __forceinline__ void hub16_scenario(const Hub16Args &a, const HubTab1
     if (kTab != kTabHash) {
         for (int j = lane; j < d; j += 64) {
             const unsigned x = cs[j];
-            if (cell_code(x) != kCodeHaz) tb.clear(cell_node(x));
+            tb.clear(cell_node(x), cell_code(x) != kCodeHaz);
         }
     }
     tab_wipe<kTab>(tb, a.H, lane);
@@ -253,7 +291,7 @@ __global__ __launch_bounds__(kHT) void car_hub16_kernel(Hub16Args a) {
     HubTab16<kTab> tb[NS];
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
-        tb[k].w = hlds + kHStage + (wave * NS + k) * a.H;
+        tb[k].w = hlds + kHStage + (wave * NS + k) * (a.H + 4);
         tb[k].mask = (unsigned)a.H - 1u;
         tb[k].shift = a.hshift;
     }
@@ -284,7 +322,7 @@ __global__ __launch_bounds__(kHT) void car_hub16_kernel(Hub16Args a) {
             if (u * kHT + tid < total) col[(e[u] & (G - 1)) * d + (e[u] >> lg)] = (c[u] << 16) | (unsigned)n[u];
         // zero the tables (each wave's clears keep them zero between scenarios)
         uint4 *t4 = reinterpret_cast<uint4 *>(hlds + kHStage);
-        for (int k = tid; k < (kHW * NS * a.H) >> 2; k += kHT) t4[k] = make_uint4(0u, 0u, 0u, 0u);
+        for (int k = tid; k < (kHW * NS * (a.H + 4)) >> 2; k += kHT) t4[k] = make_uint4(0u, 0u, 0u, 0u);
     }
     __syncthreads();
     if constexpr (NJ > 0) {
@@ -307,7 +345,9 @@ Hub16Geom hub16_geometry(int dmax, int N) {
     int H = 64;
     while (H < 2 * dmax) H <<= 1;
     static const int force = [] { const char *e = getenv("RSK_HUB16_TABLE"); return e ? atoi(e) : -1; }();
-    const bool use_hash = force >= 0 ? force == kTabHash : H < direct;
+    // direct tables (no probe chains, the fastest per scenario) while four of
+    // them fit 48 KiB beside the staging area; the hash beyond (large N)
+    const bool use_hash = force >= 0 ? force == kTabHash : (size_t)kHW * (direct + 4) * 4 > 48 * 1024;
     if (use_hash) {
         g.tab = kTabHash;
         g.H = H;
@@ -321,8 +361,9 @@ Hub16Geom hub16_geometry(int dmax, int N) {
     }
     g.nj = dmax <= 128 ? 2 : (dmax <= 256 ? 4 : 0);
     static const int ns_env = [] { const char *e = getenv("RSK_HUB16_NS"); return e ? atoi(e) : 0; }();
-    g.ns = g.nj == 0 ? 1 : (ns_env == 1 || ns_env == 2 || ns_env == 4 ? ns_env : (g.nj == 2 ? 4 : 2));
-    g.lds = ((size_t)kHStage + (size_t)kHW * g.ns * g.H) * 4;
+    // scenarios per wave at once: 1 with direct tables (LDS-bound), 2 with the hash (measured)
+    g.ns = g.nj == 0 ? 1 : (ns_env == 1 || ns_env == 2 || ns_env == 4 ? ns_env : (use_hash ? 2 : 1));
+    g.lds = ((size_t)kHStage + (size_t)kHW * g.ns * (g.H + 4)) * 4;  // tables: H words + sink / padding
     return g;
 }
 
