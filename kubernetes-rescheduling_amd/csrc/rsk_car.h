@@ -188,6 +188,37 @@ __device__ __forceinline__ void bitonic_sort(T (&v)[D]) {
         }
 }
 
+// Batcher's odd-even merge sort, ascending: the same register-only
+// compare-exchanges as bitonic_sort but fewer of them (D = 32: 191 instead of
+// 240; D = 64: 543 instead of 672).
+template <int D, class T>
+__device__ __forceinline__ void oem_sort(T (&v)[D]) {
+#pragma unroll
+    for (int p = 1; p < D; p += p)
+#pragma unroll
+        for (int k = p; k >= 1; k >>= 1) {
+#pragma unroll
+            for (int j = k % p; j + k < D; j += 2 * k)
+#pragma unroll
+                for (int i = 0; i < k; ++i)
+                    if (i + j + k < D && (i + j) / (2 * p) == (i + j + k) / (2 * p)) {
+                        const T lo = min(v[i + j], v[i + j + k]), hi = max(v[i + j], v[i + j + k]);
+                        v[i + j] = lo;
+                        v[i + j + k] = hi;
+                    }
+            if (D >= 32) __builtin_amdgcn_sched_barrier(0);
+        }
+}
+
+#ifndef RSK_OEM_SORT
+#define RSK_OEM_SORT 1
+#endif
+template <int D, class T>
+__device__ __forceinline__ void sort_cells(T (&v)[D]) {
+    if (RSK_OEM_SORT) oem_sort<D, T>(v);
+    else bitonic_sort<D, T>(v);
+}
+
 // Next work unit of the wave: lane 0 bumps the workgroup's LDS counter.
 __device__ __forceinline__ int grab(int *ctr, int lane) {
     int k = 0;

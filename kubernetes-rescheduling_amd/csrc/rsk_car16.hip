@@ -799,7 +799,7 @@ __device__ __forceinline__ void w64_ds(const Tile16Args &a, const W64 &w, cint_p
             const int row = (i & 1) ? (int)(pr >> 16) : (int)(pr & 0xffffu);
             x[i] = i < d ? w.cell(row) : kCellPad - (unsigned)i;  // distinct pads (code 0)
         }
-        bitonic_sort<D, unsigned>(x);
+        sort_cells<D, unsigned>(x);
 #if RSK_RUNS_TOP2
         t = sorted_runs<D>(x, M, bk, need);
 #else
@@ -1050,7 +1050,7 @@ __device__ __forceinline__ void mid16_row(const Mid16Args &a, const int *__restr
 #pragma unroll
         for (int t = 0; t < kC; ++t) x[j0 + t] |= cd[t] << 16;
     }
-    bitonic_sort<D, unsigned>(x);
+    sort_cells<D, unsigned>(x);
     int sc;
     unsigned bk;
     bool need;

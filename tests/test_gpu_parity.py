@@ -425,13 +425,14 @@ def test_car_pivot_kernel_every_side_row():
 
 
 def test_car_slot_table_overflow(ctx):
-    """Rows of degree 33..128 at S >= 64 with every scenario drawing fresh
+    """Rows of degree 33..255 at S >= 64 with every scenario drawing fresh
     nodes out of 5000: thousands of distinct nodes per row and 64-scenario
     chunk (with RSK_SLOT=1 the slot table fills and the lanes that could not
-    insert recount exactly; by default car_mid / hub class 0)."""
+    insert recount exactly; by default car_mid16 / car_hub16)."""
     rng = np.random.default_rng(800)
     P, N, S = 3000, 5000, 128
-    rp, ci, a, cap, use, haz = _random_case(rng, P, N, S, max_deg=3, hub_deg=[33, 50, 64, 65, 100, 128], p_haz=0.1)
+    rp, ci, a, cap, use, haz = _random_case(rng, P, N, S, max_deg=3,
+                                            hub_deg=[33, 50, 64, 65, 100, 128, 129, 200, 254, 255], p_haz=0.1)
     _check_car(ctx, rp, ci, a, S, cap, use, haz, N, rows=np.arange(0, 40, dtype=np.int32), label="slot overflow")
     a2 = a.reshape(P, S).copy()
     a2[:, ::2] = a2[:, :1]            # half the scenarios share scenario 0's nodes: tables near the degree
