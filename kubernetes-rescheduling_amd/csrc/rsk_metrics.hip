@@ -12,7 +12,7 @@
 #include <cstring>
 #include <vector>
 
-#include "rsk_common.h"
+#include "rsk_car.h"  // rsk_common.h + const_ptr (scalar loads)
 
 namespace rsk {
 
@@ -346,6 +346,76 @@ __global__ __launch_bounds__(256) void cut_cost_kernel(const int *__restrict__ r
     // rows so no address sees more than blocks / kCutBins atomics)
     const unsigned long long v = threadIdx.x < nslot ? red[threadIdx.x] : 0ull;
     if (v) atomicAdd(&out[(size_t)(blockIdx.x % kCutBins) * S + (blockIdx.x * 256u + threadIdx.x) % (unsigned)S], v);
+}
+
+// The same count with lane = scenario (S >= 32), edge-balanced: the waves of
+// a 64-scenario chunk take fixed ranges of kCutEdges edges (grid-stride), so a
+// hub row's edges spread over many waves instead of one thread walking them
+// all (the thread-per-(rows, scenario) kernel above: 1.6 ms at 1M rows x 64
+// scenarios, its hub threads the tail).  A range finds its first row by a
+// scalar binary search over row_ptr; then per step up to 16 edges: the next 16
+// row ends and the 16 neighbour ids by scalar loads, each edge's row from the
+// ends by scalar compares, 32 coalesced assignment loads in flight (the row's
+// own value and the neighbour's).  The rows' missing terms go in 64-row
+// blocks, grid-stride as well.
+constexpr int kCutEdges = 512;
+__global__ __launch_bounds__(256) void cut_cost_wave_kernel(const int *__restrict__ row_ptr, const int *__restrict__ col,
+                                                            int r0, int r1, const int *__restrict__ assign, int S,
+                                                            const int *__restrict__ missing, int nw,
+                                                            unsigned long long *__restrict__ bins) {
+    const int lane = threadIdx.x & 63;
+    const int wv = (int)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int chunk = wv / nw, w = wv - chunk * nw;
+    if (chunk * 64 >= S) return;
+    const bool live = chunk * 64 + lane < S;
+    const size_t s = (size_t)min(chunk * 64 + lane, S - 1);
+    const cint_ptr rp = const_ptr(row_ptr), cl = const_ptr(col), ms = const_ptr(missing);
+    unsigned long long c = 0;
+    if (missing) {
+        for (int b0 = r0 + w * 64; b0 < r1; b0 += nw * 64)
+            for (int b = b0; b < min(b0 + 64, r1); b += 16) {
+                int ap[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) ap[i] = assign[(size_t)min(b + i, r1 - 1) * S + s];
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    if (b + i < r1 && ap[i] != -1) c += (unsigned long long)(unsigned)ms[b + i];
+            }
+    }
+    const int ea = rp[r0], eb = rp[r1];
+    for (int ka = ea + w * kCutEdges; ka < eb; ka += nw * kCutEdges) {
+        const int kb = min(ka + kCutEdges, eb);
+        int lo = r0, hi = r1 - 1;  // the row of edge ka: the last p with row_ptr[p] <= ka
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (rp[mid] <= ka) lo = mid;
+            else hi = mid - 1;
+        }
+        int p = lo, k0 = ka;
+        while (k0 < kb) {
+            int o[16];  // ends of rows p .. p + 15
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o[i] = rp[min(p + 1 + i, r1)];
+            const int kend = min(min(kb, k0 + 16), o[15]);
+            if (kend <= k0) { p += 16; continue; }  // 16 rows without edges here
+            int aq[16], am[16], last = 0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int k = min(k0 + j, kend - 1);
+                int r = 0;
+#pragma unroll
+                for (int i = 0; i < 15; ++i) r += o[i] <= k ? 1 : 0;
+                if (k0 + j < kend) last = r;
+                aq[j] = assign[(size_t)cl[k] * S + s];
+                am[j] = assign[(size_t)(p + r) * S + s];
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) c += (k0 + j < kend && am[j] != aq[j]) ? 1ull : 0ull;
+            p += last;
+            k0 = kend;
+        }
+    }
+    if (live && c) atomicAdd(&bins[(size_t)(wv % kCutBins) * S + s], c);
 }
 
 __global__ __launch_bounds__(256) void cut_bins_sum(const unsigned long long *__restrict__ bins, int S,
@@ -705,8 +775,17 @@ int rsk_cut_cost_rows(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_i
         auto *bins = ctx->work[4].as<unsigned long long>();
         RSK_HIP(hipMemsetAsync(bins, 0, (size_t)kCutBins * S * 8, ctx->stream));
         ScopedTimer tm(ctx, "cut_cost");
-        cut_cost_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, ctx->stream>>>(d_rp, d_col, r0, r1, d_assign, S, d_miss,
-                                                                              ppt, (unsigned)tot, bins);
+        static const bool wave_kernel = !getenv("RSK_CUT_THREAD") || atoi(getenv("RSK_CUT_THREAD")) == 0;
+        if (S >= 32 && wave_kernel) {  // lane = scenario, edge-balanced (nnz may be device-resident: grid-stride)
+            const int nw = 4096;  // waves per 64-scenario chunk
+            const int64_t waves = ceil_div(S, 64) * nw;
+            RSK_CHECK(ceil_div(waves, 4) < INT32_MAX, "grid too large");
+            cut_cost_wave_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, ctx->stream>>>(d_rp, d_col, r0, r1, d_assign, S,
+                                                                                      d_miss, nw, bins);
+        } else {
+            cut_cost_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, ctx->stream>>>(d_rp, d_col, r0, r1, d_assign, S,
+                                                                                  d_miss, ppt, (unsigned)tot, bins);
+        }
         RSK_HIP(hipGetLastError());
         cut_bins_sum<<<(unsigned)ceil_div(S, 256), 256, 0, ctx->stream>>>(bins, S,
                                                                            reinterpret_cast<unsigned long long *>(d_out));

@@ -455,16 +455,20 @@ def test_car_slot_kernel_side_rows():
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
 
 
-def test_cut_cost_rows_partition_sums_to_full(ctx):
+@pytest.mark.parametrize("S", [9, 40, 64, 100])
+def test_cut_cost_rows_partition_sums_to_full(ctx, S):
     """rsk_cut_cost_rows over a partition of the rows sums to rsk_cut_cost and
-    to the oracle (the row-sharded cut-cost partials)."""
+    to the oracle (the row-sharded cut-cost partials); S >= 32
+    runs the lane = scenario kernel, with and without the missing term."""
     from oracle import oracle as orc
     from rsk import api
-    rng = np.random.default_rng(900)
-    P, N, S = 700, 40, 9
-    rp, ci, a, _, _, _ = _random_case(rng, P, N, S, max_deg=6, hub_deg=[30, 90])
+    rng = np.random.default_rng(900 + S)
+    P, N = 700, 40
+    rp, ci, a, _, _, _ = _random_case(rng, P, N, S, max_deg=6, hub_deg=[30, 90, 600])
     full = api.cut_cost(rp, ci, a, P, S, ctx=ctx)
     assert np.array_equal(full, orc.cut_cost(rp, ci, a, P, S))
+    miss = rng.integers(0, 3, P).astype(np.int32)
+    assert np.array_equal(api.cut_cost(rp, ci, a, P, S, miss, ctx=ctx), orc.cut_cost(rp, ci, a, P, S, miss))
     cuts = [0, 1, 250, 251, 699, 700]
     parts = sum(api.cut_cost_rows(rp, ci, a, P, S, cuts[k], cuts[k + 1], ctx=ctx) for k in range(len(cuts) - 1))
     assert np.array_equal(parts, full)
