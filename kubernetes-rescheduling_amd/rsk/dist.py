@@ -131,7 +131,8 @@ def gather_rows(local, shard: RowShard, S: int, group=None):
 # by nnz, ``row_shard_for``) and keeps the full assign[P*S] replica; per round:
 #
 #   monitor   per-node CPU / mem of the pods in its rows (rsk_node_reduce on
-#             its row slice) -> int64 all-reduce SUM of the N*S partials;
+#             its row slice once, then moved with its pods in the update
+#             phase) -> int64 all-reduce SUM of the N*S partials;
 #             use = base + CPU sums, base = the usage no pod accounts for
 #             (use0 minus the round-0 sums, fixed)
 #   detect    cpu_pct -> hazard / most hazardous node, replicated (N*S, tiny)
@@ -142,7 +143,8 @@ def gather_rows(local, shard: RowShard, S: int, group=None):
 #             slice (target per scenario, RSK_TARGET_NO_EVICT where not its
 #             pod) -> the element-wise max is the round's move
 #   update    assign[p_s, s] = t_s on every replica (the pod moves when
-#             t_s >= 0; its CPU moves with it through the next monitor)
+#             t_s >= 0); the owning rank moves the pod's CPU / mem from its
+#             old node's partial to the new one (exact integer deltas)
 #   cut cost  directed cut over its rows (rsk_cut_cost_rows) -> int64
 #             all-reduce SUM over S (communicationcost.py:37-45, /2 there)
 #
@@ -282,10 +284,12 @@ class RowShardedRounds:
     def __init__(self, shard: RowShard, backend, group=None):
         self.shard, self.be, self.group = shard, backend, group
 
-    def _partials(self, assign, pod_cpu, pod_mem, N, S):
+    def _local_partials(self, assign, pod_cpu, pod_mem, N, S):
         r0, r1 = self.shard.r0, self.shard.r1
-        q = r1 - r0
-        cpu, mem = self.be.node_partials(assign[r0 * S:r1 * S], pod_cpu[r0:r1], pod_mem[r0:r1], q, N, S)
+        return self.be.node_partials(assign[r0 * S:r1 * S], pod_cpu[r0:r1], pod_mem[r0:r1], r1 - r0, N, S)
+
+    def _partials(self, assign, pod_cpu, pod_mem, N, S):
+        cpu, mem = self._local_partials(assign, pod_cpu, pod_mem, N, S)
         allreduce_(cpu, "sum", self.group)
         allreduce_(mem, "sum", self.group)
         return cpu, mem
@@ -301,8 +305,15 @@ class RowShardedRounds:
             t[name] += (time.perf_counter() - t0) * 1e3
             return time.perf_counter()
 
-        cpu0, _ = self._partials(assign, pod_cpu, pod_mem, N, S)
+        # the rank's per-node partials over its rows, reduced once here and then
+        # kept in step with the moves of its pods (exact integer deltas: the
+        # same sums a full re-reduction of the rows gives, without the pass
+        # over all P x S assignments per round)
+        lp_cpu, lp_mem = self._local_partials(assign, pod_cpu, pod_mem, N, S)
+        cpu0 = lp_cpu.clone()
+        allreduce_(cpu0, "sum", self.group)
         base = use0.to(torch.int64) - cpu0            # usage no pod accounts for
+        pm64 = pod_mem.to(torch.int64)
         evs, tgs, cuts = [], [], []
         sidx = torch.arange(S, device=dev)
         pc64 = pod_cpu.to(torch.int64)
@@ -312,7 +323,9 @@ class RowShardedRounds:
             if trace:
                 print(f"[rank {self.shard.rank}] round {rnd}", file=sys.stderr, flush=True)
             c = time.perf_counter()
-            cpu, mem = self._partials(assign, pod_cpu, pod_mem, N, S)
+            cpu, mem = lp_cpu.clone(), lp_mem.clone()
+            allreduce_(cpu, "sum", self.group)
+            allreduce_(mem, "sum", self.group)
             use = (base + cpu).to(torch.int32)
             c = tick("monitor", c)
             haz, most = self.be.detect(use, cap, N, S, threshold)
@@ -328,9 +341,25 @@ class RowShardedRounds:
             c = tick("place", c)
             target = allgather(tgt_local, self.group).max(dim=0).values   # changed slices of every rank
             c = tick("exchange", c)
+            # fixed-shape ops over all S scenarios (no boolean indexing, which
+            # would sync the host): scenarios without a move write their own
+            # value back and add zero deltas at index 0
             moved = (evict >= 0) & (target >= 0)
             av = assign.view(-1, S)
-            av[evict[moved].long(), sidx[moved]] = target[moved]
+            ep = evict.clamp(min=0).long()
+            old = av[ep, sidx].long()
+            et = target.long()
+            av[ep, sidx] = torch.where(moved, target, old.to(target.dtype))
+            own = moved & (ep >= r0) & (ep < r1)   # this rank's pods: move their usage in its partials
+            src = own & (old >= 0) & (old < N)
+            dst = own & (et < N)
+            zero = torch.zeros_like(old)
+            i_src = torch.where(src, old * S + sidx, zero)
+            i_dst = torch.where(dst, et * S + sidx, zero)
+            lp_cpu.index_add_(0, i_src, torch.where(src, -pc64[ep], zero))
+            lp_mem.index_add_(0, i_src, torch.where(src, -pm64[ep], zero))
+            lp_cpu.index_add_(0, i_dst, torch.where(dst, pc64[ep], zero))
+            lp_mem.index_add_(0, i_dst, torch.where(dst, pm64[ep], zero))
             c = tick("update", c)
             cut = self.be.cut_rows(assign, S, r0, r1)
             allreduce_(cut, "sum", self.group)
