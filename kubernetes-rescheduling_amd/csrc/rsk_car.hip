@@ -1277,9 +1277,27 @@ int hub16_prepare(rsk_car_plan *plan, int S, int N, int thr) {
         plan->n_hub16[c] = 0;
         if (dmax == 0) continue;
         plan->hub16_geom[c] = hub16_geometry(dmax, N);
+        // scenario groups as large as the staging area allows, then halved
+        // (down to one scenario per wave) while the class has fewer work items
+        // than ~8 per CU: with few scenarios (config 4: S = 64) the class is
+        // one round of workgroups whose time is the per-wave scenario chain
+        static const int min_items = std::max(1, env_int("RSK_HUB16_MIN_ITEMS", 2048));
+        int shrink = 0;
+        for (;; ++shrink) {
+            int64_t n = 0;
+            bool can = false;
+            for (const HeavyItem &h : plan->h_hubrows) {
+                if (h.d <= lo || h.d > kHub16Max[c]) continue;
+                const int lg = std::max(0, hub16_lg(h.d, S) - shrink);
+                n += ceil_div(S, (int64_t)1 << lg);
+                can = can || lg > 2;
+            }
+            if (n >= min_items || !can) break;
+        }
         for (const HeavyItem &h : plan->h_hubrows) {  // degree descending
             if (h.d <= lo || h.d > kHub16Max[c]) continue;
-            const int lg = hub16_lg(h.d, S);
+            const int lg0 = hub16_lg(h.d, S);
+            const int lg = std::max(std::min(lg0, 2), lg0 - shrink);
             for (int64_t s0 = 0; s0 < S; s0 += (int64_t)1 << lg)
                 items.insert(items.end(), {h.oi, h.rb, h.d, (int)s0 | (lg << 24)});
         }
