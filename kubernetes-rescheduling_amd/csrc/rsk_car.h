@@ -338,8 +338,8 @@ struct Hub16Geom {
     int dmax, H, hshift;
     size_t lds;
 };
-constexpr int kNumHub16 = 3;                       // car_hub16 launches: degree (64,128] (128,256] (256,kHubMax]
-constexpr int kHub16Max[kNumHub16] = {128, 256, kHubMax};
+constexpr int kNumHub16 = 3;                       // car_hub16 launches: degree (64,128] (128,255] (255,kHubMax]
+constexpr int kHub16Max[kNumHub16] = {128, 255, kHubMax};  // <= 255: u8 direct counters
 Hub16Geom hub16_geometry(int dmax, int N);
 int hub16_lg(int d, int S);
 int launch_hub16(hipStream_t stream, const Hub16Args &a, const Hub16Geom &g, int n_items);

@@ -277,6 +277,85 @@ __device__ __forceinline__ void hub16_scenario(const Hub16Args &a, const HubTab1
     if (lane == 0) hub16_emit(a, oi, s, M, bw, any_tie, any_amb, ex);
 }
 
+// One scenario of a long row by the whole workgroup (NJ < 0, "team"): the
+// entries spread over all kHT threads and ONE table, the maxima and flags
+// combined across the waves through LDS (red: 16 ints + 4 u64).  A wave
+// alone would walk d / 64 entries per lane four times over; config 4's
+// 1,025..1,756-neighbour rows with only 64 scenarios left most waves idle.
+template <int kTab>
+__device__ __forceinline__ void hub16_team(const Hub16Args &a, const HubTab16<kTab> &tb, const unsigned *cs, int d,
+                                           int oi, int s, int tid, int lane, int wave, int *red) {
+    for (int j = tid; j < d; j += kHT) tb.add(cell_node(cs[j]), cell_code(cs[j]) != kCodeHaz);
+    __syncthreads();
+    int m = 0;
+    for (int j = tid; j < d; j += kHT) m = max(m, tb.get(cell_node(cs[j]), cell_code(cs[j]) != kCodeHaz));
+    m = dpp_max(m);
+    if (lane == 0) red[wave] = m;
+    __syncthreads();
+    int M = red[0];
+#pragma unroll
+    for (int w = 1; w < kHW; ++w) M = max(M, red[w]);
+    unsigned v = 0u;
+    if (M > 0)
+        for (int j = tid; j < d; j += kHT) {
+            const unsigned x = cs[j];
+            v = max(v, tb.get(cell_node(x), cell_code(x) != kCodeHaz) == M ? cell_cand(x) : 0u);
+        }
+    v = dpp_max_u32(v);
+    if (lane == 0) red[kHW + wave] = (int)v;
+    __syncthreads();
+    unsigned bw = (unsigned)red[kHW];
+#pragma unroll
+    for (int w = 1; w < kHW; ++w) bw = max(bw, (unsigned)red[kHW + w]);
+    const int bn = cand_node(bw);
+    const unsigned bk = cell_code(bw);
+    bool tie = false, amb = false;
+    if (M > 0)
+        for (int j = tid; j < d; j += kHT) {
+            const unsigned x = cs[j];
+            if (cell_code(x) != kCodeHaz && cell_node(x) != bn && tb.get(cell_node(x), true) == M) {
+                tie = true;
+                amb = amb || cell_code(x) == bk;
+            }
+        }
+    const int fl = (__builtin_amdgcn_ballot_w64(tie) != 0ull ? 1 : 0) | (__builtin_amdgcn_ballot_w64(amb) != 0ull ? 2 : 0);
+    if (lane == 0) red[2 * kHW + wave] = fl;
+    __syncthreads();
+    int f = 0;
+#pragma unroll
+    for (int w = 0; w < kHW; ++w) f |= red[2 * kHW + w];
+    const bool any_tie = f & 1, any_amb = f & 2;
+    int ex = -1;
+    if (any_tie && any_amb && code_inexact(bk)) {  // rare (workgroup-uniform): exact remaining CPU
+        unsigned long long kx = 0ull;
+        for (int j = tid; j < d; j += kHT) {
+            const unsigned x = cs[j];
+            if (cell_code(x) == bk && tb.get(cell_node(x), true) == M) {
+                const int nd = cell_node(x);
+                const int rem = a.cap[nd] - ld32(a.use, (unsigned)nd * (unsigned)a.S + (unsigned)s);
+                const unsigned long long k = pack_rn(rem, nd);
+                kx = k > kx ? k : kx;
+            }
+        }
+        kx = dpp_max_u64(kx);
+        unsigned long long *r64 = reinterpret_cast<unsigned long long *>(red + 4 * kHW);
+        if (lane == 0) r64[wave] = kx;
+        __syncthreads();
+#pragma unroll
+        for (int w = 0; w < kHW; ++w) kx = max(kx, r64[w]);
+        ex = (int)(kNodeMask - (unsigned)(kx & kNodeMask));
+    }
+    __syncthreads();  // every lookup of this scenario done: clear
+    if (kTab != kTabHash) {
+        for (int j = tid; j < d; j += kHT) tb.clear(cell_node(cs[j]), cell_code(cs[j]) != kCodeHaz);
+    } else {
+        uint4 *w4 = reinterpret_cast<uint4 *>(tb.w);
+        for (int k = tid; k <= (a.H >> 2); k += kHT) w4[k] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (tid == 0) hub16_emit(a, oi, s, M, bw, any_tie, any_amb, ex);
+    __syncthreads();  // cleared before the next scenario's adds
+}
+
 template <int kTab, int NJ, int NS>
 __global__ __launch_bounds__(kHT) void car_hub16_kernel(Hub16Args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned hlds[];
@@ -322,10 +401,17 @@ __global__ __launch_bounds__(kHT) void car_hub16_kernel(Hub16Args a) {
             if (u * kHT + tid < total) col[(e[u] & (G - 1)) * d + (e[u] >> lg)] = (c[u] << 16) | (unsigned)n[u];
         // zero the tables (each wave's clears keep them zero between scenarios)
         uint4 *t4 = reinterpret_cast<uint4 *>(hlds + kHStage);
-        for (int k = tid; k < (kHW * NS * (a.H + 4)) >> 2; k += kHT) t4[k] = make_uint4(0u, 0u, 0u, 0u);
+        constexpr int kTabs = NJ < 0 ? 1 : kHW * NS;
+        for (int k = tid; k < (kTabs * (a.H + 4)) >> 2; k += kHT) t4[k] = make_uint4(0u, 0u, 0u, 0u);
     }
     __syncthreads();
-    if constexpr (NJ > 0) {
+    if constexpr (NJ < 0) {
+        HubTab16<kTab> t1 = tb[0];
+        t1.w = hlds + kHStage;
+        int *red = reinterpret_cast<int *>(hlds + kHStage + a.H + 4);
+        for (int si = 0; si < G && s0 + si < a.S; ++si)
+            hub16_team<kTab>(a, t1, col + si * d, d, oi, s0 + si, tid, lane, wave, red);
+    } else if constexpr (NJ > 0) {
         for (int sb = wave * NS; sb < G && s0 + sb < a.S; sb += kHW * NS) {
             const unsigned *cs[NS];
 #pragma unroll
@@ -345,9 +431,14 @@ Hub16Geom hub16_geometry(int dmax, int N) {
     int H = 64;
     while (H < 2 * dmax) H <<= 1;
     static const int force = [] { const char *e = getenv("RSK_HUB16_TABLE"); return e ? atoi(e) : -1; }();
-    // direct tables (no probe chains, the fastest per scenario) while four of
-    // them fit 48 KiB beside the staging area; the hash beyond (large N)
-    const bool use_hash = force >= 0 ? force == kTabHash : (size_t)kHW * (direct + 4) * 4 > 48 * 1024;
+    // rows above 256 neighbours: one scenario at a time by the whole workgroup
+    // (one table); RSK_HUB16_TEAM=0: one wave per scenario
+    static const bool team_on = [] { const char *e = getenv("RSK_HUB16_TEAM"); return !e || atoi(e) != 0; }();
+    const bool team = dmax > 256 && team_on;
+    const int tables = team ? 1 : kHW;
+    // direct tables (no probe chains, the fastest per scenario) while they fit
+    // 48 KiB beside the staging area; the hash beyond (large N)
+    const bool use_hash = force >= 0 ? force == kTabHash : (size_t)tables * (direct + 4) * 4 > 48 * 1024;
     if (use_hash) {
         g.tab = kTabHash;
         g.H = H;
@@ -359,11 +450,12 @@ Hub16Geom hub16_geometry(int dmax, int N) {
         g.H = (direct + 3) & ~3;
         g.hshift = 0;
     }
-    g.nj = dmax <= 128 ? 2 : (dmax <= 256 ? 4 : 0);
+    g.nj = team ? -1 : (dmax <= 128 ? 2 : (dmax <= 256 ? 4 : 0));
     static const int ns_env = [] { const char *e = getenv("RSK_HUB16_NS"); return e ? atoi(e) : 0; }();
     // scenarios per wave at once: 1 with direct tables (LDS-bound), 2 with the hash (measured)
-    g.ns = g.nj == 0 ? 1 : (ns_env == 1 || ns_env == 2 || ns_env == 4 ? ns_env : (use_hash ? 2 : 1));
-    g.lds = ((size_t)kHStage + (size_t)kHW * g.ns * (g.H + 4)) * 4;  // tables: H words + sink / padding
+    g.ns = g.nj <= 0 ? 1 : (ns_env == 1 || ns_env == 2 || ns_env == 4 ? ns_env : (use_hash ? 2 : 1));
+    // tables: H words + sink / padding each; the team's reduction scratch after its one table
+    g.lds = team ? ((size_t)kHStage + (g.H + 4) + 32) * 4 : ((size_t)kHStage + (size_t)kHW * g.ns * (g.H + 4)) * 4;
     return g;
 }
 
@@ -380,7 +472,9 @@ int launch_hub16(hipStream_t stream, const Hub16Args &a, const Hub16Geom &g, int
     using K = void (*)(Hub16Args);
 #define RSK_HUB16_NS(T, J)                                                                           \
     (g.ns == 4 ? &car_hub16_kernel<T, J, 4> : g.ns == 2 ? &car_hub16_kernel<T, J, 2> : &car_hub16_kernel<T, J, 1>)
-#define RSK_HUB16_NJ(T) (g.nj == 2 ? RSK_HUB16_NS(T, 2) : g.nj == 4 ? RSK_HUB16_NS(T, 4) : &car_hub16_kernel<T, 0, 1>)
+#define RSK_HUB16_NJ(T)                                                                                         \
+    (g.nj == 2 ? RSK_HUB16_NS(T, 2) : g.nj == 4 ? RSK_HUB16_NS(T, 4) : g.nj < 0 ? &car_hub16_kernel<T, -1, 1> \
+                                                                                : &car_hub16_kernel<T, 0, 1>)
     const K kern = g.tab == kTabU8 ? RSK_HUB16_NJ(kTabU8) : g.tab == kTabU16 ? RSK_HUB16_NJ(kTabU16) : RSK_HUB16_NJ(kTabHash);
 #undef RSK_HUB16_NJ
 #undef RSK_HUB16_NS
