@@ -385,32 +385,44 @@ __global__ __launch_bounds__(256) void cut_cost_wave_kernel(const int *__restric
     const int ea = rp[r0], eb = rp[r1];
     for (int ka = ea + w * kCutEdges; ka < eb; ka += nw * kCutEdges) {
         const int kb = min(ka + kCutEdges, eb);
-        int lo = r0, hi = r1 - 1;  // the row of edge ka: the last p with row_ptr[p] <= ka
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (rp[mid] <= ka) lo = mid;
-            else hi = mid - 1;
+        // the row of edge ka (the last p with row_ptr[p] <= ka): a 16-way
+        // search, 16 independent scalar loads per round
+        int lo = r0, hi = r1 - 1;
+        while (hi - lo > 16) {
+            const int step = (hi - lo + 15) / 16;
+            int nlo = lo, nhi = hi;
+#pragma unroll
+            for (int i = 1; i < 16; ++i) {
+                const int m = min(lo + i * step, hi);
+                const bool le = rp[m] <= ka;
+                nlo = le ? max(nlo, m) : nlo;
+                nhi = le ? nhi : min(nhi, m - 1);
+            }
+            lo = nlo;
+            hi = nhi;
         }
+        while (lo < hi && rp[lo + 1] <= ka) ++lo;
         int p = lo, k0 = ka;
+        constexpr int kW = 32;  // edges per step, row ends per window
         while (k0 < kb) {
-            int o[16];  // ends of rows p .. p + 15
+            int o[kW];  // ends of rows p .. p + kW - 1
 #pragma unroll
-            for (int i = 0; i < 16; ++i) o[i] = rp[min(p + 1 + i, r1)];
-            const int kend = min(min(kb, k0 + 16), o[15]);
-            if (kend <= k0) { p += 16; continue; }  // 16 rows without edges here
-            int aq[16], am[16], last = 0;
+            for (int i = 0; i < kW; ++i) o[i] = rp[min(p + 1 + i, r1)];
+            const int kend = min(min(kb, k0 + kW), o[kW - 1]);
+            if (kend <= k0) { p += kW; continue; }  // kW rows without edges here
+            int aq[kW], am[kW], last = 0;
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
+            for (int j = 0; j < kW; ++j) {
                 const int k = min(k0 + j, kend - 1);
                 int r = 0;
 #pragma unroll
-                for (int i = 0; i < 15; ++i) r += o[i] <= k ? 1 : 0;
+                for (int i = 0; i < kW - 1; ++i) r += o[i] <= k ? 1 : 0;
                 if (k0 + j < kend) last = r;
                 aq[j] = assign[(size_t)cl[k] * S + s];
                 am[j] = assign[(size_t)(p + r) * S + s];
             }
 #pragma unroll
-            for (int j = 0; j < 16; ++j) c += (k0 + j < kend && am[j] != aq[j]) ? 1ull : 0ull;
+            for (int j = 0; j < kW; ++j) c += (k0 + j < kend && am[j] != aq[j]) ? 1ull : 0ull;
             p += last;
             k0 = kend;
         }
