@@ -374,7 +374,32 @@ def main():
             dist.all_reduce(e, op=dist.ReduceOp.MAX)
             el = float(e.item())
         R = args.row_rounds
-        rounds_leg = {"rounds": R, "threshold_pct": thr, "ms_per_round": round(el * 1e3 / R, 4),
+        # the same rounds with every librsk call, torch op and collective on the
+        # current torch stream (no host sync between phases): the loop's rate
+        a3 = T["assign"].clone()
+        s2 = torch.cuda.Stream(dev)
+        s2.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s2):
+            be2 = rdist.LibrskRoundsBackend(c.row_ptr, c.col_idx, c.pod_cpu, device=dev, stream_ordered=True)
+            rr2 = rdist.RowShardedRounds(rshard, be2)
+            rr2.run(a3, T["use_cpu"], T["cap_cpu"], pc, pm, N, S, 1, threshold=thr)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t2 = time.perf_counter()
+        with torch.cuda.stream(s2):
+            res2 = rr2.run(a3, T["use_cpu"], T["cap_cpu"], pc, pm, N, S, R, threshold=thr)
+        torch.cuda.synchronize(dev)
+        el2 = time.perf_counter() - t2
+        if world > 1:
+            e = torch.tensor([el2], dtype=torch.float64, device=dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            el2 = float(e.item())
+        same = bool(torch.equal(res2["target"], res["target"]) and torch.equal(res2["cut"], res["cut"]))
+        be2.close()
+        rounds_leg = {"rounds": R, "threshold_pct": thr, "ms_per_round": round(el2 * 1e3 / R, 4),
+                      "stream_ordered_matches_synced": same,
+                      "ms_per_round_phase_synced": round(el * 1e3 / R, 4),
                       "phase_ms_per_round": {k: round(v / R, 4) for k, v in res["ms"].items()},
                       "scoring_only_ms_per_round": round(res["ms"]["place"] / R, 4),
                       "moves": int((res["target"] >= 0).sum().item()),

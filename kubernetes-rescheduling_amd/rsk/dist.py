@@ -198,13 +198,24 @@ class LibrskRoundsBackend:
     rank's GPU; every call is asynchronous on the context's stream, which is the
     current torch stream's device)."""
 
-    def __init__(self, row_ptr, col_idx, pod_cpu, ctx=None, device=None):
+    def __init__(self, row_ptr, col_idx, pod_cpu, ctx=None, device=None, stream_ordered=False):
         import numpy as np
         import torch
         from . import api
-        from ._lib import RSK_F_DEVICE, check, default_context
-        self.ctx = ctx or default_context()
+        from ._lib import RSK_F_DEVICE, Context, check, default_context
         self.dev = torch.device(device or "cuda")
+        # stream_ordered: a context of its own whose stream IS the current torch
+        # stream, so librsk kernels, torch ops and collectives order on one
+        # stream and the host never waits between phases
+        self.stream_ordered = stream_ordered
+        if stream_ordered:
+            cur = torch.cuda.current_stream(self.dev).cuda_stream
+            if not cur:  # the legacy default stream (handle 0) would read as "the context's own"
+                raise ValueError("stream_ordered needs a non-default current torch stream (torch.cuda.stream(...))")
+            self.ctx = Context(self.dev.index if self.dev.index is not None else torch.cuda.current_device())
+            self.ctx.set_stream(cur)
+        else:
+            self.ctx = ctx or default_context()
         self.rounds = api.Rounds(row_ptr, col_idx, pod_cpu, ctx=self.ctx)   # deduplicated CSR for the CAR step
         rp = np.ascontiguousarray(row_ptr, np.int32)
         ci = np.ascontiguousarray(col_idx if len(col_idx) else [0], np.int32)
@@ -215,7 +226,8 @@ class LibrskRoundsBackend:
 
     def _sync(self):
         import torch
-        torch.cuda.synchronize(self.dev)   # torch-stream inputs ready / librsk-stream outputs done
+        if not self.stream_ordered:
+            torch.cuda.synchronize(self.dev)   # torch-stream inputs ready / librsk-stream outputs done
 
     def node_partials(self, assign_rows, pod_cpu_rows, pod_mem_rows, q, N, S):
         import torch
@@ -270,6 +282,8 @@ class LibrskRoundsBackend:
 
     def close(self):
         self.rounds.close()
+        if self.stream_ordered:
+            self.ctx.close()
 
 
 class RowShardedRounds:

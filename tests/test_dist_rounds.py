@@ -102,7 +102,7 @@ def _expected(c, pod_cpu, R):
     return np.array(ev), np.array(tg), np.array(cut), a, u
 
 
-def _worker(rank, world, port, R, out_q, use_gpu, pg="gloo"):
+def _worker(rank, world, port, R, out_q, use_gpu, pg="gloo", ordered=False):
     import sys
     sys.path[:0] = [PKG, REPO]
     import torch
@@ -120,15 +120,22 @@ def _worker(rank, world, port, R, out_q, use_gpu, pg="gloo"):
         torch.cuda.set_device(0)
     dist.init_process_group(pg, rank=rank, world_size=world)
     try:
+        import contextlib
         c, pod_cpu, pod_mem = _case()
         dev = torch.device("cuda:0" if use_gpu else "cpu")
-        be = (rdist.LibrskRoundsBackend(c.row_ptr, c.col_idx, pod_cpu, device=dev) if use_gpu
-              else OracleRoundsBackend(c.row_ptr, c.col_idx))
         sh = rdist.row_shard_for(rank, world, c.row_ptr)
         T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
         assign = T(c.assign)
-        res = rdist.RowShardedRounds(sh, be).run(assign, T(c.use_cpu), T(c.cap_cpu), T(pod_cpu), T(pod_mem), c.N, c.S,
-                                                 R)
+        args = (T(c.use_cpu), T(c.cap_cpu), T(pod_cpu), T(pod_mem), c.N, c.S, R)
+        st = torch.cuda.Stream(dev) if ordered else None
+        if st is not None:
+            st.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(st) if st is not None else contextlib.nullcontext():
+            be = (rdist.LibrskRoundsBackend(c.row_ptr, c.col_idx, pod_cpu, device=dev, stream_ordered=ordered)
+                  if use_gpu else OracleRoundsBackend(c.row_ptr, c.col_idx))
+            res = rdist.RowShardedRounds(sh, be).run(assign, *args)
+        if use_gpu:
+            torch.cuda.synchronize(dev)
         out_q.put((rank, res["evict"].cpu().numpy(), res["target"].cpu().numpy(), res["cut"].cpu().numpy(),
                    assign.cpu().numpy(), res["use"].cpu().numpy()))
     except BaseException:  # noqa: BLE001 - report to the parent instead of leaving the peer in a collective
@@ -141,11 +148,11 @@ def _worker(rank, world, port, R, out_q, use_gpu, pg="gloo"):
         dist.destroy_process_group()
 
 
-def _run(world, R, use_gpu=False, pg="gloo"):
+def _run(world, R, use_gpu=False, pg="gloo", ordered=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, R, q, use_gpu, pg)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, R, q, use_gpu, pg, ordered)) for r in range(world)]
     for p in procs:
         p.start()
     outs = []
@@ -209,5 +216,17 @@ def test_row_sharded_rounds_rccl_world1():
     c, pod_cpu, _ = _case()
     ev, tg, cut, a, u = _expected(c, pod_cpu, R)
     (rank, e, t, k, a_r, u_r), = _run(1, R, use_gpu=True, pg="nccl")
+    assert np.array_equal(e, ev) and np.array_equal(t, tg) and np.array_equal(k, cut)
+    assert np.array_equal(a_r, a) and np.array_equal(u_r, u)
+
+
+@pytest.mark.gpu
+def test_row_sharded_rounds_stream_ordered_rccl_world1():
+    """The stream-ordered backend (librsk on the current torch stream, no host
+    syncs between phases; bench.py's rounds rate) against oracle_rounds."""
+    R = 3
+    c, pod_cpu, _ = _case()
+    ev, tg, cut, a, u = _expected(c, pod_cpu, R)
+    (rank, e, t, k, a_r, u_r), = _run(1, R, use_gpu=True, pg="nccl", ordered=True)
     assert np.array_equal(e, ev) and np.array_equal(t, tg) and np.array_equal(k, cut)
     assert np.array_equal(a_r, a) and np.array_equal(u_r, u)
