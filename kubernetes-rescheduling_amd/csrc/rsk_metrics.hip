@@ -255,6 +255,31 @@ __global__ __launch_bounds__(256) void detect_kernel(const int *__restrict__ pct
     if (b) atomicMax(&most[s], b);
 }
 
+// detect_kernel with cpu_pct computed in place (get_resource_usage.py:37, the
+// same fp64 divide, multiply and rint as cpu_pct_kernel): the multi-round loop
+// needs only the hazard flags and the most hazardous node, not the pct array.
+__global__ __launch_bounds__(256) void detect_use_kernel(const int *__restrict__ use, const int *__restrict__ cap, int N,
+                                                         int S, int thr, int npb, unsigned total,
+                                                         uint8_t *__restrict__ haz, unsigned long long *__restrict__ most) {
+    const unsigned t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= total) return;
+    const int s = (int)(t % (unsigned)S);
+    const int n0 = (int)(t / (unsigned)S) * npb, n1 = min(N, n0 + npb);
+    unsigned long long b = 0;
+    for (int n = n0; n < n1; ++n) {
+        const size_t idx = (size_t)n * S + s;
+        const int c = cap[n];
+        const int v = c == 0 ? -1 : (int)rint((double)use[idx] / (double)c * 100.0);
+        const bool h = v >= thr;
+        haz[idx] = h;
+        if (h) {
+            const unsigned long long k = pack_hi_lo(v, ~(unsigned)n);
+            b = k > b ? k : b;
+        }
+    }
+    if (b) atomicMax(&most[s], b);
+}
+
 __global__ void decode_first_max(const unsigned long long *__restrict__ key, int S, int *__restrict__ out) {
     const int s = blockIdx.x * 256 + threadIdx.x;
     if (s >= S) return;
@@ -472,6 +497,18 @@ int launch_detect(hipStream_t stream, const int *pct, int N, int S, int threshol
     const unsigned total = (unsigned)(ceil_div(N, npb) * S);
     detect_kernel<<<(unsigned)ceil_div(total, 256), 256, 0, stream>>>(pct, N, S, threshold, npb, total, hazard,
                                                                        key_ws);
+    decode_first_max<<<(unsigned)ceil_div(S, 256), 256, 0, stream>>>(key_ws, S, most);
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
+}
+
+int launch_detect_use(hipStream_t stream, const int *use, const int *cap, int N, int S, int threshold, uint8_t *hazard,
+                      unsigned long long *key_ws, int *most) {
+    RSK_HIP(hipMemsetAsync(key_ws, 0, (size_t)S * 8, stream));
+    const int npb = chunk_for(N, S);
+    const unsigned total = (unsigned)(ceil_div(N, npb) * S);
+    detect_use_kernel<<<(unsigned)ceil_div(total, 256), 256, 0, stream>>>(use, cap, N, S, threshold, npb, total, hazard,
+                                                                           key_ws);
     decode_first_max<<<(unsigned)ceil_div(S, 256), 256, 0, stream>>>(key_ws, S, most);
     RSK_HIP(hipGetLastError());
     return RSK_OK;

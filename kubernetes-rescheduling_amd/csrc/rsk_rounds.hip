@@ -8,7 +8,7 @@
 // build-defined: the pod's CPU moves with it.  This file runs R
 // such rounds for S independent scenarios without a host round trip:
 //
-//   cpu_pct (a9) -> detect (a8) -> pick_max_pod (a10)   [rsk_metrics.hip]
+//   cpu_pct (a9) + detect (a8) in one pass -> pick_max_pod (a10)   [rsk_metrics.hip]
 //   car_move_kernel: CAR of the one evicted pod per scenario (a1/a2), then the
 //   update use[old] -= cpu, use[t] += cpu, assign[p] = t when t >= 0.
 //
@@ -27,14 +27,13 @@ struct rsk_rounds {
     rsk_ctx *ctx = nullptr;
     int P = 0, dmax = 0;
     rsk::DevBuf row_ptr, col, pod_cpu;
-    rsk::DevBuf pct, haz, most, evict, key_ws;
+    rsk::DevBuf haz, most, evict, key_ws;
     rsk::DevBuf asg16;  // u16 shadow of assign for the eviction scan (N <= 65535, S % 8 == 0)
     ~rsk_rounds() {
         asg16.release();
         row_ptr.release();
         col.release();
         pod_cpu.release();
-        pct.release();
         haz.release();
         most.release();
         evict.release();
@@ -294,7 +293,6 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         if (PS) RSK_HIP(hipMemcpyAsync(d_assign, assign, PS * 4, hipMemcpyHostToDevice, st));
         RSK_HIP(hipMemcpyAsync(d_use, use_cpu, NS * 4, hipMemcpyHostToDevice, st));
     }
-    RSK_TRY(r->pct.reserve(NS * 4));
     RSK_TRY(r->haz.reserve(NS));
     RSK_TRY(r->most.reserve((size_t)S * 4));
     RSK_TRY(r->key_ws.reserve((size_t)S * 8));
@@ -317,9 +315,8 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         int *ev = d_evict + (size_t)round * S;
         {
             ScopedTimer tm(ctx, "rounds_detect");
-            RSK_TRY(launch_cpu_pct(st, d_use, d_cap, N, S, r->pct.as<int>()));
-            RSK_TRY(launch_detect(st, r->pct.as<int>(), N, S, threshold, r->haz.as<uint8_t>(),
-                                  r->key_ws.as<unsigned long long>(), r->most.as<int>()));
+            RSK_TRY(launch_detect_use(st, d_use, d_cap, N, S, threshold, r->haz.as<uint8_t>(),
+                                      r->key_ws.as<unsigned long long>(), r->most.as<int>()));
         }
         {
             ScopedTimer tm(ctx, "rounds_pick");
