@@ -1621,7 +1621,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     RSK_TRY(plan->zc.reserve((size_t)S * 12 + 16));
     unsigned long long *d_zkey = plan->zc.as<unsigned long long>();
     int *d_zcnt = reinterpret_cast<int *>(d_zkey + S);
-    RSK_HIP(hipMemsetAsync(plan->zc.ptr, 0, (size_t)S * 12, ctx->stream));
+    RSK_HIP(hipMemsetAsync(plan->zc.ptr, 0, (size_t)S * 12 + 16, ctx->stream));  // + the capmax word
 
     {   // K0: node state (codes and / or exact keys) + the zero case
         Prep16Args pa;

@@ -73,16 +73,21 @@ __device__ __forceinline__ ushort4 cvec_make(const unsigned (&k)[4]) {
 // ~node)) is reduced in LDS per workgroup first — threads of one workgroup
 // that share a scenario meet in one LDS slot — so a scenario receives one
 // global atomic per workgroup, not one per thread.
-// max(cap) once per execute, for the exact code window B = max(0, max(cap) - 32766)
-__global__ __launch_bounds__(1024) void car_capmax_kernel(const int *__restrict__ cap, int N, int *__restrict__ out) {
-    __shared__ int m;
-    if (threadIdx.x == 0) m = 0;
-    __syncthreads();
+// max(cap) once per execute, for the exact code window B = max(0, max(cap) - 32766):
+// 4096 nodes per workgroup, 16 clamped loads in flight per thread, a DPP max
+// per wave and one atomicMax per wave into *out (zeroed by the caller; a
+// negative max reads as 0, which gives the same B)
+constexpr int kCapMaxPer = 4096;
+__global__ __launch_bounds__(256) void car_capmax_kernel(const int *__restrict__ cap, int N, int *__restrict__ out) {
+    const int base = (int)blockIdx.x * kCapMaxPer + (int)threadIdx.x;
+    int v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = cap[min(base + u * 256, N - 1)];
     int mc = 0;
-    for (int n = threadIdx.x; n < N; n += 1024) mc = max(mc, cap[n]);
-    atomicMax(&m, mc);
-    __syncthreads();
-    if (threadIdx.x == 0) *out = m;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) mc = max(mc, v[u]);
+    mc = dpp_max(mc);
+    if ((threadIdx.x & 63) == 0) atomicMax(out, mc);
 }
 
 template <int V, bool kCode, bool kKey>
@@ -176,7 +181,7 @@ int launch_prep(hipStream_t stream, const Prep16Args &a) {
     RSK_CHECK(a.code || a.nodekey, "prep: nothing to write");
     RSK_CHECK(!a.code || a.capmax, "prep: codes need the capmax scratch");
     if (a.code) {
-        car_capmax_kernel<<<1, 1024, 0, stream>>>(a.cap, a.N, a.capmax);
+        car_capmax_kernel<<<(unsigned)ceil_div(a.N, kCapMaxPer), 256, 0, stream>>>(a.cap, a.N, a.capmax);
         RSK_HIP(hipGetLastError());
     }
     // 4 scenarios per thread when S % 4 == 0 (16-B use / key words, 8-B codes)
