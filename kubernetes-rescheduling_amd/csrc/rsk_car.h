@@ -331,6 +331,7 @@ struct Hub16Args {
     int *out_target, *out_score;
     int S, N;
     int H, hshift;            // table words per wave, hash shift (from Hub16Geom)
+    int stage;                // staging cells: the largest d << lg of the launch's items
 };
 struct Hub16Geom {
     int tab, nj, ns;          // table kind (u8 / u16 direct, hash), register entries per lane (0: any

@@ -760,7 +760,7 @@ struct rsk_car_plan {
     std::vector<HeavyItem> h_hubrows;
     DevBuf hub16_items;
     int hub16_S = -1, hub16_thr = -1, hub16_N = -1;
-    int n_hub16[kNumHub16] = {}, hub16_off[kNumHub16] = {};
+    int n_hub16[kNumHub16] = {}, hub16_off[kNumHub16] = {}, hub16_stage[kNumHub16] = {};
     Hub16Geom hub16_geom[kNumHub16] = {};
     // hub rows (> 64)
     int n_heavy[kNumHeavy] = {};
@@ -1275,6 +1275,7 @@ int hub16_prepare(rsk_car_plan *plan, int S, int N, int thr) {
             if (h.d > lo && h.d <= kHub16Max[c]) dmax = std::max(dmax, h.d);
         plan->hub16_off[c] = (int)(items.size() / 4);
         plan->n_hub16[c] = 0;
+        plan->hub16_stage[c] = 0;
         if (dmax == 0) continue;
         plan->hub16_geom[c] = hub16_geometry(dmax, N);
         // scenario groups as large as the staging area allows, then halved
@@ -1298,6 +1299,7 @@ int hub16_prepare(rsk_car_plan *plan, int S, int N, int thr) {
             if (h.d <= lo || h.d > kHub16Max[c]) continue;
             const int lg0 = hub16_lg(h.d, S);
             const int lg = std::max(std::min(lg0, 2), lg0 - shrink);
+            plan->hub16_stage[c] = std::max(plan->hub16_stage[c], h.d << lg);
             for (int64_t s0 = 0; s0 < S; s0 += (int64_t)1 << lg)
                 items.insert(items.end(), {h.oi, h.rb, h.d, (int)s0 | (lg << 24)});
         }
@@ -1394,6 +1396,7 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t *side, int n
             const Hub16Geom &g = plan->hub16_geom[c];
             a.H = g.H;
             a.hshift = g.hshift;
+            a.stage = plan->hub16_stage[c];
             const hipStream_t stream = pick();
             static const bool per_class = env_int("RSK_HUB_TIMERS", 0) != 0;
             static const char *const kNames[kNumHub16] = {"car_hub128", "car_hub256", "car_hub4096"};

@@ -366,11 +366,11 @@ __global__ __launch_bounds__(kHT) void car_hub16_kernel(Hub16Args a) {
     const int s0 = gw & 0xffffff, lg = gw >> 24;
     const int G = 1 << lg;
     const unsigned S = (unsigned)a.S, N = (unsigned)a.N;
-    unsigned *col = hlds;  // [G][d], d * G <= kHStage
+    unsigned *col = hlds;  // [G][d], d * G <= a.stage <= kHStage
     HubTab16<kTab> tb[NS];
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
-        tb[k].w = hlds + kHStage + (wave * NS + k) * (a.H + 4);
+        tb[k].w = hlds + a.stage + (wave * NS + k) * (a.H + 4);
         tb[k].mask = (unsigned)a.H - 1u;
         tb[k].shift = a.hshift;
     }
@@ -400,15 +400,15 @@ __global__ __launch_bounds__(kHT) void car_hub16_kernel(Hub16Args a) {
         for (int u = 0; u < kHB; ++u)
             if (u * kHT + tid < total) col[(e[u] & (G - 1)) * d + (e[u] >> lg)] = (c[u] << 16) | (unsigned)n[u];
         // zero the tables (each wave's clears keep them zero between scenarios)
-        uint4 *t4 = reinterpret_cast<uint4 *>(hlds + kHStage);
+        uint4 *t4 = reinterpret_cast<uint4 *>(hlds + a.stage);
         constexpr int kTabs = NJ < 0 ? 1 : kHW * NS;
         for (int k = tid; k < (kTabs * (a.H + 4)) >> 2; k += kHT) t4[k] = make_uint4(0u, 0u, 0u, 0u);
     }
     __syncthreads();
     if constexpr (NJ < 0) {
         HubTab16<kTab> t1 = tb[0];
-        t1.w = hlds + kHStage;
-        int *red = reinterpret_cast<int *>(hlds + kHStage + a.H + 4);
+        t1.w = hlds + a.stage;
+        int *red = reinterpret_cast<int *>(hlds + a.stage + a.H + 4);
         for (int si = 0; si < G && s0 + si < a.S; ++si)
             hub16_team<kTab>(a, t1, col + si * d, d, oi, s0 + si, tid, lane, wave, red);
     } else if constexpr (NJ > 0) {
@@ -465,10 +465,16 @@ int hub16_lg(int d, int S) {  // log2 of the scenario group of a degree-d row
     return lg;
 }
 
-int launch_hub16(hipStream_t stream, const Hub16Args &a, const Hub16Geom &g, int n_items) {
+int launch_hub16(hipStream_t stream, const Hub16Args &a0, const Hub16Geom &g, int n_items) {
     if (n_items == 0) return RSK_OK;
+    // the staging area sized to the launch's largest item (a.stage cells, set by
+    // the caller from the items' d << lg; kHStage when unset): small scenario
+    // groups leave room for more workgroups per CU
+    Hub16Args a = a0;
+    a.stage = a.stage > 0 ? std::min((a.stage + 3) & ~3, kHStage) : kHStage;
+    const size_t lds = g.lds - (size_t)(kHStage - a.stage) * 4;
     RSK_CHECK(g.dmax <= kHStage, "hub row degree %d exceeds %d", g.dmax, kHStage);
-    RSK_CHECK(g.lds <= 160 * 1024, "hub rows need %zu B of LDS", g.lds);
+    RSK_CHECK(lds <= 160 * 1024, "hub rows need %zu B of LDS", lds);
     using K = void (*)(Hub16Args);
 #define RSK_HUB16_NS(T, J)                                                                           \
     (g.ns == 4 ? &car_hub16_kernel<T, J, 4> : g.ns == 2 ? &car_hub16_kernel<T, J, 2> : &car_hub16_kernel<T, J, 1>)
@@ -478,10 +484,10 @@ int launch_hub16(hipStream_t stream, const Hub16Args &a, const Hub16Geom &g, int
     const K kern = g.tab == kTabU8 ? RSK_HUB16_NJ(kTabU8) : g.tab == kTabU16 ? RSK_HUB16_NJ(kTabU16) : RSK_HUB16_NJ(kTabHash);
 #undef RSK_HUB16_NJ
 #undef RSK_HUB16_NS
-    if (g.lds > 64 * 1024)
+    if (lds > 64 * 1024)
         RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)g.lds));
-    kern<<<dim3((unsigned)n_items), dim3(kHT), g.lds, stream>>>(a);
+                                    (int)lds));
+    kern<<<dim3((unsigned)n_items), dim3(kHT), lds, stream>>>(a);
     RSK_HIP(hipGetLastError());
     return RSK_OK;
 }
