@@ -191,6 +191,24 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
 int rsk_rounds_place(rsk_rounds *r, const int32_t *assign, int32_t S, const int32_t *cap_cpu,
                      const int32_t *use_cpu, const uint8_t *hazard, int32_t N, const int32_t *evict,
                      int32_t *out_target, uint32_t flags);
+/* The row-sharded loop's per-round glue, one launch each (device pointers,
+ * RSK_F_DEVICE required):
+ * rsk_rows_evict_key: this rank's eviction candidates -> the all-reduce MAX
+ *   key of delete_replaced_pod.py:47-57's first max (cpu, lowest pod):
+ *   key[s] = local_pod[s] >= 0 ? pod_cpu[g] << 32 | (2^32 - 1 - g) : -1 with
+ *   g = r0 + local_pod[s];
+ * rsk_rows_evict_decode: the reduced key -> evict[s] (global pod, -1 none);
+ * rsk_rows_apply: the move of round r (main.py:73-91's edit + placement, the
+ *   build-defined state update): where evict[s] >= 0 and target[s] >= 0,
+ *   assign[evict*S+s] = target[s]; when the pod is in rows [r0, r1) its CPU /
+ *   memory move between this rank's per-node partials cpu_part / mem_part
+ *   [N*S] (old node only when it was in [0, N)).                            */
+int rsk_rows_evict_key(rsk_ctx *ctx, const int32_t *local_pod, int32_t S, int32_t r0, const int32_t *pod_cpu,
+                       int64_t *out_key, uint32_t flags);
+int rsk_rows_evict_decode(rsk_ctx *ctx, const int64_t *key, int32_t S, int32_t *out_evict, uint32_t flags);
+int rsk_rows_apply(rsk_ctx *ctx, int32_t *assign, int32_t S, const int32_t *evict, const int32_t *target,
+                   int32_t r0, int32_t r1, int32_t N, const int32_t *pod_cpu, const int64_t *pod_mem,
+                   int64_t *cpu_part, int64_t *mem_part, uint32_t flags);
 
 /* ---- µBench workmodel -> relation CSR (host only, no device) -----------------
  * The caller's on-disk format (workmodelC.json).  One

@@ -218,6 +218,48 @@ MoveGeom move_geometry(const rsk_rounds *r) {
     return g;
 }
 
+// Row-sharded loop glue: one thread per scenario.
+__global__ void rows_evict_key_kernel(const int *__restrict__ local_pod, int S, int r0, const int *__restrict__ pod_cpu,
+                                      long long *__restrict__ key) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (s >= S) return;
+    const int l = local_pod[s];
+    if (l < 0) { key[s] = -1; return; }
+    const long long g = (long long)r0 + l;
+    key[s] = ((long long)pod_cpu[g] << 32) | (0xffffffffll - g);
+}
+
+__global__ void rows_evict_decode_kernel(const long long *__restrict__ key, int S, int *__restrict__ evict) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (s >= S) return;
+    const long long k = key[s];
+    evict[s] = k >= 0 ? (int)(0xffffffffll - (k & 0xffffffffll)) : -1;
+}
+
+// scenario s owns assign[:, s] and the partials' column s: no two threads touch one word
+__global__ void rows_apply_kernel(int *__restrict__ assign, int S, const int *__restrict__ evict,
+                                  const int *__restrict__ target, int r0, int r1, int N,
+                                  const int *__restrict__ pod_cpu, const long long *__restrict__ pod_mem,
+                                  long long *__restrict__ cpu_part, long long *__restrict__ mem_part) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (s >= S) return;
+    const int e = evict[s], t = target[s];
+    if (e < 0 || t < 0) return;
+    int *a = assign + (size_t)e * S + s;
+    const int old = *a;
+    *a = t;
+    if (e < r0 || e >= r1) return;
+    const long long c = pod_cpu[e], m = pod_mem[e];
+    if ((unsigned)old < (unsigned)N) {
+        cpu_part[(size_t)old * S + s] -= c;
+        mem_part[(size_t)old * S + s] -= m;
+    }
+    if (t < N) {
+        cpu_part[(size_t)t * S + s] += c;
+        mem_part[(size_t)t * S + s] += m;
+    }
+}
+
 }  // namespace
 }  // namespace rsk
 
@@ -389,6 +431,41 @@ int rsk_rounds_place(rsk_rounds *r, const int32_t *assign, int32_t S, const int3
         RSK_TRY(copy_back(ctx, out_target, d_target, (size_t)S * 4, false));
         RSK_HIP(hipStreamSynchronize(ctx->stream));
     }
+    return RSK_OK;
+}
+
+// ---- row-sharded loop glue (rsk/dist.py RowShardedRounds) -----------------
+int rsk_rows_evict_key(rsk_ctx *ctx, const int32_t *local_pod, int32_t S, int32_t r0, const int32_t *pod_cpu,
+                       int64_t *out_key, uint32_t flags) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK((flags & RSK_F_DEVICE) && local_pod && pod_cpu && out_key && S > 0 && r0 >= 0,
+              "rsk_rows_evict_key: device pointers and S > 0 required");
+    rows_evict_key_kernel<<<(unsigned)ceil_div(S, 256), 256, 0, ctx->stream>>>(local_pod, S, r0, pod_cpu,
+                                                                              reinterpret_cast<long long *>(out_key));
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
+}
+
+int rsk_rows_evict_decode(rsk_ctx *ctx, const int64_t *key, int32_t S, int32_t *out_evict, uint32_t flags) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK((flags & RSK_F_DEVICE) && key && out_evict && S > 0, "rsk_rows_evict_decode: bad arguments");
+    rows_evict_decode_kernel<<<(unsigned)ceil_div(S, 256), 256, 0, ctx->stream>>>(
+        reinterpret_cast<const long long *>(key), S, out_evict);
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
+}
+
+int rsk_rows_apply(rsk_ctx *ctx, int32_t *assign, int32_t S, const int32_t *evict, const int32_t *target, int32_t r0,
+                   int32_t r1, int32_t N, const int32_t *pod_cpu, const int64_t *pod_mem, int64_t *cpu_part,
+                   int64_t *mem_part, uint32_t flags) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK((flags & RSK_F_DEVICE) && assign && evict && target && pod_cpu && pod_mem && cpu_part && mem_part &&
+                  S > 0 && N > 0 && 0 <= r0 && r0 <= r1,
+              "rsk_rows_apply: bad arguments");
+    rows_apply_kernel<<<(unsigned)ceil_div(S, 256), 256, 0, ctx->stream>>>(
+        assign, S, evict, target, r0, r1, N, pod_cpu, reinterpret_cast<const long long *>(pod_mem),
+        reinterpret_cast<long long *>(cpu_part), reinterpret_cast<long long *>(mem_part));
+    RSK_HIP(hipGetLastError());
     return RSK_OK;
 }
 

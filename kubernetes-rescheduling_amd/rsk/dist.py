@@ -270,6 +270,31 @@ class LibrskRoundsBackend:
         self._sync()
         return out
 
+    # the per-round glue of RowShardedRounds.run in one librsk launch each
+    def evict_key(self, loc, r0, pod_cpu, S):
+        import torch
+        self._sync()
+        key = torch.empty(S, dtype=torch.int64, device=self.dev)
+        self._check(self.ctx.lib.rsk_rows_evict_key(self.ctx.handle, loc.data_ptr(), S, r0, pod_cpu.data_ptr(),
+                                                    key.data_ptr(), self._F))
+        self._sync()
+        return key
+
+    def evict_decode(self, key, S):
+        import torch
+        self._sync()
+        ev = torch.empty(S, dtype=torch.int32, device=self.dev)
+        self._check(self.ctx.lib.rsk_rows_evict_decode(self.ctx.handle, key.data_ptr(), S, ev.data_ptr(), self._F))
+        self._sync()
+        return ev
+
+    def apply(self, assign, S, evict, target, r0, r1, N, pod_cpu, pod_mem, cpu_part, mem_part):
+        self._sync()
+        self._check(self.ctx.lib.rsk_rows_apply(self.ctx.handle, assign.data_ptr(), S, evict.data_ptr(),
+                                                target.data_ptr(), r0, r1, N, pod_cpu.data_ptr(), pod_mem.data_ptr(),
+                                                cpu_part.data_ptr(), mem_part.data_ptr(), self._F))
+        self._sync()
+
     def cut_rows(self, assign, S, r0, r1):
         import torch
         self._sync()
@@ -328,6 +353,8 @@ class RowShardedRounds:
         allreduce_(cpu0, "sum", self.group)
         base = use0.to(torch.int64) - cpu0            # usage no pod accounts for
         pm64 = pod_mem.to(torch.int64)
+        glue = hasattr(self.be, "apply")   # the backend's fused per-round glue (librsk), else torch ops
+        pc32, pm64c = pod_cpu.to(torch.int32).contiguous(), pm64.contiguous()
         evs, tgs, cuts = [], [], []
         sidx = torch.arange(S, device=dev)
         pc64 = pod_cpu.to(torch.int64)
@@ -344,17 +371,34 @@ class RowShardedRounds:
             c = tick("monitor", c)
             haz, most = self.be.detect(use, cap, N, S, threshold)
             c = tick("detect", c)
-            loc = self.be.pick_rows(assign[r0 * S:r1 * S], pod_cpu[r0:r1], r1 - r0, S, most).to(torch.int64)
-            gp = torch.where(loc >= 0, loc + r0, torch.zeros_like(loc))
-            key = torch.where(loc >= 0, (pc64[gp] << 32) | (mask32 - gp), torch.full_like(loc, -1))
+            loc = self.be.pick_rows(assign[r0 * S:r1 * S], pod_cpu[r0:r1], r1 - r0, S, most)
+            if glue:
+                key = self.be.evict_key(loc, r0, pc32, S)
+            else:
+                loc = loc.to(torch.int64)
+                gp = torch.where(loc >= 0, loc + r0, torch.zeros_like(loc))
+                key = torch.where(loc >= 0, (pc64[gp] << 32) | (mask32 - gp), torch.full_like(loc, -1))
             allreduce_(key, "max", self.group)
-            evict = torch.where(key >= 0, mask32 - (key & mask32), torch.full_like(key, -1)).to(torch.int32)
+            if glue:
+                evict = self.be.evict_decode(key, S)
+            else:
+                evict = torch.where(key >= 0, mask32 - (key & mask32), torch.full_like(key, -1)).to(torch.int32)
             c = tick("evict", c)
             mine = (evict >= r0) & (evict < r1)
             tgt_local = self.be.place(assign, S, cap, use, haz, N, torch.where(mine, evict, torch.full_like(evict, -1)))
             c = tick("place", c)
             target = allgather(tgt_local, self.group).max(dim=0).values   # changed slices of every rank
             c = tick("exchange", c)
+            if glue:  # one librsk launch
+                self.be.apply(assign, S, evict, target.contiguous(), r0, r1, N, pc32, pm64c, lp_cpu, lp_mem)
+                c = tick("update", c)
+                cut = self.be.cut_rows(assign, S, r0, r1)
+                allreduce_(cut, "sum", self.group)
+                tick("cut", c)
+                evs.append(evict)
+                tgs.append(target)
+                cuts.append(cut)
+                continue
             # fixed-shape ops over all S scenarios (no boolean indexing, which
             # would sync the host): scenarios without a move write their own
             # value back and add zero deltas at index 0
