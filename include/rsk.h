@@ -101,6 +101,13 @@ int rsk_car_place(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, 
                   const int32_t *assign, int32_t S, const int32_t *cap_cpu, const int32_t *use_cpu,
                   const uint8_t *hazard, int32_t N, const int32_t *rows, int32_t Q,
                   int32_t *out_target, int32_t *out_score, uint32_t flags);
+/* One CAR placement (S = 1) in one launch, for the drop-in's single call
+ * (rescheduling.py:174-218): node_of[k] = the node of each related pod (its
+ * neighbours, outside [0, N) ignored); score[n] = #{i : node_of[i] = n} over
+ * non-hazard n, then the argmax with the reference's tie-breaks, None (-1)
+ * and RSK_NO_CANDIDATE when every node is hazard.  No plan; N <= 32768. */
+int rsk_car_row(rsk_ctx *ctx, const int32_t *node_of, int32_t k, const int32_t *cap_cpu, const int32_t *use_cpu,
+                const uint8_t *hazard, int32_t N, int32_t *out_target, int32_t *out_score, uint32_t flags);
 
 /* ---- baselines --------------------------------------------------------------
  * spread  (rescheduling.py:89-101): argmin over non-hazard n of

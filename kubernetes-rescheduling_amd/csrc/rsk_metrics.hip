@@ -27,6 +27,74 @@ __device__ __forceinline__ unsigned long long pack_hi_lo(int hi, unsigned lo) {
 }
 
 // ---------------------------------------------------------------------------
+// One CAR placement in one workgroup (rsk_car_row; rescheduling.py:183-214):
+// the node histogram of the related pods in LDS, then two block maxima — the
+// best score M over non-hazard nodes, then (cap - use, -node) over the nodes
+// at M and how many they are.  M = 0 (no related pod on a candidate) is the
+// same rule: every non-hazard node ties at 0.
+constexpr int kRowThreads = 1024;
+constexpr int kRowMaxN = 32768;
+__device__ __forceinline__ void row_block_max_u64(unsigned long long &v, unsigned long long *red) {
+    // wave maxima by DPP, then across the 16 waves through LDS
+    unsigned long long w;
+    w = (unsigned long long)__shfl_xor((long long)v, 32); v = w > v ? w : v;
+    w = (unsigned long long)__shfl_xor((long long)v, 16); v = w > v ? w : v;
+    w = (unsigned long long)__shfl_xor((long long)v, 8); v = w > v ? w : v;
+    w = (unsigned long long)__shfl_xor((long long)v, 4); v = w > v ? w : v;
+    w = (unsigned long long)__shfl_xor((long long)v, 2); v = w > v ? w : v;
+    w = (unsigned long long)__shfl_xor((long long)v, 1); v = w > v ? w : v;
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    v = 0ull;
+    for (int i = 0; i < kRowThreads / 64; ++i) v = red[i] > v ? red[i] : v;
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kRowThreads) void car_row_kernel(const int *__restrict__ node_of, int k,
+                                                              const int *__restrict__ cap, const int *__restrict__ use,
+                                                              const uint8_t *__restrict__ haz, int N,
+                                                              int *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned rl[];
+    unsigned *cnt = rl;  // [N]
+    unsigned long long *red = reinterpret_cast<unsigned long long *>(rl + ((N + 3) & ~3));
+    __shared__ int nm;
+    for (int n = threadIdx.x; n < N; n += kRowThreads) cnt[n] = 0u;
+    if (threadIdx.x == 0) nm = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < k; i += kRowThreads) {
+        const int n = node_of[i];
+        if ((unsigned)n < (unsigned)N && !haz[n]) atomicAdd(&cnt[n], 1u);
+    }
+    __syncthreads();
+    // M: the best score over candidates, +1 so that "no candidate" is 0
+    unsigned long long m = 0ull;
+    for (int n = threadIdx.x; n < N; n += kRowThreads)
+        if (!haz[n]) m = max(m, (unsigned long long)cnt[n] + 1ull);
+    row_block_max_u64(m, red);
+    if (m == 0ull) {  // every node is hazard: max() of an empty sequence
+        if (threadIdx.x == 0) { out[0] = RSK_TARGET_NO_CANDIDATE; out[1] = -1; }
+        return;
+    }
+    const unsigned M = (unsigned)(m - 1ull);
+    unsigned long long b = 0ull;
+    int c = 0;
+    for (int n = threadIdx.x; n < N; n += kRowThreads)
+        if (!haz[n] && cnt[n] == M) {
+            ++c;
+            const unsigned long long key = pack_hi_lo(cap[n] - use[n], ~(unsigned)n);
+            b = key > b ? key : b;
+        }
+    if (c) atomicAdd(&nm, c);
+    row_block_max_u64(b, red);
+    if (threadIdx.x == 0) {
+        const int rem = (int)((unsigned)(b >> 32) ^ 0x80000000u);
+        const int node = (int)(~(unsigned)(b & 0xffffffffull));
+        out[0] = nm == 1 ? node : (rem >= 0 ? node : RSK_TARGET_NONE);
+        out[1] = (int)M;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // spread (rescheduling.py:89-101): min (pod_count, name_rank) over non-hazard.
 // binpack (rescheduling.py:121-133): max (cpu_pct, name_rank).
 // key = (primary ^ sign) << 32 | rank; the winning rank maps back to its node.
@@ -636,6 +704,62 @@ int32_t rsk_py_randbelow(uint64_t seed, int32_t n) {
     do r = st.next() >> (32 - k);
     while (r >= (uint32_t)n);
     return (int32_t)r;
+}
+
+int rsk_car_row(rsk_ctx *ctx, const int32_t *node_of, int32_t k, const int32_t *cap_cpu, const int32_t *use_cpu,
+                const uint8_t *hazard, int32_t N, int32_t *out_target, int32_t *out_score, uint32_t flags) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK(N > 0 && N <= kRowMaxN && k >= 0 && cap_cpu && use_cpu && hazard && out_target && (k == 0 || node_of),
+              "rsk_car_row: bad arguments (N=%d, 1..%d, k=%d)", N, kRowMaxN, k);
+    const bool dev = flags & RSK_F_DEVICE;
+    const int *d_nodes = nullptr, *d_cap, *d_use;
+    const uint8_t *d_haz;
+    int *d_out;
+    // host pointers: one staging copy of all four inputs
+    if (dev) {
+        d_nodes = node_of;
+        d_cap = cap_cpu;
+        d_use = use_cpu;
+        d_haz = hazard;
+    } else {
+        const size_t nb = (size_t)k * 4, cb = (size_t)N * 4, hb = (size_t)N;
+        const size_t o1 = (nb + 15) & ~(size_t)15, o2 = o1 + ((cb + 15) & ~(size_t)15),
+                     o3 = o2 + ((cb + 15) & ~(size_t)15), tot = o3 + hb;
+        RSK_TRY(ctx->host_stage[7].reserve(tot));
+        std::vector<char> buf(tot);
+        if (k) std::memcpy(buf.data(), node_of, nb);
+        std::memcpy(buf.data() + o1, cap_cpu, cb);
+        std::memcpy(buf.data() + o2, use_cpu, cb);
+        std::memcpy(buf.data() + o3, hazard, hb);
+        char *base = static_cast<char *>(ctx->host_stage[7].ptr);
+        RSK_HIP(hipMemcpyAsync(base, buf.data(), tot, hipMemcpyHostToDevice, ctx->stream));
+        d_nodes = reinterpret_cast<const int *>(base);
+        d_cap = reinterpret_cast<const int *>(base + o1);
+        d_use = reinterpret_cast<const int *>(base + o2);
+        d_haz = reinterpret_cast<const uint8_t *>(base + o3);
+    }
+    RSK_TRY(ctx->work[5].reserve(16));
+    d_out = ctx->work[5].as<int>();
+    const size_t lds = ((size_t)((N + 3) & ~3) + 2 * (kRowThreads / 64)) * 4;
+    if (lds > 64 * 1024)
+        RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&car_row_kernel),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    {
+        ScopedTimer tm(ctx, "car_row");
+        car_row_kernel<<<1, kRowThreads, lds, ctx->stream>>>(d_nodes, k, d_cap, d_use, d_haz, N, d_out);
+        RSK_HIP(hipGetLastError());
+    }
+    int r[2];
+    if (dev) {
+        RSK_HIP(hipMemcpyAsync(out_target, d_out, 4, hipMemcpyDeviceToDevice, ctx->stream));
+        if (out_score) RSK_HIP(hipMemcpyAsync(out_score, d_out + 1, 4, hipMemcpyDeviceToDevice, ctx->stream));
+        return RSK_OK;
+    }
+    RSK_HIP(hipMemcpyAsync(r, d_out, 8, hipMemcpyDeviceToHost, ctx->stream));
+    RSK_HIP(hipStreamSynchronize(ctx->stream));  // r[] and the staging buffer live on this frame
+    *out_target = r[0];
+    if (out_score) *out_score = r[1];
+    return r[0] == RSK_TARGET_NO_CANDIDATE ? RSK_NO_CANDIDATE : RSK_OK;
 }
 
 int rsk_random_place(rsk_ctx *ctx, const uint8_t *hazard, int32_t N, int32_t S, const uint64_t *seeds,

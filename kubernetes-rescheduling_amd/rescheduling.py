@@ -158,9 +158,12 @@ def communication(deployment_info, harzard_node, cluster_monitoring, relations, 
     N = len(req.nodes)
     if N == 0 or req.hazard.all():
         raise ValueError("max() arg is an empty sequence")
-    tgt, _ = _api.car_place(req.row_ptr, req.col_idx, req.assign, 1, req.cap_cpu, req.use_cpu, req.hazard, N,
-                            rows=[0])
-    t = int(tgt[0])
+    if N <= _api.ROW_MAX_N:  # one launch: the related pods' nodes -> histogram -> argmax
+        t, _ = _api.car_row(req.assign[1:], req.cap_cpu, req.use_cpu, req.hazard, N)
+    else:
+        tgt, _ = _api.car_place(req.row_ptr, req.col_idx, req.assign, 1, req.cap_cpu, req.use_cpu, req.hazard, N,
+                                rows=[0])
+        t = int(tgt[0])
     if t == TARGET_NO_CANDIDATE:
         raise ValueError("max() arg is an empty sequence")
     _pod_spec(deployment_info)["nodeName"] = None if t < 0 else req.nodes[t]

@@ -66,6 +66,7 @@ SIGNATURES = {
     "rsk_cut_cost_rows": (C.c_int, [_vp, _vp, _vp, C.c_int32, C.c_int32, C.c_int32, _vp, C.c_int32, _vp, _vp,
                                     C.c_uint32]),
     "rsk_rounds_place": (C.c_int, [_vp, _vp, C.c_int32, _vp, _vp, _vp, C.c_int32, _vp, _vp, C.c_uint32]),
+    "rsk_car_row": (C.c_int, [_vp, _vp, C.c_int32, _vp, _vp, _vp, C.c_int32, _vp, _vp, C.c_uint32]),
     "rsk_rows_evict_key": (C.c_int, [_vp, _vp, C.c_int32, C.c_int32, _vp, _vp, C.c_uint32]),
     "rsk_rows_evict_decode": (C.c_int, [_vp, _vp, C.c_int32, _vp, C.c_uint32]),
     "rsk_rows_apply": (C.c_int, [_vp, _vp, C.c_int32, _vp, _vp, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, _vp, _vp,

@@ -93,6 +93,23 @@ def car_place(row_ptr, col_idx, assign, S, cap_cpu, use_cpu, hazard, N, rows=Non
         plan.close()
 
 
+ROW_MAX_N = 32768
+
+
+def car_row(node_of, cap_cpu, use_cpu, hazard, N, ctx=None):
+    """One CAR placement (S = 1) from the related pods' nodes in one launch
+    (rsk_car_row): returns (target, score); target -1 is None, and
+    RSK_TARGET_NO_CANDIDATE when every node is hazard."""
+    import ctypes as C
+    ctx = ctx or default_context()
+    nb = _c(node_of, _I32) if len(node_of) else np.zeros(1, _I32)
+    cap, use, haz = _c(cap_cpu, _I32), _c(use_cpu, _I32), _c(hazard, np.uint8)
+    t, sc = C.c_int32(), C.c_int32()
+    check(ctx.lib.rsk_car_row(ctx.handle, ptr(nb), len(node_of), ptr(cap), ptr(use), ptr(haz), N, C.byref(t),
+                              C.byref(sc), 0), allow_no_candidate=True)
+    return t.value, sc.value
+
+
 class Rounds:
     """The multi-round detect -> evict -> CAR -> update loop (rsk_rounds_*,
     SURVEY §8f item 1; main.py:55-110 per scenario, the pod's CPU moving with

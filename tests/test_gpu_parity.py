@@ -490,3 +490,30 @@ def test_pick_max_pod_metric_edges_gpu(ctx):
             continue
         r = int(api.pick_max_pod(assign, cpu, len(pods), 1, [most], ctx=ctx)[0])
         assert (pods[r][0] if r >= 0 else None) == pick_edge_expected(case), case
+
+
+def test_car_row_single_launch_vs_oracle(ctx):
+    """rsk_car_row (the drop-in's one-launch CAR for S = 1) against the oracle's
+    one-row CSR: random node multisets with ties, overloaded nodes, zero
+    scores, invalid node ids, every node hazard, and N up to 32768."""
+    from oracle import oracle as orc
+    from rsk import api
+    rng = np.random.default_rng(1200)
+    for trial in range(60):
+        N = int(rng.choice([1, 2, 3, 7, 64, 5000, 32768]))
+        k = int(rng.choice([0, 1, 2, 5, 40, 300, 3000]))
+        spread = max(1, N // int(rng.choice([1, 4, 50])))
+        node_of = rng.integers(-1, spread + 1, k).astype(np.int32)
+        cap = rng.choice([4000, 8000], N).astype(np.int32)
+        use = rng.integers(0, 9000, N).astype(np.int32)
+        if trial % 3 == 0:
+            use[:] = cap - rng.integers(-2, 3, N)  # rem around 0: None vs node
+        haz = (rng.random(N) < float(rng.choice([0.0, 0.3, 1.0]))).astype(np.uint8)
+        rp = np.array([0, k] + [k] * k, np.int32)
+        ci = np.arange(1, k + 1, dtype=np.int32)
+        assign = np.concatenate([[-1], node_of]).astype(np.int32)
+        t, sc = api.car_row(node_of, cap, use, haz, N, ctx=ctx)
+        ot, osc = orc.car(rp, ci, assign, 1, cap, use, haz, N, rows=np.array([0], np.int32))
+        assert t == int(ot[0]), f"trial {trial}: N={N} k={k} target {t} != {int(ot[0])}"
+        if int(ot[0]) != -2:
+            assert sc == int(osc[0]), f"trial {trial}: score {sc} != {int(osc[0])}"
