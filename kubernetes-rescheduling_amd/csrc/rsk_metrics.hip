@@ -142,6 +142,60 @@ __global__ void pick_node_finish(const unsigned long long *__restrict__ best, co
     out[s] = r < (unsigned)N ? inv[r] : RSK_TARGET_NO_CANDIDATE;
 }
 
+// S = 1 from host arrays (the drop-in's single call): one workgroup, one
+// staging copy, one launch.  Key (val, rank) per non-hazard node, min for
+// spread (as the max of its complement), max for binpack; then the node whose
+// name rank won writes itself.
+template <bool kMin>
+__global__ __launch_bounds__(kRowThreads) void pick_node_row_kernel(const int *__restrict__ val,
+                                                                    const int *__restrict__ rank,
+                                                                    const uint8_t *__restrict__ haz, int N,
+                                                                    int *__restrict__ out) {
+    __shared__ unsigned long long red[kRowThreads / 64];
+    unsigned long long b = 0ull;
+    for (int n = threadIdx.x; n < N; n += kRowThreads)
+        if (!haz[n]) {
+            const unsigned long long k = pack_hi_lo(val[n], (unsigned)rank[n]);
+            const unsigned long long kk = kMin ? ~k : k;
+            b = kk > b ? kk : b;
+        }
+    row_block_max_u64(b, red);
+    if (b == 0ull) {
+        if (threadIdx.x == 0) out[0] = RSK_TARGET_NO_CANDIDATE;
+        return;
+    }
+    const unsigned r = (unsigned)((kMin ? ~b : b) & 0xffffffffull);
+    for (int n = threadIdx.x; n < N; n += kRowThreads)
+        if (!haz[n] && (unsigned)rank[n] == r) out[0] = n;
+}
+
+template <bool kMin>
+static int pick_node_row(rsk_ctx *ctx, const int32_t *val, const int32_t *name_rank, const uint8_t *hazard, int32_t N,
+                         int32_t *out_node, const char *tag) {
+    const size_t cb = (size_t)N * 4, o1 = (cb + 15) & ~(size_t)15, o2 = o1 + o1, tot = o2 + (size_t)N;
+    RSK_TRY(ctx->host_stage[7].reserve(tot));
+    std::vector<char> buf(tot);
+    std::memcpy(buf.data(), val, cb);
+    std::memcpy(buf.data() + o1, name_rank, cb);
+    std::memcpy(buf.data() + o2, hazard, (size_t)N);
+    char *base = static_cast<char *>(ctx->host_stage[7].ptr);
+    RSK_HIP(hipMemcpyAsync(base, buf.data(), tot, hipMemcpyHostToDevice, ctx->stream));
+    RSK_TRY(ctx->work[5].reserve(16));
+    int *d_out = ctx->work[5].as<int>();
+    {
+        ScopedTimer tm(ctx, tag);
+        pick_node_row_kernel<kMin><<<1, kRowThreads, 0, ctx->stream>>>(
+            reinterpret_cast<const int *>(base), reinterpret_cast<const int *>(base + o1),
+            reinterpret_cast<const uint8_t *>(base + o2), N, d_out);
+        RSK_HIP(hipGetLastError());
+    }
+    int r = 0;
+    RSK_HIP(hipMemcpyAsync(&r, d_out, 4, hipMemcpyDeviceToHost, ctx->stream));
+    RSK_HIP(hipStreamSynchronize(ctx->stream));  // r and the staging buffer live on this frame
+    *out_node = r;
+    return r == RSK_TARGET_NO_CANDIDATE ? RSK_NO_CANDIDATE : RSK_OK;
+}
+
 template <bool kMin>
 static int pick_node(rsk_ctx *ctx, const int32_t *val, const int32_t *name_rank, const uint8_t *hazard, int32_t N,
                      int32_t S, int32_t *out_node, uint32_t flags, const char *tag) {
@@ -149,6 +203,8 @@ static int pick_node(rsk_ctx *ctx, const int32_t *val, const int32_t *name_rank,
     RSK_CHECK(N > 0 && S > 0 && (int64_t)N * S < INT32_MAX, "bad sizes N=%d S=%d", N, S);
     RSK_CHECK(out_node, "null out_node");
     const bool dev = flags & RSK_F_DEVICE;
+    if (S == 1 && !dev && val && name_rank && hazard)
+        return pick_node_row<kMin>(ctx, val, name_rank, hazard, N, out_node, tag);
     const size_t NS = (size_t)N * S;
     const int *d_val, *d_rank;
     const uint8_t *d_haz;
