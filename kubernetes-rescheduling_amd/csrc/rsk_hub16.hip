@@ -460,8 +460,19 @@ Hub16Geom hub16_geometry(int dmax, int N) {
 }
 
 int hub16_lg(int d, int S) {  // log2 of the scenario group of a degree-d row
+    // staging cells per work item of the rows above 255 neighbours (the team
+    // class): 2048 — smaller groups, more workgroups in flight (config 4
+    // 0.273 -> 0.261 ms, config 3 within noise; RSK_HUB16_STAGE overrides,
+    // RSK_HUB16_STAGE_ALL=1 applies it to every class)
+    static const int cap = [] {
+        const char *e = getenv("RSK_HUB16_STAGE");
+        const int v = e ? atoi(e) : 2048;
+        return v >= 256 && v <= kHStage ? v : kHStage;
+    }();
+    static const bool all = [] { const char *e = getenv("RSK_HUB16_STAGE_ALL"); return e && atoi(e) != 0; }();
+    const int lim = (all || d > 255) ? std::max(cap, d) : kHStage;
     int lg = 0;
-    while (lg < 6 && ((int64_t)d << (lg + 1)) <= kHStage && (1 << lg) < S) ++lg;
+    while (lg < 6 && ((int64_t)d << (lg + 1)) <= lim && (1 << lg) < S) ++lg;
     return lg;
 }
 
