@@ -187,7 +187,15 @@ int launch_prep(hipStream_t stream, const Prep16Args &a) {
     // 4 scenarios per thread when S % 4 == 0 (16-B use / key words, 8-B codes)
     const bool v4 = a.S % 4 == 0 && ((uintptr_t)a.use % 16) == 0 && ((uintptr_t)a.haz % 4) == 0;
     const int SV = v4 ? a.S / 4 : a.S;
-    const int target_threads = 256 * 1024;  // 2^18 threads (1024 workgroups): more cost zero-case atomics, fewer cost bandwidth
+    // Threads: more cost zero-case atomics, fewer cost bandwidth.  A scenario's
+    // slot receives one atomic per workgroup over its node chunks — threads /
+    // SV of them when SV >= 256, threads / 256 below — so aim at ~256 per slot:
+    // 256 * max(SV, 256) threads within [2^16, 2^18] (config 3, SV = 1024:
+    // 2^18; config 4, SV = 16: 2^16, prep 0.029 -> 0.024 ms).  RSK_PREP_THREADS
+    // overrides (experiments).
+    static const int env_threads = [] { const char *e = getenv("RSK_PREP_THREADS"); return e ? atoi(e) : 0; }();
+    const int target_threads = env_threads >= 1024 ? env_threads
+                                                   : (int)std::min<int64_t>(256 * 1024, std::max<int64_t>(65536, 256LL * std::max(SV, 256)));
     const int npb = (int)std::max<int64_t>(1, ceil_div((int64_t)a.N * SV, target_threads));
     const int64_t chunks = ceil_div(a.N, npb);
     const unsigned total = (unsigned)(chunks * SV);
