@@ -124,3 +124,6 @@ def test_product_path_fails_loudly_without_gpu():
     info = {"metadata": {"name": "a"}, "spec": {"template": {"spec": {"affinity": None}}}}
     with pytest.raises(RskError):
         R.communication(info, [], cm, {}, ["w1"])
+    for f in (R.spread, R.binpack):   # the single-launch S = 1 paths too
+        with pytest.raises(RskError):
+            f(dict(info), [], cm)
