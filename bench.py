@@ -57,11 +57,21 @@ def cpu_model():
     return name, os.cpu_count() or 1
 
 
-def python_legs(c, N, S, budget_s=6.0):
+def cgroup_cpu_quota():
+    """The cgroup v2 CPU limit as cores (cpu.max quota / period), None when unlimited or unknown."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def python_legs(c, N, S, budget_s=6.0, numpy_budget_s=20.0):
     """SURVEY §8d CPU legs 1 and 2 (oracle/car_py.py, one core): the literal
     pure-Python restatement of rescheduling.py:183-214 on 64 evenly spaced pods
-    of scenario 0, and the numpy vectorized one on the same pods over as many
-    scenarios as fit the budget.  One call = one (pod, scenario) = N evaluations."""
+    of scenario 0, and the numpy vectorized one on every pod of scenario 0.
+    One call = one (pod, scenario) = N evaluations."""
     from oracle import car_py
     P = c.P
     pods = np.linspace(0, P - 1, 64).astype(np.int64)
@@ -82,18 +92,20 @@ def python_legs(c, N, S, budget_s=6.0):
                  "value": round(calls * N / dt, 1), "unit": "pod×node evals/s", "cores": 1,
                  "sample": f"{calls} evenly spaced pods x scenario 0 x {N} nodes",
                  "ms_per_call": round(dt * 1e3 / calls, 3)})
-    calls, s = 0, 0
+    # leg 2 (BASELINE.md "CPU-baseline plan" item 2): every pod of scenario 0,
+    # capped at numpy_budget_s (then the pods done are reported)
+    nb_all = car_py.dedup_rows(c.row_ptr, c.col_idx, range(P))
+    calls = 0
     t0 = time.perf_counter()
-    while s < S and time.perf_counter() - t0 < budget_s:
-        a, u, h = car_py.scenario_view(c.assign, c.use_cpu, c.hazard, P, N, S, s)
-        for nb in nbrs:
-            car_py.car_numpy(nb, a, c.cap_cpu, u, h, N)
-            calls += 1
-        s += 1
+    for nb in nb_all:
+        car_py.car_numpy(nb, a, c.cap_cpu, u, h, N)
+        calls += 1
+        if (calls & 255) == 0 and time.perf_counter() - t0 > numpy_budget_s:
+            break
     dt = time.perf_counter() - t0
     legs.append({"kind": "port", "impl": "numpy vectorized restatement (oracle/car_py.car_numpy)",
                  "value": round(calls * N / dt, 1), "unit": "pod×node evals/s", "cores": 1,
-                 "sample": f"64 evenly spaced pods x {s} scenarios x {N} nodes",
+                 "sample": f"{'all ' if calls == P else ''}{calls} of {P} pods x scenario 0 x {N} nodes",
                  "ms_per_call": round(dt * 1e3 / calls, 4)})
     return legs
 
@@ -111,14 +123,17 @@ def alg_bytes(kernel, P, N, S, info):
     """Algorithmic bytes per step of one kernel (DESIGN.md "Roofline accounting"):
       car_tile : the assign slice of every distinct pod in the tile images once (4·S per pod)
                  + target of its rows (4·S) + the tile plan (image lists, records)
-      car_mid  : target of each mid row (4·S) + records (neighbour slices are re-reads: not counted)
-      car_heavy: target of each hub row (4·S) + hub items / CSR
-      car_prep : use + hazard (5·N·S) + cap (4·N) read, nodekey (4·N·S) written
+      car_side : target of each side row (4·S) + side items / neighbour lists (neighbour slices
+                 are re-reads of pods the tiles stage: not counted)
+      car_mid  : target of each mid row (4·S) + records (earlier kernels, RSK_SIDE_OLD=1)
+      car_heavy: target of each hub row (4·S) + hub items / CSR (earlier kernels)
+      car_prep : use + hazard (5·N·S) + cap (4·N) read, the 16-bit code (2·N·S) written
     """
     return {"car_tile": 4 * S * info["image_pods_distinct"] + 4 * S * info["tile_rows"] + info["tile_bytes"],
+            "car_side": 4 * S * info.get("side_rows", 0) + info.get("side_bytes", 0),
             "car_mid": 4 * S * info["mid_rows"] + info["mid_bytes"],
             "car_heavy": 4 * S * info["heavy_rows"] + info["heavy_bytes"],
-            "car_prep": 9 * N * S + 4 * N}.get(kernel, 0)
+            "car_prep": 7 * N * S + 4 * N}.get(kernel, 0)
 
 
 def bench_rounds(args, cfg, world, rank, local, dev):
@@ -145,6 +160,10 @@ def bench_rounds(args, cfg, world, rank, local, dev):
     tg = torch.empty(R * S, dtype=torch.int32, device=dev)
     if args.warmup:
         rounds.run(T["assign"], S, T["cap_cpu"], T["use_cpu"], N, args.warmup, 30, ev, tg, device=True)
+    # the timed call's own starting state for its first k scenarios (parity below)
+    k = min(S, 16)
+    a_start = T["assign"].view(P, S)[:, :k].cpu().numpy().copy().reshape(-1)
+    u_start = T["use_cpu"].view(N, S)[:, :k].cpu().numpy().copy().reshape(-1)
     ctx.reset_profiling()
     ctx.set_profiling(not args.no_kernel_events)
     torch.cuda.synchronize(dev)
@@ -168,16 +187,17 @@ def bench_rounds(args, cfg, world, rank, local, dev):
         if n:
             kernels[name] = {"avg_ms": ms / n, "launches": n, "per_step_ms": ms / args.steps}
     tgt = tg.cpu().numpy()[args.warmup * S:]
-    # parity: 8 scenarios (the u16-shadow scan), 6 rounds from the initial state,
-    # GPU loop vs oracle_rounds
+    # parity of the timed call itself: its first k scenarios, all R rounds from
+    # the state it started from, against oracle_rounds (final assign / use,
+    # evictions and targets of every round)
     from oracle import oracle as orc
-    k = min(S, 8)
-    a0 = c.assign.reshape(P, S)[:, :k].copy().reshape(-1)
-    u0 = c.use_cpu.reshape(N, S)[:, :k].copy().reshape(-1)
-    exp = orc.rounds(c.row_ptr, c.col_idx, c.pod_cpu, a0, k, c.cap_cpu, u0, N, 6)
-    a1, u1 = a0.copy(), u0.copy()
-    e1, t1_ = rounds.run(a1, k, c.cap_cpu, u1, N, 6)
-    parity_ok = all(np.array_equal(g, e) for g, e in zip((a1, u1, e1, t1_), exp))
+    R = args.steps
+    ea, eu, eev, etg = orc.rounds(c.row_ptr, c.col_idx, c.pod_cpu, a_start, k, c.cap_cpu, u_start, N, R)
+    got_ev = ev.cpu().numpy()[w:].reshape(R, S)[:, :k].reshape(-1)
+    got_a = T["assign"].view(P, S)[:, :k].cpu().numpy().reshape(-1)
+    got_u = T["use_cpu"].view(N, S)[:, :k].cpu().numpy().reshape(-1)
+    parity_ok = bool(np.array_equal(tgt.reshape(R, S)[:, :k].reshape(-1), etg) and np.array_equal(got_ev, eev)
+                     and np.array_equal(got_a, ea) and np.array_equal(got_u, eu))
     ms_step = elapsed * 1e3 / args.steps
     if rank == 0:
         line = {
@@ -192,6 +212,7 @@ def bench_rounds(args, cfg, world, rank, local, dev):
             "kernels": kernels, "moves": int((tgt >= 0).sum()), "none": int((tgt == -1).sum()),
             "no_candidate": int((tgt == -2).sum()), "no_evict": int((tgt == -3).sum()),
             "parity_sample_ok": bool(parity_ok),
+            "parity_sample": f"the timed {R}-round call, scenarios 0..{k - 1}, vs oracle_rounds from its start state",
         }
         print(json.dumps(line), flush=True)
     rounds.close()
@@ -269,8 +290,9 @@ def main():
     def step():
         plan.execute(T["assign"], S, T["cap_cpu"], T["use_cpu"], T["hazard"], N, out_t, None, device=True)
 
-    names = ("car_prep", "car_tile", "car_tile_heavy", "car_side", "car_slot", "car_mid", "car_heavy", "car_hub128", "car_hub256", "car_hub512",
-             "car_hub1024", "car_hub2048", "car_hub4096")
+    names = ("car_prep", "car_tile", "car_tile_heavy", "car_side", "car_side32", "car_side128", "car_side512",
+             "car_side2048", "car_side8192", "car_side65535", "car_slot", "car_mid", "car_heavy", "car_hub128",
+             "car_hub256", "car_hub512", "car_hub1024", "car_hub2048", "car_hub4096")
 
     def collect():
         out = {}
@@ -362,6 +384,7 @@ def main():
         pm = torch.full((P,), 1 << 28, dtype=torch.int64, device=dev)   # synthetic 256 MiB per pod
         thr = 40   # the synthetic nodes run at 2-43 % CPU: only the hottest are hazards, so pods move
         rr.run(a2, T["use_cpu"], T["cap_cpu"], pc, pm, N, S, 1, threshold=thr)   # warm-up round
+        a2.copy_(T["assign"])   # the timed rounds start from the generated state (use0 matches assign)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -383,6 +406,7 @@ def main():
             be2 = rdist.LibrskRoundsBackend(c.row_ptr, c.col_idx, c.pod_cpu, device=dev, stream_ordered=True)
             rr2 = rdist.RowShardedRounds(rshard, be2)
             rr2.run(a3, T["use_cpu"], T["cap_cpu"], pc, pm, N, S, 1, threshold=thr)
+            a3.copy_(T["assign"])
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -436,7 +460,8 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
+        # every core of this process's affinity mask (SURVEY §8d leg 3)
+        threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
         model, ncpu = cpu_model()
         # grow an evenly spaced pod sample until one timed pass takes >= 60 % of
         # --cpu-seconds (about 10-30 s of CPU work at the default)
@@ -453,7 +478,8 @@ def main():
         cpu = {"value": round(nrows * S * N / dt, 1), "unit": "pod×node evals/s", "cores": threads, "kind": "port",
                "sample": f"{nrows} evenly spaced pods x {S} scenarios x {N} nodes ({dt:.1f}s), oracle/rsk_oracle.c "
                          f"literal CAR restatement, OpenMP {threads} threads",
-               "seconds": round(dt, 2), "cpu_model": model, "host_logical_cpus": ncpu,
+               "seconds": round(dt, 2), "cpu_model": model, "host_logical_cpus": ncpu, "affinity_cpus": threads,
+               "cgroup_cpu_quota": cgroup_cpu_quota(), "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
                "legs": python_legs(c, N, S)}
 
     if rank == 0:

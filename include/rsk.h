@@ -204,17 +204,20 @@ int rsk_rounds_place(rsk_rounds *r, const int32_t *assign, int32_t S, const int3
  *   key of delete_replaced_pod.py:47-57's first max (cpu, lowest pod):
  *   key[s] = local_pod[s] >= 0 ? pod_cpu[g] << 32 | (2^32 - 1 - g) : -1 with
  *   g = r0 + local_pod[s];
- * rsk_rows_evict_decode: the reduced key -> evict[s] (global pod, -1 none);
+ * rsk_rows_evict_decode: the reduced key -> evict[s] (global pod in [0, P),
+ *   -1 none; a key that decodes outside [0, P) also gives -1);
  * rsk_rows_apply: the move of round r (main.py:73-91's edit + placement, the
- *   build-defined state update): where evict[s] >= 0 and target[s] >= 0,
- *   assign[evict*S+s] = target[s]; when the pod is in rows [r0, r1) its CPU /
- *   memory move between this rank's per-node partials cpu_part / mem_part
- *   [N*S] (old node only when it was in [0, N)).                            */
+ *   build-defined state update): where evict[s] in [0, P) and target[s] in
+ *   [0, N), assign[evict*S+s] = target[s]; when the pod is in rows [r0, r1)
+ *   (r1 <= P) its CPU / memory move between this rank's per-node partials
+ *   cpu_part / mem_part [N*S] (old node only when it was in [0, N)); any
+ *   other evict / target leaves the scenario untouched.                     */
 int rsk_rows_evict_key(rsk_ctx *ctx, const int32_t *local_pod, int32_t S, int32_t r0, const int32_t *pod_cpu,
                        int64_t *out_key, uint32_t flags);
-int rsk_rows_evict_decode(rsk_ctx *ctx, const int64_t *key, int32_t S, int32_t *out_evict, uint32_t flags);
+int rsk_rows_evict_decode(rsk_ctx *ctx, const int64_t *key, int32_t S, int32_t P, int32_t *out_evict,
+                          uint32_t flags);
 int rsk_rows_apply(rsk_ctx *ctx, int32_t *assign, int32_t S, const int32_t *evict, const int32_t *target,
-                   int32_t r0, int32_t r1, int32_t N, const int32_t *pod_cpu, const int64_t *pod_mem,
+                   int32_t r0, int32_t r1, int32_t P, int32_t N, const int32_t *pod_cpu, const int64_t *pod_mem,
                    int64_t *cpu_part, int64_t *mem_part, uint32_t flags);
 
 /* ---- µBench workmodel -> relation CSR (host only, no device) -----------------

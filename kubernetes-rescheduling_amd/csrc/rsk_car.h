@@ -14,7 +14,7 @@
 namespace rsk {
 
 constexpr int kKeyHaz = INT_MIN;  // cap - use never reaches INT_MIN (both in [0, 2^31))
-constexpr int kMaxDegree = 1 << 20;                // rows above kHubMax go through the chunked hub path
+constexpr int kMaxDegree = 65535;                  // 16-bit counts in the side kernel's tables (rsk_side16.hip)
 constexpr int kLightMax = 32;                      // LDS-tile rows: deg <= 32
 constexpr int kPairMax = 16;                       // pairwise-count classes: deg <= 16
 constexpr int kPackMaxN = (1 << 24) - 1;           // wide sorted classes pack node << 8 | image row: N < kPackMaxN
@@ -344,6 +344,35 @@ constexpr int kHub16Max[kNumHub16] = {128, 255, kHubMax};  // <= 255: u8 direct 
 Hub16Geom hub16_geometry(int dmax, int N);
 int hub16_lg(int d, int S);
 int launch_hub16(hipStream_t stream, const Hub16Args &a, const Hub16Geom &g, int n_items);
+
+// Side rows of the compact path (rsk_side16.hip): every row above the tiles,
+// in launches by degree class; a work item is (row, chunk of 64 scenarios).
+constexpr int kNumSide = 6;
+constexpr int kSideMax[kNumSide] = {32, 128, 512, 2048, 8192, kMaxDegree};  // class upper degrees
+struct SideArgs {
+    const int *items;         // [n_rows][4]: out row, offset into col, degree, 0 (degree descending)
+    int n_rows, nchunk;       // work items = n_rows * nchunk, chunk-major
+    const int *col;           // neighbour lists
+    const int *assign;
+    const unsigned short *code;
+    const int *cap, *use;
+    const int *zc_cnt;
+    const unsigned long long *zc_key;
+    int *out_target, *out_score;
+    int S, N;
+    int H, hshift, K, cells;  // per-team LDS geometry (side16_geometry), word offsets below
+    int off_umask, off_srt, off_lvl, off_dl, off_ndl;
+    unsigned lds_team;
+    int xcd_per;              // workgroups per XCD run (set by launch_side16)
+    int ablate;               // profiling only: 1 skips the exact per-scenario recounts
+};
+struct SideGeom {
+    int dmax, Dc, H, hshift, K, T, W, kB, cells;
+    int off_umask, off_srt, off_lvl, off_dl, off_ndl;
+    size_t lds_team;
+};
+SideGeom side16_geometry(int dmax, int N);
+int launch_side16(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32);
 
 int launch_prep(hipStream_t stream, const Prep16Args &a);
 int launch_mid16(hipStream_t stream, const Mid16Args &a);

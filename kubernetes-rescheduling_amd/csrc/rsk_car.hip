@@ -750,6 +750,7 @@ struct rsk_car_plan {
     int light_max = kLightMax;  // rows with deg <= light_max go to the tiles
     // tiles
     int T = 0, T_lean = 0, rmax = 0, recmax = 0, n_tile_rows = 0, n_sorted_rows = 0;  // tiles [T_lean, T): heavy
+    int n_lean_rows = 0;  // tile rows in the lean tiles
     int owners_cap = kTileOwners, rows_cap = kTileRows;  // tile limits (RSK_TILE_OWNERS / RSK_TILE_ROWS)
     int64_t img_rows_total = 0, img_pods_distinct = 0, n_img_pods = 0, n_recs = 0;
     DevBuf img_pods, meta, recs;
@@ -776,6 +777,11 @@ struct rsk_car_plan {
     int n_slot[2] = {0, 0};
     int slot_dmax[2] = {0, 0};
     DevBuf slot_items[2];
+    // compact path: every side row (deg > light_max) for car_side16, degree
+    // descending, split into the kSideMax classes (neighbours in pcol)
+    DevBuf side_items;
+    int side_beg[kNumSide] = {}, side_end[kNumSide] = {};
+    int side_dmax[kNumSide] = {};
     // per-execute workspace
     DevBuf nodekey, code, zc;
     // the inputs, kept for the N >= kPackMaxN variant (built on first use)
@@ -793,6 +799,7 @@ struct rsk_car_plan {
         hcol.release();
         for (auto &b : piv_items) b.release();
         for (auto &b : slot_items) b.release();
+        side_items.release();
         pcol.release();
         nodekey.release();
         code.release();
@@ -972,7 +979,7 @@ struct TileBuilder {
     std::vector<int> cur_pods;
     std::unordered_map<int, int> cur_slot;
     std::vector<int> cur_rec[kNumCls];
-    int cur_rows = 0, cur_rec_ints = 0, T = 0, rmax = 0, recmax = 0, n_sorted = 0;
+    int cur_rows = 0, cur_rec_ints = 0, T = 0, rmax = 0, recmax = 0, n_sorted = 0, n_rows = 0;
     int owners_cap = kTileOwners, rows_cap = kTileRows;
     int64_t img_total = 0;
 
@@ -1010,6 +1017,7 @@ struct TileBuilder {
             for (int j = 0; j < d; ++j) e[o + r0 + j / 2] |= lr[j] << ((j & 1) * 16);
         }
         n_sorted += c >= 5;
+        ++n_rows;
         cur_rec_ints += kClsW[c];
         ++cur_rows;
     }
@@ -1126,6 +1134,7 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
     tl.close();
     th.close();
     plan->T_lean = tl.T;
+    plan->n_lean_rows = tl.n_rows;
     TileBuilder &tb = tl;  // lean tiles first, then the heavy ones (offsets shifted)
     for (int t = 0; t < th.T; ++t) {
         int *m = th.meta.data() + (size_t)t * kMetaW;
@@ -1173,6 +1182,25 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
         RSK_TRY(upload(plan->piv_items[c], pitems[c].data(), pitems[c].size() * sizeof(HeavyItem)));
     }
     RSK_TRY(upload(plan->pcol, pcol.data(), pcol.size() * 4));
+    {   // car_side16 classes: all side rows, degree descending; class c holds
+        // the rows of degree (kSideMax[c - 1], kSideMax[c]] at [side_beg[c], side_end[c])
+        std::vector<HeavyItem> all;
+        for (const auto &v : pitems) all.insert(all.end(), v.begin(), v.end());
+        std::stable_sort(all.begin(), all.end(), [](const HeavyItem &x, const HeavyItem &y) { return x.d > y.d; });
+        int end = (int)all.size();
+        for (int c = 0; c < kNumSide; ++c) {
+            int b = end;
+            while (b > 0 && all[b - 1].d <= kSideMax[c]) --b;
+            plan->side_beg[c] = b;
+            plan->side_end[c] = end;
+            plan->side_dmax[c] = b < end ? all[b].d : 0;
+            end = b;
+        }
+        std::vector<int32_t> flat;
+        flat.reserve(all.size() * 4);
+        for (const HeavyItem &h : all) flat.insert(flat.end(), {h.oi, h.rb, h.d, 0});
+        RSK_TRY(upload(plan->side_items, flat.data(), flat.size() * 4));
+    }
     {
         std::vector<HeavyItem> sl[2];
         for (const HeavyItem &h : pitems[0])
@@ -1231,6 +1259,13 @@ struct SideBufs {
 // hub rows (> 64) still go through the wide hub kernel, which reads exact keys.
 bool mid16_on() {
     static const bool on = env_int("RSK_MID16", 0) != 0;  // car_mid16 (codes) instead of car_mid (exact keys)
+    return on;
+}
+
+// Compact side rows through car_side16 (rsk_side16.hip, default); RSK_SIDE_OLD=1
+// restores the earlier kernels below (A/B only).
+bool side_new_on() {
+    static const bool on = env_int("RSK_SIDE_OLD", 0) == 0;
     return on;
 }
 
@@ -1327,6 +1362,39 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t *side, int n
     int *d_target = b.target, *d_score = b.score;
     int next = 0;
     auto pick = [&]() { return side[next++ % nside]; };
+    if (compact && side_new_on()) {  // car_side16: every side row, one launch per degree class, longest first
+        const bool off32 = (int64_t)std::max(plan->P, plan->Q) * S * 4 < ((int64_t)1 << 32);
+        static const int sablate = env_int("RSK_ABLATE_SIDE", 0);
+        static const bool per_class = env_int("RSK_SIDE_TIMERS", 0) != 0;
+        static const char *const kNames[kNumSide] = {"car_side32", "car_side128", "car_side512",
+                                                     "car_side2048", "car_side8192", "car_side65535"};
+        for (int c = kNumSide - 1; c >= 0; --c) {
+            const int n = plan->side_end[c] - plan->side_beg[c];
+            if (n == 0) continue;
+            SideArgs a;
+            std::memset(&a, 0, sizeof(a));
+            a.items = plan->side_items.as<int>() + (size_t)plan->side_beg[c] * 4;
+            a.n_rows = n;
+            a.nchunk = (int)ceil_div(S, 64);
+            a.col = plan->pcol.as<int>();
+            a.assign = d_assign;
+            a.code = b.code;
+            a.cap = b.cap;
+            a.use = b.use;
+            a.zc_cnt = d_zcnt;
+            a.zc_key = d_zkey;
+            a.out_target = d_target;
+            a.out_score = d_score;
+            a.S = S;
+            a.N = N;
+            a.ablate = sablate;
+            const SideGeom g = side16_geometry(plan->side_dmax[c], N);
+            const hipStream_t stream = pick();
+            ScopedTimer tm(ctx, per_class ? kNames[c] : "car_side", stream);
+            RSK_TRY(launch_side16(stream, a, g, off32));
+        }
+        return RSK_OK;
+    }
     if (compact) {  // pivot-delta kernel: every side row (RSK_PIVOT=1) or the rows above kHubMax
         for (int c = pivot_on() ? 0 : kNumPiv - 1; c < kNumPiv; ++c) {
             if (!plan->n_piv[c]) continue;
@@ -1541,7 +1609,10 @@ int rsk_car_plan_create(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col
         RSK_CHECK(col_idx[k] >= 0 && col_idx[k] < P, "col_idx[%lld]=%d out of range", (long long)k, col_idx[k]);
     if (rows)
         for (int32_t i = 0; i < Q; ++i) RSK_CHECK(rows[i] >= 0 && rows[i] < P, "rows[%d]=%d out of range", i, rows[i]);
-    return plan_create(ctx, row_ptr, col_idx, P, rows, Q, kLightMax, out);
+    // rows up to light_max go to the LDS tiles, the rest to the side kernels;
+    // RSK_LIGHT_MAX = 16 sends the 17..32 rows to car_side16 (no heavy tiles)
+    static const int light_max = env_int("RSK_LIGHT_MAX", kLightMax) == kPairMax ? kPairMax : kLightMax;
+    return plan_create(ctx, row_ptr, col_idx, P, rows, Q, light_max, out);
 }
 
 int rsk_car_plan_info(const rsk_car_plan *plan, int64_t *out, int n) {
@@ -1557,10 +1628,13 @@ int rsk_car_plan_info(const rsk_car_plan *plan, int64_t *out, int n) {
         heavy_bytes += (int64_t)plan->n_heavy[c] * (int64_t)sizeof(HeavyItem);
     }
     const int64_t tile_bytes = plan->T > 0 ? (int64_t)(plan->img_pods.bytes + plan->meta.bytes + plan->recs.bytes) : 0;
-    const int64_t v[15] = {plan->n_tile_rows, 0, mid, heavy, plan->T, plan->rmax, plan->owners_cap,
+    const int64_t side = plan->side_end[0] - plan->side_beg[kNumSide - 1];
+    const int64_t side_bytes = (int64_t)plan->side_items.bytes + (int64_t)plan->pcol.bytes;
+    const int64_t v[20] = {plan->n_tile_rows, 0, mid, heavy, plan->T, plan->rmax, plan->owners_cap,
                            tile_bytes, 0, mid_bytes, heavy_bytes, plan->max_deg, plan->img_rows_total,
-                           plan->img_pods_distinct, plan->n_sorted_rows};
-    const int m = n < 15 ? n : 15;
+                           plan->img_pods_distinct, plan->n_sorted_rows, side, side_bytes, plan->light_max,
+                           plan->n_lean_rows, plan->T_lean};
+    const int m = n < 20 ? n : 20;
     for (int i = 0; i < m; ++i) out[i] = v[i];
     return m;
 }

@@ -155,8 +155,11 @@ __global__ __launch_bounds__(kRowThreads) void pick_node_row_kernel(const int *_
     unsigned long long b = 0ull;
     for (int n = threadIdx.x; n < N; n += kRowThreads)
         if (!haz[n]) {
+            // rank < N < 2^31 leaves bit 31 free: set in every candidate's key (the
+            // complement sets it for spread), so 0 means "no candidate" even for
+            // binpack's (INT32_MIN, rank 0)
             const unsigned long long k = pack_hi_lo(val[n], (unsigned)rank[n]);
-            const unsigned long long kk = kMin ? ~k : k;
+            const unsigned long long kk = kMin ? ~k : (k | 0x80000000ull);
             b = kk > b ? kk : b;
         }
     row_block_max_u64(b, red);
@@ -164,7 +167,7 @@ __global__ __launch_bounds__(kRowThreads) void pick_node_row_kernel(const int *_
         if (threadIdx.x == 0) out[0] = RSK_TARGET_NO_CANDIDATE;
         return;
     }
-    const unsigned r = (unsigned)((kMin ? ~b : b) & 0xffffffffull);
+    const unsigned r = (unsigned)((kMin ? ~b : b) & 0x7fffffffull);
     for (int n = threadIdx.x; n < N; n += kRowThreads)
         if (!haz[n] && (unsigned)rank[n] == r) out[0] = n;
 }
@@ -521,8 +524,9 @@ __global__ __launch_bounds__(256) void cut_cost_wave_kernel(const int *__restric
     const cint_ptr rp = const_ptr(row_ptr), cl = const_ptr(col), ms = const_ptr(missing);
     unsigned long long c = 0;
     if (missing) {
-        for (int b0 = r0 + w * 64; b0 < r1; b0 += nw * 64)
-            for (int b = b0; b < min(b0 + 64, r1); b += 16) {
+        // 64-bit strides: b0 + nw * 64 may pass INT32_MAX near the end
+        for (long long b0 = r0 + (long long)w * 64; b0 < r1; b0 += (long long)nw * 64)
+            for (int b = (int)b0; b < (int)min(b0 + 64, (long long)r1); b += 16) {
                 int ap[16];
 #pragma unroll
                 for (int i = 0; i < 16; ++i) ap[i] = assign[(size_t)min(b + i, r1 - 1) * S + s];
@@ -532,8 +536,9 @@ __global__ __launch_bounds__(256) void cut_cost_wave_kernel(const int *__restric
             }
     }
     const int ea = rp[r0], eb = rp[r1];
-    for (int ka = ea + w * kCutEdges; ka < eb; ka += nw * kCutEdges) {
-        const int kb = min(ka + kCutEdges, eb);
+    for (long long ka64 = ea + (long long)w * kCutEdges; ka64 < eb; ka64 += (long long)nw * kCutEdges) {
+        const int ka = (int)ka64;
+        const int kb = (int)min(ka64 + kCutEdges, (long long)eb);
         // the row of edge ka (the last p with row_ptr[p] <= ka): a 16-way
         // search, 16 independent scalar loads per round
         int lo = r0, hi = r1 - 1;

@@ -229,22 +229,27 @@ __global__ void rows_evict_key_kernel(const int *__restrict__ local_pod, int S, 
     key[s] = ((long long)pod_cpu[g] << 32) | (0xffffffffll - g);
 }
 
-__global__ void rows_evict_decode_kernel(const long long *__restrict__ key, int S, int *__restrict__ evict) {
+// A key that does not decode to a pod in [0, P) (a reduced buffer read before
+// its producer finished, or garbage) becomes "no eviction", never an index.
+__global__ void rows_evict_decode_kernel(const long long *__restrict__ key, int S, int P, int *__restrict__ evict) {
     const int s = blockIdx.x * 256 + threadIdx.x;
     if (s >= S) return;
     const long long k = key[s];
-    evict[s] = k >= 0 ? (int)(0xffffffffll - (k & 0xffffffffll)) : -1;
+    const long long g = k >= 0 ? 0xffffffffll - (k & 0xffffffffll) : -1;
+    evict[s] = g >= 0 && g < P ? (int)g : -1;
 }
 
 // scenario s owns assign[:, s] and the partials' column s: no two threads touch one word
 __global__ void rows_apply_kernel(int *__restrict__ assign, int S, const int *__restrict__ evict,
-                                  const int *__restrict__ target, int r0, int r1, int N,
+                                  const int *__restrict__ target, int r0, int r1, int P, int N,
                                   const int *__restrict__ pod_cpu, const long long *__restrict__ pod_mem,
                                   long long *__restrict__ cpu_part, long long *__restrict__ mem_part) {
     const int s = blockIdx.x * 256 + threadIdx.x;
     if (s >= S) return;
     const int e = evict[s], t = target[s];
-    if (e < 0 || t < 0) return;
+    // no move (None / no candidate / no eviction), and never an index outside
+    // the replica: e in [0, P), t in [0, N)
+    if (e < 0 || e >= P || t < 0 || t >= N) return;
     int *a = assign + (size_t)e * S + s;
     const int old = *a;
     *a = t;
@@ -254,10 +259,8 @@ __global__ void rows_apply_kernel(int *__restrict__ assign, int S, const int *__
         cpu_part[(size_t)old * S + s] -= c;
         mem_part[(size_t)old * S + s] -= m;
     }
-    if (t < N) {
-        cpu_part[(size_t)t * S + s] += c;
-        mem_part[(size_t)t * S + s] += m;
-    }
+    cpu_part[(size_t)t * S + s] += c;
+    mem_part[(size_t)t * S + s] += m;
 }
 
 }  // namespace
@@ -446,24 +449,24 @@ int rsk_rows_evict_key(rsk_ctx *ctx, const int32_t *local_pod, int32_t S, int32_
     return RSK_OK;
 }
 
-int rsk_rows_evict_decode(rsk_ctx *ctx, const int64_t *key, int32_t S, int32_t *out_evict, uint32_t flags) {
+int rsk_rows_evict_decode(rsk_ctx *ctx, const int64_t *key, int32_t S, int32_t P, int32_t *out_evict, uint32_t flags) {
     RSK_TRY(activate(ctx));
-    RSK_CHECK((flags & RSK_F_DEVICE) && key && out_evict && S > 0, "rsk_rows_evict_decode: bad arguments");
+    RSK_CHECK((flags & RSK_F_DEVICE) && key && out_evict && S > 0 && P > 0, "rsk_rows_evict_decode: bad arguments");
     rows_evict_decode_kernel<<<(unsigned)ceil_div(S, 256), 256, 0, ctx->stream>>>(
-        reinterpret_cast<const long long *>(key), S, out_evict);
+        reinterpret_cast<const long long *>(key), S, P, out_evict);
     RSK_HIP(hipGetLastError());
     return RSK_OK;
 }
 
 int rsk_rows_apply(rsk_ctx *ctx, int32_t *assign, int32_t S, const int32_t *evict, const int32_t *target, int32_t r0,
-                   int32_t r1, int32_t N, const int32_t *pod_cpu, const int64_t *pod_mem, int64_t *cpu_part,
+                   int32_t r1, int32_t P, int32_t N, const int32_t *pod_cpu, const int64_t *pod_mem, int64_t *cpu_part,
                    int64_t *mem_part, uint32_t flags) {
     RSK_TRY(activate(ctx));
     RSK_CHECK((flags & RSK_F_DEVICE) && assign && evict && target && pod_cpu && pod_mem && cpu_part && mem_part &&
-                  S > 0 && N > 0 && 0 <= r0 && r0 <= r1,
-              "rsk_rows_apply: bad arguments");
+                  S > 0 && N > 0 && 0 <= r0 && r0 <= r1 && r1 <= P,
+              "rsk_rows_apply: bad arguments (S=%d N=%d rows [%d, %d) of P=%d)", S, N, r0, r1, P);
     rows_apply_kernel<<<(unsigned)ceil_div(S, 256), 256, 0, ctx->stream>>>(
-        assign, S, evict, target, r0, r1, N, pod_cpu, reinterpret_cast<const long long *>(pod_mem),
+        assign, S, evict, target, r0, r1, P, N, pod_cpu, reinterpret_cast<const long long *>(pod_mem),
         reinterpret_cast<long long *>(cpu_part), reinterpret_cast<long long *>(mem_part));
     RSK_HIP(hipGetLastError());
     return RSK_OK;

@@ -68,9 +68,9 @@ SIGNATURES = {
     "rsk_rounds_place": (C.c_int, [_vp, _vp, C.c_int32, _vp, _vp, _vp, C.c_int32, _vp, _vp, C.c_uint32]),
     "rsk_car_row": (C.c_int, [_vp, _vp, C.c_int32, _vp, _vp, _vp, C.c_int32, _vp, _vp, C.c_uint32]),
     "rsk_rows_evict_key": (C.c_int, [_vp, _vp, C.c_int32, C.c_int32, _vp, _vp, C.c_uint32]),
-    "rsk_rows_evict_decode": (C.c_int, [_vp, _vp, C.c_int32, _vp, C.c_uint32]),
-    "rsk_rows_apply": (C.c_int, [_vp, _vp, C.c_int32, _vp, _vp, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, _vp, _vp,
-                                 C.c_uint32]),
+    "rsk_rows_evict_decode": (C.c_int, [_vp, _vp, C.c_int32, C.c_int32, _vp, C.c_uint32]),
+    "rsk_rows_apply": (C.c_int, [_vp, _vp, C.c_int32, _vp, _vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _vp, _vp,
+                                 _vp, _vp, C.c_uint32]),
     "rsk_workmodel_parse": (C.c_int, [C.c_char_p, C.c_int64, C.POINTER(_vp)]),
     "rsk_workmodel_load": (C.c_int, [C.c_char_p, C.POINTER(_vp)]),
     "rsk_workmodel_sizes": (C.c_int, [_vp, _i32p, _i64p, _i64p]),

@@ -47,7 +47,8 @@ class CarPlan:
 
     INFO_FIELDS = ("tile_rows", "direct_rows", "mid_rows", "heavy_rows", "tiles", "tile_image_rows",
                    "tile_pods", "tile_bytes", "direct_bytes", "mid_bytes", "heavy_bytes", "max_degree",
-                   "image_rows_total", "image_pods_distinct", "sorted_rows")
+                   "image_rows_total", "image_pods_distinct", "sorted_rows", "side_rows", "side_bytes",
+                   "light_max", "tile_rows_lean", "tiles_lean")
 
     def info(self) -> dict:
         """How the plan routed its rows (rsk_car_plan_info)."""

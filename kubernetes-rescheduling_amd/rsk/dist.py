@@ -284,14 +284,16 @@ class LibrskRoundsBackend:
         import torch
         self._sync()
         ev = torch.empty(S, dtype=torch.int32, device=self.dev)
-        self._check(self.ctx.lib.rsk_rows_evict_decode(self.ctx.handle, key.data_ptr(), S, ev.data_ptr(), self._F))
+        self._check(self.ctx.lib.rsk_rows_evict_decode(self.ctx.handle, key.data_ptr(), S, self.P, ev.data_ptr(),
+                                                       self._F))
         self._sync()
         return ev
 
     def apply(self, assign, S, evict, target, r0, r1, N, pod_cpu, pod_mem, cpu_part, mem_part):
         self._sync()
         self._check(self.ctx.lib.rsk_rows_apply(self.ctx.handle, assign.data_ptr(), S, evict.data_ptr(),
-                                                target.data_ptr(), r0, r1, N, pod_cpu.data_ptr(), pod_mem.data_ptr(),
+                                                target.data_ptr(), r0, r1, self.P, N, pod_cpu.data_ptr(),
+                                                pod_mem.data_ptr(),
                                                 cpu_part.data_ptr(), mem_part.data_ptr(), self._F))
         self._sync()
 

@@ -127,3 +127,21 @@ def test_product_path_fails_loudly_without_gpu():
     for f in (R.spread, R.binpack):   # the single-launch S = 1 paths too
         with pytest.raises(RskError):
             f(dict(info), [], cm)
+
+
+def test_stream_ordered_backend_rejects_default_stream(monkeypatch):
+    """The row-sharded loop's stream-ordered backend binds librsk to the current
+    torch stream; handle 0 (the legacy default stream) would read as "the
+    context's own stream" and leave librsk and torch unordered — the cause of
+    round 2's faulting gather.  It must refuse before any call."""
+    torch = pytest.importorskip("torch")
+    from rsk import dist as rdist
+
+    class _Default:
+        cuda_stream = 0
+
+    monkeypatch.setattr(torch.cuda, "current_stream", lambda *a, **k: _Default())
+    rp = np.array([0, 1, 2], np.int32)
+    ci = np.array([1, 0], np.int32)
+    with pytest.raises(ValueError, match="non-default"):
+        rdist.LibrskRoundsBackend(rp, ci, np.array([100, 200], np.int32), device="cuda:0", stream_ordered=True)
