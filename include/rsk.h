@@ -128,6 +128,12 @@ int rsk_random_count(rsk_ctx *ctx, const uint8_t *hazard, int32_t N, int32_t S, 
                      uint32_t flags);
 int rsk_random_select(rsk_ctx *ctx, const uint8_t *hazard, int32_t N, int32_t S, const int32_t *r,
                       int32_t *out_node, uint32_t flags);
+/* random's candidate list for the drop-in's single call (S = 1, host
+ * pointers; rescheduling.py:149-150): out_nodes[0 .. *out_count) = the
+ * non-hazard nodes in index order (nodes_name order), in one launch; the
+ * caller draws r = rd.choice(range(count)) and takes out_nodes[r]
+ * (rescheduling.py:153).  out_nodes holds N entries. */
+int rsk_random_candidates(rsk_ctx *ctx, const uint8_t *hazard, int32_t N, int32_t *out_nodes, int32_t *out_count);
 int rsk_random_place(rsk_ctx *ctx, const uint8_t *hazard, int32_t N, int32_t S, const uint64_t *seeds,
                      int32_t *out_node, uint32_t flags);
 /* CPython random.Random(seed)._randbelow(n) (host only; 0 < n < 2^31). */

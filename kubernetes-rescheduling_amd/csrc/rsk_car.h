@@ -364,7 +364,7 @@ struct SideArgs {
     int off_umask, off_srt, off_lvl, off_dl, off_ndl;
     unsigned lds_team;
     int xcd_per;              // workgroups per XCD run (set by launch_side16)
-    int ablate;               // profiling only: 1 skips the exact per-scenario recounts
+    int ablate;               // profiling only: 1 no exact recounts, 2 stop after the marks, 4 no walk, 8 no touched
 };
 struct SideGeom {
     int dmax, Dc, H, hshift, K, T, W, kB, cells;

@@ -48,6 +48,16 @@ struct DevBuf {
     template <class T> T *as() const { return static_cast<T *>(ptr); }
 };
 
+// Grow-only pinned host buffer mapped into the device's address space: the
+// single-call (S = 1) host paths write their inputs here and kernels read them
+// and write their results straight through `dev` (no staging copies).
+struct PinBuf {
+    void *host = nullptr, *dev = nullptr;
+    size_t bytes = 0;
+    int reserve(size_t need);
+    void release();
+};
+
 struct EventPair {
     hipEvent_t start, stop;
 };
@@ -68,6 +78,7 @@ struct rsk_ctx {
     hipEvent_t fork = nullptr, join[kAux] = {};
     rsk::DevBuf host_stage[12];  // device staging for host-pointer calls
     rsk::DevBuf work[6];         // per-call device workspace
+    rsk::PinBuf pin;             // mapped pinned host memory of the single-call paths
     std::vector<uint8_t> pinned;  // host scratch
 };
 

@@ -172,29 +172,84 @@ __global__ __launch_bounds__(kRowThreads) void pick_node_row_kernel(const int *_
         if (!haz[n] && (unsigned)rank[n] == r) out[0] = n;
 }
 
+// Host inputs of a single-call (S = 1) kernel: packed at 16-B offsets into the
+// context's mapped pinned buffer, followed by the result words.  Up to
+// kZeroCopyMax bytes the kernel reads the inputs there over PCIe (no copy);
+// above, one DMA copy to device staging.  The kernel writes its result words
+// straight into the pinned buffer, host-visible once the stream has synced.
+constexpr size_t kZeroCopyMax = 64 * 1024;
+struct RowIO {
+    const char *in;       // device view of the packed inputs
+    char *out_dev;        // device view of the result words
+    const char *out_host;
+    size_t off[4];        // input offsets
+};
+static int row_io(rsk_ctx *ctx, const void *const *src, const size_t *len, int n, size_t out_bytes, RowIO *io) {
+    size_t tot = 0;
+    for (int i = 0; i < n; ++i) {
+        io->off[i] = tot;
+        tot += (len[i] + 15) & ~(size_t)15;
+    }
+    RSK_TRY(ctx->pin.reserve(tot + out_bytes));
+    char *h = static_cast<char *>(ctx->pin.host);
+    for (int i = 0; i < n; ++i)
+        if (len[i]) std::memcpy(h + io->off[i], src[i], len[i]);
+    if (tot <= kZeroCopyMax) {
+        io->in = static_cast<const char *>(ctx->pin.dev);
+    } else {
+        RSK_TRY(ctx->host_stage[7].reserve(tot));
+        RSK_HIP(hipMemcpyAsync(ctx->host_stage[7].ptr, h, tot, hipMemcpyHostToDevice, ctx->stream));
+        io->in = static_cast<const char *>(ctx->host_stage[7].ptr);
+    }
+    io->out_dev = static_cast<char *>(ctx->pin.dev) + tot;
+    io->out_host = h + tot;
+    return RSK_OK;
+}
+
+// The candidate list of one scenario (rescheduling.py:149-150): non-hazard
+// node indices in order, compacted by one workgroup chunk by chunk.
+__global__ __launch_bounds__(kRowThreads) void candidates_row_kernel(const uint8_t *__restrict__ haz, int N,
+                                                                     int *__restrict__ out_nodes,
+                                                                     int *__restrict__ out_count) {
+    __shared__ int wsum[kRowThreads / 64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int base = 0;
+    for (int n0 = 0; n0 < N; n0 += kRowThreads) {
+        const int n = n0 + tid;
+        const bool c = n < N && !haz[n];
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(c);
+        if (lane == 0) wsum[w] = __builtin_popcountll(m);
+        __syncthreads();
+        int before = 0, total = 0;
+#pragma unroll
+        for (int i = 0; i < kRowThreads / 64; ++i) {
+            before += i < w ? wsum[i] : 0;
+            total += wsum[i];
+        }
+        if (c) out_nodes[base + before + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] = n;
+        base += total;
+        __syncthreads();
+    }
+    if (tid == 0) *out_count = base;
+}
+
 template <bool kMin>
 static int pick_node_row(rsk_ctx *ctx, const int32_t *val, const int32_t *name_rank, const uint8_t *hazard, int32_t N,
                          int32_t *out_node, const char *tag) {
-    const size_t cb = (size_t)N * 4, o1 = (cb + 15) & ~(size_t)15, o2 = o1 + o1, tot = o2 + (size_t)N;
-    RSK_TRY(ctx->host_stage[7].reserve(tot));
-    std::vector<char> buf(tot);
-    std::memcpy(buf.data(), val, cb);
-    std::memcpy(buf.data() + o1, name_rank, cb);
-    std::memcpy(buf.data() + o2, hazard, (size_t)N);
-    char *base = static_cast<char *>(ctx->host_stage[7].ptr);
-    RSK_HIP(hipMemcpyAsync(base, buf.data(), tot, hipMemcpyHostToDevice, ctx->stream));
-    RSK_TRY(ctx->work[5].reserve(16));
-    int *d_out = ctx->work[5].as<int>();
+    const void *src[3] = {val, name_rank, hazard};
+    const size_t len[3] = {(size_t)N * 4, (size_t)N * 4, (size_t)N};
+    RowIO io;
+    RSK_TRY(row_io(ctx, src, len, 3, 16, &io));
     {
         ScopedTimer tm(ctx, tag);
         pick_node_row_kernel<kMin><<<1, kRowThreads, 0, ctx->stream>>>(
-            reinterpret_cast<const int *>(base), reinterpret_cast<const int *>(base + o1),
-            reinterpret_cast<const uint8_t *>(base + o2), N, d_out);
+            reinterpret_cast<const int *>(io.in + io.off[0]), reinterpret_cast<const int *>(io.in + io.off[1]),
+            reinterpret_cast<const uint8_t *>(io.in + io.off[2]), N, reinterpret_cast<int *>(io.out_dev));
         RSK_HIP(hipGetLastError());
     }
-    int r = 0;
-    RSK_HIP(hipMemcpyAsync(&r, d_out, 4, hipMemcpyDeviceToHost, ctx->stream));
-    RSK_HIP(hipStreamSynchronize(ctx->stream));  // r and the staging buffer live on this frame
+    RSK_HIP(hipStreamSynchronize(ctx->stream));
+    const int r = *reinterpret_cast<const volatile int *>(io.out_host);
     *out_node = r;
     return r == RSK_TARGET_NO_CANDIDATE ? RSK_NO_CANDIDATE : RSK_OK;
 }
@@ -776,31 +831,25 @@ int rsk_car_row(rsk_ctx *ctx, const int32_t *node_of, int32_t k, const int32_t *
     const int *d_nodes = nullptr, *d_cap, *d_use;
     const uint8_t *d_haz;
     int *d_out;
-    // host pointers: one staging copy of all four inputs
+    // host pointers: the inputs packed into the mapped pinned buffer, the result written back there
+    RowIO io;
     if (dev) {
         d_nodes = node_of;
         d_cap = cap_cpu;
         d_use = use_cpu;
         d_haz = hazard;
+        RSK_TRY(ctx->work[5].reserve(16));
+        d_out = ctx->work[5].as<int>();
     } else {
-        const size_t nb = (size_t)k * 4, cb = (size_t)N * 4, hb = (size_t)N;
-        const size_t o1 = (nb + 15) & ~(size_t)15, o2 = o1 + ((cb + 15) & ~(size_t)15),
-                     o3 = o2 + ((cb + 15) & ~(size_t)15), tot = o3 + hb;
-        RSK_TRY(ctx->host_stage[7].reserve(tot));
-        std::vector<char> buf(tot);
-        if (k) std::memcpy(buf.data(), node_of, nb);
-        std::memcpy(buf.data() + o1, cap_cpu, cb);
-        std::memcpy(buf.data() + o2, use_cpu, cb);
-        std::memcpy(buf.data() + o3, hazard, hb);
-        char *base = static_cast<char *>(ctx->host_stage[7].ptr);
-        RSK_HIP(hipMemcpyAsync(base, buf.data(), tot, hipMemcpyHostToDevice, ctx->stream));
-        d_nodes = reinterpret_cast<const int *>(base);
-        d_cap = reinterpret_cast<const int *>(base + o1);
-        d_use = reinterpret_cast<const int *>(base + o2);
-        d_haz = reinterpret_cast<const uint8_t *>(base + o3);
+        const void *src[4] = {node_of, cap_cpu, use_cpu, hazard};
+        const size_t len[4] = {(size_t)k * 4, (size_t)N * 4, (size_t)N * 4, (size_t)N};
+        RSK_TRY(row_io(ctx, src, len, 4, 16, &io));
+        d_nodes = reinterpret_cast<const int *>(io.in + io.off[0]);
+        d_cap = reinterpret_cast<const int *>(io.in + io.off[1]);
+        d_use = reinterpret_cast<const int *>(io.in + io.off[2]);
+        d_haz = reinterpret_cast<const uint8_t *>(io.in + io.off[3]);
+        d_out = reinterpret_cast<int *>(io.out_dev);
     }
-    RSK_TRY(ctx->work[5].reserve(16));
-    d_out = ctx->work[5].as<int>();
     const size_t lds = ((size_t)((N + 3) & ~3) + 2 * (kRowThreads / 64)) * 4;
     if (lds > 64 * 1024)
         RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&car_row_kernel),
@@ -810,17 +859,39 @@ int rsk_car_row(rsk_ctx *ctx, const int32_t *node_of, int32_t k, const int32_t *
         car_row_kernel<<<1, kRowThreads, lds, ctx->stream>>>(d_nodes, k, d_cap, d_use, d_haz, N, d_out);
         RSK_HIP(hipGetLastError());
     }
-    int r[2];
     if (dev) {
         RSK_HIP(hipMemcpyAsync(out_target, d_out, 4, hipMemcpyDeviceToDevice, ctx->stream));
         if (out_score) RSK_HIP(hipMemcpyAsync(out_score, d_out + 1, 4, hipMemcpyDeviceToDevice, ctx->stream));
         return RSK_OK;
     }
-    RSK_HIP(hipMemcpyAsync(r, d_out, 8, hipMemcpyDeviceToHost, ctx->stream));
-    RSK_HIP(hipStreamSynchronize(ctx->stream));  // r[] and the staging buffer live on this frame
+    RSK_HIP(hipStreamSynchronize(ctx->stream));
+    const volatile int *r = reinterpret_cast<const volatile int *>(io.out_host);
     *out_target = r[0];
     if (out_score) *out_score = r[1];
     return r[0] == RSK_TARGET_NO_CANDIDATE ? RSK_NO_CANDIDATE : RSK_OK;
+}
+
+int rsk_random_candidates(rsk_ctx *ctx, const uint8_t *hazard, int32_t N, int32_t *out_nodes, int32_t *out_count) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK(N > 0 && hazard && out_nodes && out_count, "rsk_random_candidates: bad arguments (N=%d)", N);
+    const void *src[1] = {hazard};
+    const size_t len[1] = {(size_t)N};
+    RowIO io;
+    RSK_TRY(row_io(ctx, src, len, 1, (size_t)N * 4 + 16, &io));
+    {
+        ScopedTimer tm(ctx, "random_candidates");
+        candidates_row_kernel<<<1, kRowThreads, 0, ctx->stream>>>(reinterpret_cast<const uint8_t *>(io.in + io.off[0]),
+                                                                  N, reinterpret_cast<int *>(io.out_dev) + 4,
+                                                                  reinterpret_cast<int *>(io.out_dev));
+        RSK_HIP(hipGetLastError());
+    }
+    RSK_HIP(hipStreamSynchronize(ctx->stream));
+    const volatile int *r = reinterpret_cast<const volatile int *>(io.out_host);
+    const int cnt = r[0];
+    RSK_CHECK(cnt >= 0 && cnt <= N, "rsk_random_candidates: bad count %d", cnt);
+    std::memcpy(out_nodes, const_cast<const int *>(r) + 4, (size_t)cnt * 4);
+    *out_count = cnt;
+    return RSK_OK;
 }
 
 int rsk_random_place(rsk_ctx *ctx, const uint8_t *hazard, int32_t N, int32_t S, const uint64_t *seeds,

@@ -95,6 +95,28 @@ int aux_join(rsk_ctx *ctx, int k) {
     return RSK_OK;
 }
 
+int PinBuf::reserve(size_t need) {
+    if (need <= bytes) return RSK_OK;
+    release();
+    size_t n = 4096;
+    while (n < need) n <<= 1;
+    RSK_HIP(hipHostMalloc(&host, n, hipHostMallocMapped));
+    if (hipHostGetDevicePointer(&dev, host, 0) != hipSuccess) {
+        (void)hipHostFree(host);
+        host = nullptr;
+        set_error("hipHostGetDevicePointer failed");
+        return RSK_EHIP;
+    }
+    bytes = n;
+    return RSK_OK;
+}
+
+void PinBuf::release() {
+    if (host) (void)hipHostFree(host);
+    host = dev = nullptr;
+    bytes = 0;
+}
+
 int stage_in(rsk_ctx *ctx, int slot, const void *src, size_t bytes, bool device, const void **out) {
     if (device || bytes == 0) { *out = src; return RSK_OK; }
     RSK_CHECK(src, "null input pointer");
@@ -159,6 +181,7 @@ int rsk_ctx_destroy(rsk_ctx *ctx) {
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     for (auto &b : ctx->host_stage) b.release();
     for (auto &b : ctx->work) b.release();
+    ctx->pin.release();
     for (int i = 0; i < rsk_ctx::kAux; ++i)
         if (ctx->aux[i]) {
             (void)hipStreamSynchronize(ctx->aux[i]);

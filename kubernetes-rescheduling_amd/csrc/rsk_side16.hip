@@ -274,6 +274,10 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(S
     }
     if (kT > 1) __syncthreads();
     if (tw != 0) return;  // the rest is one wave's (no more barriers)
+    if (a.ablate & 2) {  // profiling: pass 1 and the marks only (results are wrong)
+        if (s0 + lane < a.S) a.out_target[(size_t)(unsigned)oi * S + (unsigned)(s0 + lane)] = nd;
+        return;
+    }
     const int ndmax = __builtin_amdgcn_readfirstlane(dpp_max(ndk));
 
     // ---- levels: distinct pivot nodes by count, descending ----
@@ -298,7 +302,7 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(S
 
     // ---- walk: unflagged pivot nodes, level by level ----
     unsigned long long k1 = 0ull, k2 = 0ull;
-    {
+    if (!(a.ablate & 4)) {
         const unsigned lsh = (unsigned)lane & 31u;
         const bool hiw = lane >= 32;
         unsigned long long lm = __builtin_amdgcn_ballot_w64(lc > 0);
@@ -334,7 +338,7 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(S
     }
 
     // ---- touched: exact counts of the lane's flagged / new nodes ----
-    for (int k0 = 0; k0 < ndmax; k0 += 4) {
+    for (int k0 = 0; k0 < ((a.ablate & 8) ? 0 : ndmax); k0 += 4) {
         unsigned t[8];
         int delta[8];
         bool seen[8];

@@ -133,13 +133,12 @@ def random(deployment_info, harzard_node, nodes_name):
     apps_v1, namespace = _setup(deployment_info, harzard_node, False)
     nodes = list(nodes_name)
     haz = _cluster.candidate_mask(harzard_node, nodes)
-    count = int(_api.random_count(haz, len(nodes), 1)[0]) if nodes else 0
-    if count == 0:
+    cand = _api.random_candidates(haz, len(nodes)) if nodes else ()
+    if len(cand) == 0:
         raise RuntimeError(_NO_CANDIDATES)
     # random.choice(seq) is seq[_randbelow(len(seq))]: draw the same index.
-    r = _pyrandom.choice(range(count))
-    idx = int(_api.random_select(haz, len(nodes), 1, [r])[0])
-    _pod_spec(deployment_info)["nodeName"] = nodes[idx]
+    r = _pyrandom.choice(range(len(cand)))
+    _pod_spec(deployment_info)["nodeName"] = nodes[int(cand[r])]
     return create(apps_v1, namespace, deployment_info)
 
 

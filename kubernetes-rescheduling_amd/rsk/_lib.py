@@ -51,6 +51,7 @@ SIGNATURES = {
     "rsk_binpack_place": (C.c_int, [_vp, _vp, _vp, _vp, C.c_int32, C.c_int32, _vp, C.c_uint32]),
     "rsk_random_count": (C.c_int, [_vp, _vp, C.c_int32, C.c_int32, _vp, C.c_uint32]),
     "rsk_random_select": (C.c_int, [_vp, _vp, C.c_int32, C.c_int32, _vp, _vp, C.c_uint32]),
+    "rsk_random_candidates": (C.c_int, [_vp, _vp, C.c_int32, _vp, _vp]),
     "rsk_random_place": (C.c_int, [_vp, _vp, C.c_int32, C.c_int32, _vp, _vp, C.c_uint32]),
     "rsk_py_randbelow": (C.c_int32, [C.c_uint64, C.c_int32]),
     "rsk_node_reduce": (C.c_int, [_vp, _vp, C.c_int32, C.c_int32, _vp, _vp, C.c_int32, _vp, _vp, _vp, C.c_uint32]),

@@ -199,6 +199,18 @@ def binpack_place(cpu_pct, name_rank, hazard, N, S, ctx=None, out=None, device=F
     return out
 
 
+def random_candidates(hazard, N, ctx=None):
+    """random's candidate list in one launch (rsk_random_candidates, S = 1):
+    the non-hazard node indices in index order (rescheduling.py:149-150)."""
+    import ctypes as C
+    ctx = ctx or default_context()
+    h = _c(hazard, np.uint8)
+    out = np.empty(max(N, 1), _I32)
+    cnt = C.c_int32(0)
+    check(ctx.lib.rsk_random_candidates(ctx.handle, ptr(h), N, ptr(out), C.byref(cnt)))
+    return out[:cnt.value]
+
+
 def random_count(hazard, N, S, ctx=None):
     ctx = ctx or default_context()
     h = _c(hazard, np.uint8)

@@ -37,3 +37,7 @@ bench head_old headline RSK_SIDE_OLD=1
 bench 1m50k 1m50k
 bench 1m50k_l16 1m50k RSK_LIGHT_MAX=16
 for v in "$@"; do bench "v_$(echo "$v" | tr ",=/" "___" | cut -c1-60)" headline $(echo "$v" | tr "," " "); done
+if [ -n "$DROPIN" ]; then
+    step dropin 300 python -u tools/dropin_latency.py --calls 40 --out "$out/dropin.json"
+    grep -o '"config.*' "$out/dropin.log" | cut -c1-200
+fi
