@@ -216,15 +216,29 @@ int rsk_rounds_place(rsk_rounds *r, const int32_t *assign, int32_t S, const int3
  *   build-defined state update): where evict[s] in [0, P) and target[s] in
  *   [0, N), assign[evict*S+s] = target[s]; when the pod is in rows [r0, r1)
  *   (r1 <= P) its CPU / memory move between this rank's per-node partials
- *   cpu_part / mem_part [N*S] (old node only when it was in [0, N)); any
- *   other evict / target leaves the scenario untouched.                     */
+ *   cpu_part / mem_part [N*S] (old node only when it was in [0, N)), and
+ *   its u16 shadow shadow16[(e-r0)*S+s] (the rank's rows; null: none) takes
+ *   the target; any other evict / target leaves the scenario untouched.
+ * rsk_rows_cut_delta: before rsk_rows_apply, cut_inout[s] += the change of
+ *   the directed cut over rows [r0, r1) (rsk_cut_cost_rows' count,
+ *   communicationcost.py:37-45) that the round's move of evict[s] to
+ *   target[s] makes: the edges of row e and the rows holding e (rev_ptr /
+ *   rev_idx: the CSR's transpose); same move rule as rsk_rows_apply.
+ * rsk_pick_max_pod16: rsk_pick_max_pod over a u16 shadow of assign (node ids
+ *   < N <= 65535, 0xffff elsewhere; S % 8 == 0, 16-B aligned): half the
+ *   bytes of the scan.                                                       */
 int rsk_rows_evict_key(rsk_ctx *ctx, const int32_t *local_pod, int32_t S, int32_t r0, const int32_t *pod_cpu,
                        int64_t *out_key, uint32_t flags);
 int rsk_rows_evict_decode(rsk_ctx *ctx, const int64_t *key, int32_t S, int32_t P, int32_t *out_evict,
                           uint32_t flags);
 int rsk_rows_apply(rsk_ctx *ctx, int32_t *assign, int32_t S, const int32_t *evict, const int32_t *target,
                    int32_t r0, int32_t r1, int32_t P, int32_t N, const int32_t *pod_cpu, const int64_t *pod_mem,
-                   int64_t *cpu_part, int64_t *mem_part, uint32_t flags);
+                   int64_t *cpu_part, int64_t *mem_part, uint16_t *shadow16, uint32_t flags);
+int rsk_rows_cut_delta(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, const int32_t *rev_ptr,
+                       const int32_t *rev_idx, int32_t P, int32_t r0, int32_t r1, const int32_t *assign, int32_t S,
+                       const int32_t *evict, const int32_t *target, int32_t N, int64_t *cut_inout, uint32_t flags);
+int rsk_pick_max_pod16(rsk_ctx *ctx, const uint16_t *assign16, const int32_t *pod_cpu, int32_t P, int32_t S,
+                       const int32_t *most, int32_t *out_pod, uint32_t flags);
 
 /* ---- µBench workmodel -> relation CSR (host only, no device) -----------------
  * The caller's on-disk format (workmodelC.json).  One

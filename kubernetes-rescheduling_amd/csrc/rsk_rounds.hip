@@ -243,7 +243,8 @@ __global__ void rows_evict_decode_kernel(const long long *__restrict__ key, int 
 __global__ void rows_apply_kernel(int *__restrict__ assign, int S, const int *__restrict__ evict,
                                   const int *__restrict__ target, int r0, int r1, int P, int N,
                                   const int *__restrict__ pod_cpu, const long long *__restrict__ pod_mem,
-                                  long long *__restrict__ cpu_part, long long *__restrict__ mem_part) {
+                                  long long *__restrict__ cpu_part, long long *__restrict__ mem_part,
+                                  unsigned short *__restrict__ shadow) {
     const int s = blockIdx.x * 256 + threadIdx.x;
     if (s >= S) return;
     const int e = evict[s], t = target[s];
@@ -254,6 +255,7 @@ __global__ void rows_apply_kernel(int *__restrict__ assign, int S, const int *__
     const int old = *a;
     *a = t;
     if (e < r0 || e >= r1) return;
+    if (shadow) shadow[(size_t)(e - r0) * S + s] = (unsigned short)t;
     const long long c = pod_cpu[e], m = pod_mem[e];
     if ((unsigned)old < (unsigned)N) {
         cpu_part[(size_t)old * S + s] -= c;
@@ -261,6 +263,43 @@ __global__ void rows_apply_kernel(int *__restrict__ assign, int S, const int *__
     }
     cpu_part[(size_t)t * S + s] += c;
     mem_part[(size_t)t * S + s] += m;
+}
+
+// The change of the directed cut over rows [r0, r1) (communicationcost.py:
+// 37-45 restricted to this rank's rows, as rsk_cut_cost_rows counts it) when
+// scenario s moves pod e from o = assign[e, s] to t — read before the move.
+// Only edges at e change: e -> q (row e, when e is this rank's) and q -> e
+// (rows q of this rank whose lists hold e: the reverse CSR).  One wave per
+// scenario, lanes over the edges; cut[s] += delta.
+__global__ __launch_bounds__(256) void rows_cut_delta_kernel(const int *__restrict__ rp, const int *__restrict__ ci,
+                                                             const int *__restrict__ rvp, const int *__restrict__ rvi,
+                                                             int P, int r0, int r1, const int *__restrict__ assign,
+                                                             int S, const int *__restrict__ evict,
+                                                             const int *__restrict__ target, int N,
+                                                             long long *__restrict__ cut) {
+    const int lane = threadIdx.x & 63;
+    const int s = (int)blockIdx.x * 4 + ((int)threadIdx.x >> 6);
+    if (s >= S) return;  // whole wave
+    const int e = evict[s], t = target[s];
+    if (e < 0 || e >= P || t < 0 || t >= N) return;  // no move (rows_apply's rule)
+    const int o = assign[(size_t)e * S + s];
+    int d = 0;
+    if (e >= r0 && e < r1)
+        for (int k = rp[e] + lane; k < rp[e + 1]; k += 64) {
+            const int q = ci[k];
+            if (q == e) continue;
+            const int a = assign[(size_t)q * S + s];
+            d += (int)(t != a) - (int)(o != a);
+        }
+    for (int k = rvp[e] + lane; k < rvp[e + 1]; k += 64) {
+        const int q = rvi[k];
+        if (q == e || q < r0 || q >= r1) continue;
+        const int a = assign[(size_t)q * S + s];
+        d += (int)(a != t) - (int)(a != o);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
+    if (lane == 0 && d) cut[s] += d;
 }
 
 }  // namespace
@@ -460,16 +499,53 @@ int rsk_rows_evict_decode(rsk_ctx *ctx, const int64_t *key, int32_t S, int32_t P
 
 int rsk_rows_apply(rsk_ctx *ctx, int32_t *assign, int32_t S, const int32_t *evict, const int32_t *target, int32_t r0,
                    int32_t r1, int32_t P, int32_t N, const int32_t *pod_cpu, const int64_t *pod_mem, int64_t *cpu_part,
-                   int64_t *mem_part, uint32_t flags) {
+                   int64_t *mem_part, uint16_t *shadow16, uint32_t flags) {
     RSK_TRY(activate(ctx));
     RSK_CHECK((flags & RSK_F_DEVICE) && assign && evict && target && pod_cpu && pod_mem && cpu_part && mem_part &&
                   S > 0 && N > 0 && 0 <= r0 && r0 <= r1 && r1 <= P,
               "rsk_rows_apply: bad arguments (S=%d N=%d rows [%d, %d) of P=%d)", S, N, r0, r1, P);
     rows_apply_kernel<<<(unsigned)ceil_div(S, 256), 256, 0, ctx->stream>>>(
         assign, S, evict, target, r0, r1, P, N, pod_cpu, reinterpret_cast<const long long *>(pod_mem),
-        reinterpret_cast<long long *>(cpu_part), reinterpret_cast<long long *>(mem_part));
+        reinterpret_cast<long long *>(cpu_part), reinterpret_cast<long long *>(mem_part), shadow16);
     RSK_HIP(hipGetLastError());
     return RSK_OK;
+}
+
+int rsk_rows_cut_delta(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, const int32_t *rev_ptr,
+                       const int32_t *rev_idx, int32_t P, int32_t r0, int32_t r1, const int32_t *assign, int32_t S,
+                       const int32_t *evict, const int32_t *target, int32_t N, int64_t *cut_inout, uint32_t flags) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK((flags & RSK_F_DEVICE) && row_ptr && col_idx && rev_ptr && rev_idx && assign && evict && target &&
+                  cut_inout && P > 0 && S > 0 && N > 0 && 0 <= r0 && r0 <= r1 && r1 <= P,
+              "rsk_rows_cut_delta: bad arguments (device pointers, rows [%d, %d) of P=%d)", r0, r1, P);
+    ScopedTimer tm(ctx, "rows_cut_delta");
+    rows_cut_delta_kernel<<<(unsigned)ceil_div(S, 4), 256, 0, ctx->stream>>>(
+        row_ptr, col_idx, rev_ptr, rev_idx, P, r0, r1, assign, S, evict, target, N,
+        reinterpret_cast<long long *>(cut_inout));
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
+}
+
+int rsk_pick_max_pod16(rsk_ctx *ctx, const uint16_t *assign16, const int32_t *pod_cpu, int32_t P, int32_t S,
+                       const int32_t *most, int32_t *out_pod, uint32_t flags) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK((flags & RSK_F_DEVICE) && assign16 && pod_cpu && most && out_pod && P >= 0 && S > 0 && S % 8 == 0 &&
+                  ((uintptr_t)assign16 % 16) == 0,
+              "rsk_pick_max_pod16: device pointers, S %% 8 == 0 and a 16-B aligned shadow required (S=%d)", S);
+    RSK_TRY(ctx->work[0].reserve((size_t)S * 8));
+    unsigned long long *key = ctx->work[0].as<unsigned long long>();
+    ScopedTimer tm(ctx, "pick_max_pod16");
+    RSK_HIP(hipMemsetAsync(key, 0, (size_t)S * 8, ctx->stream));
+    if (P > 0) {
+        const int S8 = S / 8;
+        const int ppt = (int)std::max<int64_t>(1, ceil_div((int64_t)P * S8, (int64_t)256 * 4096));
+        const int64_t tot = ceil_div(P, ppt) * S8;
+        RSK_CHECK(tot < INT32_MAX, "grid too large");
+        pick16_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, ctx->stream>>>(
+            reinterpret_cast<const uint4 *>(assign16), pod_cpu, P, S8, most, ppt, (unsigned)tot, key);
+        RSK_HIP(hipGetLastError());
+    }
+    return launch_decode_first_max(ctx->stream, key, S, out_pod);
 }
 
 }  // extern "C"

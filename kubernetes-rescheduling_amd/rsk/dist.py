@@ -222,6 +222,14 @@ class LibrskRoundsBackend:
         self.row_ptr = torch.from_numpy(rp).to(self.dev)
         self.col_idx = torch.from_numpy(ci).to(self.dev)
         self.P = rp.shape[0] - 1
+        # the CSR's transpose (rows holding each pod), for the cut's per-move delta
+        nnz = int(rp[-1])
+        src = np.repeat(np.arange(self.P, dtype=np.int32), np.diff(rp))
+        order = np.argsort(ci[:nnz], kind="stable")
+        rvp = np.zeros(self.P + 1, np.int32)
+        np.cumsum(np.bincount(ci[:nnz], minlength=self.P), out=rvp[1:])
+        self.rev_ptr = torch.from_numpy(rvp).to(self.dev)
+        self.rev_idx = torch.from_numpy(np.ascontiguousarray(src[order] if nnz else np.zeros(1, np.int32))).to(self.dev)
         self._F, self._check = RSK_F_DEVICE, check
 
     def _sync(self):
@@ -270,6 +278,26 @@ class LibrskRoundsBackend:
         self._sync()
         return out
 
+    def pick_rows16(self, shadow_rows, pod_cpu_rows, q, S, most):
+        """pick_rows over the rank's u16 shadow (N <= 65535, S % 8 == 0)."""
+        import torch
+        self._sync()
+        out = torch.empty(S, dtype=torch.int32, device=self.dev)
+        self._check(self.ctx.lib.rsk_pick_max_pod16(self.ctx.handle, shadow_rows.data_ptr(), pod_cpu_rows.data_ptr(),
+                                                    q, S, most.data_ptr(), out.data_ptr(), self._F))
+        self._sync()
+        return out
+
+    def cut_delta(self, assign, S, evict, target, r0, r1, N, cut):
+        """cut[s] += the change of the rank's directed cut that the round's moves make
+        (called before apply: assign still holds the old nodes)."""
+        self._sync()
+        self._check(self.ctx.lib.rsk_rows_cut_delta(self.ctx.handle, self.row_ptr.data_ptr(), self.col_idx.data_ptr(),
+                                                    self.rev_ptr.data_ptr(), self.rev_idx.data_ptr(), self.P, r0, r1,
+                                                    assign.data_ptr(), S, evict.data_ptr(), target.data_ptr(), N,
+                                                    cut.data_ptr(), self._F))
+        self._sync()
+
     # the per-round glue of RowShardedRounds.run in one librsk launch each
     def evict_key(self, loc, r0, pod_cpu, S):
         import torch
@@ -289,12 +317,12 @@ class LibrskRoundsBackend:
         self._sync()
         return ev
 
-    def apply(self, assign, S, evict, target, r0, r1, N, pod_cpu, pod_mem, cpu_part, mem_part):
+    def apply(self, assign, S, evict, target, r0, r1, N, pod_cpu, pod_mem, cpu_part, mem_part, shadow=None):
         self._sync()
         self._check(self.ctx.lib.rsk_rows_apply(self.ctx.handle, assign.data_ptr(), S, evict.data_ptr(),
                                                 target.data_ptr(), r0, r1, self.P, N, pod_cpu.data_ptr(),
-                                                pod_mem.data_ptr(),
-                                                cpu_part.data_ptr(), mem_part.data_ptr(), self._F))
+                                                pod_mem.data_ptr(), cpu_part.data_ptr(), mem_part.data_ptr(),
+                                                None if shadow is None else shadow.data_ptr(), self._F))
         self._sync()
 
     def cut_rows(self, assign, S, r0, r1):
@@ -357,6 +385,16 @@ class RowShardedRounds:
         pm64 = pod_mem.to(torch.int64)
         glue = hasattr(self.be, "apply")   # the backend's fused per-round glue (librsk), else torch ops
         pc32, pm64c = pod_cpu.to(torch.int32).contiguous(), pm64.contiguous()
+        # the cut kept as a running count: the full count over the rank's rows
+        # once, then per round the exact delta of the round's moves (only edges
+        # at the moved pod change, communicationcost.py:40-43)
+        delta = hasattr(self.be, "cut_delta")
+        cut_local = self.be.cut_rows(assign, S, r0, r1) if delta else None
+        # the eviction scan over a u16 shadow of the rank's rows when node ids fit
+        shadow = None
+        if hasattr(self.be, "pick_rows16") and N <= 65535 and S % 8 == 0 and r1 > r0:
+            rows = assign[r0 * S:r1 * S]
+            shadow = torch.where((rows >= 0) & (rows < N), rows, torch.full_like(rows, 65535)).to(torch.int16)
         evs, tgs, cuts = [], [], []
         sidx = torch.arange(S, device=dev)
         pc64 = pod_cpu.to(torch.int64)
@@ -373,7 +411,10 @@ class RowShardedRounds:
             c = tick("monitor", c)
             haz, most = self.be.detect(use, cap, N, S, threshold)
             c = tick("detect", c)
-            loc = self.be.pick_rows(assign[r0 * S:r1 * S], pod_cpu[r0:r1], r1 - r0, S, most)
+            if shadow is not None:
+                loc = self.be.pick_rows16(shadow, pc32[r0:r1], r1 - r0, S, most)
+            else:
+                loc = self.be.pick_rows(assign[r0 * S:r1 * S], pod_cpu[r0:r1], r1 - r0, S, most)
             if glue:
                 key = self.be.evict_key(loc, r0, pc32, S)
             else:
@@ -392,9 +433,13 @@ class RowShardedRounds:
             target = allgather(tgt_local, self.group).max(dim=0).values   # changed slices of every rank
             c = tick("exchange", c)
             if glue:  # one librsk launch
-                self.be.apply(assign, S, evict, target.contiguous(), r0, r1, N, pc32, pm64c, lp_cpu, lp_mem)
+                target = target.contiguous()
+                if delta:
+                    self.be.cut_delta(assign, S, evict, target, r0, r1, N, cut_local)
+                c = tick("cut", c)
+                self.be.apply(assign, S, evict, target, r0, r1, N, pc32, pm64c, lp_cpu, lp_mem, shadow)
                 c = tick("update", c)
-                cut = self.be.cut_rows(assign, S, r0, r1)
+                cut = cut_local.clone() if delta else self.be.cut_rows(assign, S, r0, r1)
                 allreduce_(cut, "sum", self.group)
                 tick("cut", c)
                 evs.append(evict)
@@ -404,6 +449,8 @@ class RowShardedRounds:
             # fixed-shape ops over all S scenarios (no boolean indexing, which
             # would sync the host): scenarios without a move write their own
             # value back and add zero deltas at index 0
+            if delta:
+                self.be.cut_delta(assign, S, evict, target, r0, r1, N, cut_local)
             moved = (evict >= 0) & (target >= 0)
             av = assign.view(-1, S)
             ep = evict.clamp(min=0).long()
@@ -421,7 +468,7 @@ class RowShardedRounds:
             lp_cpu.index_add_(0, i_dst, torch.where(dst, pc64[ep], zero))
             lp_mem.index_add_(0, i_dst, torch.where(dst, pm64[ep], zero))
             c = tick("update", c)
-            cut = self.be.cut_rows(assign, S, r0, r1)
+            cut = cut_local.clone() if delta else self.be.cut_rows(assign, S, r0, r1)
             allreduce_(cut, "sum", self.group)
             tick("cut", c)
             evs.append(evict)

@@ -35,6 +35,10 @@ class OracleRoundsBackend:
         self.rp, self.ci = np.asarray(row_ptr, np.int32), np.asarray(col_idx, np.int32)
         self.drp, self.dci = orc.dedup_csr(self.rp, self.ci)
         self.P = len(self.rp) - 1
+        self.rev = [[] for _ in range(self.P)]   # rows holding each pod (the CSR's transpose)
+        for p in range(self.P):
+            for q in self.ci[self.rp[p]:self.rp[p + 1]]:
+                self.rev[int(q)].append(p)
 
     @staticmethod
     def _t(a):
@@ -62,6 +66,24 @@ class OracleRoundsBackend:
                                 rows=np.array([e[s]], np.int32))
             out[s] = t[0]
         return self._t(out)
+
+    def cut_delta(self, assign, S, evict, target, r0, r1, N, cut):
+        """cut[s] += the change of the directed cut over rows [r0, r1) that
+        scenario s's move makes (assign still holds the old node)."""
+        a, ev, tg, out = assign.numpy().reshape(-1, S), evict.numpy(), target.numpy(), cut.numpy()
+        for s in range(S):
+            e, t = int(ev[s]), int(tg[s])
+            if e < 0 or e >= self.P or t < 0 or t >= N:
+                continue
+            o, d = a[e, s], 0
+            if r0 <= e < r1:
+                for q in self.ci[self.rp[e]:self.rp[e + 1]]:
+                    if q != e:
+                        d += int(t != a[q, s]) - int(o != a[q, s])
+            for q in self.rev[e]:
+                if q != e and r0 <= q < r1:
+                    d += int(a[q, s] != t) - int(a[q, s] != o)
+            out[s] += d
 
     def cut_rows(self, assign, S, r0, r1):
         deg = np.diff(self.rp)
@@ -230,3 +252,17 @@ def test_row_sharded_rounds_stream_ordered_rccl_world1():
     (rank, e, t, k, a_r, u_r), = _run(1, R, use_gpu=True, pg="nccl", ordered=True)
     assert np.array_equal(e, ev) and np.array_equal(t, tg) and np.array_equal(k, cut)
     assert np.array_equal(a_r, a) and np.array_equal(u_r, u)
+
+
+@pytest.mark.gpu
+def test_row_sharded_rounds_stream_ordered_gloo_world2():
+    """The stream-ordered backend with real multi-rank collectives (two ranks on
+    the one GPU, gloo on device tensors): librsk kernels, torch ops and every
+    all-reduce / all-gather ordered on each rank's torch stream, against
+    oracle_rounds."""
+    R = 4
+    c, pod_cpu, _ = _case()
+    ev, tg, cut, a, u = _expected(c, pod_cpu, R)
+    for rank, e, t, k, a_r, u_r in _run(2, R, use_gpu=True, ordered=True):
+        assert np.array_equal(e, ev) and np.array_equal(t, tg), f"rank {rank}"
+        assert np.array_equal(k, cut) and np.array_equal(a_r, a) and np.array_equal(u_r, u), f"rank {rank}"
