@@ -368,6 +368,7 @@ struct SideArgs {
 };
 struct SideGeom {
     int dmax, Dc, H, hshift, K, T, W, kB, cells;
+    bool fast;
     int off_umask, off_srt, off_lvl, off_dl, off_ndl;
     size_t lds_team;
 };

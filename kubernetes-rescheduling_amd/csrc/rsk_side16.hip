@@ -34,6 +34,7 @@
 // whole wave (lanes = neighbours) — rare.
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 
 #include "rsk_car.h"
 
@@ -47,13 +48,14 @@ struct SideTab {
     unsigned mask;
     int shift;
     __device__ __forceinline__ unsigned home(unsigned k) const { return (k * 2654435761u) >> shift; }
-    // lane-parallel: key k (node + 1) gets +1 (claims a free slot or adds to its own)
-    __device__ __forceinline__ void add(unsigned k) const {
+    // lane-parallel: key k (node + 1) gets +1 (claims a free slot or adds to its
+    // own); true when this lane claimed the key's slot
+    __device__ __forceinline__ bool add(unsigned k) const {
         unsigned h = home(k);
         while (true) {
             const unsigned prev = atomicCAS(&tab[h], 0u, (k << 16) | 1u);
-            if (prev == 0u) break;
-            if ((prev >> 16) == k) { atomicAdd(&tab[h], 1u); break; }
+            if (prev == 0u) return true;
+            if ((prev >> 16) == k) { atomicAdd(&tab[h], 1u); return false; }
             h = (h + 1u) & mask;
         }
     }
@@ -186,9 +188,14 @@ __device__ int side_exact(const SideArgs &a, const SideTab &tb, unsigned *cells,
 
 // kW waves per workgroup, teams of kT waves (kT == 1: every wave its own item;
 // kT == kW: one item per workgroup, barriers), kB neighbour loads in flight.
-template <int kW, int kT, int kB, bool kOff32>
+// kFast (single-wave teams): pass 1 also gathers each lane's codes and keeps
+// its two best (1, code, -node) keys; when the pivots are distinct and no
+// lane's deviations land on a pivot node or on each other, every candidate
+// node counts 1 in every lane and those keys are the answer (no walk).
+template <int kW, int kT, int kB, bool kOff32, bool kFast>
 __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(SideArgs a) {
     static_assert(kT == 1 || kT == kW, "a team is one wave or the whole workgroup");
+    static_assert(!kFast || kT == 1, "the fast path is per wave");
     extern __shared__ __attribute__((aligned(16))) unsigned slds[];
     const int lane = (int)threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
@@ -228,10 +235,20 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(S
 
     // ---- pass 1: pivots, deviations, pivot counts ----
     int nd = 0;  // kT == 1: this lane's deviations (teams count in ndl)
+    int n_piv = 0, n_new = 0;              // kFast: pivots inserted, distinct pivot keys
+    unsigned long long f1 = 0ull, f2 = 0ull;  // kFast: the lane's two best (1, code, -node) keys
     for (int j0 = tw * kB; j0 < d; j0 += kB * kT) {
         int v[kB];
 #pragma unroll
         for (int u = 0; u < kB; ++u) v[u] = side_ld_assign<kOff32>(a.assign, (unsigned)nb[min(j0 + u, d - 1)], S, (unsigned)s);
+        if (kFast) {
+            unsigned c[kB];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) c[u] = ld16(a.code, min((unsigned)v[u], N) * S + (unsigned)s);  // row N: 0
+#pragma unroll
+            for (int u = 0; u < kB; ++u)
+                if (j0 + u < d && c[u] != kCodeHaz) top2(side_key(1u, c[u], (unsigned)v[u]), f1, f2);
+        }
         unsigned mine = 0u;  // lane u: key of entry j0 + u's pivot
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
@@ -248,13 +265,37 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(S
                 mine = (lane == u && p < (int)N) ? (unsigned)p + 1u : mine;
             }
         }
-        if (mine) tb.add(mine);
+        bool fresh = false;
+        if (mine) fresh = tb.add(mine);
+        if (kFast) {
+            n_piv += __builtin_popcountll(__builtin_amdgcn_ballot_w64(mine != 0u));
+            n_new += __builtin_popcountll(__builtin_amdgcn_ballot_w64(fresh));
+        }
     }
     if (kT > 1) {
         __syncthreads();
         nd = ndl[lane];
     }
     const int ndk = min(nd, K);
+
+    unsigned long long k1 = 0ull, k2 = 0ull;
+    bool fast = false;
+    if (kFast && n_new == n_piv) {  // distinct pivots: is every lane's multiset of nodes duplicate-free?
+        const int ndm = __builtin_amdgcn_readfirstlane(dpp_max(ndk));
+        bool clean = nd <= K;
+        for (int k = 0; k < ndm; ++k) {
+            const unsigned x = k < ndk ? dl[k * 64 + lane] & 0xffffu : 0xffffu;
+            if (x < N) {
+                clean = clean && tb.find(x + 1u) < 0;  // lands on a pivot node (maybe one whose entry left too: conservative)
+                for (int i = 0; i < k; ++i) clean = clean && (dl[i * 64 + lane] & 0xffffu) != x;
+            }
+        }
+        fast = !__builtin_amdgcn_ballot_w64(!clean);
+    }
+    if (fast) {
+        k1 = f1;
+        k2 = f2;
+    } else {
 
     // ---- marks: the pivot nodes whose count differs in the lane's scenario ----
     {
@@ -301,7 +342,6 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(S
     }
 
     // ---- walk: unflagged pivot nodes, level by level ----
-    unsigned long long k1 = 0ull, k2 = 0ull;
     if (!(a.ablate & 4)) {
         const unsigned lsh = (unsigned)lane & 31u;
         const bool hiw = lane >= 32;
@@ -373,6 +413,7 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(S
         for (int m = 0; m < 8; ++m)
             if (cnt[m] > 0 && c[m] != kCodeHaz) top2(side_key((unsigned)cnt[m], c[m], t[m]), k1, k2);
     }
+    }  // !fast
 
     // ---- decide ----
     const int M = (int)(k1 >> 32);
@@ -419,6 +460,9 @@ SideGeom side16_geometry(int dmax, int N) {
     g.hshift = 32 - l;
     g.K = std::min(64, 8 + dmax / 32);  // deviation slots per lane (overflow: the exact recount)
     g.T = dmax <= 256 ? 1 : (dmax <= 1024 ? 4 : 8);
+    // the duplicate-free fast path where distinct pivots are the common case
+    static const int fast_max = [] { const char *e = getenv("RSK_SIDE_FAST_MAX"); return e ? atoi(e) : 128; }();
+    g.fast = g.T == 1 && dmax <= fast_max;
     g.kB = dmax <= 32 ? 8 : (dmax <= 64 ? 16 : 32);
     // words: tab H | umask 2H | srt 4 Dc (also the recount's cells) | lvl 128 | dl 64 K | ndl 64
     g.cells = std::max(4 * g.Dc, std::min(dmax, 4096));
@@ -458,14 +502,16 @@ int launch_side16(hipStream_t stream, const SideArgs &a0, const SideGeom &g, boo
     a.xcd_per = (int)ceil_div(blocks_needed, 8);
     const int64_t blocks = 8 * (int64_t)a.xcd_per;
     using K = void (*)(SideArgs);
-#define RSK_SIDE_B(W, T)                                                                                       \
-    (g.kB == 8 ? (off32 ? &car_side16_kernel<W, T, 8, true> : &car_side16_kernel<W, T, 8, false>)             \
-               : g.kB == 16 ? (off32 ? &car_side16_kernel<W, T, 16, true> : &car_side16_kernel<W, T, 16, false>) \
-                            : (off32 ? &car_side16_kernel<W, T, 32, true> : &car_side16_kernel<W, T, 32, false>))
-    const K kern = g.T == 8 ? RSK_SIDE_B(8, 8)
-                            : g.T == 4 ? RSK_SIDE_B(4, 4)
-                                       : (g.W == 4 ? RSK_SIDE_B(4, 1) : g.W == 2 ? RSK_SIDE_B(2, 1) : RSK_SIDE_B(1, 1));
+#define RSK_SIDE_O(W, T, B, F) (off32 ? &car_side16_kernel<W, T, B, true, F> : &car_side16_kernel<W, T, B, false, F>)
+#define RSK_SIDE_B(W, T, F) \
+    (g.kB == 8 ? RSK_SIDE_O(W, T, 8, F) : g.kB == 16 ? RSK_SIDE_O(W, T, 16, F) : RSK_SIDE_O(W, T, 32, F))
+#define RSK_SIDE_F(W) (g.fast ? RSK_SIDE_B(W, 1, true) : RSK_SIDE_B(W, 1, false))
+    const K kern = g.T == 8 ? RSK_SIDE_B(8, 8, false)
+                            : g.T == 4 ? RSK_SIDE_B(4, 4, false)
+                                       : (g.W == 4 ? RSK_SIDE_F(4) : g.W == 2 ? RSK_SIDE_F(2) : RSK_SIDE_F(1));
+#undef RSK_SIDE_F
 #undef RSK_SIDE_B
+#undef RSK_SIDE_O
     if (lds > 64 * 1024)
         RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds));
