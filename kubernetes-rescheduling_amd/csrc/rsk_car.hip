@@ -1355,6 +1355,50 @@ bool plan_side_compact(const rsk_car_plan *plan, int S) {
     return slot || mid16_on() || plan->n_mid[0] + plan->n_mid[1] == 0;
 }
 
+// car_side16 launches of classes [c0, c1) on `stream`, the longest rows first.
+// Classes from kSideBig up (rows above 128 neighbours: few work items, each
+// latency-bound) run on a side stream beside the tiles (rsk_car_plan_execute).
+constexpr int kSideBig = 2;
+int launch_side16_classes(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, const SideBufs &b, int S, int N,
+                          int c0, int c1) {
+    const bool off32 = (int64_t)std::max(plan->P, plan->Q) * S * 4 < ((int64_t)1 << 32);
+    static const int sablate = env_int("RSK_ABLATE_SIDE", 0);
+    static const bool per_class = env_int("RSK_SIDE_TIMERS", 0) != 0;
+    static const char *const kNames[kNumSide] = {"car_side32", "car_side128", "car_side512",
+                                                 "car_side2048", "car_side8192", "car_side65535"};
+    for (int c = c1 - 1; c >= c0; --c) {
+        const int n = plan->side_end[c] - plan->side_beg[c];
+        if (n == 0) continue;
+        SideArgs a;
+        std::memset(&a, 0, sizeof(a));
+        a.items = plan->side_items.as<int>() + (size_t)plan->side_beg[c] * 4;
+        a.n_rows = n;
+        a.nchunk = (int)ceil_div(S, 64);
+        a.col = plan->pcol.as<int>();
+        a.assign = b.assign;
+        a.code = b.code;
+        a.cap = b.cap;
+        a.use = b.use;
+        a.zc_cnt = b.zcnt;
+        a.zc_key = b.zkey;
+        a.out_target = b.target;
+        a.out_score = b.score;
+        a.S = S;
+        a.N = N;
+        a.ablate = sablate;
+        const SideGeom g = side16_geometry(plan->side_dmax[c], N);
+        ScopedTimer tm(ctx, per_class ? kNames[c] : "car_side", stream);
+        RSK_TRY(launch_side16(stream, a, g, off32));
+    }
+    return RSK_OK;
+}
+
+bool side16_has_big(const rsk_car_plan *plan) {
+    for (int c = kSideBig; c < kNumSide; ++c)
+        if (plan->side_end[c] > plan->side_beg[c]) return true;
+    return false;
+}
+
 int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t *side, int nside, const SideBufs &b, int S, int N,
                 bool compact) {
     const int *d_assign = b.assign, *d_key = b.key, *d_zcnt = b.zcnt;
@@ -1362,37 +1406,8 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t *side, int n
     int *d_target = b.target, *d_score = b.score;
     int next = 0;
     auto pick = [&]() { return side[next++ % nside]; };
-    if (compact && side_new_on()) {  // car_side16: every side row, one launch per degree class, longest first
-        const bool off32 = (int64_t)std::max(plan->P, plan->Q) * S * 4 < ((int64_t)1 << 32);
-        static const int sablate = env_int("RSK_ABLATE_SIDE", 0);
-        static const bool per_class = env_int("RSK_SIDE_TIMERS", 0) != 0;
-        static const char *const kNames[kNumSide] = {"car_side32", "car_side128", "car_side512",
-                                                     "car_side2048", "car_side8192", "car_side65535"};
-        for (int c = kNumSide - 1; c >= 0; --c) {
-            const int n = plan->side_end[c] - plan->side_beg[c];
-            if (n == 0) continue;
-            SideArgs a;
-            std::memset(&a, 0, sizeof(a));
-            a.items = plan->side_items.as<int>() + (size_t)plan->side_beg[c] * 4;
-            a.n_rows = n;
-            a.nchunk = (int)ceil_div(S, 64);
-            a.col = plan->pcol.as<int>();
-            a.assign = d_assign;
-            a.code = b.code;
-            a.cap = b.cap;
-            a.use = b.use;
-            a.zc_cnt = d_zcnt;
-            a.zc_key = d_zkey;
-            a.out_target = d_target;
-            a.out_score = d_score;
-            a.S = S;
-            a.N = N;
-            a.ablate = sablate;
-            const SideGeom g = side16_geometry(plan->side_dmax[c], N);
-            const hipStream_t stream = pick();
-            ScopedTimer tm(ctx, per_class ? kNames[c] : "car_side", stream);
-            RSK_TRY(launch_side16(stream, a, g, off32));
-        }
+    if (compact && side_new_on()) {  // car_side16 (the caller launches the few-row classes: launch_side16_big)
+        RSK_TRY(launch_side16_classes(plan, ctx, ctx->stream, b, S, N, 0, kSideBig));
         return RSK_OK;
     }
     if (compact) {  // pivot-delta kernel: every side row (RSK_PIVOT=1) or the rows above kHubMax
@@ -1723,8 +1738,14 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     static const int overlap = std::max(0, std::min(rsk_ctx::kAux, env_int("RSK_OVERLAP", 0)));
     static const bool side_first = env_int("RSK_SIDE_FIRST", 0) != 0;
     hipStream_t side[rsk_ctx::kAux] = {ctx->stream, ctx->stream, ctx->stream};
-    const int nside = side_rows && plan->T > 0 ? overlap : 0;
-    const int nfork = nside;
+    const bool new_side = compact && side_new_on();
+    const int nside = side_rows && plan->T > 0 && !new_side ? overlap : 0;
+    // car_side16's few-row classes (rows above 128 neighbours) on a side stream
+    // beside the tiles: a handful of latency-bound workgroups that would
+    // otherwise run alone on the GPU (RSK_SIDE_BIG_AUX=0: on the main stream)
+    static const bool big_aux = env_int("RSK_SIDE_BIG_AUX", 1) != 0;
+    const bool big_fork = new_side && big_aux && plan->T > 0 && side16_has_big(plan);
+    const int nfork = big_fork ? 1 : nside;
     if (nfork) {
         RSK_TRY(aux_fork(ctx, nfork));
         for (int i = 0; i < nside; ++i) side[i] = ctx->aux[i];
@@ -1739,6 +1760,8 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     sb.zkey = d_zkey;
     sb.target = d_target;
     sb.score = d_score;
+    if (new_side)
+        RSK_TRY(launch_side16_classes(plan, ctx, big_fork ? ctx->aux[0] : ctx->stream, sb, S, N, kSideBig, kNumSide));
     RSK_TRY(launch_side(plan, ctx, side, std::max(nside, 1), sb, S, N, compact));
     if (nfork && side_first) RSK_TRY(aux_join(ctx, nfork));
     static const int ablate = env_int("RSK_ABLATE_TILE", 0);

@@ -399,19 +399,26 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(S
                 seen[m] = seen[m] || (i < k0 + m / 2 && (io == t[m] || in == t[m]));
             }
         }
-        unsigned c[8];
         int cnt[8];
+        bool any = false;
+        const int mcur = max(1, (int)(k1 >> 32));  // a node below the best count so far can neither win nor tie
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
             const bool ok = t[m] < N && !seen[m];
             int h = -1;
             if (ok) h = tb.find(t[m] + 1u);
             cnt[m] = ok ? (h >= 0 ? (int)(tb.tab[h] & 0xffffu) : 0) + delta[m] : 0;
-            c[m] = ld16(a.code, (cnt[m] > 0 ? t[m] : N) * S + (unsigned)s);  // row N: code 0
+            cnt[m] = cnt[m] >= mcur ? cnt[m] : 0;
+            any = any || cnt[m] > 0;
         }
+        if (__builtin_amdgcn_ballot_w64(any)) {  // wave-uniform: the codes of the nodes that can matter
+            unsigned c[8];
 #pragma unroll
-        for (int m = 0; m < 8; ++m)
-            if (cnt[m] > 0 && c[m] != kCodeHaz) top2(side_key((unsigned)cnt[m], c[m], t[m]), k1, k2);
+            for (int m = 0; m < 8; ++m) c[m] = ld16(a.code, (cnt[m] > 0 ? t[m] : N) * S + (unsigned)s);  // row N: 0
+#pragma unroll
+            for (int m = 0; m < 8; ++m)
+                if (cnt[m] > 0 && c[m] != kCodeHaz) top2(side_key((unsigned)cnt[m], c[m], t[m]), k1, k2);
+        }
     }
     }  // !fast
 
@@ -459,11 +466,13 @@ SideGeom side16_geometry(int dmax, int N) {
     while ((1 << l) < H) ++l;
     g.hshift = 32 - l;
     g.K = std::min(64, 8 + dmax / 32);  // deviation slots per lane (overflow: the exact recount)
-    g.T = dmax <= 256 ? 1 : (dmax <= 1024 ? 4 : 8);
+    g.T = dmax <= 256 ? 1 : 8;
     // the duplicate-free fast path where distinct pivots are the common case
     static const int fast_max = [] { const char *e = getenv("RSK_SIDE_FAST_MAX"); return e ? atoi(e) : 128; }();
     g.fast = g.T == 1 && dmax <= fast_max;
-    g.kB = dmax <= 32 ? 8 : (dmax <= 64 ? 16 : 32);
+    // neighbour loads in flight per wave: 32 where registers allow (the fast
+    // path's codes double the batch's registers: 16)
+    g.kB = dmax <= 32 ? 8 : (dmax <= 64 || g.fast ? 16 : 32);
     // words: tab H | umask 2H | srt 4 Dc (also the recount's cells) | lvl 128 | dl 64 K | ndl 64
     g.cells = std::max(4 * g.Dc, std::min(dmax, 4096));
     g.off_umask = H;
@@ -507,8 +516,7 @@ int launch_side16(hipStream_t stream, const SideArgs &a0, const SideGeom &g, boo
     (g.kB == 8 ? RSK_SIDE_O(W, T, 8, F) : g.kB == 16 ? RSK_SIDE_O(W, T, 16, F) : RSK_SIDE_O(W, T, 32, F))
 #define RSK_SIDE_F(W) (g.fast ? RSK_SIDE_B(W, 1, true) : RSK_SIDE_B(W, 1, false))
     const K kern = g.T == 8 ? RSK_SIDE_B(8, 8, false)
-                            : g.T == 4 ? RSK_SIDE_B(4, 4, false)
-                                       : (g.W == 4 ? RSK_SIDE_F(4) : g.W == 2 ? RSK_SIDE_F(2) : RSK_SIDE_F(1));
+                            : (g.W == 4 ? RSK_SIDE_F(4) : g.W == 2 ? RSK_SIDE_F(2) : RSK_SIDE_F(1));
 #undef RSK_SIDE_F
 #undef RSK_SIDE_B
 #undef RSK_SIDE_O
