@@ -219,7 +219,7 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(S
     tb.umask = reinterpret_cast<unsigned long long *>(base + a.off_umask);
     tb.mask = (unsigned)H - 1u;
     tb.shift = a.hshift;
-    uint4 *srt = reinterpret_cast<uint4 *>(base + a.off_srt);  // level-sorted {count << 16 | node, mask lo, hi, -}
+    uint2 *srt = reinterpret_cast<uint2 *>(base + a.off_srt);  // level-sorted {count << 16 | node, table slot}
     unsigned *lvl = base + a.off_lvl;                           // [64] level counts, [64] level cursors
     unsigned *dl = base + a.off_dl;                             // [K][64] deviations (pivot << 16 | own node)
     int *ndl = reinterpret_cast<int *>(base + a.off_ndl);       // [64] deviations per lane (teams)
@@ -336,8 +336,7 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(S
         const unsigned w = tb.tab[h];
         if (w) {
             const unsigned p = atomicAdd(&lvl[64 + min(w & 0xffffu, 64u) - 1u], 1u);
-            const unsigned long long m = tb.umask[h];
-            srt[p] = make_uint4(((w & 0xffffu) << 16) | ((w >> 16) - 1u), (unsigned)m, (unsigned)(m >> 32), 0u);
+            srt[p] = make_uint2(((w & 0xffffu) << 16) | ((w >> 16) - 1u), (unsigned)h);
         }
     }
 
@@ -355,10 +354,11 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(S
                 unsigned key[kU], ml[kU], c[kU];
 #pragma unroll
                 for (int w = 0; w < kU; ++w) {
-                    const uint4 e = srt[min(i0 + w, p1 - 1)];
+                    const uint2 e = srt[min(i0 + w, p1 - 1)];
                     key[w] = (unsigned)__builtin_amdgcn_readfirstlane((int)e.x);
-                    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)e.y);
-                    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)e.z);
+                    const unsigned long long m = tb.umask[__builtin_amdgcn_readfirstlane((int)e.y)];
+                    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)m);
+                    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(m >> 32));
                     ml[w] = hiw ? hi : lo;
                 }
 #pragma unroll
@@ -473,8 +473,8 @@ SideGeom side16_geometry(int dmax, int N) {
     // neighbour loads in flight per wave: 32 where registers allow (the fast
     // path's codes double the batch's registers: 16)
     g.kB = dmax <= 32 ? 8 : (dmax <= 64 || g.fast ? 16 : 32);
-    // words: tab H | umask 2H | srt 4 Dc (also the recount's cells) | lvl 128 | dl 64 K | ndl 64
-    g.cells = std::max(4 * g.Dc, std::min(dmax, 4096));
+    // words: tab H | umask 2H | srt 2 Dc (also the recount's cells) | lvl 128 | dl 64 K | ndl 64
+    g.cells = std::max(2 * g.Dc, std::min(dmax, 4096));
     g.off_umask = H;
     g.off_srt = 3 * H;
     g.off_lvl = g.off_srt + ((g.cells + 3) & ~3);

@@ -423,6 +423,57 @@ def test_car_row_above_4096_neighbours(ctx, S):
     _check_car(ctx, rp, ci, a, S, cap, use, haz, N, rows=np.arange(0, 40, dtype=np.int32), label=f"deg>4096 S={S}")
 
 
+@pytest.mark.parametrize("S", [1, 64])
+def test_car_row_5000_distinct_nodes(ctx, S):
+    """A row of degree 5000 over N = 6000 nodes: 5000 distinct
+    neighbour nodes, the side kernel's largest table (one team per workgroup),
+    with per-scenario random placements (every lane overflows its deviation
+    list: the exact per-scenario recount)."""
+    rng = np.random.default_rng(900 + S)
+    P, N = 7000, 6000
+    rows = [rng.integers(0, P, int(rng.integers(0, 3))).tolist() for _ in range(P)]
+    rows[0] = rng.choice(np.arange(1, P), 5000, replace=False).tolist()
+    rp = np.zeros(P + 1, np.int32)
+    rp[1:] = np.cumsum([len(r) for r in rows])
+    ci = np.array([q for r in rows for q in r], np.int32)
+    base = rng.permutation(P) % N
+    a = np.repeat(base[:, None], S, axis=1).astype(np.int32)
+    flip = rng.random((P, S)) < 0.3
+    a[flip] = rng.integers(-1, N, flip.sum())
+    cap = rng.choice([4000, 8000], N).astype(np.int32)
+    use = rng.integers(0, 8000, N * S).astype(np.int32)
+    haz = (rng.random(N * S) < 0.2).astype(np.uint8)
+    _check_car(ctx, rp, ci, a.reshape(-1), S, cap, use, haz, N, rows=np.arange(0, 16, dtype=np.int32),
+               label=f"deg 5000 N {N} S={S}")
+
+
+def test_dropin_communication_5000_related_above_row_max_n(ctx):
+    """The drop-in's `communication` with N > 32768 nodes goes through
+    car_place; a deployment related to 5000 others gets the
+    oracle's node."""
+    import rescheduling as R
+    from kubernetes import client
+    from oracle import oracle as orc
+    from rsk import synth
+    c = synth.make_cluster(8000, 33000, S=1, seed=3)
+    rng = np.random.default_rng(3)
+    rows = [c.col_idx[c.row_ptr[p]:c.row_ptr[p + 1]].tolist() for p in range(c.P)]
+    rows[0] = rng.choice(np.arange(1, c.P), 5000, replace=False).tolist()
+    c.row_ptr = np.zeros(c.P + 1, np.int32)
+    c.row_ptr[1:] = np.cumsum([len(r) for r in rows])
+    c.col_idx = np.array([q for r in rows for q in r], np.int32)
+    names, cm, rel = synth.to_cluster_monitoring(c, 0)
+    hz = [n for n in names if cm[n]["cpu_pct"] >= 30]
+    info = {"metadata": {"name": "d0", "namespace": "default"},
+            "spec": {"template": {"spec": {"affinity": None}}}}
+    client.CREATED.clear()
+    R.communication(info, hz, cm, rel, names)
+    t, _ = orc.car(c.row_ptr, c.col_idx, c.assign, 1, c.cap_cpu, c.use_cpu, c.hazard, c.N,
+                   rows=np.array([0], np.int32))
+    got = client.CREATED[-1][1]["spec"]["template"]["spec"]["nodeName"]
+    assert got == (names[int(t[0])] if t[0] >= 0 else None)
+
+
 def test_car_pivot_kernel_every_side_row():
     """RSK_PIVOT=1 routes every side row (deg > 32) of the compact path through
     the pivot-delta kernel: the random-graph, bucket-boundary and collision
