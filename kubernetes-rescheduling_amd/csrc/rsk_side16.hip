@@ -237,10 +237,18 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(S
     int nd = 0;  // kT == 1: this lane's deviations (teams count in ndl)
     int n_piv = 0, n_new = 0;              // kFast: pivots inserted, distinct pivot keys
     unsigned long long f1 = 0ull, f2 = 0ull;  // kFast: the lane's two best (1, code, -node) keys
+    // each batch's neighbour ids in one vector load (lane u: entry j0 + u),
+    // broadcast by readlane (no chain of dependent scalar loads), the next
+    // batch's ids loaded behind this batch's assign rows
+    const int *__restrict__ nbv = a.col + itp[1];
+    int qnext = nbv[min(tw * kB + lane, d - 1)];
     for (int j0 = tw * kB; j0 < d; j0 += kB * kT) {
+        const int myq = qnext;
         int v[kB];
 #pragma unroll
-        for (int u = 0; u < kB; ++u) v[u] = side_ld_assign<kOff32>(a.assign, (unsigned)nb[min(j0 + u, d - 1)], S, (unsigned)s);
+        for (int u = 0; u < kB; ++u)
+            v[u] = side_ld_assign<kOff32>(a.assign, (unsigned)__builtin_amdgcn_readlane(myq, u), S, (unsigned)s);
+        qnext = nbv[min(j0 + kB * kT + lane, d - 1)];
         if (kFast) {
             unsigned c[kB];
 #pragma unroll
