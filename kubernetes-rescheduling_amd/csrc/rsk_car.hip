@@ -1358,7 +1358,11 @@ bool plan_side_compact(const rsk_car_plan *plan, int S) {
 // car_side16 launches of classes [c0, c1) on `stream`, the longest rows first.
 // Classes from kSideBig up (rows above 128 neighbours: few work items, each
 // latency-bound) run on a side stream beside the tiles (rsk_car_plan_execute).
-constexpr int kSideBig = 2;
+int side_big_class() {  // RSK_SIDE_AUX_FROM: the first class on the side stream (experiments)
+    static const int c = std::max(0, std::min(kNumSide, env_int("RSK_SIDE_AUX_FROM", 2)));
+    return c;
+}
+#define kSideBig side_big_class()
 int launch_side16_classes(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, const SideBufs &b, int S, int N,
                           int c0, int c1) {
     const bool off32 = (int64_t)std::max(plan->P, plan->Q) * S * 4 < ((int64_t)1 << 32);

@@ -463,6 +463,271 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(S
     }
 }
 
+// ---------------------------------------------------------------------------
+// Single-wave items (rows up to 256 neighbours): the same algorithm with the
+// per-entry work kept on the vector unit — majority-of-three pivots, deviation
+// appends without branches (lanes that do not deviate write a dummy word), the
+// running best as (count, two 32-bit candidate words) — and a fast path:
+//   kFast  pass 1 also gathers each lane's codes and keeps the best two
+//          count-1 words.  When the pivots are distinct and a lane's
+//          deviations land neither on a pivot node nor on each other, every
+//          candidate node counts 1 in that lane: those words are its answer.
+//          Up to kFastSlowMax lanes that fail this are recounted exactly one by
+//          one; more, or repeated pivots, take the walk.
+// ---------------------------------------------------------------------------
+constexpr int kFastSlowMax = 6;
+
+// Running best over distinct nodes: the largest count M and the two largest
+// candidate words (code << 16 | 0xffff - node) among the nodes at M.
+struct Best {
+    int M;
+    unsigned w1, w2;
+    __device__ __forceinline__ void init() { M = 0; w1 = w2 = 0u; }
+    __device__ __forceinline__ void put(bool ok, int c, unsigned w) {
+        const bool gt = ok && c > M, eq = ok && c == M;
+        const bool g1 = eq && w > w1;
+        w2 = gt ? 0u : (g1 ? w1 : ((eq && w > w2) ? w : w2));
+        w1 = (gt || g1) ? w : w1;
+        M = gt ? c : M;
+    }
+};
+
+__device__ __forceinline__ int side_pivot3(int x) {  // majority of lanes 0, 21, 42 (lane 0 without one)
+    const int a = __builtin_amdgcn_readlane(x, 0), b = __builtin_amdgcn_readlane(x, 21),
+              c = __builtin_amdgcn_readlane(x, 42);
+    return (a == b || a == c) ? a : (b == c ? b : a);
+}
+
+template <int kW, int kB, bool kOff32, bool kFast>
+__global__ __launch_bounds__(64 * kW, 8) void car_side16_wave_kernel(SideArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned slds[];
+    const int lane = (int)threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    int blk = (int)blockIdx.x;
+    if (a.xcd_per) blk = (int)(blockIdx.x & 7u) * a.xcd_per + (int)(blockIdx.x >> 3);  // blocks b, b + 8 share an XCD
+    const int item = blk * kW + wave;
+    if (item >= a.n_rows * a.nchunk) return;  // whole wave (no barriers in this kernel)
+    const int chunk = item / a.n_rows, r = item - chunk * a.n_rows;
+    const cint_ptr itp = const_ptr(a.items) + 4 * r;
+    const int oi = itp[0], d = itp[2];
+    const int *__restrict__ nbv = a.col + itp[1];
+    const cint_ptr nb = const_ptr(a.col) + itp[1];
+    const unsigned S = (unsigned)a.S, N = (unsigned)a.N;
+    const int s0 = chunk * 64;
+    const int s = min(s0 + lane, a.S - 1);
+    const int H = a.H, K = a.K;
+
+    unsigned *base = slds + (size_t)wave * (a.lds_team >> 2);
+    SideTab tb;
+    tb.tab = base;
+    tb.umask = reinterpret_cast<unsigned long long *>(base + a.off_umask);
+    tb.mask = (unsigned)H - 1u;
+    tb.shift = a.hshift;
+    uint2 *srt = reinterpret_cast<uint2 *>(base + a.off_srt);
+    unsigned *lvl = base + a.off_lvl;
+    unsigned *dl = base + a.off_dl;
+    unsigned *dummy = base + a.off_ndl;  // [64] sink of the non-deviating lanes' writes
+    for (int i = lane; i < H; i += 64) tb.tab[i] = 0u;
+
+    // ---- pass 1 ----
+    int nd = 0, n_piv = 0, n_new = 0;
+    Best fb;
+    fb.init();
+    int qnext = nbv[min(lane, d - 1)];
+    for (int j0 = 0; j0 < d; j0 += kB) {
+        const int myq = qnext;
+        int v[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u)
+            v[u] = side_ld_assign<kOff32>(a.assign, (unsigned)__builtin_amdgcn_readlane(myq, u), S, (unsigned)s);
+        qnext = nbv[min(j0 + kB + lane, d - 1)];
+        unsigned c[kB];
+        if (kFast) {
+#pragma unroll
+            for (int u = 0; u < kB; ++u) c[u] = ld16(a.code, min((unsigned)v[u], N) * S + (unsigned)s);  // row N: 0
+        }
+        const int nu = min(kB, d - j0);
+        unsigned mine = 0u;
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            if (u < nu) {  // wave-uniform
+                const int x = (int)min((unsigned)v[u], N);
+                const int p = side_pivot3(x);
+                const bool dv = x != p;
+                unsigned *dst = (dv && nd < K) ? dl + nd * 64 + lane : dummy + lane;
+                *dst = ((unsigned)p << 16) | (unsigned)x;
+                nd += dv ? 1 : 0;
+                mine = lane == u ? (unsigned)p + 1u : mine;
+                if (kFast) fb.put(c[u] != kCodeHaz, 1, (c[u] << 16) | (0xffffu - (unsigned)x));
+            }
+        }
+        const bool ins = mine != 0u && mine <= N;  // pivot node < N (N: unassigned, never counted)
+        bool fresh = false;
+        if (ins) fresh = tb.add(mine);
+        if (kFast) {
+            n_piv += __builtin_popcountll(__builtin_amdgcn_ballot_w64(ins));
+            n_new += __builtin_popcountll(__builtin_amdgcn_ballot_w64(fresh));
+        }
+    }
+    const int ndk = min(nd, K);
+    const int ndmax = __builtin_amdgcn_readfirstlane(dpp_max(ndk));
+
+    Best b;
+    bool slow = nd > K, done = false;
+    if (kFast && n_new == n_piv) {  // distinct pivots: which lanes hold a node twice?
+        bool clean = nd <= K;
+        for (int k = 0; k < ndmax; ++k) {
+            const unsigned x = k < ndk ? dl[k * 64 + lane] & 0xffffu : 0xffffu;
+            if (x < N) {
+                clean = clean && tb.find(x + 1u) < 0;  // on a pivot node (whose entry may have left too: conservative)
+                for (int i = 0; i < k; ++i) clean = clean && (dl[i * 64 + lane] & 0xffffu) != x;
+            }
+        }
+        if (__builtin_popcountll(__builtin_amdgcn_ballot_w64(!clean)) <= kFastSlowMax) {
+            b = fb;
+            slow = slow || !clean;
+            done = true;
+        }
+    }
+    if (!done) {
+        b.init();
+        for (int i = lane; i < H; i += 64) tb.umask[i] = 0ull;
+        // ---- marks ----
+        const unsigned long long bit = 1ull << lane;
+        for (int k = 0; k < ndmax; ++k) {
+            if (k < ndk) {
+                const unsigned x = dl[k * 64 + lane];
+                const unsigned po = x >> 16, pn = x & 0xffffu;
+                if (po < N) atomicOr(&tb.umask[tb.find(po + 1u)], bit);
+                if (pn < N) {
+                    const int h = tb.find(pn + 1u);
+                    if (h >= 0) atomicOr(&tb.umask[h], bit);
+                }
+            }
+        }
+        // ---- levels ----
+        lvl[lane] = 0u;
+        for (int h = lane; h < H; h += 64) {
+            const unsigned w = tb.tab[h];
+            if (w) atomicAdd(&lvl[min(w & 0xffffu, 64u) - 1u], 1u);
+        }
+        const int lc = (int)lvl[lane];
+        const int incl = wave_incl_sum(lc, lane);
+        const int lstart = __builtin_amdgcn_readlane(incl, 63) - incl;
+        lvl[64 + lane] = (unsigned)lstart;
+        for (int h = lane; h < H; h += 64) {
+            const unsigned w = tb.tab[h];
+            if (w) {
+                const unsigned p = atomicAdd(&lvl[64 + min(w & 0xffffu, 64u) - 1u], 1u);
+                srt[p] = make_uint2(((w & 0xffffu) << 16) | ((w >> 16) - 1u), (unsigned)h);
+            }
+        }
+        // ---- walk: level by level, until every lane's best count beats what is left ----
+        const unsigned lsh = (unsigned)lane & 31u;
+        const bool hiw = lane >= 32;
+        unsigned long long lm = __builtin_amdgcn_ballot_w64(lc > 0);
+        constexpr int kU = 8;
+        while (lm) {
+            const int L = 63 - __builtin_clzll(lm);
+            lm &= ~(1ull << L);
+            const int p0 = __builtin_amdgcn_readlane(lstart, L), p1 = p0 + __builtin_amdgcn_readlane(lc, L);
+            for (int i0 = p0; i0 < p1; i0 += kU) {
+                unsigned key[kU], ml[kU], c[kU];
+#pragma unroll
+                for (int w = 0; w < kU; ++w) {
+                    const uint2 e = srt[min(i0 + w, p1 - 1)];
+                    key[w] = e.x;
+                    const unsigned long long m = tb.umask[e.y];
+                    ml[w] = hiw ? (unsigned)(m >> 32) : (unsigned)m;
+                }
+#pragma unroll
+                for (int w = 0; w < kU; ++w) c[w] = ld16(a.code, (key[w] & 0xffffu) * S + (unsigned)s);
+#pragma unroll
+                for (int w = 0; w < kU; ++w) {
+                    const bool ok = i0 + w < p1 && c[w] != kCodeHaz && ((ml[w] >> lsh) & 1u) == 0u;
+                    b.put(ok, (int)(key[w] >> 16), (c[w] << 16) | (0xffffu - (key[w] & 0xffffu)));
+                }
+            }
+            if (!lm) break;
+            const int next = 64 - __builtin_clzll(lm);  // the largest count left (exact below 64)
+            if (!__builtin_amdgcn_ballot_w64(b.M <= next)) break;
+        }
+        // ---- touched ----
+        for (int k0 = 0; k0 < ndmax; k0 += 4) {
+            unsigned t[8];
+            int delta[8];
+            bool seen[8];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const unsigned x = k0 + m < ndk ? dl[(k0 + m) * 64 + lane] : 0xffffffffu;
+                t[2 * m] = x >> 16;
+                t[2 * m + 1] = x & 0xffffu;
+            }
+#pragma unroll
+            for (int m = 0; m < 8; ++m) { delta[m] = 0; seen[m] = false; }
+            for (int i = 0; i < ndmax; ++i) {
+                const unsigned xi = i < ndk ? dl[i * 64 + lane] : 0xffffffffu;
+                const unsigned io = xi >> 16, in = xi & 0xffffu;
+#pragma unroll
+                for (int m = 0; m < 8; ++m) {
+                    delta[m] += (int)(in == t[m]) - (int)(io == t[m]);
+                    seen[m] = seen[m] || (i < k0 + m / 2 && (io == t[m] || in == t[m]));
+                }
+            }
+            int cnt[8];
+            bool any = false;
+            const int mcur = max(1, b.M);
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const bool ok = t[m] < N && !seen[m];
+                int h = -1;
+                if (ok) h = tb.find(t[m] + 1u);
+                cnt[m] = ok ? (h >= 0 ? (int)(tb.tab[h] & 0xffffu) : 0) + delta[m] : 0;
+                cnt[m] = cnt[m] >= mcur ? cnt[m] : 0;
+                any = any || cnt[m] > 0;
+            }
+            if (__builtin_amdgcn_ballot_w64(any)) {
+                unsigned c[8];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) c[m] = ld16(a.code, (cnt[m] > 0 ? t[m] : N) * S + (unsigned)s);
+#pragma unroll
+                for (int m = 0; m < 8; ++m)
+                    b.put(cnt[m] > 0 && c[m] != kCodeHaz, cnt[m], (c[m] << 16) | (0xffffu - t[m]));
+            }
+        }
+    }
+
+    // ---- decide ----
+    int tg, sc;
+    if (b.M == 0) {
+        tg = zero_target(load_zc(a.zc_cnt, a.zc_key, s), sc);
+    } else {
+        sc = b.M;
+        const unsigned bk = b.w1 >> 16;
+        const bool tie = b.w2 != 0u;
+        tg = !tie ? cand_node(b.w1) : (bk >= 2u ? cand_node(b.w1) : RSK_TARGET_NONE);
+        slow = slow || (tie && code_inexact(bk) && (b.w2 >> 16) == bk);
+    }
+    unsigned long long sm = __builtin_amdgcn_ballot_w64(slow);
+    if (sm && !(a.ablate & 1)) {  // rare: the wave, one scenario at a time
+        while (sm) {
+            const int ln = __builtin_ctzll(sm);
+            sm &= sm - 1ull;
+            int sx;
+            const int tx = side_exact<kOff32>(a, tb, reinterpret_cast<unsigned *>(srt), a.cells, nb, d,
+                                              min(s0 + ln, a.S - 1), lane, H, sx);
+            tg = lane == ln ? tx : tg;
+            sc = lane == ln ? sx : sc;
+        }
+    }
+    if (s0 + lane < a.S) {
+        const size_t o = kOff32 ? (size_t)((unsigned)oi * S + (unsigned)(s0 + lane))
+                                : (size_t)(unsigned)oi * S + (unsigned)(s0 + lane);
+        a.out_target[o] = tg;
+        if (a.out_score) a.out_score[o] = sc;
+    }
+}
+
 SideGeom side16_geometry(int dmax, int N) {
     SideGeom g;
     g.dmax = dmax;
@@ -522,10 +787,15 @@ int launch_side16(hipStream_t stream, const SideArgs &a0, const SideGeom &g, boo
 #define RSK_SIDE_O(W, T, B, F) (off32 ? &car_side16_kernel<W, T, B, true, F> : &car_side16_kernel<W, T, B, false, F>)
 #define RSK_SIDE_B(W, T, F) \
     (g.kB == 8 ? RSK_SIDE_O(W, T, 8, F) : g.kB == 16 ? RSK_SIDE_O(W, T, 16, F) : RSK_SIDE_O(W, T, 32, F))
-#define RSK_SIDE_F(W) (g.fast ? RSK_SIDE_B(W, 1, true) : RSK_SIDE_B(W, 1, false))
+#define RSK_WAVE_O(W, B, F) (off32 ? &car_side16_wave_kernel<W, B, true, F> : &car_side16_wave_kernel<W, B, false, F>)
+#define RSK_WAVE_B(W, F) \
+    (g.kB == 8 ? RSK_WAVE_O(W, 8, F) : g.kB == 16 ? RSK_WAVE_O(W, 16, F) : RSK_WAVE_O(W, 32, F))
+#define RSK_SIDE_F(W) (g.fast ? RSK_WAVE_B(W, true) : RSK_WAVE_B(W, false))
     const K kern = g.T == 8 ? RSK_SIDE_B(8, 8, false)
                             : (g.W == 4 ? RSK_SIDE_F(4) : g.W == 2 ? RSK_SIDE_F(2) : RSK_SIDE_F(1));
 #undef RSK_SIDE_F
+#undef RSK_WAVE_B
+#undef RSK_WAVE_O
 #undef RSK_SIDE_B
 #undef RSK_SIDE_O
     if (lds > 64 * 1024)
