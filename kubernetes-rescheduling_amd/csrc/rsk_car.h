@@ -360,16 +360,15 @@ struct SideArgs {
     const unsigned long long *zc_key;
     int *out_target, *out_score;
     int S, N;
-    int H, hshift, K, cells;  // per-team LDS geometry (side16_geometry), word offsets below
-    int off_umask, off_srt, off_lvl, off_dl, off_ndl;
+    int H, hshift, K;         // per-team LDS geometry (side16_geometry), word offsets below
+    int off_dl, off_ndl, off_dummy, off_fx, off_h2;
     unsigned lds_team;
     int xcd_per;              // workgroups per XCD run (set by launch_side16)
-    int ablate;               // profiling only: 1 no exact recounts, 2 stop after the marks, 4 no walk, 8 no touched
+    int ablate;               // profiling only (results wrong): 1 no exact recounts, 2 pass 1 only, 4 no (1), 8 no (2)
 };
 struct SideGeom {
-    int dmax, Dc, H, hshift, K, T, W, kB, cells;
-    bool fast;
-    int off_umask, off_srt, off_lvl, off_dl, off_ndl;
+    int dmax, Dc, H, hshift, K, T, W, kB;
+    int off_dl, off_ndl, off_dummy, off_fx, off_h2;
     size_t lds_team;
 };
 SideGeom side16_geometry(int dmax, int N);

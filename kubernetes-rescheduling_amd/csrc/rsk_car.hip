@@ -1819,7 +1819,11 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
             a.xcd_per = (int)ceil_div(units, 8);
             const int64_t blocks = order == 2 ? 8 * (int64_t)a.xcd_per : units;
             RSK_CHECK(blocks < INT32_MAX, "tile grid too large");
-            RSK_TRY(launch_tile16(ts, a, d_score != nullptr, off32, part == 1, (unsigned)blocks, lds));
+            // RSK_TILE_LDS_PAD: extra LDS per lean workgroup (experiments: 7 lean
+            // workgroups per CU leave a slot to side rows on the aux stream)
+            static const size_t lean_pad = (size_t)std::max(0, env_int("RSK_TILE_LDS_PAD", 0));
+            RSK_TRY(launch_tile16(ts, a, d_score != nullptr, off32, part == 1, (unsigned)blocks,
+                                  lds + (part == 0 ? lean_pad : 0)));
         }
     } else if (plan->T > 0) {   // K1 tiles, wide {node, key} pairs
         TileArgs a;
