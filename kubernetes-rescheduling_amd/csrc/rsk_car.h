@@ -2,7 +2,8 @@
 //   rsk_car.hip    plan building, execute, the wide tile path (N > 65535),
 //                  mid / hub rows for the wide path;
 //   rsk_car16.hip  the compact path (N <= 65535): node-state prep, tiles with
-//                  32-bit {code, node} cells, pivot-delta mid / hub rows.
+//                  32-bit {code, node} cells;
+//   rsk_side16.hip the compact path's side rows (degree above the tiles).
 // Reference semantics: rescheduling.py:183-214 (see rsk_car.hip's header).
 #pragma once
 
@@ -25,8 +26,6 @@ constexpr int kNumHeavy = 6;                       // hub classes: (64,128] (128
 constexpr int kHeavyMax[kNumHeavy] = {128, 255, 512, 1024, 2048, 4096};  // <= 255: u8 counters
 constexpr int kHeavyNJ[kNumHeavy] = {2, 4, 8, 16, 0, 0};  // register entries per lane (0: LDS re-reads)
 constexpr int kHubMax = 4096;                      // wide hub kernel: rows up to this degree
-constexpr int kNumPiv = 5;                         // compact side rows by degree: (32,128] (128,512] (512,2048]
-constexpr int kPivMax[kNumPiv - 1] = {128, 512, 2048, kHubMax};  // (2048,4096] (4096,..): the last only here
 
 // Light-row tiles.
 constexpr int kTileOwners = 128;                   // max rows scored per tile
@@ -290,61 +289,6 @@ struct Tile16Args {
     unsigned n_assign, n_out, n_pods, n_recs, n_key;  // element counts (debug bounds build)
 };
 
-// Pivot-delta rows: every side row (deg > 32) of the compact path (rsk_pivot.hip).
-struct PivotArgs {
-    const HeavyItem *items;   // {out_row, offset into hcol, deg}
-    int n_items;
-    const int *hcol;          // neighbour lists
-    const int *assign;
-    const unsigned short *code;
-    const int *cap, *use;
-    const int *zc_cnt;
-    const unsigned long long *zc_key;
-    int *out_target;
-    int *out_score;
-    int S, N;
-    int ablate;               // profiling only (RSK_ABLATE_PIVOT): 1 skip the slow lanes, 2 stop after pass A
-};
-
-// Mid rows (17..64) of the compact path: buckets D = 32, 64 (records kMidW ints).
-struct Mid16Args {
-    const int *rec[2];        // buckets D = 32, 64
-    int n_items[2];
-    const int *assign;
-    const unsigned short *code;
-    const int *cap, *use;
-    const int *zc_cnt;
-    const unsigned long long *zc_key;
-    int *out_target, *out_score;
-    int S, N, SL, PS;         // SL, PS set by launch_mid16
-};
-
-// Hub rows of the compact path (rsk_hub16.hip), every degree class in one grid.
-struct Hub16Args {
-    const int *items;         // [n][4]: out row, offset into hcol, degree, s0 | lg << 24
-    const int *hcol;          // neighbour lists
-    const int *assign;
-    const unsigned short *code;
-    const int *cap, *use;
-    const int *zc_cnt;
-    const unsigned long long *zc_key;
-    int *out_target, *out_score;
-    int S, N;
-    int H, hshift;            // table words per wave, hash shift (from Hub16Geom)
-    int stage;                // staging cells: the largest d << lg of the launch's items
-};
-struct Hub16Geom {
-    int tab, nj, ns;          // table kind (u8 / u16 direct, hash), register entries per lane (0: any
-                              // degree), scenarios per wave at once (tables per wave)
-    int dmax, H, hshift;
-    size_t lds;
-};
-constexpr int kNumHub16 = 3;                       // car_hub16 launches: degree (64,128] (128,255] (255,kHubMax]
-constexpr int kHub16Max[kNumHub16] = {128, 255, kHubMax};  // <= 255: u8 direct counters
-Hub16Geom hub16_geometry(int dmax, int N);
-int hub16_lg(int d, int S);
-int launch_hub16(hipStream_t stream, const Hub16Args &a, const Hub16Geom &g, int n_items);
-
 // Side rows of the compact path (rsk_side16.hip): every row above the tiles,
 // in launches by degree class; a work item is (row, chunk of 64 scenarios).
 constexpr int kNumSide = 6;
@@ -361,27 +305,24 @@ struct SideArgs {
     int *out_target, *out_score;
     int S, N;
     int H, hshift, K;         // per-team LDS geometry (side16_geometry), word offsets below
-    int off_dl, off_ndl, off_dummy, off_fx, off_h2;
+    int off_dl, off_ndl, off_dummy, off_fx, off_h2, h2cap;
     unsigned lds_team;
     int xcd_per;              // workgroups per XCD run (set by launch_side16)
     int ablate;               // profiling only (results wrong): 1 no exact recounts, 2 pass 1 only, 4 no (1), 8 no (2)
 };
 struct SideGeom {
     int dmax, Dc, H, hshift, K, T, W, kB;
-    int off_dl, off_ndl, off_dummy, off_fx, off_h2;
+    int off_dl, off_ndl, off_dummy, off_fx, off_h2, h2cap;
     size_t lds_team;
 };
 SideGeom side16_geometry(int dmax, int N);
 int launch_side16(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32);
 
 int launch_prep(hipStream_t stream, const Prep16Args &a);
-int launch_mid16(hipStream_t stream, const Mid16Args &a);
 int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off32, bool heavy, unsigned blocks,
                   size_t lds);
 size_t tile16_lds_bytes(int rmax, int lsl, int rec_cap);
-int launch_pivot(hipStream_t stream, const PivotArgs &a, int max_distinct);
-int launch_slot(hipStream_t stream, const PivotArgs &a, int dmax);  // rsk_slot.hip: degree 33..128, S >= 64
 unsigned tile16_debug_take();
-int tile16_rows_built();       // image rows per tile the compact kernels are compiled for (RSK_TILE16_ROWS)  // debug bounds build: violation flags of the compact kernels (cleared)
+int tile16_rows_built();       // image rows per tile the compact kernels are compiled for (RSK_TILE16_ROWS)
 
 }  // namespace rsk

@@ -16,7 +16,9 @@
 //   * M == 0: every non-hazard node ties at 0 -> a per-scenario constant
 //     ("zero case"), computed once by car_prep_kernel.
 //
-// Kernels (all integer, no atomics on the decision path):
+// Kernels (all integer, no order-dependent atomics on the decision path).
+// N <= 65535 (the compact path): car_prep16 / car_tile16 (rsk_car16.hip) and
+// car_side16 (rsk_side16.hip).  N > 65535 (the wide path, this file):
 //   car_prep_kernel   nodekey[n*S+s] = hazard ? KEY_HAZ : cap[n]-use[n*S+s]
 //                     (one gather word per node later) + the zero case.
 //   car_tile_kernel   deg <= 32 rows, grouped into tiles of <= 128 rows whose
@@ -25,12 +27,10 @@
 //                     scoring runs from LDS with per-degree-class scorers
 //                     (register pairwise counts up to deg 16, register bitonic
 //                     sort of packed (node, image row) words up to deg 32).
-//   car_hub_kernel    deg > 64 (side stream, overlapping the tiles): columns of
-//                     {node, key} staged in LDS, per-wave LDS count tables,
-//                     DPP wave reductions.
 //   car_mid_kernel    33..64 rows (17..64 when N is too large for the packed
-//                     sort, N >= 2^24 - 1), side stream: per-lane register sort
-//                     of node ids.
+//                     sort, N >= 2^24 - 1): per-lane register sort of node ids.
+//   car_hub_kernel    deg 65..4096: columns of {node, key} staged in LDS,
+//                     per-wave LDS count tables, DPP wave reductions.
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
@@ -757,29 +757,14 @@ struct rsk_car_plan {
     // mid rows (17..64), only in a plan with light_max = kPairMax
     int n_mid[kNumMid] = {0, 0};
     DevBuf mid[kNumMid];
-    // compact path: the hub rows (65..kHubMax) for car_hub16, whose work items depend on S
-    std::vector<HeavyItem> h_hubrows;
-    DevBuf hub16_items;
-    int hub16_S = -1, hub16_thr = -1, hub16_N = -1;
-    int n_hub16[kNumHub16] = {}, hub16_off[kNumHub16] = {}, hub16_stage[kNumHub16] = {};
-    Hub16Geom hub16_geom[kNumHub16] = {};
-    // hub rows (> 64)
+    // hub rows (> 64) of the wide path
     int n_heavy[kNumHeavy] = {};
     int heavy_dmax[kNumHeavy] = {};
     DevBuf heavy_items[kNumHeavy];
     DevBuf hcol;
-    // every side row (deg > light_max) for the compact path's pivot kernel, by degree class
-    int n_piv[kNumPiv] = {};
-    int piv_dmax[kNumPiv] = {};
-    DevBuf piv_items[kNumPiv];
-    DevBuf pcol;
-    // pivot class 0 (degree 33..128) split for the slot kernel: 33..64, 65..128 (into pcol), degree descending
-    int n_slot[2] = {0, 0};
-    int slot_dmax[2] = {0, 0};
-    DevBuf slot_items[2];
     // compact path: every side row (deg > light_max) for car_side16, degree
     // descending, split into the kSideMax classes (neighbours in pcol)
-    DevBuf side_items;
+    DevBuf side_items, pcol;
     int side_beg[kNumSide] = {}, side_end[kNumSide] = {};
     int side_dmax[kNumSide] = {};
     // per-execute workspace
@@ -794,11 +779,8 @@ struct rsk_car_plan {
         meta.release();
         recs.release();
         for (auto &b : mid) b.release();
-        hub16_items.release();
         for (auto &b : heavy_items) b.release();
         hcol.release();
-        for (auto &b : piv_items) b.release();
-        for (auto &b : slot_items) b.release();
         side_items.release();
         pcol.release();
         nodekey.release();
@@ -809,11 +791,6 @@ struct rsk_car_plan {
 
 namespace {
 
-int pivot_class(int d) {
-    for (int c = 0; c < kNumPiv - 1; ++c)
-        if (d <= kPivMax[c]) return c;
-    return kNumPiv - 1;
-}
 
 int heavy_class(int d) {
     for (int c = 0; c < kNumHeavy; ++c)
@@ -1077,7 +1054,7 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
     std::vector<std::vector<int>> midr(kNumMid);
     std::vector<std::vector<HeavyItem>> hitems(kNumHeavy);
     std::vector<int> hcol, pcol;
-    std::vector<std::vector<HeavyItem>> pitems(kNumPiv);
+    std::vector<HeavyItem> sitems;  // compact path: every side row
     for (int i = 0; i < Q; ++i) {
         const int p = rows ? rows[i] : i;
         const int d = rp[p + 1] - rp[p];
@@ -1098,16 +1075,13 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
         } else if (d <= kHubMax) {
             const int c = heavy_class(d);
             hitems[c].push_back({i, (int)hcol.size(), d, 0});
-            plan->h_hubrows.push_back({i, (int)hcol.size(), d, 0});
             hcol.insert(hcol.end(), nbp, nbp + d);
             plan->n_heavy[c] += 1;
             plan->heavy_dmax[c] = std::max(plan->heavy_dmax[c], d);
         }
-        if (d > plan->light_max) {  // compact path: every side row through the pivot kernel
-            const int c = pivot_class(d);
-            pitems[c].push_back({i, (int)pcol.size(), d, 0});
+        if (d > plan->light_max) {  // compact path: every side row through car_side16
+            sitems.push_back({i, (int)pcol.size(), d, 0});
             pcol.insert(pcol.end(), nbp, nbp + d);
-            plan->piv_dmax[c] = std::max(plan->piv_dmax[c], d);
         }
     }
     std::stable_sort(light.begin(), light.end(), [&](int x, int y) {
@@ -1171,21 +1145,13 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
         RSK_TRY(upload(plan->recs, tb.recs.data(), tb.recs.size() * 4));
     }
     for (int b = 0; b < kNumMid; ++b) RSK_TRY(upload(plan->mid[b], midr[b].data(), midr[b].size() * 4));
-    // the longest hub rows first in the car_hub16 grid
-    std::stable_sort(plan->h_hubrows.begin(), plan->h_hubrows.end(),
-                     [](const HeavyItem &x, const HeavyItem &y) { return x.d > y.d; });
     for (int c = 0; c < kNumHeavy; ++c)
         RSK_TRY(upload(plan->heavy_items[c], hitems[c].data(), hitems[c].size() * sizeof(HeavyItem)));
     RSK_TRY(upload(plan->hcol, hcol.data(), hcol.size() * 4));
-    for (int c = 0; c < kNumPiv; ++c) {
-        plan->n_piv[c] = (int)pitems[c].size();
-        RSK_TRY(upload(plan->piv_items[c], pitems[c].data(), pitems[c].size() * sizeof(HeavyItem)));
-    }
     RSK_TRY(upload(plan->pcol, pcol.data(), pcol.size() * 4));
     {   // car_side16 classes: all side rows, degree descending; class c holds
         // the rows of degree (kSideMax[c - 1], kSideMax[c]] at [side_beg[c], side_end[c])
-        std::vector<HeavyItem> all;
-        for (const auto &v : pitems) all.insert(all.end(), v.begin(), v.end());
+        std::vector<HeavyItem> &all = sitems;
         std::stable_sort(all.begin(), all.end(), [](const HeavyItem &x, const HeavyItem &y) { return x.d > y.d; });
         int end = (int)all.size();
         for (int c = 0; c < kNumSide; ++c) {
@@ -1200,17 +1166,6 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
         flat.reserve(all.size() * 4);
         for (const HeavyItem &h : all) flat.insert(flat.end(), {h.oi, h.rb, h.d, 0});
         RSK_TRY(upload(plan->side_items, flat.data(), flat.size() * 4));
-    }
-    {
-        std::vector<HeavyItem> sl[2];
-        for (const HeavyItem &h : pitems[0])
-            if (h.d <= kPivMax[0]) sl[h.d <= 64 ? 0 : 1].push_back(h);
-        for (int k = 0; k < 2; ++k) {
-            std::stable_sort(sl[k].begin(), sl[k].end(), [](const HeavyItem &x, const HeavyItem &y) { return x.d > y.d; });
-            plan->n_slot[k] = (int)sl[k].size();
-            plan->slot_dmax[k] = sl[k].empty() ? 0 : sl[k][0].d;
-            RSK_TRY(upload(plan->slot_items[k], sl[k].data(), sl[k].size() * sizeof(HeavyItem)));
-        }
     }
     return RSK_OK;
 }
@@ -1254,106 +1209,6 @@ struct SideBufs {
     const unsigned long long *zkey;
     int *target, *score;
 };
-
-// Side rows of the compact path: mid rows (17..64) read codes (car_mid16);
-// hub rows (> 64) still go through the wide hub kernel, which reads exact keys.
-bool mid16_on() {
-    static const bool on = env_int("RSK_MID16", 0) != 0;  // car_mid16 (codes) instead of car_mid (exact keys)
-    return on;
-}
-
-// Compact side rows through car_side16 (rsk_side16.hip, default); RSK_SIDE_OLD=1
-// restores the earlier kernels below (A/B only).
-bool side_new_on() {
-    static const bool on = env_int("RSK_SIDE_OLD", 0) == 0;
-    return on;
-}
-
-// Compact side rows: car_mid (33..64) + car_hub (65..4096) by default; the
-// pivot-delta kernel for rows above kHubMax always, and for every side row
-// with RSK_PIVOT=1 (exact too, slower at the headline shapes: DESIGN.md §4).
-bool pivot_on() {
-    static const bool on = env_int("RSK_PIVOT", 0) != 0;
-    return on;
-}
-
-// Slot kernel (rsk_slot.hip) for the compact side rows of degree 33..128
-// (mid rows and hub class 0) when S >= 64 and RSK_SLOT=1 (32-bit assign
-// offsets: P * S * 4 < 2^32).  Opt-in: exact, but its per-entry LDS probe
-// chain measured slower than car_mid + hub class 0.
-bool slot_on(const rsk_car_plan *plan, int S) {
-    static const bool on = env_int("RSK_SLOT", 0) != 0;
-    return on && S >= 64 && !pivot_on() && (int64_t)plan->P * S * 4 < ((int64_t)1 << 32);
-}
-
-// Compact side rows through car_mid16 + car_hub16 (codes only; default), or
-// with RSK_SIDE16=0 through the wide car_mid / car_hub kernels (exact keys).
-bool side16_on() {
-    static const bool on = env_int("RSK_SIDE16", 1) != 0;
-    return on;
-}
-
-// Rows of degree 65..128 go to car_hub16 (a D = 128 car_mid16 — lane =
-// scenario, register sort of 128 cells — does not compile in reasonable time).
-int mid16_max() { return kMidMax; }
-
-// car_hub16 work items for the hub rows of degree > thr at S scenarios:
-// (row, group of 2^lg scenarios), built on the host when S, thr or N change.
-int hub16_prepare(rsk_car_plan *plan, int S, int N, int thr) {
-    if (plan->hub16_S == S && plan->hub16_thr == thr && plan->hub16_N == N) return RSK_OK;
-    plan->hub16_S = -1;
-    std::vector<int32_t> items;
-    for (int c = 0; c < kNumHub16; ++c) {
-        const int lo = c ? kHub16Max[c - 1] : thr;
-        int dmax = 0;
-        for (const HeavyItem &h : plan->h_hubrows)
-            if (h.d > lo && h.d <= kHub16Max[c]) dmax = std::max(dmax, h.d);
-        plan->hub16_off[c] = (int)(items.size() / 4);
-        plan->n_hub16[c] = 0;
-        plan->hub16_stage[c] = 0;
-        if (dmax == 0) continue;
-        plan->hub16_geom[c] = hub16_geometry(dmax, N);
-        // scenario groups as large as the staging area allows, then halved
-        // (down to one scenario per wave) while the class has fewer work items
-        // than ~8 per CU: with few scenarios (config 4: S = 64) the class is
-        // one round of workgroups whose time is the per-wave scenario chain
-        static const int min_items = std::max(1, env_int("RSK_HUB16_MIN_ITEMS", 2048));
-        int shrink = 0;
-        for (;; ++shrink) {
-            int64_t n = 0;
-            bool can = false;
-            for (const HeavyItem &h : plan->h_hubrows) {
-                if (h.d <= lo || h.d > kHub16Max[c]) continue;
-                const int lg = std::max(0, hub16_lg(h.d, S) - shrink);
-                n += ceil_div(S, (int64_t)1 << lg);
-                can = can || lg > 2;
-            }
-            if (n >= min_items || !can) break;
-        }
-        for (const HeavyItem &h : plan->h_hubrows) {  // degree descending
-            if (h.d <= lo || h.d > kHub16Max[c]) continue;
-            const int lg0 = hub16_lg(h.d, S);
-            const int lg = std::max(std::min(lg0, 2), lg0 - shrink);
-            plan->hub16_stage[c] = std::max(plan->hub16_stage[c], h.d << lg);
-            for (int64_t s0 = 0; s0 < S; s0 += (int64_t)1 << lg)
-                items.insert(items.end(), {h.oi, h.rb, h.d, (int)s0 | (lg << 24)});
-        }
-        plan->n_hub16[c] = (int)(items.size() / 4) - plan->hub16_off[c];
-    }
-    RSK_CHECK(items.size() / 4 < (size_t)INT32_MAX, "hub grid too large");
-    RSK_TRY(upload(plan->hub16_items, items.data(), items.size() * 4));
-    plan->hub16_S = S, plan->hub16_thr = thr, plan->hub16_N = N;
-    return RSK_OK;
-}
-
-// Whether the side rows need codes only (no exact node keys from the prep kernel).
-bool plan_side_compact(const rsk_car_plan *plan, int S) {
-    if (pivot_on() || side16_on()) return true;
-    const bool slot = slot_on(plan, S);
-    for (int c = slot ? 1 : 0; c < kNumHeavy; ++c)
-        if (plan->n_heavy[c]) return false;
-    return slot || mid16_on() || plan->n_mid[0] + plan->n_mid[1] == 0;
-}
 
 // car_side16 launches of classes [c0, c1) on `stream`, the longest rows first.
 // Classes from kSideBig up (rows above 128 neighbours: few work items, each
@@ -1403,119 +1258,14 @@ bool side16_has_big(const rsk_car_plan *plan) {
     return false;
 }
 
-int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t *side, int nside, const SideBufs &b, int S, int N,
-                bool compact) {
+// Side rows on `stream`: the compact path's classes below kSideBig (the rest
+// are launched beside the tiles by the caller); the wide path's mid (17..64,
+// N >= kPackMaxN variant only) and hub (> 64) rows, exact keys.
+int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, const SideBufs &b, int S, int N, bool compact) {
+    if (compact) return launch_side16_classes(plan, ctx, stream, b, S, N, 0, kSideBig);
     const int *d_assign = b.assign, *d_key = b.key, *d_zcnt = b.zcnt;
     const unsigned long long *d_zkey = b.zkey;
     int *d_target = b.target, *d_score = b.score;
-    int next = 0;
-    auto pick = [&]() { return side[next++ % nside]; };
-    if (compact && side_new_on()) {  // car_side16 (the caller launches the few-row classes: launch_side16_big)
-        RSK_TRY(launch_side16_classes(plan, ctx, ctx->stream, b, S, N, 0, kSideBig));
-        return RSK_OK;
-    }
-    if (compact) {  // pivot-delta kernel: every side row (RSK_PIVOT=1) or the rows above kHubMax
-        for (int c = pivot_on() ? 0 : kNumPiv - 1; c < kNumPiv; ++c) {
-            if (!plan->n_piv[c]) continue;
-            PivotArgs a;
-            std::memset(&a, 0, sizeof(a));
-            a.items = plan->piv_items[c].as<HeavyItem>();
-            a.n_items = plan->n_piv[c];
-            a.hcol = plan->pcol.as<int>();
-            a.assign = d_assign;
-            a.code = b.code;
-            a.cap = b.cap;
-            a.use = b.use;
-            a.zc_cnt = d_zcnt;
-            a.zc_key = d_zkey;
-            a.out_target = d_target;
-            a.out_score = d_score;
-            a.S = S;
-            a.N = N;
-            static const int pablate = env_int("RSK_ABLATE_PIVOT", 0);
-            a.ablate = pablate;
-            const hipStream_t stream = pick();
-            ScopedTimer tm(ctx, "car_side", stream);
-            RSK_TRY(launch_pivot(stream, a, std::min(plan->piv_dmax[c], N)));
-        }
-        if (pivot_on()) return RSK_OK;
-    }
-    if (compact && side16_on()) {
-        const int thr = mid16_max();
-        if (plan->n_mid[0] + plan->n_mid[1] > 0) {  // K2 mid rows (33..thr), codes
-            Mid16Args a;
-            std::memset(&a, 0, sizeof(a));
-            for (int k = 0; k < kNumMid; ++k) {
-                a.rec[k] = plan->mid[k].as<int>();
-                a.n_items[k] = plan->n_mid[k];
-            }
-            a.assign = d_assign;
-            a.code = b.code;
-            a.cap = b.cap;
-            a.use = b.use;
-            a.zc_cnt = d_zcnt;
-            a.zc_key = d_zkey;
-            a.out_target = d_target;
-            a.out_score = d_score;
-            a.S = S;
-            a.N = N;
-            const hipStream_t stream = pick();
-            ScopedTimer tm(ctx, "car_mid", stream);
-            RSK_TRY(launch_mid16(stream, a));
-        }
-        RSK_TRY(hub16_prepare(plan, S, N, thr));
-        for (int c = 0; c < kNumHub16; ++c) {  // K3 hub rows (thr..kHubMax), three degree classes
-            if (!plan->n_hub16[c]) continue;
-            Hub16Args a;
-            std::memset(&a, 0, sizeof(a));
-            a.items = plan->hub16_items.as<int>() + (size_t)plan->hub16_off[c] * 4;
-            a.hcol = plan->hcol.as<int>();
-            a.assign = d_assign;
-            a.code = b.code;
-            a.cap = b.cap;
-            a.use = b.use;
-            a.zc_cnt = d_zcnt;
-            a.zc_key = d_zkey;
-            a.out_target = d_target;
-            a.out_score = d_score;
-            a.S = S;
-            a.N = N;
-            const Hub16Geom &g = plan->hub16_geom[c];
-            a.H = g.H;
-            a.hshift = g.hshift;
-            a.stage = plan->hub16_stage[c];
-            const hipStream_t stream = pick();
-            static const bool per_class = env_int("RSK_HUB_TIMERS", 0) != 0;
-            static const char *const kNames[kNumHub16] = {"car_hub128", "car_hub256", "car_hub4096"};
-            ScopedTimer tm(ctx, per_class ? kNames[c] : "car_heavy", stream);
-            RSK_TRY(launch_hub16(stream, a, g, plan->n_hub16[c]));
-        }
-        return RSK_OK;
-    }
-    const bool slot = compact && slot_on(plan, S);
-    if (slot) {  // degree 33..128: slot tables (replaces car_mid and hub class 0)
-        for (int k = 0; k < 2; ++k) {
-            if (!plan->n_slot[k]) continue;
-            PivotArgs a;
-            std::memset(&a, 0, sizeof(a));
-            a.items = plan->slot_items[k].as<HeavyItem>();
-            a.n_items = plan->n_slot[k];
-            a.hcol = plan->pcol.as<int>();
-            a.assign = d_assign;
-            a.code = b.code;
-            a.cap = b.cap;
-            a.use = b.use;
-            a.zc_cnt = d_zcnt;
-            a.zc_key = d_zkey;
-            a.out_target = d_target;
-            a.out_score = d_score;
-            a.S = S;
-            a.N = N;
-            const hipStream_t stream = pick();
-            ScopedTimer tm(ctx, "car_slot", stream);
-            RSK_TRY(launch_slot(stream, a, plan->slot_dmax[k]));
-        }
-    }
     ScoreCtx sc;
     sc.nodekey = d_key;
     sc.zc_cnt = d_zcnt;
@@ -1527,38 +1277,16 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t *side, int n
     const int SL = std::min(S, 64);
     sc.PS = 64 / SL;
     const int64_t chunks = ceil_div(S, SL);
-    if (slot) {
-        // mid rows done by the slot kernel
-    } else if (compact && mid16_on() && plan->n_mid[0] + plan->n_mid[1] > 0) {   // K2 mid rows, codes
-        Mid16Args a;
-        std::memset(&a, 0, sizeof(a));
-        for (int k = 0; k < kNumMid; ++k) {
-            a.rec[k] = plan->mid[k].as<int>();
-            a.n_items[k] = plan->n_mid[k];
-        }
-        a.assign = d_assign;
-        a.code = b.code;
-        a.cap = b.cap;
-        a.use = b.use;
-        a.zc_cnt = d_zcnt;
-        a.zc_key = d_zkey;
-        a.out_target = d_target;
-        a.out_score = d_score;
-        a.S = S;
-        a.N = N;
-        const hipStream_t stream = pick();
-        ScopedTimer tm(ctx, "car_mid", stream);
-        RSK_TRY(launch_mid16(stream, a));
-    } else {   // K2 mid rows, exact keys
+    {   // K2 mid rows, exact keys
         MidArgs a;
         std::memset(&a, 0, sizeof(a));
         a.sc = sc;
         a.SL = SL;
         a.prefix[0] = 0;
-        for (int b = 0; b < kNumMid; ++b) {
-            a.rec[b] = plan->mid[b].as<int>();
-            a.n_items[b] = plan->n_mid[b];
-            a.prefix[b + 1] = a.prefix[b] + (int)ceil_div(plan->n_mid[b], sc.PS);
+        for (int k = 0; k < kNumMid; ++k) {
+            a.rec[k] = plan->mid[k].as<int>();
+            a.n_items[k] = plan->n_mid[k];
+            a.prefix[k + 1] = a.prefix[k] + (int)ceil_div(plan->n_mid[k], sc.PS);
         }
         a.assign = d_assign;
         const int waves = a.prefix[kNumMid];
@@ -1566,16 +1294,14 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t *side, int n
             a.blocks_per_chunk = (int)ceil_div(waves, 4);
             const int64_t blocks = chunks * a.blocks_per_chunk;
             RSK_CHECK(blocks < INT32_MAX, "mid grid too large");
-            const hipStream_t stream = pick();
             ScopedTimer tm(ctx, "car_mid", stream);
             car_mid_kernel<<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(a);
             RSK_HIP(hipGetLastError());
         }
     }
-    for (int c = slot ? 1 : 0; c < kNumHeavy; ++c) {   // K3 hub rows (class 0 by the slot kernel)
+    for (int c = 0; c < kNumHeavy; ++c) {   // K3 hub rows
         const int n = plan->n_heavy[c];
         if (!n) continue;
-        const hipStream_t stream = pick();
         const HeavyGeom g = heavy_geometry(plan->heavy_dmax[c], S, N);
         RSK_CHECK(g.lds <= 160 * 1024, "hub class %d needs %zu B of LDS", c, g.lds);
         const int64_t groups = ceil_div(S, 1 << g.lg);
@@ -1600,12 +1326,6 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, const hipStream_t *side, int n
     return RSK_OK;
 }
 
-bool plan_has_side(const rsk_car_plan *plan) {
-    int n = plan->n_mid[0] + plan->n_mid[1];
-    for (int c = 0; c < kNumHeavy; ++c) n += plan->n_heavy[c];
-    for (int c = 0; c < kNumPiv; ++c) n += plan->n_piv[c];
-    return n > 0;
-}
 
 }  // namespace
 
@@ -1703,10 +1423,9 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     RSK_TRY(stage_out(ctx, 4, out_target, QS * 4, dev, reinterpret_cast<void **>(&d_target)));
     if (out_score) RSK_TRY(stage_out(ctx, 5, out_score, QS * 4, dev, reinterpret_cast<void **>(&d_score)));
 
-    const bool side_rows = plan_has_side(plan);
     int *d_key = nullptr;
     unsigned short *d_code = nullptr;
-    if (!compact || (side_rows && !plan_side_compact(plan, S))) {
+    if (!compact) {
         RSK_TRY(plan->nodekey.reserve(NS * 4));
         d_key = plan->nodekey.as<int>();
     }
@@ -1734,26 +1453,16 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         ScopedTimer tm(ctx, "car_prep");
         RSK_TRY(launch_prep(ctx->stream, pa));
     }
-    // mid and hub rows run after the tiles on the same stream by default; with
-    // RSK_OVERLAP = k on k side streams beside the tile kernel (or, with
-    // RSK_SIDE_FIRST=1, ahead of it).  Overlap does not shorten the step (the
-    // lean tile kernel holds every CU's LDS and VGPRs) and it
-    // stretches the tile kernel, so it is off.
-    static const int overlap = std::max(0, std::min(rsk_ctx::kAux, env_int("RSK_OVERLAP", 0)));
-    static const bool side_first = env_int("RSK_SIDE_FIRST", 0) != 0;
-    hipStream_t side[rsk_ctx::kAux] = {ctx->stream, ctx->stream, ctx->stream};
-    const bool new_side = compact && side_new_on();
-    const int nside = side_rows && plan->T > 0 && !new_side ? overlap : 0;
     // car_side16's few-row classes (rows above 128 neighbours) on a side stream
-    // beside the tiles: a handful of latency-bound workgroups that would
-    // otherwise run alone on the GPU (RSK_SIDE_BIG_AUX=0: on the main stream)
+    // beside the tiles: a handful of latency-bound workgroups per class that
+    // would otherwise run alone on the GPU (RSK_SIDE_BIG_AUX=0: on the main
+    // stream).  The other side rows run on the main stream before the tiles:
+    // sharing the CUs with the memory-bound tiles did not shorten the step
+    // (DESIGN.md §4).
     static const bool big_aux = env_int("RSK_SIDE_BIG_AUX", 1) != 0;
-    const bool big_fork = new_side && big_aux && plan->T > 0 && side16_has_big(plan);
-    const int nfork = big_fork ? 1 : nside;
-    if (nfork) {
-        RSK_TRY(aux_fork(ctx, nfork));
-        for (int i = 0; i < nside; ++i) side[i] = ctx->aux[i];
-    }
+    const bool big_fork = compact && big_aux && plan->T > 0 && side16_has_big(plan);
+    const int nfork = big_fork ? 1 : 0;
+    if (nfork) RSK_TRY(aux_fork(ctx, nfork));
     SideBufs sb;
     sb.assign = d_assign;
     sb.key = d_key;
@@ -1764,10 +1473,9 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     sb.zkey = d_zkey;
     sb.target = d_target;
     sb.score = d_score;
-    if (new_side)
+    if (compact)
         RSK_TRY(launch_side16_classes(plan, ctx, big_fork ? ctx->aux[0] : ctx->stream, sb, S, N, kSideBig, kNumSide));
-    RSK_TRY(launch_side(plan, ctx, side, std::max(nside, 1), sb, S, N, compact));
-    if (nfork && side_first) RSK_TRY(aux_join(ctx, nfork));
+    RSK_TRY(launch_side(plan, ctx, ctx->stream, sb, S, N, compact));
     static const int ablate = env_int("RSK_ABLATE_TILE", 0);
     static const int order = env_int("RSK_TILE_ORDER", 2);
     const bool off32 = (int64_t)std::max(plan->P, plan->Q) * S * 4 < ((int64_t)1 << 32);
@@ -1870,7 +1578,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         kern<<<dim3((unsigned)blocks), dim3(kTileThreads), lds, ctx->stream>>>(a);
         RSK_HIP(hipGetLastError());
     }
-    if (nfork && !side_first) RSK_TRY(aux_join(ctx, nfork));
+    if (nfork) RSK_TRY(aux_join(ctx, nfork));
 #ifdef RSK_DEBUG_BOUNDS
     {
         unsigned flags_h = 0, zero = 0;

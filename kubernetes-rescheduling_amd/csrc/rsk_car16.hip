@@ -999,124 +999,6 @@ __global__ __launch_bounds__(kTileThreads, (kHeavy || !kL64) ? RSK_TILE16_WGS_HE
     }
 }
 
-// ---------------------------------------------------------------------------
-// car_mid16: rows of degree 17..64 (buckets D = 32, 64; records [oi, d,
-// neighbour pods...]), one wave per (row, chunk of SL scenarios), lane =
-// scenario (PS = 64 / SL rows per wave when S < 64).  Each lane gathers its
-// neighbours' cells (assign row, then the node's code), sorts the D cells in
-// registers (equal nodes become runs) and walks the runs twice: the maximal
-// run length M and the number of runs at it, then the best (code, -node)
-// among those runs and how many share its code; equal codes >= 2 on distinct
-// nodes are resolved exactly from cap / use in a third, rare walk.
-// ---------------------------------------------------------------------------
-// Exact tie resolution of a mid row (rare, kept out of registers): among the
-// row's distinct nodes with code bk and count M, the largest exact remaining
-// CPU, then the lower node — a dynamic double loop re-reading the row's
-// assignments (L2-resident) instead of the register copies.
-__device__ __forceinline__ int mid16_exact(const Mid16Args &a, const int *__restrict__ nb, int d, int s, int M,
-                                           unsigned bk) {
-    const unsigned S = (unsigned)a.S, N = (unsigned)a.N;
-    int br = INT_MIN, bn = INT_MAX;
-#pragma unroll 1
-    for (int e = 0; e < d; ++e) {
-        const int ne = a.assign[(size_t)nb[e] * S + (unsigned)s];
-        if ((unsigned)ne >= N || ld16(a.code, (unsigned)ne * S + (unsigned)s) != bk) continue;
-        int cnt = 0;
-#pragma unroll 1
-        for (int i = 0; i < d; ++i) cnt += a.assign[(size_t)nb[i] * S + (unsigned)s] == ne;
-        if (cnt != M) continue;
-        const int ex = a.cap[ne] - ld32(a.use, (unsigned)ne * S + (unsigned)s);
-        if (ex > br || (ex == br && ne < bn)) { br = ex; bn = ne; }
-    }
-    return bn;
-}
-
-template <int D, int W>
-__device__ __forceinline__ void mid16_row(const Mid16Args &a, const int *__restrict__ rec, int s, bool lane_ok) {
-    const unsigned S = (unsigned)a.S, N = (unsigned)a.N;
-    const int s_ld = min(s, a.S - 1);
-    const int4 *r4 = reinterpret_cast<const int4 *>(rec);
-    const int2 hd = *reinterpret_cast<const int2 *>(rec);
-    const int oi = hd.x, d = hd.y;
-    // assignments: pads (j >= d) and values outside [0, N) become node N, whose
-    // code row is zero (never a candidate)
-    unsigned x[D];
-#pragma unroll
-    for (int w = 0; w < W / 4; ++w) {
-        const int4 q4 = r4[w];
-        const int q[4] = {q4.x, q4.y, q4.z, q4.w};
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int j = 4 * w + t - 2;
-            if (j >= 0 && j < D) x[j] = (unsigned)a.assign[(size_t)(j < d ? q[t] : 0) * S + (unsigned)s_ld];
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < D; ++j) x[j] = j < d ? min(x[j], N) : N;
-    // code gathers, all in flight
-    constexpr int kC = D;
-#pragma unroll
-    for (int j0 = 0; j0 < D; j0 += kC) {
-        unsigned cd[kC];
-#pragma unroll
-        for (int t = 0; t < kC; ++t) cd[t] = ld16(a.code, x[j0 + t] * S + (unsigned)s_ld);
-#pragma unroll
-        for (int t = 0; t < kC; ++t) x[j0 + t] |= cd[t] << 16;
-    }
-    sort_cells<D, unsigned>(x);
-    int sc;
-    unsigned bk;
-    bool need;
-    int t = sorted_runs<D>(x, sc, bk, need);
-    if (__builtin_amdgcn_ballot_w64(need)) {  // rare: wave-uniform branch
-        const int te = mid16_exact(a, rec + 2, d, s_ld, sc, bk);
-        t = need ? te : t;
-    }
-    if (t == INT_MIN) t = zero_target(load_zc(a.zc_cnt, a.zc_key, s_ld), sc);
-    if (lane_ok) {
-        const size_t o = (size_t)oi * S + s;
-        a.out_target[o] = t;
-        if (a.out_score) a.out_score[o] = sc;
-    }
-}
-
-// One launch per bucket (registers sized for its D): blocks of 4 waves, wave =
-// (PS rows, chunk of SL scenarios).
-template <int D, int W>
-__global__ __launch_bounds__(256) void car_mid16_kernel(Mid16Args a, const int *__restrict__ recs, int n_items,
-                                                        int blocks_per_chunk) {
-    const int chunk = blockIdx.x / blocks_per_chunk;
-    const int wave = (blockIdx.x % blocks_per_chunk) * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int slot = lane / a.SL;
-    const int s = chunk * a.SL + lane % a.SL;
-    const int item = wave * a.PS + slot;
-    if (wave * a.PS >= n_items) return;  // whole wave
-    const bool lane_ok = slot < a.PS && s < a.S && item < n_items;
-    const int it = min(item, n_items - 1);
-    mid16_row<D, W>(a, recs + (size_t)it * W, s, lane_ok);
-}
-
-int launch_mid16(hipStream_t stream, const Mid16Args &a0) {
-    Mid16Args a = a0;
-    a.SL = std::min(a.S, 64);
-    a.PS = 64 / a.SL;
-    for (int b = 1; b >= 0; --b) {  // the longest rows first
-        const int n = a.n_items[b];
-        if (n == 0) continue;
-        const int waves = (int)ceil_div(n, a.PS);
-        const int bpc = (int)ceil_div(waves, 4);
-        const int64_t blocks = ceil_div(a.S, a.SL) * bpc;
-        RSK_CHECK(blocks < INT32_MAX, "mid grid too large");
-        if (b == 0)
-            car_mid16_kernel<32, 36><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(a, a.rec[0], n, bpc);
-        else
-            car_mid16_kernel<64, 68><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>(a, a.rec[1], n, bpc);
-        RSK_HIP(hipGetLastError());
-    }
-    return RSK_OK;
-}
-
 int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off32, bool heavy, unsigned blocks,
                   size_t lds) {
     using K = void (*)(Tile16Args);

@@ -227,8 +227,8 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(S
     int *ndl = reinterpret_cast<int *>(base + a.off_ndl);  // [64] deviations per lane (teams)
     unsigned *dummy = base + a.off_dummy;                  // [64] sink of the non-deviating lanes' writes
     unsigned *fx = base + a.off_fx;                        // teams: [kT][2][64] the waves' top-2 words
-    unsigned *bx = fx + 128 * kT;                          // teams: [kT][3][64] the waves' count >= 2 bests
     unsigned *h2 = base + a.off_h2;                        // [1 + n2] counter, table words counted >= 2
+    unsigned *bx = h2;                                     // teams, after the list: [kT][3][64] the waves' bests
 
     for (int i = tw * 64 + lane; i < H; i += 64 * kT) tb.tab[i] = 0u;
     if (kT > 1) {
@@ -331,7 +331,7 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(S
         } else {
             pos = big ? (int)atomicAdd(&h2[0], 1u) : 0;
         }
-        if (big) h2[1 + pos] = w;
+        if (big && pos < a.h2cap) h2[1 + pos] = w;
     }
     if (kT > 1) {
         __syncthreads();
@@ -339,6 +339,8 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(S
     } else {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the list's LDS writes before its reads
     }
+    const bool h2over = n2 > a.h2cap;  // more nodes counted twice than the list holds: every lane recounts
+    n2 = min(n2, a.h2cap);
     Best b;
     b.init();
     // (1) the listed nodes, eight at a time (their codes gathered together); the
@@ -391,6 +393,7 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(S
         }
     }
     if (kT > 1) {  // the waves' bests (disjoint node sets) and top-2 words to wave 0
+        __syncthreads();  // every wave is done with the list bx overwrites
         bx[(3 * tw) * 64 + lane] = (unsigned)b.M;
         bx[(3 * tw + 1) * 64 + lane] = b.w1;
         bx[(3 * tw + 2) * 64 + lane] = b.w2;
@@ -411,7 +414,7 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(S
     const bool two = b.M >= 2;
     const int M = two ? b.M : (f.w1 ? 1 : 0);
     const unsigned w1 = two ? b.w1 : f.w1, w2 = two ? b.w2 : f.w2;
-    bool slow = nd > K;
+    bool slow = nd > K || h2over;
     int tg, sc;
     if (M == 0) {
         tg = zero_target(load_zc(a.zc_cnt, a.zc_key, s), sc);
@@ -444,6 +447,8 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(S
     }
 }
 
+constexpr int kSideH2Cap = 2048;  // listed nodes counted >= 2 (e.g. degree 5000 over 6000 nodes: ~1200)
+
 SideGeom side16_geometry(int dmax, int N) {
     SideGeom g;
     g.dmax = dmax;
@@ -459,13 +464,17 @@ SideGeom side16_geometry(int dmax, int N) {
     // neighbour loads in flight per wave (with their code gathers: 2 kB VGPRs)
     g.kB = dmax <= 32 ? 8 : (g.T == 1 ? 16 : 32);
     // words: tab H | dl 64 K (also the recount's cells) | ndl 64 | dummy 64 |
-    // h2 1 + n2 (n2 <= min(Dc, dmax / 2) entries counted >= 2) | fx 128 T, bx 192 T (teams)
+    // h2 1 + h2cap (the entries counted >= 2: at most min(Dc, dmax / 2); a
+    // longer list sends the item to the exact recount; teams: bx 192 T after
+    // the list is done) | fx 128 T (teams)
     g.off_dl = H;
     g.off_ndl = g.off_dl + 64 * g.K;
     g.off_dummy = g.off_ndl + 64;
     g.off_h2 = g.off_dummy + 64;
-    g.off_fx = g.off_h2 + ((1 + std::min(g.Dc, std::max(1, dmax / 2)) + 3) & ~3);
-    g.lds_team = ((size_t)(g.off_fx + (g.T > 1 ? 320 * g.T : 0)) * 4 + 15) & ~(size_t)15;
+    g.h2cap = std::min(kSideH2Cap, std::min(g.Dc, std::max(1, dmax / 2)));
+    const int h2words = std::max(1 + g.h2cap, g.T > 1 ? 192 * g.T : 0);
+    g.off_fx = g.off_h2 + ((h2words + 3) & ~3);
+    g.lds_team = ((size_t)(g.off_fx + (g.T > 1 ? 128 * g.T : 0)) * 4 + 15) & ~(size_t)15;
     // teams per workgroup: 4 single-wave teams while they fit 40 KiB, else fewer
     if (g.T > 1) g.W = g.T;
     else g.W = 4 * g.lds_team <= 40 * 1024 ? 4 : (2 * g.lds_team <= 80 * 1024 ? 2 : 1);
@@ -488,6 +497,7 @@ int launch_side16(hipStream_t stream, const SideArgs &a0, const SideGeom &g, boo
     a.off_dummy = g.off_dummy;
     a.off_fx = g.off_fx;
     a.off_h2 = g.off_h2;
+    a.h2cap = g.h2cap;
     const int64_t items = (int64_t)a.n_rows * a.nchunk;
     RSK_CHECK(items < INT32_MAX / 8, "side grid too large");
     const int teams = g.T > 1 ? 1 : g.W;

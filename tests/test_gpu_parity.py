@@ -406,8 +406,8 @@ def test_car_score_variant_matches(ctx):
 @pytest.mark.parametrize("S", [1, 64])
 def test_car_row_above_4096_neighbours(ctx, S):
     """A deployment related to more than 4096 others: the compact
-    path scores it with the pivot-delta kernel (any degree with min(deg, N)
-    distinct nodes within its LDS table)."""
+    path scores it with the side kernel (any degree with min(deg, N) distinct
+    nodes within its LDS table)."""
     rng = np.random.default_rng(700 + S)
     P, N = 9000, 300
     rows = [rng.integers(0, P, int(rng.integers(0, 4))).tolist() for _ in range(P)]
@@ -447,6 +447,30 @@ def test_car_row_5000_distinct_nodes(ctx, S):
                label=f"deg 5000 N {N} S={S}")
 
 
+@pytest.mark.parametrize("P,N,deg,S", [(23000, 21845, 21000, 1), (23000, 21845, 21000, 64), (13000, 3000, 12000, 64)])
+def test_car_row_largest_tables(ctx, P, N, deg, S):
+    """The side kernel's LDS limits: a row with 21,000 distinct neighbour nodes
+    (the largest table that fits, 32,768 words) and a degree-12,000 row over
+    3,000 nodes whose ~2,900 nodes counted twice overflow the 2,048-entry list
+    (every lane takes the exact recount).  1 % of placements redrawn per
+    scenario, as in the synthetic what-if batches."""
+    rng = np.random.default_rng(deg + S)
+    rows = [rng.integers(0, P, int(rng.integers(0, 3))).tolist() for _ in range(P)]
+    rows[0] = rng.choice(np.arange(1, P), deg, replace=False).tolist()
+    rp = np.zeros(P + 1, np.int32)
+    rp[1:] = np.cumsum([len(r) for r in rows])
+    ci = np.array([q for r in rows for q in r], np.int32)
+    base = rng.permutation(P) % N
+    a = np.repeat(base[:, None], S, axis=1).astype(np.int32)
+    flip = rng.random((P, S)) < 0.01
+    a[flip] = rng.integers(-1, N, flip.sum())
+    cap = rng.choice([4000, 8000], N).astype(np.int32)
+    use = rng.integers(0, 8000, N * S).astype(np.int32)
+    haz = (rng.random(N * S) < 0.2).astype(np.uint8)
+    _check_car(ctx, rp, ci, a.reshape(-1), S, cap, use, haz, N, rows=np.arange(0, 8, dtype=np.int32),
+               label=f"deg {deg} N {N} S={S}")
+
+
 def test_dropin_communication_5000_related_above_row_max_n(ctx):
     """The drop-in's `communication` with N > 32768 nodes goes through
     car_place; a deployment related to 5000 others gets the
@@ -474,50 +498,21 @@ def test_dropin_communication_5000_related_above_row_max_n(ctx):
     assert got == (names[int(t[0])] if t[0] >= 0 else None)
 
 
-def test_car_pivot_kernel_every_side_row():
-    """RSK_PIVOT=1 routes every side row (deg > 32) of the compact path through
-    the pivot-delta kernel: the random-graph, bucket-boundary and collision
-    cases against the oracle (a subprocess: the switch is read once)."""
-    import os
-    import subprocess
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    env = dict(os.environ, RSK_PIVOT="1")
-    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", os.path.join(here, "test_gpu_parity.py"),
-                        "-k", "random_graphs or bucket_boundaries or hub_exact or code_collisions or above_4096 or hash_path",
-                        "--timeout", "300"], env=env, capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-
-
-def test_car_slot_table_overflow(ctx):
+def test_car_side_rows_fresh_nodes(ctx):
     """Rows of degree 33..255 at S >= 64 with every scenario drawing fresh
     nodes out of 5000: thousands of distinct nodes per row and 64-scenario
-    chunk (with RSK_SLOT=1 the slot table fills and the lanes that could not
-    insert recount exactly; by default car_mid16 / car_hub16)."""
+    chunk, so the side kernel's per-lane deviation lists overflow and every
+    lane takes the exact recount; then half the scenarios sharing scenario 0's
+    nodes (mixed pivots and deviations)."""
     rng = np.random.default_rng(800)
     P, N, S = 3000, 5000, 128
     rp, ci, a, cap, use, haz = _random_case(rng, P, N, S, max_deg=3,
                                             hub_deg=[33, 50, 64, 65, 100, 128, 129, 200, 254, 255], p_haz=0.1)
-    _check_car(ctx, rp, ci, a, S, cap, use, haz, N, rows=np.arange(0, 40, dtype=np.int32), label="slot overflow")
+    _check_car(ctx, rp, ci, a, S, cap, use, haz, N, rows=np.arange(0, 40, dtype=np.int32), label="fresh nodes")
     a2 = a.reshape(P, S).copy()
     a2[:, ::2] = a2[:, :1]            # half the scenarios share scenario 0's nodes: tables near the degree
     _check_car(ctx, rp, ci, a2.reshape(-1), S, cap, use, haz, N, rows=np.arange(0, 40, dtype=np.int32),
-               label="slot mixed")
-
-
-def test_car_slot_kernel_side_rows():
-    """RSK_SLOT=1 routes degree 33..128 through the slot-table kernel
-    (rsk_slot.hip) instead of car_mid / hub class 0: the same oracle cases,
-    including the table overflow above (a subprocess: the switch is read once)."""
-    import os
-    import subprocess
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    env = dict(os.environ, RSK_SLOT="1")
-    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", os.path.join(here, "test_gpu_parity.py"),
-                        "-k", "random_graphs or bucket_boundaries or code_collisions or invalid_assign or slot_table",
-                        "--timeout", "300"], env=env, capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+               label="mixed")
 
 
 @pytest.mark.parametrize("S", [9, 40, 64, 100])

@@ -17,7 +17,7 @@ step() {  # step <name> <seconds> <cmd...>
     return 0
 }
 if [ "$mode" = test ]; then
-    [ -n "$SKIP_BASE_TEST" ] || step pytest_car 500 python -u -m pytest ${TESTS:-tests} -m gpu -x -v -k "not pivot_kernel_every and not slot_kernel_side" --timeout 200 --timeout-method thread
+    [ -n "$SKIP_BASE_TEST" ] || step pytest_car 500 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 200 --timeout-method thread
     [ -n "$SKIP_L16_TEST" ] || step pytest_car_l16 400 env RSK_LIGHT_MAX=16 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_headline.py -m gpu -x -v -k "car" --timeout 200 --timeout-method thread
 fi
 bench() {  # bench <name> <config> [env...]
@@ -33,7 +33,6 @@ EOF
 }
 bench head headline
 bench head_l16 headline RSK_LIGHT_MAX=16
-[ -n "$SKIP_OLD" ] || bench head_old headline RSK_SIDE_OLD=1
 bench 1m50k 1m50k
 bench 1m50k_l16 1m50k RSK_LIGHT_MAX=16
 for v in "$@"; do bench "v_$(echo "$v" | tr ",=/" "___" | cut -c1-60)" headline $(echo "$v" | tr "," " "); done
