@@ -267,6 +267,7 @@ struct Prep16Args {
     int *zc_cnt;                 // [S]
     unsigned long long *zc_key;  // [S]
     int *capmax;                 // [1] scratch: max(cap), written by launch_prep before the prep kernel
+                                 // (zc_key, zc_cnt: contiguous, zeroed there too)
 };
 
 struct Tile16Args {
@@ -315,7 +316,16 @@ struct SideGeom {
     int off_dl, off_ndl, off_dummy, off_fx, off_h2, h2cap;
     size_t lds_team;
 };
-SideGeom side16_geometry(int dmax, int N);
+SideGeom side16_geometry(int dmax, int N, int T = 0);  // T: waves per item (0: 1 up to 256 neighbours, else 8)
+void side16_apply_geometry(SideArgs &a, const SideGeom &g);  // the geometry's LDS layout into the launch arguments
+struct FuseMap {
+    int big_blocks;    // the first big_blocks blocks: 4-wave side teams (ba), a multiple of 8
+    int R, side_rows;  // then every R-th row of 8 blocks is a single-wave side row (sa), side_rows of them
+};
+// lean tiles + single-wave side items of one class (4 per workgroup, kB 16) +
+// optionally 4-wave side teams (kB 16) in one grid; ba.n_rows == 0: no teams
+int launch_fused16(hipStream_t stream, const Tile16Args &a, const SideArgs &sa, int side_blocks, const SideArgs &ba,
+                   bool score, bool off32, unsigned tile_blocks, size_t lds);
 int launch_side16(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32);
 
 int launch_prep(hipStream_t stream, const Prep16Args &a);

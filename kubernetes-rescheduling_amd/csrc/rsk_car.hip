@@ -1218,33 +1218,38 @@ int side_big_class() {  // RSK_SIDE_AUX_FROM: the first class on the side stream
     return c;
 }
 #define kSideBig side_big_class()
-int launch_side16_classes(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, const SideBufs &b, int S, int N,
-                          int c0, int c1) {
-    const bool off32 = (int64_t)std::max(plan->P, plan->Q) * S * 4 < ((int64_t)1 << 32);
+SideArgs side16_class_args(const rsk_car_plan *plan, int c, const SideBufs &b, int S, int N) {
     static const int sablate = env_int("RSK_ABLATE_SIDE", 0);
+    SideArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.items = plan->side_items.as<int>() + (size_t)plan->side_beg[c] * 4;
+    a.n_rows = plan->side_end[c] - plan->side_beg[c];
+    a.nchunk = (int)ceil_div(S, 64);
+    a.col = plan->pcol.as<int>();
+    a.assign = b.assign;
+    a.code = b.code;
+    a.cap = b.cap;
+    a.use = b.use;
+    a.zc_cnt = b.zcnt;
+    a.zc_key = b.zkey;
+    a.out_target = b.target;
+    a.out_score = b.score;
+    a.S = S;
+    a.N = N;
+    a.ablate = sablate;
+    return a;
+}
+
+// classes [c0, c1) except `skip` (the class fused into the tile launch)
+int launch_side16_classes(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, const SideBufs &b, int S, int N,
+                          int c0, int c1, int skip = -1) {
+    const bool off32 = (int64_t)std::max(plan->P, plan->Q) * S * 4 < ((int64_t)1 << 32);
     static const bool per_class = env_int("RSK_SIDE_TIMERS", 0) != 0;
     static const char *const kNames[kNumSide] = {"car_side32", "car_side128", "car_side512",
                                                  "car_side2048", "car_side8192", "car_side65535"};
     for (int c = c1 - 1; c >= c0; --c) {
-        const int n = plan->side_end[c] - plan->side_beg[c];
-        if (n == 0) continue;
-        SideArgs a;
-        std::memset(&a, 0, sizeof(a));
-        a.items = plan->side_items.as<int>() + (size_t)plan->side_beg[c] * 4;
-        a.n_rows = n;
-        a.nchunk = (int)ceil_div(S, 64);
-        a.col = plan->pcol.as<int>();
-        a.assign = b.assign;
-        a.code = b.code;
-        a.cap = b.cap;
-        a.use = b.use;
-        a.zc_cnt = b.zcnt;
-        a.zc_key = b.zkey;
-        a.out_target = b.target;
-        a.out_score = b.score;
-        a.S = S;
-        a.N = N;
-        a.ablate = sablate;
+        if (c == skip || plan->side_end[c] == plan->side_beg[c]) continue;
+        const SideArgs a = side16_class_args(plan, c, b, S, N);
         const SideGeom g = side16_geometry(plan->side_dmax[c], N);
         ScopedTimer tm(ctx, per_class ? kNames[c] : "car_side", stream);
         RSK_TRY(launch_side16(stream, a, g, off32));
@@ -1252,17 +1257,12 @@ int launch_side16_classes(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, 
     return RSK_OK;
 }
 
-bool side16_has_big(const rsk_car_plan *plan) {
-    for (int c = kSideBig; c < kNumSide; ++c)
-        if (plan->side_end[c] > plan->side_beg[c]) return true;
-    return false;
-}
-
 // Side rows on `stream`: the compact path's classes below kSideBig (the rest
 // are launched beside the tiles by the caller); the wide path's mid (17..64,
 // N >= kPackMaxN variant only) and hub (> 64) rows, exact keys.
-int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, const SideBufs &b, int S, int N, bool compact) {
-    if (compact) return launch_side16_classes(plan, ctx, stream, b, S, N, 0, kSideBig);
+int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, const SideBufs &b, int S, int N, bool compact,
+                int skip = -1) {
+    if (compact) return launch_side16_classes(plan, ctx, stream, b, S, N, 0, kSideBig, skip);
     const int *d_assign = b.assign, *d_key = b.key, *d_zcnt = b.zcnt;
     const unsigned long long *d_zkey = b.zkey;
     int *d_target = b.target, *d_score = b.score;
@@ -1436,7 +1436,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     RSK_TRY(plan->zc.reserve((size_t)S * 12 + 16));
     unsigned long long *d_zkey = plan->zc.as<unsigned long long>();
     int *d_zcnt = reinterpret_cast<int *>(d_zkey + S);
-    RSK_HIP(hipMemsetAsync(plan->zc.ptr, 0, (size_t)S * 12 + 16, ctx->stream));  // + the capmax word
+    // zc_key[S] u64, zc_cnt[S], the capmax word: zeroed / written by launch_prep
 
     {   // K0: node state (codes and / or exact keys) + the zero case
         Prep16Args pa;
@@ -1453,16 +1453,6 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         ScopedTimer tm(ctx, "car_prep");
         RSK_TRY(launch_prep(ctx->stream, pa));
     }
-    // car_side16's few-row classes (rows above 128 neighbours) on a side stream
-    // beside the tiles: a handful of latency-bound workgroups per class that
-    // would otherwise run alone on the GPU (RSK_SIDE_BIG_AUX=0: on the main
-    // stream).  The other side rows run on the main stream before the tiles:
-    // sharing the CUs with the memory-bound tiles did not shorten the step
-    // (DESIGN.md §4).
-    static const bool big_aux = env_int("RSK_SIDE_BIG_AUX", 1) != 0;
-    const bool big_fork = compact && big_aux && plan->T > 0 && side16_has_big(plan);
-    const int nfork = big_fork ? 1 : 0;
-    if (nfork) RSK_TRY(aux_fork(ctx, nfork));
     SideBufs sb;
     sb.assign = d_assign;
     sb.key = d_key;
@@ -1473,11 +1463,62 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     sb.zkey = d_zkey;
     sb.target = d_target;
     sb.score = d_score;
-    if (compact)
-        RSK_TRY(launch_side16_classes(plan, ctx, big_fork ? ctx->aux[0] : ctx->stream, sb, S, N, kSideBig, kNumSide));
-    RSK_TRY(launch_side(plan, ctx, ctx->stream, sb, S, N, compact));
     static const int ablate = env_int("RSK_ABLATE_TILE", 0);
     static const int order = env_int("RSK_TILE_ORDER", 2);
+    static const int sl_max = [] { int v = env_int("RSK_TILE_SL", 64); return v >= 1 && v <= 64 ? v : 64; }();
+    // The compact side rows run inside the lean tile launch (car_fused16_kernel)
+    // where they fit its footprint: their latency-bound workgroups share the
+    // CUs with the memory-bound tiles instead of running alone (RSK_FUSE=0:
+    // launches of their own).
+    //   class 1 (33..128 neighbours): single-wave items interleaved with the tiles;
+    //   classes >= kSideBig (above 128): 4-wave teams at the front of the grid,
+    //     while the largest row's table fits the tile's LDS; otherwise on a side
+    //     stream beside the tiles (RSK_SIDE_BIG_AUX=0: on the main stream).
+    static const bool fuse_env = env_int("RSK_FUSE", 1) != 0;
+    const size_t lean_lds = tile16_lds_bytes(plan->rmax, 6, 0);
+    int fuse_c = -1, fside_blocks = 0;
+    SideArgs fsa, fba;
+    std::memset(&fsa, 0, sizeof(fsa));
+    std::memset(&fba, 0, sizeof(fba));
+    const bool fuse_ok = compact && fuse_env && plan->T_lean > 0 && S >= 64 && sl_max == 64 && order == 2;
+    if (fuse_ok && plan->side_end[1] > plan->side_beg[1]) {
+        const SideGeom g = side16_geometry(plan->side_dmax[1], N);
+        if (g.T == 1 && g.W == 4 && g.kB == 16 && 4 * g.lds_team <= lean_lds) {
+            fsa = side16_class_args(plan, 1, sb, S, N);
+            side16_apply_geometry(fsa, g);
+            fsa.xcd_per = 0;
+            fside_blocks = (int)ceil_div((int64_t)fsa.n_rows * fsa.nchunk, 4);
+            fuse_c = 1;
+        }
+    }
+    // the classes from kSideBig up to big_hi (exclusive) go into the fused grid
+    int big_hi = kSideBig;
+    if (fuse_ok)
+        for (int c = kSideBig; c < kNumSide; ++c) {
+            if (plan->side_end[c] == plan->side_beg[c]) continue;
+            const SideGeom g = side16_geometry(plan->side_dmax[c], N, 4);
+            if (g.kB != 16 || g.lds_team > lean_lds) break;
+            big_hi = c + 1;
+        }
+    const bool fuse_big = big_hi > kSideBig;
+    if (fuse_big) {  // rows [side_beg[big_hi - 1], side_end[kSideBig]): degree descending
+        int dmax = 0;
+        for (int c = kSideBig; c < big_hi; ++c) dmax = std::max(dmax, plan->side_dmax[c]);
+        fba = side16_class_args(plan, kSideBig, sb, S, N);
+        fba.items = plan->side_items.as<int>() + (size_t)plan->side_beg[big_hi - 1] * 4;
+        fba.n_rows = plan->side_end[kSideBig] - plan->side_beg[big_hi - 1];
+        side16_apply_geometry(fba, side16_geometry(dmax, N, 4));
+        fba.xcd_per = 0;
+    }
+    static const bool big_aux = env_int("RSK_SIDE_BIG_AUX", 1) != 0;
+    bool big_left = false;  // classes above the fused ones
+    for (int c = big_hi; c < kNumSide; ++c) big_left = big_left || plan->side_end[c] > plan->side_beg[c];
+    const bool big_fork = compact && big_left && big_aux && plan->T > 0;
+    const int nfork = big_fork ? 1 : 0;
+    if (nfork) RSK_TRY(aux_fork(ctx, nfork));
+    if (compact && big_left)
+        RSK_TRY(launch_side16_classes(plan, ctx, big_fork ? ctx->aux[0] : ctx->stream, sb, S, N, big_hi, kNumSide));
+    RSK_TRY(launch_side(plan, ctx, ctx->stream, sb, S, N, compact, fuse_c));
     const bool off32 = (int64_t)std::max(plan->P, plan->Q) * S * 4 < ((int64_t)1 << 32);
     if (plan->T > 0 && compact) {   // K1 tiles, 32-bit {code, node} cells
         Tile16Args a;
@@ -1501,7 +1542,6 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         a.n_pods = (unsigned)plan->n_img_pods;
         a.n_recs = (unsigned)plan->n_recs;
         a.n_key = (unsigned)NS;
-        static const int sl_max = [] { int v = env_int("RSK_TILE_SL", 64); return v >= 1 && v <= 64 ? v : 64; }();
         const int SL = std::min(next_pow2(S), next_pow2(sl_max));
         a.lsl = 0;
         while ((1 << a.lsl) < SL) ++a.lsl;
@@ -1527,11 +1567,10 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
             a.xcd_per = (int)ceil_div(units, 8);
             const int64_t blocks = order == 2 ? 8 * (int64_t)a.xcd_per : units;
             RSK_CHECK(blocks < INT32_MAX, "tile grid too large");
-            // RSK_TILE_LDS_PAD: extra LDS per lean workgroup (experiments: 7 lean
-            // workgroups per CU leave a slot to side rows on the aux stream)
-            static const size_t lean_pad = (size_t)std::max(0, env_int("RSK_TILE_LDS_PAD", 0));
-            RSK_TRY(launch_tile16(ts, a, d_score != nullptr, off32, part == 1, (unsigned)blocks,
-                                  lds + (part == 0 ? lean_pad : 0)));
+            if (part == 0 && (fuse_c >= 0 || fuse_big))
+                RSK_TRY(launch_fused16(ts, a, fsa, fside_blocks, fba, d_score != nullptr, off32, (unsigned)blocks, lds));
+            else
+                RSK_TRY(launch_tile16(ts, a, d_score != nullptr, off32, part == 1, (unsigned)blocks, lds));
         }
     } else if (plan->T > 0) {   // K1 tiles, wide {node, key} pairs
         TileArgs a;

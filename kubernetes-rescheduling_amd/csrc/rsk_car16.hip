@@ -22,7 +22,7 @@
 #include <climits>
 #include <cstdlib>
 
-#include "rsk_car.h"
+#include "rsk_side16.h"
 
 namespace rsk {
 
@@ -73,21 +73,26 @@ __device__ __forceinline__ ushort4 cvec_make(const unsigned (&k)[4]) {
 // ~node)) is reduced in LDS per workgroup first — threads of one workgroup
 // that share a scenario meet in one LDS slot — so a scenario receives one
 // global atomic per workgroup, not one per thread.
-// max(cap) once per execute, for the exact code window B = max(0, max(cap) - 32766):
-// 4096 nodes per workgroup, 16 clamped loads in flight per thread, a DPP max
-// per wave and one atomicMax per wave into *out (zeroed by the caller; a
-// negative max reads as 0, which gives the same B)
-constexpr int kCapMaxPer = 4096;
-__global__ __launch_bounds__(256) void car_capmax_kernel(const int *__restrict__ cap, int N, int *__restrict__ out) {
-    const int base = (int)blockIdx.x * kCapMaxPer + (int)threadIdx.x;
-    int v[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) v[u] = cap[min(base + u * 256, N - 1)];
+// Ahead of the prep kernel, one workgroup: zero the zero-case words
+// (zc_key[S] u64, zc_cnt[S]) and, for the codes, max(cap) once per execute —
+// the exact code window B = max(0, max(cap) - 32766) — into *capmax (a
+// negative max reads as 0, which gives the same B).
+constexpr int kPrep0Threads = 1024;
+__global__ __launch_bounds__(kPrep0Threads) void car_prep0_kernel(const int *__restrict__ cap, int N,
+                                                                 unsigned *__restrict__ zc, int zc_words,
+                                                                 int *__restrict__ capmax) {
+    __shared__ int red[kPrep0Threads / 64];
+    for (int i = (int)threadIdx.x; i < zc_words; i += kPrep0Threads) zc[i] = 0u;
+    if (!capmax) return;
     int mc = 0;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) mc = max(mc, v[u]);
+    for (int n = (int)threadIdx.x; n < N; n += kPrep0Threads) mc = max(mc, cap[n]);
     mc = dpp_max(mc);
-    if ((threadIdx.x & 63) == 0) atomicMax(out, mc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kPrep0Threads / 64; ++w) mc = max(mc, red[w]);
+        *capmax = mc;
+    }
 }
 
 template <int V, bool kCode, bool kKey>
@@ -180,10 +185,9 @@ static int prep_launch(hipStream_t stream, const Prep16Args &a, int SV, int npb,
 int launch_prep(hipStream_t stream, const Prep16Args &a) {
     RSK_CHECK(a.code || a.nodekey, "prep: nothing to write");
     RSK_CHECK(!a.code || a.capmax, "prep: codes need the capmax scratch");
-    if (a.code) {
-        car_capmax_kernel<<<(unsigned)ceil_div(a.N, kCapMaxPer), 256, 0, stream>>>(a.cap, a.N, a.capmax);
-        RSK_HIP(hipGetLastError());
-    }
+    car_prep0_kernel<<<1, kPrep0Threads, 0, stream>>>(a.cap, a.N, reinterpret_cast<unsigned *>(a.zc_key), 3 * a.S,
+                                                      a.code ? a.capmax : nullptr);
+    RSK_HIP(hipGetLastError());
     // 4 scenarios per thread when S % 4 == 0 (16-B use / key words, 8-B codes)
     const bool v4 = a.S % 4 == 0 && ((uintptr_t)a.use % 16) == 0 && ((uintptr_t)a.haz % 4) == 0;
     const int SV = v4 ? a.S / 4 : a.S;
@@ -907,16 +911,17 @@ __device__ __forceinline__ void w64_score(const Tile16Args &a, const W64 &w, cin
     w64_score_light<kScore, kOff32>(a, w, m, R, wave, s0);
 }
 
+// One tile workgroup; bid plays blockIdx.x (the fused kernel below maps its
+// own blocks onto tile blocks and side blocks).
 template <bool kScore, bool kOff32, bool kL64, bool kHeavy>
-__global__ __launch_bounds__(kTileThreads, (kHeavy || !kL64) ? RSK_TILE16_WGS_HEAVY : RSK_TILE16_WGS) void car_tile16_kernel(
-    Tile16Args a) {
+__device__ __forceinline__ void tile16_block(const Tile16Args &a, unsigned bid) {
     extern __shared__ __attribute__((aligned(16))) int lds[];  // img cells [rmax][SL] (+ records, unit counter: !kL64)
     const int lsl = kL64 ? 6 : a.lsl;
     const int SL = 1 << lsl;
     const int nchunk = (a.S + SL - 1) >> lsl;
-    int unit = blockIdx.x;
+    int unit = (int)bid;
     if (a.order == 2) {  // XCD-contiguous: blocks b and b + 8 share an XCD
-        unit = (int)(blockIdx.x & 7u) * a.xcd_per + (int)(blockIdx.x >> 3);
+        unit = (int)(bid & 7u) * a.xcd_per + (int)(bid >> 3);
         if (unit >= nchunk * a.T) return;  // whole workgroup, before any barrier
     }
     const int tile = a.tile0 + (a.order == 1 ? unit / nchunk : unit % a.T);
@@ -999,6 +1004,39 @@ __global__ __launch_bounds__(kTileThreads, (kHeavy || !kL64) ? RSK_TILE16_WGS_HE
     }
 }
 
+template <bool kScore, bool kOff32, bool kL64, bool kHeavy>
+__global__ __launch_bounds__(kTileThreads, (kHeavy || !kL64) ? RSK_TILE16_WGS_HEAVY : RSK_TILE16_WGS) void car_tile16_kernel(
+    Tile16Args a) {
+    tile16_block<kScore, kOff32, kL64, kHeavy>(a, blockIdx.x);
+}
+
+// Lean tiles and side rows (rsk_side16.h) in one grid, so the latency- and
+// VALU-bound side work shares each CU with the memory-bound tile workgroups
+// instead of running alone before them:
+//   blocks [0, big_blocks)  one 4-wave side team each (the rows above 128
+//                           neighbours): dispatched first, they run the
+//                           longest;
+//   then rows of 8 blocks (one block per XCD): every R-th row, until they run
+//   out, 4 single-wave side items (33..128 neighbours), the rest tiles.
+// Every side workgroup fits the tile's footprint (4 waves, <= 64 VGPRs, its
+// LDS within the tile's).
+template <bool kScore, bool kOff32>
+__global__ __launch_bounds__(kTileThreads, RSK_TILE16_WGS) void car_fused16_kernel(Tile16Args ta, SideArgs sa,
+                                                                                  SideArgs ba, FuseMap f) {
+    if (blockIdx.x < (unsigned)f.big_blocks) {
+        side16_block<4, 4, 16, kOff32, false>(ba, (int)blockIdx.x);
+        return;
+    }
+    const unsigned v = blockIdx.x - (unsigned)f.big_blocks, row = v >> 3, x = v & 7u;
+    const unsigned k = row / (unsigned)f.R;
+    if (row - k * (unsigned)f.R == (unsigned)f.R - 1u && k < (unsigned)f.side_rows) {
+        side16_block<4, 1, 16, kOff32, false>(sa, (int)(k * 8u + x));
+        return;
+    }
+    const unsigned ns = min((unsigned)f.side_rows, (row + 1u) / (unsigned)f.R);  // side rows before this one
+    tile16_block<kScore, kOff32, true, false>(ta, ((row - ns) << 3) | x);
+}
+
 int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off32, bool heavy, unsigned blocks,
                   size_t lds) {
     using K = void (*)(Tile16Args);
@@ -1021,6 +1059,32 @@ int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off3
         RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds));
     kern<<<dim3(blocks), dim3(kTileThreads), lds, stream>>>(a);
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
+}
+
+int launch_fused16(hipStream_t stream, const Tile16Args &a, const SideArgs &sa, int side_blocks, const SideArgs &ba,
+                   bool score, bool off32, unsigned tile_blocks, size_t lds) {
+    RSK_CHECK(a.lsl == 6 && (size_t)a.img_cells * 4 <= (size_t)kT16Rows * 256 && tile_blocks % 8 == 0,
+              "fused launch needs 64-scenario tiles");
+    static const int spread = [] { const char *e = getenv("RSK_FUSE_SPREAD"); return e ? std::max(1, atoi(e)) : 2; }();
+    FuseMap f;
+    f.big_blocks = (int)(8 * ceil_div((int64_t)ba.n_rows * ba.nchunk, 8));
+    f.side_rows = (int)ceil_div(side_blocks, 8);
+    const int tile_rows = (int)(tile_blocks / 8);
+    // side rows every R rows, spread over the first 1 / spread of the grid
+    f.R = std::max(2, tile_rows / std::max(1, f.side_rows * spread));
+    const int64_t blocks = (int64_t)f.big_blocks + tile_blocks + 8LL * f.side_rows;
+    RSK_CHECK(blocks < INT32_MAX, "fused grid too large");
+    using K = void (*)(Tile16Args, SideArgs, SideArgs, FuseMap);
+    static const K kerns[4] = {&car_fused16_kernel<false, false>, &car_fused16_kernel<false, true>,
+                               &car_fused16_kernel<true, false>, &car_fused16_kernel<true, true>};
+    const K kern = kerns[(score ? 2 : 0) + (off32 ? 1 : 0)];
+    RSK_CHECK(lds <= 160 * 1024, "fused tile needs %zu B of LDS", lds);
+    if (lds > 64 * 1024)
+        RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds));
+    kern<<<dim3((unsigned)blocks), dim3(kTileThreads), lds, stream>>>(a, sa, ba, f);
     RSK_HIP(hipGetLastError());
     return RSK_OK;
 }

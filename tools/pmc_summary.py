@@ -31,8 +31,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 # kernel symbol -> the timer name bench.py reports (librsk ScopedTimer names)
-BENCH_NAME = {"car_tile16": "car_tile", "car_hub": "car_heavy", "car_hub16": "car_heavy", "car_mid16": "car_mid",
-              "car_pivot": "car_side"}
+BENCH_NAME = {"car_tile16": "car_tile", "car_fused16": "car_tile", "car_hub": "car_heavy", "car_side16": "car_side"}
 # bench timers that bracket several launches of one step (car_tile: the lean and
 # the heavy tile launch, two grid sizes of car_tile16): their per-"launch"
 # traffic is the sum over the grids, not the mean
