@@ -166,6 +166,11 @@ def _coll_tensor(t):
     return t, False
 
 
+def _multi_rank() -> bool:
+    import torch.distributed as dist
+    return dist.is_initialized() and dist.get_world_size() > 1
+
+
 def allreduce_(t, op="sum", group=None):
     """In-place all-reduce of t (SUM or MAX) on whatever device the backend
     needs; a no-op without a process group (one rank)."""
@@ -404,9 +409,12 @@ class RowShardedRounds:
             if trace:
                 print(f"[rank {self.shard.rank}] round {rnd}", file=sys.stderr, flush=True)
             c = time.perf_counter()
-            cpu, mem = lp_cpu.clone(), lp_mem.clone()
-            allreduce_(cpu, "sum", self.group)
-            allreduce_(mem, "sum", self.group)
+            if _multi_rank():   # the monitor's exchange: every rank's CPU / mem partials summed
+                cpu, mem = lp_cpu.clone(), lp_mem.clone()
+                allreduce_(cpu, "sum", self.group)
+                allreduce_(mem, "sum", self.group)
+            else:               # one rank: its partials are the totals (no copies)
+                cpu = lp_cpu
             use = (base + cpu).to(torch.int32)
             c = tick("monitor", c)
             haz, most = self.be.detect(use, cap, N, S, threshold)
@@ -430,7 +438,8 @@ class RowShardedRounds:
             mine = (evict >= r0) & (evict < r1)
             tgt_local = self.be.place(assign, S, cap, use, haz, N, torch.where(mine, evict, torch.full_like(evict, -1)))
             c = tick("place", c)
-            target = allgather(tgt_local, self.group).max(dim=0).values   # changed slices of every rank
+            # the changed slices of every rank (one rank: its own)
+            target = allgather(tgt_local, self.group).max(dim=0).values if _multi_rank() else tgt_local
             c = tick("exchange", c)
             if glue:  # one librsk launch
                 target = target.contiguous()
