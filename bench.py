@@ -4,7 +4,7 @@
 Workload (BASELINE.json configs[2]): 100k pods, 5k
 nodes, preferential-attachment relation tree, S = 4096 what-if scenarios per
 GPU.  One step = one pass of the hot path over one batch: librsk's CAR pipeline
-(car_prep + car_light + car_heavy) scores every pod in every scenario against
+(car_prep, the lean tiles fused with the side rows, the heavy tiles) scores every pod in every scenario against
 every node — P·N·S evaluations — with all inputs resident in HBM.
 
 Multi-GPU (``torchrun --nproc-per-node N``): scenario sharding, rank r scores
@@ -120,17 +120,19 @@ def algorithmic_bytes(P, N, S, nnz, Q_light=None, light_rec_bytes=0):
 
 
 def alg_bytes(kernel, P, N, S, info):
-    """Algorithmic bytes per step of one kernel (DESIGN.md "Roofline accounting"):
-      car_tile : the assign slice of every distinct pod in the tile images once (4·S per pod)
-                 + target of its rows (4·S) + the tile plan (image lists, records)
-      car_side : target of each side row (4·S) + side items / neighbour lists (neighbour slices
-                 are re-reads of pods the tiles stage: not counted)
-      car_mid  : target of each mid row (4·S) + records (earlier kernels, RSK_SIDE_OLD=1)
-      car_heavy: target of each hub row (4·S) + hub items / CSR (earlier kernels)
+    """Algorithmic bytes per step of one kernel timer (DESIGN.md "Roofline accounting"):
+      car_tile : the lean launch (tiles + the side rows fused into it) and the heavy tile launch:
+                 the assign slice of every distinct neighbour pod of those rows once (4·S per pod)
+                 + every row's target (4·S) + the tile plan and side items
+      car_side : target of each side row launched on its own (4·S) + side items / neighbour lists
+                 (its neighbours' slices: re-reads of pods the tiles stage, not counted)
       car_prep : use + hazard (5·N·S) + cap (4·N) read, the 16-bit code (2·N·S) written
     """
-    return {"car_tile": 4 * S * info["image_pods_distinct"] + 4 * S * info["tile_rows"] + info["tile_bytes"],
-            "car_side": 4 * S * info.get("side_rows", 0) + info.get("side_bytes", 0),
+    fused = info.get("fused_side_rows", 0)
+    nb = info.get("fused_nb_pods_distinct", info["image_pods_distinct"])
+    return {"car_tile": 4 * S * nb + 4 * S * (info["tile_rows"] + fused) + info["tile_bytes"]
+                        + (info.get("side_bytes", 0) if fused else 0),
+            "car_side": 4 * S * (info.get("side_rows", 0) - fused) + info.get("side_bytes", 0),
             "car_mid": 4 * S * info["mid_rows"] + info["mid_bytes"],
             "car_heavy": 4 * S * info["heavy_rows"] + info["heavy_bytes"],
             "car_prep": 7 * N * S + 4 * N}.get(kernel, 0)
@@ -456,7 +458,7 @@ def main():
     step_ach = B / (ms_step / 1e3) / 1e9
     roof_step = {"bound": "hbm", "achieved": round(step_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                  "frac": round(step_ach / HBM_PEAK_GBS, 4), "algorithmic_bytes": B,
-                 "note": "whole CAR step (prep+light+heavy launches, wall clock) vs SURVEY §8d B"}
+                 "note": "whole CAR step (every launch of one execute, wall clock) vs SURVEY §8d B"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

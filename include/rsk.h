@@ -93,7 +93,12 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
  * out[7] tile plan bytes   out[8] (unused, 0)   out[9] mid record bytes
  * out[10] hub item + CSR bytes   out[11] max row degree
  * out[12] image rows over all tiles   out[13] distinct pods in the images
- * out[14] rows on the sorted tile class (17..32).
+ * out[14] rows on the sorted tile class (17..32)   out[15] side rows (> 32)
+ * out[16] side item + neighbour bytes   out[17] light_max (tile degree bound)
+ * out[18] rows in lean tiles   out[19] lean tiles
+ * out[20] side rows the last execute ran inside the lean tile launch
+ * out[21] distinct neighbour pods of the tile rows and those side rows
+ * out[22] distinct neighbour pods of every row.
  * Returns the number of fields written (<= n).                             */
 int rsk_car_plan_info(const rsk_car_plan *plan, int64_t *out, int n);
 /* One-shot convenience: plan_create + execute + destroy. */

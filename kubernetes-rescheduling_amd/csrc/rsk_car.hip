@@ -765,6 +765,12 @@ struct rsk_car_plan {
     // compact path: every side row (deg > light_max) for car_side16, degree
     // descending, split into the kSideMax classes (neighbours in pcol)
     DevBuf side_items, pcol;
+    // distinct neighbour pods of the tile rows plus the side classes [1, hi)
+    // (nb_distinct[hi], hi = 1..kNumSide): the algorithmic assign bytes of the
+    // fused launch; fused_lo / fused_hi: the side classes the last execute ran
+    // inside the lean tile launch ([lo, hi), empty when lo == hi)
+    int64_t nb_distinct[kNumSide + 1] = {};
+    int fused_lo = 1, fused_hi = 1;
     int side_beg[kNumSide] = {}, side_end[kNumSide] = {};
     int side_dmax[kNumSide] = {};
     // per-execute workspace
@@ -1162,6 +1168,21 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
             plan->side_dmax[c] = b < end ? all[b].d : 0;
             end = b;
         }
+        {   // cumulative distinct neighbour pods: the images, then side classes 1, 2, ...
+            std::vector<char> seen(P, 0);
+            int64_t n = 0;
+            for (int q : tb.img_pods) n += !seen[q], seen[q] = 1;
+            plan->nb_distinct[1] = n;
+            for (int c = 1; c < kNumSide; ++c) {
+                for (int k = plan->side_beg[c]; k < plan->side_end[c]; ++k)
+                    for (int j = 0; j < all[k].d; ++j) {
+                        const int q = pcol[all[k].rb + j];
+                        n += !seen[q], seen[q] = 1;
+                    }
+                plan->nb_distinct[c + 1] = n;
+            }
+            plan->nb_distinct[0] = plan->nb_distinct[1];
+        }
         std::vector<int32_t> flat;
         flat.reserve(all.size() * 4);
         for (const HeavyItem &h : all) flat.insert(flat.end(), {h.oi, h.rb, h.d, 0});
@@ -1369,11 +1390,16 @@ int rsk_car_plan_info(const rsk_car_plan *plan, int64_t *out, int n) {
     const int64_t tile_bytes = plan->T > 0 ? (int64_t)(plan->img_pods.bytes + plan->meta.bytes + plan->recs.bytes) : 0;
     const int64_t side = plan->side_end[0] - plan->side_beg[kNumSide - 1];
     const int64_t side_bytes = (int64_t)plan->side_items.bytes + (int64_t)plan->pcol.bytes;
-    const int64_t v[20] = {plan->n_tile_rows, 0, mid, heavy, plan->T, plan->rmax, plan->owners_cap,
+    int64_t fused_rows = 0;
+    for (int c = plan->fused_lo; c < plan->fused_hi; ++c) fused_rows += plan->side_end[c] - plan->side_beg[c];
+    // the tile rows' and the fused side rows' distinct neighbour pods (classes [1, hi) counted when lo == 1)
+    const int64_t fused_nb = plan->fused_lo == 1 ? plan->nb_distinct[plan->fused_hi] : plan->nb_distinct[1];
+    const int64_t v[23] = {plan->n_tile_rows, 0, mid, heavy, plan->T, plan->rmax, plan->owners_cap,
                            tile_bytes, 0, mid_bytes, heavy_bytes, plan->max_deg, plan->img_rows_total,
                            plan->img_pods_distinct, plan->n_sorted_rows, side, side_bytes, plan->light_max,
-                           plan->n_lean_rows, plan->T_lean};
-    const int m = n < 20 ? n : 20;
+                           plan->n_lean_rows, plan->T_lean, fused_rows, fused_nb,
+                           plan->nb_distinct[kNumSide]};
+    const int m = n < 23 ? n : 23;
     for (int i = 0; i < m; ++i) out[i] = v[i];
     return m;
 }
@@ -1511,6 +1537,9 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         fba.xcd_per = 0;
     }
     static const bool big_aux = env_int("RSK_SIDE_BIG_AUX", 1) != 0;
+    plan->fused_lo = fuse_c >= 0 || plan->side_end[1] == plan->side_beg[1] ? 1 : kSideBig;
+    plan->fused_hi = std::max(big_hi, fuse_c >= 0 ? 2 : 1);
+    if (!fuse_ok || (fuse_c < 0 && !fuse_big)) plan->fused_lo = plan->fused_hi = 1;
     bool big_left = false;  // classes above the fused ones
     for (int c = big_hi; c < kNumSide; ++c) big_left = big_left || plan->side_end[c] > plan->side_beg[c];
     const bool big_fork = compact && big_left && big_aux && plan->T > 0;

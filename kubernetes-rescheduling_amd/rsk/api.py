@@ -48,7 +48,8 @@ class CarPlan:
     INFO_FIELDS = ("tile_rows", "direct_rows", "mid_rows", "heavy_rows", "tiles", "tile_image_rows",
                    "tile_pods", "tile_bytes", "direct_bytes", "mid_bytes", "heavy_bytes", "max_degree",
                    "image_rows_total", "image_pods_distinct", "sorted_rows", "side_rows", "side_bytes",
-                   "light_max", "tile_rows_lean", "tiles_lean")
+                   "light_max", "tile_rows_lean", "tiles_lean", "fused_side_rows", "fused_nb_pods_distinct",
+                   "nb_pods_distinct")
 
     def info(self) -> dict:
         """How the plan routed its rows (rsk_car_plan_info)."""
