@@ -320,7 +320,8 @@ SideGeom side16_geometry(int dmax, int N, int T = 0);  // T: waves per item (0: 
 void side16_apply_geometry(SideArgs &a, const SideGeom &g);  // the geometry's LDS layout into the launch arguments
 struct FuseMap {
     int big_blocks;    // the first big_blocks blocks: 4-wave side teams (ba), a multiple of 8
-    int R, side_rows;  // then every R-th row of 8 blocks is a single-wave side row (sa), side_rows of them
+    int R, k1;         // then k1 periods of R rows of 8 blocks: R - 1 tile rows, one single-wave side row (sa)
+    int side_rows, tile_rows;  // then the tile rows left, then the side rows left
 };
 // lean tiles + single-wave side items of one class (4 per workgroup, kB 16) +
 // optionally 4-wave side teams (kB 16) in one grid; ba.n_rows == 0: no teams

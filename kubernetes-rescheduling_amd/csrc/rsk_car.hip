@@ -765,12 +765,12 @@ struct rsk_car_plan {
     // compact path: every side row (deg > light_max) for car_side16, degree
     // descending, split into the kSideMax classes (neighbours in pcol)
     DevBuf side_items, pcol;
-    // distinct neighbour pods of the tile rows plus the side classes [1, hi)
-    // (nb_distinct[hi], hi = 1..kNumSide): the algorithmic assign bytes of the
-    // fused launch; fused_lo / fused_hi: the side classes the last execute ran
-    // inside the lean tile launch ([lo, hi), empty when lo == hi)
+    // distinct neighbour pods of the tile rows plus the side classes [0, hi)
+    // (nb_distinct[hi]; [0]: the tile rows alone): the algorithmic assign
+    // bytes of the fused launch; fused_lo / fused_hi: the side classes the last
+    // execute ran inside the lean tile launch ([lo, hi), empty when lo == hi)
     int64_t nb_distinct[kNumSide + 1] = {};
-    int fused_lo = 1, fused_hi = 1;
+    int fused_lo = 0, fused_hi = 0;
     int side_beg[kNumSide] = {}, side_end[kNumSide] = {};
     int side_dmax[kNumSide] = {};
     // per-execute workspace
@@ -1168,12 +1168,12 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
             plan->side_dmax[c] = b < end ? all[b].d : 0;
             end = b;
         }
-        {   // cumulative distinct neighbour pods: the images, then side classes 1, 2, ...
+        {   // cumulative distinct neighbour pods: the images, then side classes 0, 1, ...
             std::vector<char> seen(P, 0);
             int64_t n = 0;
             for (int q : tb.img_pods) n += !seen[q], seen[q] = 1;
-            plan->nb_distinct[1] = n;
-            for (int c = 1; c < kNumSide; ++c) {
+            plan->nb_distinct[0] = n;
+            for (int c = 0; c < kNumSide; ++c) {
                 for (int k = plan->side_beg[c]; k < plan->side_end[c]; ++k)
                     for (int j = 0; j < all[k].d; ++j) {
                         const int q = pcol[all[k].rb + j];
@@ -1181,7 +1181,6 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
                     }
                 plan->nb_distinct[c + 1] = n;
             }
-            plan->nb_distinct[0] = plan->nb_distinct[1];
         }
         std::vector<int32_t> flat;
         flat.reserve(all.size() * 4);
@@ -1261,7 +1260,7 @@ SideArgs side16_class_args(const rsk_car_plan *plan, int c, const SideBufs &b, i
     return a;
 }
 
-// classes [c0, c1) except `skip` (the class fused into the tile launch)
+// classes [c0, c1) except `skip` (fused into the tile launch)
 int launch_side16_classes(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, const SideBufs &b, int S, int N,
                           int c0, int c1, int skip = -1) {
     const bool off32 = (int64_t)std::max(plan->P, plan->Q) * S * 4 < ((int64_t)1 << 32);
@@ -1392,8 +1391,8 @@ int rsk_car_plan_info(const rsk_car_plan *plan, int64_t *out, int n) {
     const int64_t side_bytes = (int64_t)plan->side_items.bytes + (int64_t)plan->pcol.bytes;
     int64_t fused_rows = 0;
     for (int c = plan->fused_lo; c < plan->fused_hi; ++c) fused_rows += plan->side_end[c] - plan->side_beg[c];
-    // the tile rows' and the fused side rows' distinct neighbour pods (classes [1, hi) counted when lo == 1)
-    const int64_t fused_nb = plan->fused_lo == 1 ? plan->nb_distinct[plan->fused_hi] : plan->nb_distinct[1];
+    // the tile rows' and the fused side rows' distinct neighbour pods (classes [0, hi) counted when lo == 0)
+    const int64_t fused_nb = plan->fused_lo == 0 ? plan->nb_distinct[plan->fused_hi] : plan->nb_distinct[0];
     const int64_t v[23] = {plan->n_tile_rows, 0, mid, heavy, plan->T, plan->rmax, plan->owners_cap,
                            tile_bytes, 0, mid_bytes, heavy_bytes, plan->max_deg, plan->img_rows_total,
                            plan->img_pods_distinct, plan->n_sorted_rows, side, side_bytes, plan->light_max,
@@ -1537,9 +1536,11 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         fba.xcd_per = 0;
     }
     static const bool big_aux = env_int("RSK_SIDE_BIG_AUX", 1) != 0;
-    plan->fused_lo = fuse_c >= 0 || plan->side_end[1] == plan->side_beg[1] ? 1 : kSideBig;
+    // fused classes [lo, hi): class 0 (17..32, RSK_LIGHT_MAX=16 plans only) runs on its own
+    const bool c0 = plan->side_end[0] > plan->side_beg[0];
+    plan->fused_lo = c0 ? kNumSide : (fuse_c >= 0 || plan->side_end[1] == plan->side_beg[1] ? 0 : kSideBig);
     plan->fused_hi = std::max(big_hi, fuse_c >= 0 ? 2 : 1);
-    if (!fuse_ok || (fuse_c < 0 && !fuse_big)) plan->fused_lo = plan->fused_hi = 1;
+    if (!fuse_ok || (fuse_c < 0 && !fuse_big) || plan->fused_lo == kNumSide) plan->fused_lo = plan->fused_hi = 0;
     bool big_left = false;  // classes above the fused ones
     for (int c = big_hi; c < kNumSide; ++c) big_left = big_left || plan->side_end[c] > plan->side_beg[c];
     const bool big_fork = compact && big_left && big_aux && plan->T > 0;

@@ -1016,8 +1016,11 @@ __global__ __launch_bounds__(kTileThreads, (kHeavy || !kL64) ? RSK_TILE16_WGS_HE
 //   blocks [0, big_blocks)  one 4-wave side team each (the rows above 128
 //                           neighbours): dispatched first, they run the
 //                           longest;
-//   then rows of 8 blocks (one block per XCD): every R-th row, until they run
-//   out, 4 single-wave side items (33..128 neighbours), the rest tiles.
+//   then rows of 8 blocks (one block per XCD): in the first K1 periods of R
+//   rows, the last row holds 4 single-wave side items per block (33..128
+//   neighbours) and the other R - 1 are tile rows; then the remaining tile
+//   rows; then the remaining side rows (when side rows outnumber the tile
+//   rows the periods can hold).
 // Every side workgroup fits the tile's footprint (4 waves, <= 64 VGPRs, its
 // LDS within the tile's).
 template <bool kScore, bool kOff32>
@@ -1028,13 +1031,22 @@ __global__ __launch_bounds__(kTileThreads, RSK_TILE16_WGS) void car_fused16_kern
         return;
     }
     const unsigned v = blockIdx.x - (unsigned)f.big_blocks, row = v >> 3, x = v & 7u;
-    const unsigned k = row / (unsigned)f.R;
-    if (row - k * (unsigned)f.R == (unsigned)f.R - 1u && k < (unsigned)f.side_rows) {
-        side16_block<4, 1, 16, kOff32, false>(sa, (int)(k * 8u + x));
+    const unsigned R = (unsigned)f.R, K1 = (unsigned)f.k1, P1 = K1 * R;
+    unsigned side = 0xffffffffu, tile;
+    if (row < P1) {
+        const unsigned k = row / R, m = row - k * R;
+        if (m == R - 1u) side = k;
+        tile = k * (R - 1u) + m;
+    } else {
+        const unsigned t_rem = (unsigned)f.tile_rows - K1 * (R - 1u);
+        tile = K1 * (R - 1u) + (row - P1);
+        if (row - P1 >= t_rem) side = K1 + (row - P1 - t_rem);
+    }
+    if (side != 0xffffffffu) {
+        side16_block<4, 1, 16, kOff32, false>(sa, (int)(side * 8u + x));
         return;
     }
-    const unsigned ns = min((unsigned)f.side_rows, (row + 1u) / (unsigned)f.R);  // side rows before this one
-    tile16_block<kScore, kOff32, true, false>(ta, ((row - ns) << 3) | x);
+    tile16_block<kScore, kOff32, true, false>(ta, (tile << 3) | x);
 }
 
 int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off32, bool heavy, unsigned blocks,
@@ -1071,9 +1083,11 @@ int launch_fused16(hipStream_t stream, const Tile16Args &a, const SideArgs &sa, 
     FuseMap f;
     f.big_blocks = (int)(8 * ceil_div((int64_t)ba.n_rows * ba.nchunk, 8));
     f.side_rows = (int)ceil_div(side_blocks, 8);
-    const int tile_rows = (int)(tile_blocks / 8);
-    // side rows every R rows, spread over the first 1 / spread of the grid
-    f.R = std::max(2, tile_rows / std::max(1, f.side_rows * spread));
+    f.tile_rows = (int)(tile_blocks / 8);
+    // one side row every R rows over the first 1 / spread of the tile rows; the
+    // side rows the periods cannot hold go after the tiles
+    f.R = std::max(2, f.tile_rows / std::max(1, f.side_rows * spread));
+    f.k1 = std::min(f.side_rows, f.tile_rows / (f.R - 1));
     const int64_t blocks = (int64_t)f.big_blocks + tile_blocks + 8LL * f.side_rows;
     RSK_CHECK(blocks < INT32_MAX, "fused grid too large");
     using K = void (*)(Tile16Args, SideArgs, SideArgs, FuseMap);

@@ -67,7 +67,8 @@ SideGeom side16_geometry(int dmax, int N, int T) {
     // neighbour loads in flight per wave (with their code gathers: 2 kB VGPRs;
     // 4-wave teams live in the fused tile launch: <= 64 VGPRs; 16-wave teams:
     // <= 128)
-    g.kB = dmax <= 32 ? 8 : (g.T == 8 ? 32 : 16);
+    static const bool kb16 = getenv("RSK_SIDE_KB16") && atoi(getenv("RSK_SIDE_KB16")) != 0;  // debug
+    g.kB = dmax <= 32 && !kb16 ? 8 : (g.T == 8 ? 32 : 16);
     // words: tab H | dl 64 K (also the recount's cells) | ndl 64 | dummy 64 |
     // h2 1 + h2cap (the entries counted >= 2: at most min(Dc, dmax / 2); a
     // longer list sends the item to the exact recount; teams: bx 192 T after

@@ -471,6 +471,29 @@ def test_car_row_largest_tables(ctx, P, N, deg, S):
                label=f"deg {deg} N {N} S={S}")
 
 
+@pytest.mark.parametrize("S", [64, 200])
+def test_car_fused_side_rows_outnumber_tiles(ctx, S):
+    """The fused tile + side launch when the side rows (33..128 and above)
+    outnumber what the tile periods hold: 2,600 rows of degree 33..300 against
+    ~400 tile rows (the side rows left over run after the tiles)."""
+    rng = np.random.default_rng(1300 + S)
+    P, N = 3000, 400
+    deg = np.where(rng.random(P) < 0.86, rng.integers(33, 130, P), rng.integers(0, 5, P))
+    deg[:20] = rng.integers(129, 300, 20)
+    rows = [rng.integers(0, P, int(d)).tolist() for d in deg]
+    rp = np.zeros(P + 1, np.int32)
+    rp[1:] = np.cumsum([len(r) for r in rows])
+    ci = np.array([q for r in rows for q in r], np.int32)
+    base = rng.integers(0, N, P)
+    a = np.repeat(base[:, None], S, axis=1).astype(np.int32)
+    flip = rng.random((P, S)) < 0.02
+    a[flip] = rng.integers(-1, N, flip.sum())
+    cap = rng.choice([4000, 8000], N).astype(np.int32)
+    use = rng.integers(0, 8000, N * S).astype(np.int32)
+    haz = (rng.random(N * S) < 0.15).astype(np.uint8)
+    _check_car(ctx, rp, ci, a.reshape(-1), S, cap, use, haz, N, label=f"side rows > tiles S={S}")
+
+
 def test_dropin_communication_5000_related_above_row_max_n(ctx):
     """The drop-in's `communication` with N > 32768 nodes goes through
     car_place; a deployment related to 5000 others gets the
