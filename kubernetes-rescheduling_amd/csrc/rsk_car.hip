@@ -1543,7 +1543,8 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     if (!fuse_ok || (fuse_c < 0 && !fuse_big) || plan->fused_lo == kNumSide) plan->fused_lo = plan->fused_hi = 0;
     bool big_left = false;  // classes above the fused ones
     for (int c = big_hi; c < kNumSide; ++c) big_left = big_left || plan->side_end[c] > plan->side_beg[c];
-    const bool big_fork = compact && big_left && big_aux && plan->T > 0;
+    // (S < 64: the tiles are short, the fork's events would cost more than the overlap)
+    const bool big_fork = compact && big_left && big_aux && plan->T > 0 && S >= 64;
     const int nfork = big_fork ? 1 : 0;
     if (nfork) RSK_TRY(aux_fork(ctx, nfork));
     if (compact && big_left)
@@ -1585,8 +1586,10 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         static const bool split = env_int("RSK_TILE_TIMERS", 0) != 0;
         std::unique_ptr<ScopedTimer> tm(split ? nullptr : new ScopedTimer(ctx, "car_tile"));
         // lean tiles [0, T_lean) at full occupancy, then the heavy tiles (17..32 rows)
+        // S < 64: one generic kernel scores every tile (no lean / heavy split)
+        const int t_split = a.lsl == 6 ? plan->T_lean : plan->T;
         for (int part = 0; part < 2; ++part) {
-            const int t0 = part ? plan->T_lean : 0, nt = part ? plan->T - plan->T_lean : plan->T_lean;
+            const int t0 = part ? t_split : 0, nt = part ? plan->T - t_split : t_split;
             if (nt <= 0) continue;
             const hipStream_t ts = ctx->stream;
             std::unique_ptr<ScopedTimer> tp(split ? new ScopedTimer(ctx, part ? "car_tile_heavy" : "car_tile", ts)

@@ -14,6 +14,8 @@ step() {  # step <name> <seconds> <cmd...>
     [ $rc -ne 0 ] && { tail -15 "$out/$name.log"; exit $rc; }
     return 0
 }
+step pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread
+step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
 step bench_headline 600 python -u bench.py
 step bench_2k64 300 python -u bench.py --config 2k64 --no-cpu-baseline
 step bench_1m50k 600 python -u bench.py --config 1m50k --no-cpu-baseline
