@@ -1023,11 +1023,12 @@ __global__ __launch_bounds__(kTileThreads, (kHeavy || !kL64) ? RSK_TILE16_WGS_HE
 //   rows the periods can hold).
 // Every side workgroup fits the tile's footprint (4 waves, <= 64 VGPRs, its
 // LDS within the tile's).
-template <bool kScore, bool kOff32>
+// kPipe: the side items' next assign rows in flight while a batch is scored
+template <bool kScore, bool kOff32, bool kPipe>
 __global__ __launch_bounds__(kTileThreads, RSK_TILE16_WGS) void car_fused16_kernel(Tile16Args ta, SideArgs sa,
                                                                                   SideArgs ba, FuseMap f) {
     if (blockIdx.x < (unsigned)f.big_blocks) {
-        side16_block<4, 4, 16, kOff32, false>(ba, (int)blockIdx.x);
+        side16_block<4, 4, 16, kOff32, kPipe>(ba, (int)blockIdx.x);
         return;
     }
     const unsigned v = blockIdx.x - (unsigned)f.big_blocks, row = v >> 3, x = v & 7u;
@@ -1043,7 +1044,7 @@ __global__ __launch_bounds__(kTileThreads, RSK_TILE16_WGS) void car_fused16_kern
         if (row - P1 >= t_rem) side = K1 + (row - P1 - t_rem);
     }
     if (side != 0xffffffffu) {
-        side16_block<4, 1, 16, kOff32, false>(sa, (int)(side * 8u + x));
+        side16_block<4, 1, 16, kOff32, kPipe>(sa, (int)(side * 8u + x));
         return;
     }
     tile16_block<kScore, kOff32, true, false>(ta, (tile << 3) | x);
@@ -1091,9 +1092,12 @@ int launch_fused16(hipStream_t stream, const Tile16Args &a, const SideArgs &sa, 
     const int64_t blocks = (int64_t)f.big_blocks + tile_blocks + 8LL * f.side_rows;
     RSK_CHECK(blocks < INT32_MAX, "fused grid too large");
     using K = void (*)(Tile16Args, SideArgs, SideArgs, FuseMap);
-    static const K kerns[4] = {&car_fused16_kernel<false, false>, &car_fused16_kernel<false, true>,
-                               &car_fused16_kernel<true, false>, &car_fused16_kernel<true, true>};
-    const K kern = kerns[(score ? 2 : 0) + (off32 ? 1 : 0)];
+    static const K kerns[8] = {&car_fused16_kernel<false, false, false>, &car_fused16_kernel<false, true, false>,
+                               &car_fused16_kernel<true, false, false>,  &car_fused16_kernel<true, true, false>,
+                               &car_fused16_kernel<false, false, true>,  &car_fused16_kernel<false, true, true>,
+                               &car_fused16_kernel<true, false, true>,   &car_fused16_kernel<true, true, true>};
+    static const bool pipe = [] { const char *e = getenv("RSK_FUSE_PIPE"); return e ? atoi(e) != 0 : true; }();
+    const K kern = kerns[(pipe ? 4 : 0) + (score ? 2 : 0) + (off32 ? 1 : 0)];
     RSK_CHECK(lds <= 160 * 1024, "fused tile needs %zu B of LDS", lds);
     if (lds > 64 * 1024)
         RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
