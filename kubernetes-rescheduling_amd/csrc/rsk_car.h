@@ -310,6 +310,7 @@ struct SideArgs {
     unsigned lds_team;
     int xcd_per;              // workgroups per XCD run (set by launch_side16)
     int ablate;               // profiling only (results wrong): 1 no exact recounts, 2 pass 1 only, 4 no (1), 8 no (2)
+    unsigned *gscratch;       // teams whose table exceeds the LDS: lds_team bytes per block in global memory
 };
 struct SideGeom {
     int dmax, Dc, H, hshift, K, T, W, kB;
@@ -327,7 +328,8 @@ struct FuseMap {
 // optionally 4-wave side teams (kB 16) in one grid; ba.n_rows == 0: no teams
 int launch_fused16(hipStream_t stream, const Tile16Args &a, const SideArgs &sa, int side_blocks, const SideArgs &ba,
                    bool score, bool off32, unsigned tile_blocks, size_t lds);
-int launch_side16(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32);
+// scratch: device memory for rows whose table exceeds the LDS (grown on demand)
+int launch_side16(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch);
 
 int launch_prep(hipStream_t stream, const Prep16Args &a);
 int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off32, bool heavy, unsigned blocks,

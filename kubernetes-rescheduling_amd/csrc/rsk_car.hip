@@ -765,6 +765,7 @@ struct rsk_car_plan {
     // compact path: every side row (deg > light_max) for car_side16, degree
     // descending, split into the kSideMax classes (neighbours in pcol)
     DevBuf side_items, pcol;
+    DevBuf side_scratch;  // work areas of side rows whose table exceeds the LDS
     // distinct neighbour pods of the tile rows plus the side classes [0, hi)
     // (nb_distinct[hi]; [0]: the tile rows alone): the algorithmic assign
     // bytes of the fused launch; fused_lo / fused_hi: the side classes the last
@@ -788,6 +789,7 @@ struct rsk_car_plan {
         for (auto &b : heavy_items) b.release();
         hcol.release();
         side_items.release();
+        side_scratch.release();
         pcol.release();
         nodekey.release();
         code.release();
@@ -1272,7 +1274,7 @@ int launch_side16_classes(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, 
         const SideArgs a = side16_class_args(plan, c, b, S, N);
         const SideGeom g = side16_geometry(plan->side_dmax[c], N);
         ScopedTimer tm(ctx, per_class ? kNames[c] : "car_side", stream);
-        RSK_TRY(launch_side16(stream, a, g, off32));
+        RSK_TRY(launch_side16(stream, a, g, off32, &plan->side_scratch));
     }
     return RSK_OK;
 }

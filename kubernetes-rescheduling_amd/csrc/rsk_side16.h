@@ -170,7 +170,7 @@ __device__ __forceinline__ int side_pivot3(int x) {  // majority of lanes 0, 21,
 // deviations away from u plus its deviations onto u.  So the exact count >= 2
 // candidates are: the table's entries with C >= 2 (a handful), and the lane's
 // deviation nodes — both small sets.
-template <int kW, int kT, int kB, bool kOff32, bool kPipe>
+template <int kW, int kT, int kB, bool kOff32, bool kPipe, bool kGlobal = false>
 __device__ __forceinline__ void side16_block(const SideArgs &a, int blk) {
     static_assert(kT == 1 || kT == kW, "a team is one wave or the whole workgroup");
     extern __shared__ __attribute__((aligned(16))) unsigned slds[];
@@ -189,7 +189,10 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk) {
     const int s = min(s0 + lane, a.S - 1);
     const int H = a.H, K = a.K;
 
-    unsigned *base = slds + (size_t)team * (a.lds_team >> 2);
+    // kGlobal (one team per workgroup): the team's table, lists and merge area in
+    // global scratch (a table beyond the LDS); the same code with global atomics
+    unsigned *base = kGlobal ? a.gscratch + (size_t)(unsigned)blk * (a.lds_team >> 2)
+                             : slds + (size_t)team * (a.lds_team >> 2);
     SideTab tb;
     tb.tab = base;
     tb.mask = (unsigned)H - 1u;

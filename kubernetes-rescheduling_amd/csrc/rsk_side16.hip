@@ -37,11 +37,11 @@ namespace rsk {
 
 // kW waves per workgroup, teams of kT waves; blocks b and b + 8 share an XCD
 // (a.xcd_per: workgroups per XCD run).
-template <int kW, int kT, int kB, bool kOff32, bool kPipe>
+template <int kW, int kT, int kB, bool kOff32, bool kPipe, bool kGlobal = false>
 __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(SideArgs a) {
     int blk = (int)blockIdx.x;
     if (a.xcd_per) blk = (int)(blockIdx.x & 7u) * a.xcd_per + (int)(blockIdx.x >> 3);
-    side16_block<kW, kT, kB, kOff32, kPipe>(a, blk);
+    side16_block<kW, kT, kB, kOff32, kPipe, kGlobal>(a, blk);
 }
 
 constexpr int kSideH2Cap = 2048;  // listed nodes counted >= 2 (e.g. degree 5000 over 6000 nodes: ~1200)
@@ -100,12 +100,12 @@ void side16_apply_geometry(SideArgs &a, const SideGeom &g) {
     a.h2cap = g.h2cap;
 }
 
-int launch_side16(hipStream_t stream, const SideArgs &a0, const SideGeom &g, bool off32) {
+int launch_side16(hipStream_t stream, const SideArgs &a0, const SideGeom &g0, bool off32, DevBuf *scratch) {
     if (a0.n_rows == 0) return RSK_OK;
-    const size_t lds = (size_t)(g.T > 1 ? 1 : g.W) * g.lds_team;
-    RSK_CHECK(lds <= 160 * 1024,
-              "a relation row of degree %d needs %zu B of LDS for its %d distinct nodes (limit 160 KiB)", g.dmax,
-              g.lds_team, g.Dc);
+    // a table beyond the LDS: 8-wave teams with their work area in global memory
+    const bool global = (size_t)(g0.T > 1 ? 1 : g0.W) * g0.lds_team > 160 * 1024;
+    const SideGeom g = global ? side16_geometry(g0.dmax, g0.Dc, 8) : g0;
+    const size_t lds = global ? 0 : (size_t)(g.T > 1 ? 1 : g.W) * g.lds_team;
     SideArgs a = a0;
     side16_apply_geometry(a, g);
     const int64_t items = (int64_t)a.n_rows * a.nchunk;
@@ -114,6 +114,17 @@ int launch_side16(hipStream_t stream, const SideArgs &a0, const SideGeom &g, boo
     const int64_t blocks_needed = ceil_div(items, teams);
     a.xcd_per = (int)ceil_div(blocks_needed, 8);
     const int64_t blocks = 8 * (int64_t)a.xcd_per;
+    a.gscratch = nullptr;
+    if (global) {
+        RSK_CHECK(scratch, "a relation row of degree %d needs a %zu-B table: no scratch", g.dmax, g.lds_team);
+        RSK_TRY(scratch->reserve((size_t)blocks * g.lds_team));
+        a.gscratch = scratch->as<unsigned>();
+        using KG = void (*)(SideArgs);
+        const KG kg = off32 ? &car_side16_kernel<8, 8, 32, true, false, true> : &car_side16_kernel<8, 8, 32, false, false, true>;
+        kg<<<dim3((unsigned)blocks), dim3(64 * 8), 0, stream>>>(a);
+        RSK_HIP(hipGetLastError());
+        return RSK_OK;
+    }
     using K = void (*)(SideArgs);
     static const bool pipe = [] { const char *e = getenv("RSK_SIDE_PIPE"); return e ? atoi(e) != 0 : true; }();
 #define RSK_SIDE_P(W, T, B, O) (pipe ? &car_side16_kernel<W, T, B, O, true> : &car_side16_kernel<W, T, B, O, false>)

@@ -447,13 +447,15 @@ def test_car_row_5000_distinct_nodes(ctx, S):
                label=f"deg 5000 N {N} S={S}")
 
 
-@pytest.mark.parametrize("P,N,deg,S", [(23000, 21845, 21000, 1), (23000, 21845, 21000, 64), (13000, 3000, 12000, 64)])
+@pytest.mark.parametrize("P,N,deg,S", [(23000, 21845, 21000, 1), (23000, 21845, 21000, 64), (13000, 3000, 12000, 64),
+                                       (32000, 30000, 26000, 1), (32000, 30000, 26000, 64)])
 def test_car_row_largest_tables(ctx, P, N, deg, S):
-    """The side kernel's LDS limits: a row with 21,000 distinct neighbour nodes
-    (the largest table that fits, 32,768 words) and a degree-12,000 row over
-    3,000 nodes whose ~2,900 nodes counted twice overflow the 2,048-entry list
-    (every lane takes the exact recount).  1 % of placements redrawn per
-    scenario, as in the synthetic what-if batches."""
+    """The side kernel's table limits: a row with 21,000 distinct neighbour
+    nodes (the largest table the LDS holds, 32,768 words), a degree-12,000 row
+    over 3,000 nodes whose ~2,900 nodes counted twice overflow the 2,048-entry
+    list (every lane takes the exact recount), and a degree-26,000 row over
+    30,000 nodes whose table (65,536 words) lives in global memory.  1 % of
+    placements redrawn per scenario, as in the synthetic what-if batches."""
     rng = np.random.default_rng(deg + S)
     rows = [rng.integers(0, P, int(rng.integers(0, 3))).tolist() for _ in range(P)]
     rows[0] = rng.choice(np.arange(1, P), deg, replace=False).tolist()
