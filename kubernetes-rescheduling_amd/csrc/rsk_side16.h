@@ -51,11 +51,21 @@ __device__ __forceinline__ unsigned long long side_key(unsigned cnt, unsigned co
 // reference's decision (rescheduling.py:188-214) with exact remaining CPU for
 // ties on an inexact code.  cells: scratch of >= min(d, ncap) words; the
 // table is zeroed here and left dirty.
+// Work areas in global memory (a.gscratch, tables beyond the LDS): plain loads
+// may hit stale L1 lines after other lanes' stores or atomics (performed in L2),
+// so every switch from writing to reading such an area goes through an
+// agent-scope fence, which invalidates the L1.
+__device__ __forceinline__ void glob_fence(bool glob) {
+    if (glob) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+}
+
 template <bool kOff32>
 __device__ int side_exact(const SideArgs &a, const SideTab &tb, unsigned *cells, int ncap, cint_ptr nb, int d, int ss,
                           int lane, int H, int &score) {
     const unsigned S = (unsigned)a.S, N = (unsigned)a.N;
+    const bool glob = a.gscratch != nullptr;
     for (int i = lane; i < H; i += 64) tb.tab[i] = 0u;
+    glob_fence(glob);
     // neighbour cells (code << 16 | node) staged in LDS segments of ncap, all counted
     unsigned long long best = 0ull, sec = 0ull;
     for (int pass = 0; pass < 3; ++pass) {  // 0: count, 1: best key, 2: second key (another node)
@@ -75,6 +85,7 @@ __device__ int side_exact(const SideArgs &a, const SideTab &tb, unsigned *cells,
                     }
                 }
             }
+            glob_fence(glob);  // the staged cells and the pass-0 counts before they are read
             for (int j = lane; j < gn; j += 64) {
                 const unsigned x = cells[j];
                 const unsigned c = x >> 16, n = x & 0xffffu;
@@ -89,6 +100,7 @@ __device__ int side_exact(const SideArgs &a, const SideTab &tb, unsigned *cells,
             }
         }
         if (pass == 1) best = dpp_max_u64(best);
+        glob_fence(glob);
     }
     const unsigned long long k1 = best, k2 = dpp_max_u64(sec);
     const int M = (int)(k1 >> 32);
@@ -108,6 +120,7 @@ __device__ int side_exact(const SideArgs &a, const SideTab &tb, unsigned *cells,
                 const unsigned n = min((unsigned)side_ld_assign<kOff32>(a.assign, (unsigned)nb[g0 + j], S, (unsigned)ss), N);
                 cells[j] = (ld16(a.code, n * S + (unsigned)ss) << 16) | n;
             }
+            glob_fence(glob);
         }
         for (int j = lane; j < gn; j += 64) {
             const unsigned x = cells[j];
@@ -210,6 +223,7 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk) {
             ndl[lane] = 0;
             if (lane == 0) h2[0] = 0u;
         }
+        glob_fence(kGlobal);
         __syncthreads();
     }
 
@@ -280,7 +294,9 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk) {
     if (kT > 1) {
         fx[(2 * tw) * 64 + lane] = f.w1;
         fx[(2 * tw + 1) * 64 + lane] = f.w2;
+        glob_fence(kGlobal);
         __syncthreads();
+        glob_fence(kGlobal);
         nd = ndl[lane];
     }
     const int ndk = min(nd, K);
@@ -308,7 +324,9 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk) {
         if (big && pos < a.h2cap) h2[1 + pos] = w;
     }
     if (kT > 1) {
+        glob_fence(kGlobal);
         __syncthreads();
+        glob_fence(kGlobal);
         n2 = (int)h2[0];
     } else {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the list's LDS writes before its reads
@@ -371,7 +389,9 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk) {
         bx[(3 * tw) * 64 + lane] = (unsigned)b.M;
         bx[(3 * tw + 1) * 64 + lane] = b.w1;
         bx[(3 * tw + 2) * 64 + lane] = b.w2;
+        glob_fence(kGlobal);
         __syncthreads();
+        glob_fence(kGlobal);
         if (tw != 0) return;  // the rest is one wave's (no more barriers)
 #pragma unroll 1
         for (int w = 1; w < kT; ++w) {

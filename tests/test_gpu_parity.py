@@ -473,6 +473,29 @@ def test_car_row_largest_tables(ctx, P, N, deg, S):
                label=f"deg {deg} N {N} S={S}")
 
 
+def test_car_global_table_exact_recount(ctx):
+    """The global-memory work area with every lane's deviation list
+    overflowing (30 % of placements redrawn per scenario): each of the 64
+    scenarios of a degree-26,000 row over 30,000 nodes is recounted exactly
+    through the global table."""
+    rng = np.random.default_rng(2600)
+    P, N, S, deg = 32000, 30000, 64, 26000
+    rows = [rng.integers(0, P, int(rng.integers(0, 3))).tolist() for _ in range(P)]
+    rows[0] = rng.choice(np.arange(1, P), deg, replace=False).tolist()
+    rp = np.zeros(P + 1, np.int32)
+    rp[1:] = np.cumsum([len(r) for r in rows])
+    ci = np.array([q for r in rows for q in r], np.int32)
+    base = rng.permutation(P) % N
+    a = np.repeat(base[:, None], S, axis=1).astype(np.int32)
+    flip = rng.random((P, S)) < 0.3
+    a[flip] = rng.integers(-1, N, flip.sum())
+    cap = rng.choice([4000, 8000], N).astype(np.int32)
+    use = rng.integers(0, 8000, N * S).astype(np.int32)
+    haz = (rng.random(N * S) < 0.2).astype(np.uint8)
+    _check_car(ctx, rp, ci, a.reshape(-1), S, cap, use, haz, N, rows=np.arange(0, 4, dtype=np.int32),
+               label="global table, exact recount")
+
+
 @pytest.mark.parametrize("S", [64, 200])
 def test_car_fused_side_rows_outnumber_tiles(ctx, S):
     """The fused tile + side launch when the side rows (33..128 and above)
