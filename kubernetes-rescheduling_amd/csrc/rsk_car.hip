@@ -744,6 +744,102 @@ __global__ __launch_bounds__(64 * kW) void car_hub_kernel(const HeavyItem *__res
 using namespace rsk;
 
 
+// Wide path (N > 65535), rows above kHubMax neighbours: one workgroup per
+// (row, scenario), looping over them; each workgroup owns an open-addressing
+// table of (node + 1, count) in global memory (2^lg slots, load <= 1/2).  The
+// scores are rescheduling.py:183-195's histogram over the candidate nodes; the
+// decision :199-214 — the largest count, a single best node wins, else the
+// largest cap - use (first index), None when it is < 0; no candidate at all:
+// the zero case.  Every table access is an atomic performed in L2 (the slots
+// are reused across items: no stale L1 lines).
+struct BigRowArgs {
+    const HeavyItem *items;  // {out row, offset into col, degree}
+    int n_items;
+    const int *col, *assign, *nodekey;
+    const int *zc_cnt;
+    const unsigned long long *zc_key;
+    int *out_target, *out_score;
+    int S, N, lg;
+    unsigned *keys, *cnts;  // [gridDim.x][1 << lg]
+};
+constexpr int kBigThreads = 256;
+__global__ __launch_bounds__(kBigThreads) void car_bigrow_kernel(BigRowArgs a) {
+    __shared__ unsigned long long red[kBigThreads / 64];
+    __shared__ int redi[kBigThreads / 64];
+    const int H = 1 << a.lg;
+    const unsigned mask = (unsigned)H - 1u;
+    unsigned *keys = a.keys + (size_t)blockIdx.x * (size_t)H, *cnts = a.cnts + (size_t)blockIdx.x * (size_t)H;
+    const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
+    const int64_t total = (int64_t)a.n_items * a.S;
+    for (int64_t it = blockIdx.x; it < total; it += gridDim.x) {  // workgroup-uniform
+        const int r = (int)(it / a.S), s = (int)(it - (int64_t)r * a.S);
+        const HeavyItem h = a.items[r];
+        for (int i = (int)threadIdx.x; i < H; i += kBigThreads) {
+            __hip_atomic_store(&keys[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&cnts[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        for (int j = (int)threadIdx.x; j < h.d; j += kBigThreads) {
+            const int n = a.assign[(size_t)a.col[h.rb + j] * a.S + s];
+            if (n < 0 || n >= a.N || a.nodekey[(size_t)n * a.S + s] == kKeyHaz) continue;  // not a candidate
+            const unsigned k = (unsigned)n + 1u;
+            unsigned slot = (k * 2654435761u) >> (32 - a.lg);
+            while (true) {
+                const unsigned prev = atomicCAS(&keys[slot], 0u, k);
+                if (prev == 0u || prev == k) break;
+                slot = (slot + 1u) & mask;
+            }
+            atomicAdd(&cnts[slot], 1u);
+        }
+        __syncthreads();
+        // the largest count
+        int mc = 0;
+        for (int i = (int)threadIdx.x; i < H; i += kBigThreads)
+            mc = max(mc, (int)__hip_atomic_load(&cnts[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        mc = dpp_max(mc);
+        if (lane == 0) redi[wave] = mc;
+        __syncthreads();
+        int M = 0;
+        for (int w = 0; w < kBigThreads / 64; ++w) M = max(M, redi[w]);
+        __syncthreads();
+        // among the nodes at M: the largest (cap - use, -node) and how many there are
+        unsigned long long best = 0ull;
+        int cnt_at_m = 0;
+        if (M > 0)
+            for (int i = (int)threadIdx.x; i < H; i += kBigThreads) {
+                if ((int)__hip_atomic_load(&cnts[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != M) continue;
+                const int n = (int)__hip_atomic_load(&keys[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1;
+                const unsigned long long k = pack_rn(a.nodekey[(size_t)n * a.S + s], n);
+                best = k > best ? k : best;
+                ++cnt_at_m;
+            }
+        best = dpp_max_u64(best);
+        if (lane == 0) red[wave] = best;
+        for (int o = 32; o >= 1; o >>= 1) cnt_at_m += __shfl_xor(cnt_at_m, o, 64);
+        __syncthreads();  // every wave has read redi (M) and written red
+        if (lane == 0) redi[wave] = cnt_at_m;
+        __syncthreads();
+        for (int w = 0; w < kBigThreads / 64; ++w) best = red[w] > best ? red[w] : best;
+        if (threadIdx.x == 0) {
+            int nbest = 0;
+            for (int w = 0; w < kBigThreads / 64; ++w) nbest += redi[w];
+            int t, sc;
+            if (M == 0) {
+                t = zero_target(load_zc(a.zc_cnt, a.zc_key, s), sc);
+            } else {
+                sc = M;
+                const int bn = (int)(kNodeMask - (unsigned)(best & kNodeMask));
+                const int br = (int)((unsigned)(best >> kNodeBits) ^ 0x80000000u);
+                t = nbest == 1 ? bn : (br >= 0 ? bn : RSK_TARGET_NONE);
+            }
+            const size_t o = (size_t)(unsigned)h.oi * (size_t)a.S + (size_t)s;
+            a.out_target[o] = t;
+            if (a.out_score) a.out_score[o] = sc;
+        }
+        __syncthreads();
+    }
+}
+
 struct rsk_car_plan {
     rsk_ctx *ctx = nullptr;
     int P = 0, Q = 0, max_deg = 0;
@@ -766,6 +862,9 @@ struct rsk_car_plan {
     // descending, split into the kSideMax classes (neighbours in pcol)
     DevBuf side_items, pcol;
     DevBuf side_scratch;  // work areas of side rows whose table exceeds the LDS
+    // wide path: rows above kHubMax neighbours (car_bigrow_kernel), neighbours in pcol
+    DevBuf big_items;
+    int n_big = 0, big_dmax = 0;
     // distinct neighbour pods of the tile rows plus the side classes [0, hi)
     // (nb_distinct[hi]; [0]: the tile rows alone): the algorithmic assign
     // bytes of the fused launch; fused_lo / fused_hi: the side classes the last
@@ -790,6 +889,7 @@ struct rsk_car_plan {
         hcol.release();
         side_items.release();
         side_scratch.release();
+        big_items.release();
         pcol.release();
         nodekey.release();
         code.release();
@@ -1161,6 +1261,13 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
         // the rows of degree (kSideMax[c - 1], kSideMax[c]] at [side_beg[c], side_end[c])
         std::vector<HeavyItem> &all = sitems;
         std::stable_sort(all.begin(), all.end(), [](const HeavyItem &x, const HeavyItem &y) { return x.d > y.d; });
+        {   // the wide path's rows above kHubMax (degree descending: a prefix)
+            int nb = 0;
+            while (nb < (int)all.size() && all[nb].d > kHubMax) ++nb;
+            plan->n_big = nb;
+            plan->big_dmax = nb ? all[0].d : 0;
+            if (nb) RSK_TRY(upload(plan->big_items, all.data(), (size_t)nb * sizeof(HeavyItem)));
+        }
         int end = (int)all.size();
         for (int c = 0; c < kNumSide; ++c) {
             int b = end;
@@ -1345,6 +1452,32 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, const Side
             g.H, gpw, d_zcnt, d_zkey, d_target, d_score);
         RSK_HIP(hipGetLastError());
     }
+    if (plan->n_big > 0) {  // K4: rows above kHubMax neighbours
+        BigRowArgs a;
+        std::memset(&a, 0, sizeof(a));
+        a.items = plan->big_items.as<HeavyItem>();
+        a.n_items = plan->n_big;
+        a.col = plan->pcol.as<int>();
+        a.assign = d_assign;
+        a.nodekey = d_key;
+        a.zc_cnt = d_zcnt;
+        a.zc_key = d_zkey;
+        a.out_target = d_target;
+        a.out_score = d_score;
+        a.S = S;
+        a.N = N;
+        a.lg = 1;
+        while ((1 << a.lg) < 2 * std::min(plan->big_dmax, N)) ++a.lg;
+        const size_t H = (size_t)1 << a.lg;
+        const int64_t items = (int64_t)plan->n_big * S;
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>({items, 1024, (int64_t)((256u << 20) / (H * 8))}));
+        RSK_TRY(plan->side_scratch.reserve((size_t)grid * H * 8));
+        a.keys = plan->side_scratch.as<unsigned>();
+        a.cnts = a.keys + (size_t)grid * H;
+        ScopedTimer tm(ctx, "car_heavy", stream);
+        car_bigrow_kernel<<<dim3((unsigned)grid), dim3(kBigThreads), 0, stream>>>(a);
+        RSK_HIP(hipGetLastError());
+    }
     return RSK_OK;
 }
 
@@ -1435,8 +1568,6 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
                                 plan->has_rows ? plan->h_rows.data() : nullptr, plan->Q, kPairMax, &plan->alt));
         return rsk_car_plan_execute(plan->alt, assign, S, cap_cpu, use_cpu, hazard, N, out_target, out_score, flags);
     }
-    RSK_CHECK(compact || plan->max_deg <= kHubMax, "a row has degree %d > %d: supported for N <= %d only",
-              plan->max_deg, kHubMax, kMaxNodes16);
     const bool dev = (flags & RSK_F_DEVICE) != 0;
     const size_t PS_ = (size_t)plan->P * S, NS = (size_t)N * S, QS = (size_t)plan->Q * S;
 

@@ -473,6 +473,30 @@ def test_car_row_largest_tables(ctx, P, N, deg, S):
                label=f"deg {deg} N {N} S={S}")
 
 
+@pytest.mark.parametrize("S", [1, 64])
+def test_car_wide_path_rows_above_4096(ctx, S):
+    """N > 65535 (the wide path, 32-bit node ids): rows of degree 5,000 and
+    9,000 (above the hub kernel's 4096) through car_bigrow_kernel, with
+    neighbours piled onto few nodes in some scenarios (counts in the
+    thousands), hazards, unassigned pods and overloaded ties."""
+    rng = np.random.default_rng(4100 + S)
+    P, N = 12000, 70000
+    rows = [rng.integers(0, P, int(rng.integers(0, 4))).tolist() for _ in range(P)]
+    rows[0] = rng.choice(np.arange(1, P), 5000, replace=False).tolist()
+    rows[1] = rng.choice(np.arange(2, P), 9000, replace=False).tolist()
+    rp = np.zeros(P + 1, np.int32)
+    rp[1:] = np.cumsum([len(r) for r in rows])
+    ci = np.array([q for r in rows for q in r], np.int32)
+    a = rng.integers(-1, N, (P, S)).astype(np.int32)
+    crowd = rng.random((P, S)) < 0.5
+    a[crowd] = rng.integers(0, 40, crowd.sum())           # half the placements on 40 nodes
+    cap = rng.choice([4000, 8000], N).astype(np.int32)
+    use = rng.integers(0, 8000, N * S).astype(np.int32)
+    haz = (rng.random(N * S) < 0.2).astype(np.uint8)
+    _check_car(ctx, rp, ci, a.reshape(-1), S, cap, use, haz, N, rows=np.arange(0, 6, dtype=np.int32),
+               label=f"wide path deg > 4096 S={S}")
+
+
 def test_car_global_table_exact_recount(ctx):
     """The global-memory work area with every lane's deviation list
     overflowing (30 % of placements redrawn per scenario): each of the 64
