@@ -857,47 +857,57 @@ __device__ __forceinline__ void w64_ds(const Tile16Args &a, const W64 &w, cint_p
     emit64<kScore, kOff32>(a, r[0], s0, w, M == 0 ? w.zt : t, M == 0 ? w.zs : M);
 }
 
-// kL64 phase 2, part 1: the multi-neighbour classes (d >= 3), most expensive first.
+// kL64 phase 2, part 1: the multi-neighbour classes (d >= 3), most expensive
+// first.  Record j of a class goes to wave (rot + j) % 4, rot carried from
+// class to class (and into part 2), so a tile's few records of each class do
+// not all start on wave 0.
 template <bool kScore, bool kOff32, bool kHeavy>
-__device__ __forceinline__ void w64_score_heavy(const Tile16Args &a, const W64 &w, cint_ptr m, cint_ptr R, int wave,
-                                                int s0) {
+__device__ __forceinline__ int w64_score_heavy(const Tile16Args &a, const W64 &w, cint_ptr m, cint_ptr R, int wave,
+                                               int s0) {
+    int rot = 0;
     if (kHeavy) {  // d = 17..32: heavy tiles only (own instantiation, registers for 32 cells)
         const cint_ptr Rc = R + m[15];
-        for (int j = wave; j < m[9]; j += 4) w64_ds<kScore, kOff32>(a, w, Rc, j, s0);
+        for (int j = (wave - rot) & 3; j < m[9]; j += 4) w64_ds<kScore, kOff32>(a, w, Rc, j, s0);
+        rot = (rot + m[9]) & 3;
     }
     {
         const cint_ptr Rc = R + m[14];
-        for (int j = wave; j < m[8]; j += 4) w64_dm<16, 12, 2, kScore, kOff32>(a, w, Rc, j, s0);
+        for (int j = (wave - rot) & 3; j < m[8]; j += 4) w64_dm<16, 12, 2, kScore, kOff32>(a, w, Rc, j, s0);
+        rot = (rot + m[8]) & 3;
     }
     {
         const cint_ptr Rc = R + m[13];
-        for (int j = wave; j < m[7]; j += 4) w64_dm<8, 8, 2, kScore, kOff32>(a, w, Rc, j, s0);
+        for (int j = (wave - rot) & 3; j < m[7]; j += 4) w64_dm<8, 8, 2, kScore, kOff32>(a, w, Rc, j, s0);
+        rot = (rot + m[7]) & 3;
     }
     {
         const cint_ptr Rc = R + m[12];
-        for (int j = wave; j < m[6]; j += 4) w64_dm<4, 4, 2, kScore, kOff32>(a, w, Rc, j, s0);
+        for (int j = (wave - rot) & 3; j < m[6]; j += 4) w64_dm<4, 4, 2, kScore, kOff32>(a, w, Rc, j, s0);
+        rot = (rot + m[6]) & 3;
     }
+    return rot;
 }
 
-// kL64 phase 2, part 2: d = 2 and d = 1 records in blocks of 8.
+// kL64 phase 2, part 2: d = 2 and d = 1 records in blocks of 8 (block b to
+// wave (rot + b) % 4).
 template <bool kScore, bool kOff32>
 __device__ __forceinline__ void w64_score_light(const Tile16Args &a, const W64 &w, cint_ptr m, cint_ptr R, int wave,
-                                                int s0) {
+                                                int s0, int rot) {
+    constexpr int U = 8;
     {
-        constexpr int U = 8;
         const cint_ptr Rc = R + m[11];
         const int n = m[5];
-        for (int k = wave * U; k < n; k += 4 * U) w64_d2<U, kScore, kOff32>(a, w, Rc, n, k, s0);
+        for (int k = ((wave - rot) & 3) * U; k < n; k += 4 * U) w64_d2<U, kScore, kOff32>(a, w, Rc, n, k, s0);
+        rot = (rot + (n + U - 1) / U) & 3;
     }
     {
-        constexpr int U = 8;
         const cint_ptr Rc = R + m[10];
         const int n = m[4];
-        for (int k = wave * U; k < n; k += 4 * U) w64_d1<U, kScore, kOff32>(a, w, Rc, n, k, s0);
+        for (int k = ((wave - rot) & 3) * U; k < n; k += 4 * U) w64_d1<U, kScore, kOff32>(a, w, Rc, n, k, s0);
     }
 }
 
-// kL64 phase 2: the records of each class, block b to wave b % 4.
+// kL64 phase 2: the records of each class, spread over the 4 waves.
 template <bool kScore, bool kOff32, bool kHeavy>
 __device__ __forceinline__ void w64_score(const Tile16Args &a, const W64 &w, cint_ptr m, cint_ptr R, int wave, int s0) {
     if (a.ablate & 4) {  // profiling: the target stores alone (every record, zero-case value, no LDS reads)
@@ -907,8 +917,8 @@ __device__ __forceinline__ void w64_score(const Tile16Args &a, const W64 &w, cin
         }
         return;
     }
-    w64_score_heavy<kScore, kOff32, kHeavy>(a, w, m, R, wave, s0);
-    w64_score_light<kScore, kOff32>(a, w, m, R, wave, s0);
+    const int rot = w64_score_heavy<kScore, kOff32, kHeavy>(a, w, m, R, wave, s0);
+    w64_score_light<kScore, kOff32>(a, w, m, R, wave, s0, rot);
 }
 
 // One tile workgroup; bid plays blockIdx.x (the fused kernel below maps its
