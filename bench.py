@@ -7,17 +7,23 @@ GPU.  One step = one pass of the hot path over one batch: librsk's CAR pipeline
 (car_prep, the lean tiles fused with the side rows, the heavy tiles) scores every pod in every scenario against
 every node — P·N·S evaluations — with all inputs resident in HBM.
 
-Multi-GPU (``torchrun --nproc-per-node N``): scenario sharding, rank r scores
-global scenarios [r·S, (r+1)·S) with no data-path collective; ``value`` is the
-whole-job rate (weak scaling).  Timing: barrier + device sync around exactly
-``--steps`` steps, max over ranks.  Per-kernel times come from HIP events on the
-stream the kernels run on (librsk's profiler).
+Multi-GPU: ``python bench.py --gpus N`` with no ``WORLD_SIZE`` in the
+environment starts ``torch.distributed.run --nproc-per-node N`` on itself as a
+child process (the parent touches no GPU) and exits with its status; under a
+launcher (``WORLD_SIZE`` set) it must equal ``--gpus``.  Scenario sharding: rank
+r scores global scenarios [r·S, (r+1)·S) with no data-path collective;
+``value`` is the whole-job rate (weak scaling).  Timing: barrier + device sync
+around exactly ``--steps`` steps, max over ranks.  Per-kernel times come from
+HIP events on the stream the kernels run on (librsk's profiler).
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -65,6 +71,80 @@ def cgroup_cpu_quota():
         return None if q == "max" else round(int(q) / int(per), 2)
     except (OSError, ValueError):
         return None
+
+
+def cpu_threads():
+    """Threads for the OpenMP CPU leg: the affinity mask capped by the cgroup's
+    CPU quota (a quota of 16 cores on a 256-CPU host gives 16 threads)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = cgroup_cpu_quota()
+    return max(1, min(aff, math.ceil(quota))) if quota else aff, aff
+
+
+# Environment knobs the benchmark records.  librsk.so reads none of them (its
+# tuning switches exist only in `make variant` builds); an ablation variable
+# means someone expected wrong-result switches, so no line is printed.
+ABLATION_VARS = ("RSK_ABLATE_TILE", "RSK_ABLATE_SIDE")
+
+
+def rsk_env():
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("RSK_")}
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`--gpus N` without a launcher: run N ranks of this script under
+    torch.distributed.run (one process per GPU, 127.0.0.1 rendezvous) and return
+    its exit status (non-zero when any rank fails).  Called before anything
+    touches a GPU, so the parent never initialises HIP; rank 0 prints the line
+    straight to the inherited stdout."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    log(f"[bench] launching {n} ranks: {' '.join(cmd[1:])}")
+    return subprocess.call(cmd, env=dict(os.environ))
+
+
+def dry_run(args, world, rank):
+    """`--dry-run`: the multi-rank skeleton on the CPU (gloo, no GPU, no librsk):
+    rendezvous, the scenario shard of every rank, exactly --steps barrier-
+    bracketed no-op steps, the MAX-over-ranks time, and rank 0's line naming
+    every rank that took part.  tests/test_bench_launcher.py runs it at --gpus 2."""
+    import torch
+    import torch.distributed as dist
+    from rsk import dist as rdist
+    if world > 1:
+        dist.init_process_group("gloo")
+    S = CONFIGS[args.config]["S"]
+    sh = rdist.shard_for(rank, world, S)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    mine = torch.tensor([rank, sh.s0, sh.s0 + sh.s_local, os.getpid()], dtype=torch.int64)
+    rows = [mine]
+    if world > 1:
+        rows = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(rows, mine)
+        e = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        el = float(e.item())
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "rccl_world": dist.get_world_size() if world > 1 else 1,
+                          "backend": "gloo" if world > 1 else None, "steps": args.steps,
+                          "ranks": [int(r[0]) for r in rows], "pids": [int(r[3]) for r in rows],
+                          "scenario_shards": [[int(r[1]), int(r[2])] for r in rows],
+                          "ms_per_step": el * 1e3 / max(args.steps, 1), "env": rsk_env()}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def python_legs(c, N, S, budget_s=6.0, numpy_budget_s=20.0):
@@ -215,6 +295,7 @@ def bench_rounds(args, cfg, world, rank, local, dev):
             "no_candidate": int((tgt == -2).sum()), "no_evict": int((tgt == -3).sum()),
             "parity_sample_ok": bool(parity_ok),
             "parity_sample": f"the timed {R}-round call, scenarios 0..{k - 1}, vs oracle_rounds from its start state",
+            "rccl_world": args.rccl_world, "env": rsk_env(),
         }
         print(json.dumps(line), flush=True)
     rounds.close()
@@ -240,21 +321,40 @@ def main():
                     help="time the steps without per-kernel HIP events")
     ap.add_argument("--pmc-json", default=PMC_JSON,
                     help="per-config PMC traffic (tools/pmc_summary.py, FETCH_SIZE x2-corrected)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU-only rehearsal of the multi-rank skeleton over gloo (no GPU, no librsk)")
     args = ap.parse_args()
     args.steps_default = args.steps is None
     if args.steps is None:
         args.steps = 20
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    ablated = [k for k in ABLATION_VARS if os.environ.get(k, "0") not in ("", "0")]
+    if ablated:
+        sys.exit(f"[bench] refusing to run with wrong-result ablation switches set: {ablated}")
+
+    # one process per GPU: without a launcher, --gpus N > 1 re-launches this
+    # script as N ranks before anything here touches a GPU
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        sys.exit(f"[bench] WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {args.gpus}: "
+                 "launch one rank per GPU with matching counts")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    args.rccl_world = dist.get_world_size() if world > 1 else 1
 
     from rsk import _lib, api, synth
     from rsk import dist as rdist
@@ -462,8 +562,9 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        # every core of this process's affinity mask (SURVEY §8d leg 3)
-        threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+        # the cores this process may use (SURVEY §8d leg 3): the affinity mask
+        # capped by the cgroup CPU quota, so no thread waits for CPU time
+        threads, aff = cpu_threads()
         model, ncpu = cpu_model()
         # grow an evenly spaced pod sample until one timed pass takes >= 60 % of
         # --cpu-seconds (about 10-30 s of CPU work at the default)
@@ -480,7 +581,7 @@ def main():
         cpu = {"value": round(nrows * S * N / dt, 1), "unit": "pod×node evals/s", "cores": threads, "kind": "port",
                "sample": f"{nrows} evenly spaced pods x {S} scenarios x {N} nodes ({dt:.1f}s), oracle/rsk_oracle.c "
                          f"literal CAR restatement, OpenMP {threads} threads",
-               "seconds": round(dt, 2), "cpu_model": model, "host_logical_cpus": ncpu, "affinity_cpus": threads,
+               "seconds": round(dt, 2), "cpu_model": model, "host_logical_cpus": ncpu, "affinity_cpus": aff,
                "cgroup_cpu_quota": cgroup_cpu_quota(), "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
                "legs": python_legs(c, N, S)}
 
@@ -494,7 +595,7 @@ def main():
                        "parallelism": f"{'pod-row' if by_rows else 'scenario'}-sharded x{world}"},
             "roofline": roof, "roofline_step": roof_step, "cpu_baseline": cpu, "kernels": kernels,
             "parity_sample_ok": parity_ok, "hbm_bytes_algorithmic_per_step": B, "plan": info,
-            "plan_create_ms": round(plan_ms, 1),
+            "plan_create_ms": round(plan_ms, 1), "rccl_world": args.rccl_world, "env": rsk_env(),
         }
         if by_rows:
             line["rows_per_rank"] = Q

@@ -378,7 +378,7 @@ __global__ __launch_bounds__(kTileThreads, 4) void car_tile_kernel(TileArgs a) {
         *reinterpret_cast<int4 *>(rec + i) =
             *reinterpret_cast<const int4 *>(a.recs + RSK_BOUND(rec_off + i + 3, a.n_recs, 16u) - 3);
     }
-    if (!(a.ablate & 1)) tile_load_image<kOff32>(a, img, img_off, nrows, s0);
+    if (!(RSK_ABL(a) & 1)) tile_load_image<kOff32>(a, img, img_off, nrows, s0);
 
     TileLane L;
     L.PS = 64 >> a.lsl;
@@ -392,7 +392,7 @@ __global__ __launch_bounds__(kTileThreads, 4) void car_tile_kernel(TileArgs a) {
     }
     if (threadIdx.x == 0) rec[a.rec_cap] = 0;  // work-unit counter
     __syncthreads();
-    if (a.ablate & 2) return;  // profiling ablation: no scoring (results are wrong)
+    if (RSK_ABL(a) & 2) return;  // profiling ablation: no scoring (results are wrong)
     // Scoring work units (pairs of PS records: d1 4 pairs, d2 2, the rest 1),
     // most expensive class first, handed out by an LDS counter so the few
     // costly high-degree records do not all land on one wave.
@@ -912,11 +912,6 @@ int next_pow2(int x) {
     return p;
 }
 
-int env_int(const char *name, int dflt) {
-    const char *e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
-
 struct HeavyGeom {
     int lg, dpad, H, mode, waves;
     size_t lds;
@@ -1307,8 +1302,8 @@ int plan_create(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, in
     // tile limits: the image rows the compact kernels are built for (RSK_TILE16_ROWS), owners
     // in the 128 : 144 ratio; RSK_TILE_ROWS / RSK_TILE_OWNERS override (experiments)
     const int rows_built = tile16_rows_built();
-    plan->owners_cap = std::min(kTileOwners, std::max(8, env_int("RSK_TILE_OWNERS", rows_built * kTileOwners / kTileRows)));
-    plan->rows_cap = std::min(rows_built, std::max(kLightMax, env_int("RSK_TILE_ROWS", rows_built)));  // a row fits alone
+    plan->owners_cap = std::min(kTileOwners, std::max(8, RSK_KNOB(RSK_TILE_OWNERS, rows_built * kTileOwners / kTileRows)));
+    plan->rows_cap = std::min(rows_built, std::max(kLightMax, RSK_KNOB(RSK_TILE_ROWS, rows_built)));  // a row fits alone
     plan->P = P;
     plan->Q = Q;
     const int rc = build_plan(plan, row_ptr, col_idx, P, rows, Q);
@@ -1343,12 +1338,12 @@ struct SideBufs {
 // Classes from kSideBig up (rows above 128 neighbours: few work items, each
 // latency-bound) run on a side stream beside the tiles (rsk_car_plan_execute).
 int side_big_class() {  // RSK_SIDE_AUX_FROM: the first class on the side stream (experiments)
-    static const int c = std::max(0, std::min(kNumSide, env_int("RSK_SIDE_AUX_FROM", 2)));
+    static const int c = std::max(2, std::min(kNumSide, RSK_KNOB(RSK_SIDE_AUX_FROM, 2)));
     return c;
 }
 #define kSideBig side_big_class()
 SideArgs side16_class_args(const rsk_car_plan *plan, int c, const SideBufs &b, int S, int N) {
-    static const int sablate = env_int("RSK_ABLATE_SIDE", 0);
+    static const int sablate = RSK_ABLATION(RSK_ABLATE_SIDE);
     SideArgs a;
     std::memset(&a, 0, sizeof(a));
     a.items = plan->side_items.as<int>() + (size_t)plan->side_beg[c] * 4;
@@ -1373,7 +1368,7 @@ SideArgs side16_class_args(const rsk_car_plan *plan, int c, const SideBufs &b, i
 int launch_side16_classes(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, const SideBufs &b, int S, int N,
                           int c0, int c1, int skip = -1) {
     const bool off32 = (int64_t)std::max(plan->P, plan->Q) * S * 4 < ((int64_t)1 << 32);
-    static const bool per_class = env_int("RSK_SIDE_TIMERS", 0) != 0;
+    static const bool per_class = RSK_KNOB(RSK_SIDE_TIMERS, 0) != 0;
     static const char *const kNames[kNumSide] = {"car_side32", "car_side128", "car_side512",
                                                  "car_side2048", "car_side8192", "car_side65535"};
     for (int c = c1 - 1; c >= c0; --c) {
@@ -1435,7 +1430,7 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, const Side
         RSK_CHECK(g.lds <= 160 * 1024, "hub class %d needs %zu B of LDS", c, g.lds);
         const int64_t groups = ceil_div(S, 1 << g.lg);
         // scenario groups per workgroup: enough workgroups to fill the GPU twice over
-        static const int gpw_env = env_int("RSK_HUB_GPW", 0);
+        static const int gpw_env = RSK_KNOB(RSK_HUB_GPW, 0);
         const int gpw = gpw_env > 0 ? gpw_env : (int)std::max<int64_t>(1, std::min<int64_t>(8, groups * n / 1024));
         const int64_t gblocks = ceil_div(groups, gpw);
         RSK_CHECK(gblocks * n < INT32_MAX, "hub grid too large");
@@ -1445,7 +1440,7 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, const Side
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds));
         static const char *const kHubNames[kNumHeavy] = {"car_hub128", "car_hub256", "car_hub512",
                                                          "car_hub1024", "car_hub2048", "car_hub4096"};
-        static const bool per_class = env_int("RSK_HUB_TIMERS", 0) != 0;
+        static const bool per_class = RSK_KNOB(RSK_HUB_TIMERS, 0) != 0;
         ScopedTimer tm(ctx, per_class ? kHubNames[c] : "car_heavy", stream);
         kern<<<dim3((unsigned)(gblocks * n)), dim3(64 * g.waves), g.lds, stream>>>(
             plan->heavy_items[c].as<HeavyItem>(), n, plan->hcol.as<int>(), d_assign, d_key, S, N, g.lg, g.dpad,
@@ -1505,7 +1500,7 @@ int rsk_car_plan_create(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col
         for (int32_t i = 0; i < Q; ++i) RSK_CHECK(rows[i] >= 0 && rows[i] < P, "rows[%d]=%d out of range", i, rows[i]);
     // rows up to light_max go to the LDS tiles, the rest to the side kernels;
     // RSK_LIGHT_MAX = 16 sends the 17..32 rows to car_side16 (no heavy tiles)
-    static const int light_max = env_int("RSK_LIGHT_MAX", kLightMax) == kPairMax ? kPairMax : kLightMax;
+    static const int light_max = RSK_KNOB(RSK_LIGHT_MAX, kLightMax) == kPairMax ? kPairMax : kLightMax;
     return plan_create(ctx, row_ptr, col_idx, P, rows, Q, light_max, out);
 }
 
@@ -1557,7 +1552,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
               "N*S too large (N=%d S=%d; need N*S < 2^30, N < 2^25)", N, S);
     RSK_CHECK(out_target, "null out_target");
     // compact path (rsk_car16.hip) whenever node ids fit 16 bits
-    static const bool compact_ok = env_int("RSK_COMPACT", 1) != 0;
+    static const bool compact_ok = RSK_KNOB(RSK_COMPACT, 1) != 0;
     // (S < 2^23: the tile kernel's 24-bit code offsets, rsk_car16.hip t16_rows64)
     const bool compact = N <= kMaxNodes16 && S < (1 << 23) && compact_ok;
     if (!compact && N >= kPackMaxN && plan->n_sorted_rows > 0) {
@@ -1621,9 +1616,9 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     sb.zkey = d_zkey;
     sb.target = d_target;
     sb.score = d_score;
-    static const int ablate = env_int("RSK_ABLATE_TILE", 0);
-    static const int order = env_int("RSK_TILE_ORDER", 2);
-    static const int sl_max = [] { int v = env_int("RSK_TILE_SL", 64); return v >= 1 && v <= 64 ? v : 64; }();
+    static const int ablate = RSK_ABLATION(RSK_ABLATE_TILE);
+    static const int order = RSK_KNOB(RSK_TILE_ORDER, 2);
+    static const int sl_max = [] { int v = RSK_KNOB(RSK_TILE_SL, 64); return v >= 1 && v <= 64 ? v : 64; }();
     // The compact side rows run inside the lean tile launch (car_fused16_kernel)
     // where they fit its footprint: their latency-bound workgroups share the
     // CUs with the memory-bound tiles instead of running alone (RSK_FUSE=0:
@@ -1632,7 +1627,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     //   classes >= kSideBig (above 128): 4-wave teams at the front of the grid,
     //     while the largest row's table fits the tile's LDS; otherwise on a side
     //     stream beside the tiles (RSK_SIDE_BIG_AUX=0: on the main stream).
-    static const bool fuse_env = env_int("RSK_FUSE", 1) != 0;
+    static const bool fuse_env = RSK_KNOB(RSK_FUSE, 1) != 0;
     const size_t lean_lds = tile16_lds_bytes(plan->rmax, 6, 0);
     int fuse_c = -1, fside_blocks = 0;
     SideArgs fsa, fba;
@@ -1668,7 +1663,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         side16_apply_geometry(fba, side16_geometry(dmax, N, 4));
         fba.xcd_per = 0;
     }
-    static const bool big_aux = env_int("RSK_SIDE_BIG_AUX", 1) != 0;
+    static const bool big_aux = RSK_KNOB(RSK_SIDE_BIG_AUX, 1) != 0;
     // fused classes [lo, hi): class 0 (17..32, RSK_LIGHT_MAX=16 plans only) runs on its own
     const bool c0 = plan->side_end[0] > plan->side_beg[0];
     plan->fused_lo = c0 ? kNumSide : (fuse_c >= 0 || plan->side_end[1] == plan->side_beg[1] ? 0 : kSideBig);
@@ -1716,7 +1711,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         const size_t lds = tile16_lds_bytes(plan->rmax, a.lsl, a.rec_cap);
         RSK_CHECK(plan->recmax <= kTileRecInts, "tile records exceed %d ints", kTileRecInts);
         // one timer over both launches; RSK_TILE_TIMERS=1: car_tile (lean) and car_tile_heavy apart
-        static const bool split = env_int("RSK_TILE_TIMERS", 0) != 0;
+        static const bool split = RSK_KNOB(RSK_TILE_TIMERS, 0) != 0;
         std::unique_ptr<ScopedTimer> tm(split ? nullptr : new ScopedTimer(ctx, "car_tile"));
         // lean tiles [0, T_lean) at full occupancy, then the heavy tiles (17..32 rows)
         // S < 64: one generic kernel scores every tile (no lean / heavy split)

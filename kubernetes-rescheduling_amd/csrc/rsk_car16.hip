@@ -197,7 +197,7 @@ int launch_prep(hipStream_t stream, const Prep16Args &a) {
     // 256 * max(SV, 256) threads within [2^16, 2^18] (config 3, SV = 1024:
     // 2^18; config 4, SV = 16: 2^16, prep 0.029 -> 0.024 ms).  RSK_PREP_THREADS
     // overrides (experiments).
-    static const int env_threads = [] { const char *e = getenv("RSK_PREP_THREADS"); return e ? atoi(e) : 0; }();
+    static const int env_threads = RSK_KNOB(RSK_PREP_THREADS, 0);
     const int target_threads = env_threads >= 1024 ? env_threads
                                                    : (int)std::min<int64_t>(256 * 1024, std::max<int64_t>(65536, 256LL * std::max(SV, 256)));
     const int npb = (int)std::max<int64_t>(1, ceil_div((int64_t)a.N * SV, target_threads));
@@ -910,7 +910,7 @@ __device__ __forceinline__ void w64_score_light(const Tile16Args &a, const W64 &
 // kL64 phase 2: the records of each class, spread over the 4 waves.
 template <bool kScore, bool kOff32, bool kHeavy>
 __device__ __forceinline__ void w64_score(const Tile16Args &a, const W64 &w, cint_ptr m, cint_ptr R, int wave, int s0) {
-    if (a.ablate & 4) {  // profiling: the target stores alone (every record, zero-case value, no LDS reads)
+    if (RSK_ABL(a) & 4) {  // profiling: the target stores alone (every record, zero-case value, no LDS reads)
         for (int c = 0; c < kNumCls; ++c) {
             const cint_ptr Rc = R + m[10 + c];
             for (int j = wave; j < m[4 + c]; j += 4) emit64<kScore, kOff32>(a, Rc[kClsW[c] * j], s0, w, w.zt, w.zs);
@@ -942,7 +942,7 @@ __device__ __forceinline__ void tile16_block(const Tile16Args &a, unsigned bid) 
     const cint_ptr m = const_ptr(a.meta) + (size_t)tile * kMetaW;
     const int img_off = m[0], nrows = m[1], rec_off = m[2], rec_ints = m[3];
     if (kL64) {
-        if (!(a.ablate & 1)) t16_load_image<true, kOff32>(a, img, img_off, nrows, s0);
+        if (!(RSK_ABL(a) & 1)) t16_load_image<true, kOff32>(a, img, img_off, nrows, s0);
         else for (int i = threadIdx.x; i < nrows * 64; i += kTileThreads) img[i] = kCellPad;  // ablation: no loads, no garbage
         W64 w;
         w.img = reinterpret_cast<const char *>(lds);
@@ -954,7 +954,7 @@ __device__ __forceinline__ void tile16_block(const Tile16Args &a, unsigned bid) 
             w.zs = zs;
         }
         __syncthreads();
-        if (a.ablate & 2) return;  // profiling ablation: no scoring (results are wrong)
+        if (RSK_ABL(a) & 2) return;  // profiling ablation: no scoring (results are wrong)
         const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
         w64_score<kScore, kOff32, kHeavy>(a, w, m, const_ptr(a.recs) + RSK_B16(rec_off, a.n_recs, 16u), wave, s0);
         return;
@@ -965,7 +965,7 @@ __device__ __forceinline__ void tile16_block(const Tile16Args &a, unsigned bid) 
         *reinterpret_cast<int4 *>(rec + i) =
             *reinterpret_cast<const int4 *>(a.recs + RSK_B16(rec_off + i + 3, a.n_recs, 16u) - 3);
     }
-    if (!(a.ablate & 1)) t16_load_image<false, kOff32>(a, img, img_off, nrows, s0);
+    if (!(RSK_ABL(a) & 1)) t16_load_image<false, kOff32>(a, img, img_off, nrows, s0);
     else for (int i = threadIdx.x; i < (nrows << lsl); i += kTileThreads) img[i] = kCellPad;
 
     Lane16 L;
@@ -980,7 +980,7 @@ __device__ __forceinline__ void tile16_block(const Tile16Args &a, unsigned bid) 
     }
     if (threadIdx.x == 0) rec[a.rec_cap] = 0;  // work-unit counter
     __syncthreads();
-    if (a.ablate & 2) return;  // profiling ablation: no scoring (results are wrong)
+    if (RSK_ABL(a) & 2) return;  // profiling ablation: no scoring (results are wrong)
     Img16 im;
     im.w = img;
     im.lsl = lsl;
@@ -1090,7 +1090,7 @@ int launch_fused16(hipStream_t stream, const Tile16Args &a, const SideArgs &sa, 
                    bool score, bool off32, unsigned tile_blocks, size_t lds) {
     RSK_CHECK(a.lsl == 6 && (size_t)a.img_cells * 4 <= (size_t)kT16Rows * 256 && tile_blocks % 8 == 0,
               "fused launch needs 64-scenario tiles");
-    static const int spread = [] { const char *e = getenv("RSK_FUSE_SPREAD"); return e ? std::max(1, atoi(e)) : 2; }();
+    static const int spread = std::max(1, RSK_KNOB(RSK_FUSE_SPREAD, 2));
     FuseMap f;
     f.big_blocks = (int)(8 * ceil_div((int64_t)ba.n_rows * ba.nchunk, 8));
     f.side_rows = (int)ceil_div(side_blocks, 8);
@@ -1106,7 +1106,7 @@ int launch_fused16(hipStream_t stream, const Tile16Args &a, const SideArgs &sa, 
                                &car_fused16_kernel<true, false, false>,  &car_fused16_kernel<true, true, false>,
                                &car_fused16_kernel<false, false, true>,  &car_fused16_kernel<false, true, true>,
                                &car_fused16_kernel<true, false, true>,   &car_fused16_kernel<true, true, true>};
-    static const bool pipe = [] { const char *e = getenv("RSK_FUSE_PIPE"); return e ? atoi(e) != 0 : true; }();
+    static const bool pipe = RSK_KNOB(RSK_FUSE_PIPE, 1) != 0;
     const K kern = kerns[(pipe ? 4 : 0) + (score ? 2 : 0) + (off32 ? 1 : 0)];
     RSK_CHECK(lds <= 160 * 1024, "fused tile needs %zu B of LDS", lds);
     if (lds > 64 * 1024)

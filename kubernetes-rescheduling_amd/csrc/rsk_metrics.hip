@@ -1080,7 +1080,7 @@ int rsk_cut_cost_rows(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_i
         auto *bins = ctx->work[4].as<unsigned long long>();
         RSK_HIP(hipMemsetAsync(bins, 0, (size_t)kCutBins * S * 8, ctx->stream));
         ScopedTimer tm(ctx, "cut_cost");
-        static const bool wave_kernel = !getenv("RSK_CUT_THREAD") || atoi(getenv("RSK_CUT_THREAD")) == 0;
+        static const bool wave_kernel = RSK_KNOB(RSK_CUT_THREAD, 0) == 0;
         if (S >= 32 && wave_kernel) {  // lane = scenario, edge-balanced (nnz may be device-resident: grid-stride)
             const int nw = 4096;  // waves per 64-scenario chunk
             const int64_t waves = ceil_div(S, 64) * nw;

@@ -1,6 +1,7 @@
 // rsk_runtime.hip — contexts, errors, staging and kernel timing for librsk.so.
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "rsk_common.h"
@@ -17,6 +18,11 @@ void set_error(const char *fmt, ...) {
 }
 
 const char *last_error() { return g_err; }
+
+int env_int(const char *name, int dflt) {  // RSK_KNOB in -DRSK_ENV_KNOBS variant builds only
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
 
 int DevBuf::reserve(size_t need) {
     if (need <= bytes && ptr) return RSK_OK;
@@ -76,7 +82,7 @@ int aux_fork(rsk_ctx *ctx, int k) {
         if (!ctx->aux[i]) {
             // side work is short and latency-bound: with RSK_SIDE_PRIO=1 its
             // workgroups are dispatched ahead of the tile kernel's as CUs free up
-            static const bool prio = getenv("RSK_SIDE_PRIO") && atoi(getenv("RSK_SIDE_PRIO")) != 0;
+            static const bool prio = RSK_KNOB(RSK_SIDE_PRIO, 0) != 0;
             int lo = 0, hi = 0;
             if (prio) RSK_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
             RSK_HIP(hipStreamCreateWithPriority(&ctx->aux[i], hipStreamNonBlocking, prio ? hi : lo));

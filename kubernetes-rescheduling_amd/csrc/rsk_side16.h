@@ -301,7 +301,7 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk) {
     }
     const int ndk = min(nd, K);
     const int ndmax = __builtin_amdgcn_readfirstlane(dpp_max(ndk));
-    if (a.ablate & 2) {  // profiling: pass 1 only (results are wrong)
+    if (RSK_ABL(a) & 2) {  // profiling: pass 1 only (results are wrong)
         if (tw == 0 && s0 + lane < a.S) a.out_target[(size_t)(unsigned)oi * S + (unsigned)(s0 + lane)] = (int)f.w1 + nd;
         return;
     }
@@ -337,7 +337,7 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk) {
     b.init();
     // (1) the listed nodes, eight at a time (their codes gathered together); the
     // team's waves take turns
-    for (int i0 = tw * 8; i0 < ((a.ablate & 4) ? 0 : n2); i0 += 8 * kT) {
+    for (int i0 = tw * 8; i0 < ((RSK_ABL(a) & 4) ? 0 : n2); i0 += 8 * kT) {
         unsigned key[8], c[8];
         int delta[8];
 #pragma unroll
@@ -361,7 +361,7 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk) {
     }
     // (2) the lane's deviation nodes (first occurrence each) not counted >= 2 as a
     // pivot; the team's waves take turns
-    for (int k = tw; k < ((a.ablate & 8) ? 0 : ndmax); k += kT) {
+    for (int k = tw; k < ((RSK_ABL(a) & 8) ? 0 : ndmax); k += kT) {
         const unsigned t = k < ndk ? dl[k * 64 + lane] & 0xffffu : 0xffffu;
         bool ok = t < N;
         int cnt = 0;
@@ -423,7 +423,7 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk) {
     // the wave recounts those scenarios exactly, one at a time (the table and
     // the deviation lists are scratch from here on)
     unsigned long long sm = __builtin_amdgcn_ballot_w64(slow);
-    if (sm && !(a.ablate & 1)) {
+    if (sm && !(RSK_ABL(a) & 1)) {
         while (sm) {
             const int ln = __builtin_ctzll(sm);
             sm &= sm - 1ull;

@@ -67,7 +67,7 @@ SideGeom side16_geometry(int dmax, int N, int T) {
     // neighbour loads in flight per wave (with their code gathers: 2 kB VGPRs;
     // 4-wave teams live in the fused tile launch: <= 64 VGPRs; 16-wave teams:
     // <= 128)
-    static const bool kb16 = getenv("RSK_SIDE_KB16") && atoi(getenv("RSK_SIDE_KB16")) != 0;  // debug
+    static const bool kb16 = RSK_KNOB(RSK_SIDE_KB16, 0) != 0;  // debug
     g.kB = dmax <= 32 && !kb16 ? 8 : (g.T == 8 ? 32 : 16);
     // words: tab H | dl 64 K (also the recount's cells) | ndl 64 | dummy 64 |
     // h2 1 + h2cap (the entries counted >= 2: at most min(Dc, dmax / 2); a
@@ -126,7 +126,7 @@ int launch_side16(hipStream_t stream, const SideArgs &a0, const SideGeom &g0, bo
         return RSK_OK;
     }
     using K = void (*)(SideArgs);
-    static const bool pipe = [] { const char *e = getenv("RSK_SIDE_PIPE"); return e ? atoi(e) != 0 : true; }();
+    static const bool pipe = RSK_KNOB(RSK_SIDE_PIPE, 1) != 0;
 #define RSK_SIDE_P(W, T, B, O) (pipe ? &car_side16_kernel<W, T, B, O, true> : &car_side16_kernel<W, T, B, O, false>)
 #define RSK_SIDE_O(W, T, B) (off32 ? RSK_SIDE_P(W, T, B, true) : RSK_SIDE_P(W, T, B, false))
 #define RSK_SIDE_W(W) (g.kB == 8 ? RSK_SIDE_O(W, 1, 8) : RSK_SIDE_O(W, 1, 16))
