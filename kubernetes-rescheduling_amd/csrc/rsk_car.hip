@@ -1162,7 +1162,6 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
         const int p = rows ? rows[i] : i;
         const int d = rp[p + 1] - rp[p];
         plan->max_deg = std::max(plan->max_deg, d);
-        RSK_CHECK(d <= kMaxDegree, "a row has degree %d > %d (unsupported)", d, kMaxDegree);
         const int *nbp = ci.data() + rp[p];
         if (d <= plan->light_max) {
             light.push_back(i);
@@ -1554,7 +1553,9 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     // compact path (rsk_car16.hip) whenever node ids fit 16 bits
     static const bool compact_ok = RSK_KNOB(RSK_COMPACT, 1) != 0;
     // (S < 2^23: the tile kernel's 24-bit code offsets, rsk_car16.hip t16_rows64)
-    const bool compact = N <= kMaxNodes16 && S < (1 << 23) && compact_ok;
+    // (rows above kMaxDegree neighbours: the side tables count in 16 bits, so
+    // such a plan runs the wide path, whose car_bigrow counts in 32)
+    const bool compact = N <= kMaxNodes16 && S < (1 << 23) && plan->max_deg <= kMaxDegree && compact_ok;
     if (!compact && N >= kPackMaxN && plan->n_sorted_rows > 0) {
         // the wide sorted tile classes pack node << 8 | row into 32 bits: route
         // 17..64 rows through the mid kernel instead (variant built once)

@@ -184,7 +184,7 @@ __device__ __forceinline__ int side_pivot3(int x) {  // majority of lanes 0, 21,
 // candidates are: the table's entries with C >= 2 (a handful), and the lane's
 // deviation nodes — both small sets.
 template <int kW, int kT, int kB, bool kOff32, bool kPipe, bool kGlobal = false>
-__device__ __forceinline__ void side16_block(const SideArgs &a, int blk) {
+__device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slot = -1) {
     static_assert(kT == 1 || kT == kW, "a team is one wave or the whole workgroup");
     extern __shared__ __attribute__((aligned(16))) unsigned slds[];
     const int lane = (int)threadIdx.x & 63;
@@ -204,7 +204,7 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk) {
 
     // kGlobal (one team per workgroup): the team's table, lists and merge area in
     // global scratch (a table beyond the LDS); the same code with global atomics
-    unsigned *base = kGlobal ? a.gscratch + (size_t)(unsigned)blk * (a.lds_team >> 2)
+    unsigned *base = kGlobal ? a.gscratch + (size_t)(unsigned)(slot >= 0 ? slot : blk) * (a.lds_team >> 2)
                              : slds + (size_t)team * (a.lds_team >> 2);
     SideTab tb;
     tb.tab = base;

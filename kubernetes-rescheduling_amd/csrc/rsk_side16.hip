@@ -39,6 +39,16 @@ namespace rsk {
 // (a.xcd_per: workgroups per XCD run).
 template <int kW, int kT, int kB, bool kOff32, bool kPipe, bool kGlobal = false>
 __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(SideArgs a) {
+    if (kGlobal) {  // a capped grid strides over the items; work area = the resident block's slot
+        static_assert(!kGlobal || kT == kW, "global work areas are per workgroup team");
+        const int items = a.n_rows * a.nchunk;
+        for (int blk = (int)blockIdx.x; blk < items; blk += (int)gridDim.x) {
+            side16_block<kW, kT, kB, kOff32, kPipe, kGlobal>(a, blk, (int)blockIdx.x);
+            glob_fence(true);
+            __syncthreads();  // every wave is done with the area before the next item clears it
+        }
+        return;
+    }
     int blk = (int)blockIdx.x;
     if (a.xcd_per) blk = (int)(blockIdx.x & 7u) * a.xcd_per + (int)(blockIdx.x >> 3);
     side16_block<kW, kT, kB, kOff32, kPipe, kGlobal>(a, blk);
@@ -117,11 +127,14 @@ int launch_side16(hipStream_t stream, const SideArgs &a0, const SideGeom &g0, bo
     a.gscratch = nullptr;
     if (global) {
         RSK_CHECK(scratch, "a relation row of degree %d needs a %zu-B table: no scratch", g.dmax, g.lds_team);
-        RSK_TRY(scratch->reserve((size_t)blocks * g.lds_team));
+        // one work area per resident workgroup, not per item: at most 1024
+        // workgroups (4 per CU) and 256 MiB of areas; they stride over the items
+        const int64_t gblocks = std::max<int64_t>(1, std::min<int64_t>({items, 1024, (int64_t)((256u << 20) / g.lds_team)}));
+        RSK_TRY(scratch->reserve((size_t)gblocks * g.lds_team));
         a.gscratch = scratch->as<unsigned>();
         using KG = void (*)(SideArgs);
         const KG kg = off32 ? &car_side16_kernel<8, 8, 32, true, false, true> : &car_side16_kernel<8, 8, 32, false, false, true>;
-        kg<<<dim3((unsigned)blocks), dim3(64 * 8), 0, stream>>>(a);
+        kg<<<dim3((unsigned)gblocks), dim3(64 * 8), 0, stream>>>(a);
         RSK_HIP(hipGetLastError());
         return RSK_OK;
     }

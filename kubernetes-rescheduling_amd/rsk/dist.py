@@ -460,7 +460,8 @@ class RowShardedRounds:
             # value back and add zero deltas at index 0
             if delta:
                 self.be.cut_delta(assign, S, evict, target, r0, r1, N, cut_local)
-            moved = (evict >= 0) & (target >= 0)
+            # the move rule of rsk_rows_apply / rsk_rows_cut_delta: evict in [0, P), target in [0, N)
+            moved = (evict >= 0) & (evict < assign.numel() // S) & (target >= 0) & (target < N)
             av = assign.view(-1, S)
             ep = evict.clamp(min=0).long()
             old = av[ep, sidx].long()

@@ -32,6 +32,8 @@ def lib():
         vp, i32 = C.c_void_p, C.c_int32
         L.oracle_car.argtypes = [vp, vp, i32, vp, i32, vp, vp, vp, i32, vp, i32, vp, vp, C.c_int]
         L.oracle_car.restype = C.c_int
+        L.oracle_car_sparse.argtypes = L.oracle_car.argtypes
+        L.oracle_car_sparse.restype = C.c_int
         for f in (L.oracle_spread, L.oracle_binpack):
             f.argtypes = [vp, vp, vp, i32, i32, vp]
             f.restype = None
@@ -76,6 +78,21 @@ def car(row_ptr, col_idx, assign, S, cap, use, hazard, N, rows=None, threads=1):
     assign, cap, use, hazard = _c(assign, np.int32), _c(cap, np.int32), _c(use, np.int32), _c(hazard, np.uint8)
     lib().oracle_car(_p(row_ptr), _p(col_idx), P, _p(assign), S, _p(cap), _p(use), _p(hazard), N, _p(rows_a), Q,
                      _p(tgt), _p(sc), threads)
+    return tgt, sc
+
+
+def car_sparse(row_ptr, col_idx, assign, S, cap, use, hazard, N, rows=None, threads=1, want_score=True):
+    """CAR by the sparse restatement (oracle_car_sparse: the row's entries plus a
+    per-scenario zero case, the same decisions as `car`); (target[Q*S], score or None)."""
+    row_ptr, col_idx = _c(row_ptr, np.int32), _c(col_idx if len(col_idx) else [0], np.int32)
+    P = row_ptr.shape[0] - 1
+    rows_a = None if rows is None else _c(rows, np.int32)
+    Q = P if rows_a is None else rows_a.shape[0]
+    tgt = np.empty(Q * S, np.int32)
+    sc = np.empty(Q * S, np.int32) if want_score else None
+    assign, cap, use, hazard = _c(assign, np.int32), _c(cap, np.int32), _c(use, np.int32), _c(hazard, np.uint8)
+    lib().oracle_car_sparse(_p(row_ptr), _p(col_idx), P, _p(assign), S, _p(cap), _p(use), _p(hazard), N, _p(rows_a),
+                            Q, _p(tgt), _p(sc), threads)
     return tgt, sc
 
 

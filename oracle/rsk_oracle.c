@@ -109,6 +109,121 @@ int oracle_car(const int32_t *row_ptr, const int32_t *col_idx, int32_t P,
 }
 
 /* ------------------------------------------------------------------------
+ * CAR, sparse restatement — the same decision as car_one (rescheduling.py:
+ * 188-214) without the O(N) passes per cell, so every cell of a full-size
+ * batch can be checked (tests/test_gpu_headline.py).  Every non-hazard node
+ * the row does not reach scores 0, so:
+ *   - no neighbour lands on a non-hazard node -> max score 0 (or no candidate):
+ *     every non-hazard node ties, a per-scenario constant ("zero case")
+ *     computed once per scenario by car_one's own tie rule;
+ *   - otherwise the maximum is >= 1 and only reached nodes can hold it: count
+ *     the row's entries per node (duplicates count, as in car_one), take the
+ *     nodes at the maximum, a single one wins outright, else the first in index
+ *     order with the largest rem > -1 (None when every rem <= -1).
+ * Pinned to car_one (oracle_car) on random graphs and to the golden fixtures
+ * in tests/test_oracle_golden.py.  Work is split over (16-scenario block, row
+ * chunk) items so one block's hazard / use bytes stay in the core's cache.
+ * ---------------------------------------------------------------------- */
+int oracle_car_sparse(const int32_t *row_ptr, const int32_t *col_idx, int32_t P,
+                      const int32_t *assign, int32_t S, const int32_t *cap,
+                      const int32_t *use, const uint8_t *hazard, int32_t N,
+                      const int32_t *rows, int32_t Q, int32_t *out_target,
+                      int32_t *out_score, int nthreads)
+{
+    if (!rows) Q = P;
+    int32_t *zt = (int32_t *)malloc(sizeof(int32_t) * (S > 0 ? S : 1));
+    int32_t *zm = (int32_t *)malloc(sizeof(int32_t) * (S > 0 ? S : 1));
+    int32_t maxdeg = 1;
+    for (int64_t i = 0; i < (int64_t)Q; ++i) {
+        int32_t p = rows ? rows[i] : (int32_t)i;
+        int32_t d = row_ptr[p + 1] - row_ptr[p];
+        if (d > maxdeg) maxdeg = d;
+    }
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(static)
+#endif
+    for (int32_t s = 0; s < S; ++s) {  /* the zero case: car_one with an empty row */
+        int32_t nc = 0, first = -1, t = TGT_NONE;
+        int64_t rmax = -1;
+        for (int32_t n = 0; n < N; ++n) {
+            if (hazard[(int64_t)n * S + s]) continue;
+            if (first < 0) first = n;
+            ++nc;
+            int64_t rem = (int64_t)cap[n] - (int64_t)use[(int64_t)n * S + s];
+            if (rem > rmax) { rmax = rem; t = n; }
+        }
+        zt[s] = nc == 0 ? TGT_NO_CANDIDATE : (nc == 1 ? first : t);
+        zm[s] = nc == 0 ? -1 : 0;
+    }
+    const int32_t SB = 16, RC = 2048;
+    const int64_t nblk = ((int64_t)S + SB - 1) / SB, nrc = ((int64_t)Q + RC - 1) / RC;
+    int any_nc = 0;
+#ifdef _OPENMP
+#pragma omp parallel reduction(|| : any_nc)
+#endif
+    {
+        int32_t *cnt = (int32_t *)calloc((size_t)(N > 0 ? N : 1), sizeof(int32_t));
+        int32_t *touched = (int32_t *)malloc(sizeof(int32_t) * (size_t)maxdeg);
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+        for (int64_t item = 0; item < nblk * nrc; ++item) {
+            const int32_t s0 = (int32_t)(item / nrc) * SB;
+            const int32_t s1 = s0 + SB < S ? s0 + SB : S;
+            const int64_t i0 = (item % nrc) * RC, i1 = i0 + RC < Q ? i0 + RC : Q;
+            for (int64_t i = i0; i < i1; ++i) {
+                const int32_t p = rows ? rows[i] : (int32_t)i;
+                for (int32_t s = s0; s < s1; ++s) {
+                    int32_t nt = 0;
+                    for (int32_t k = row_ptr[p]; k < row_ptr[p + 1]; ++k) {
+                        const int32_t q = col_idx[k];
+                        if (q == p) continue;
+                        const int32_t a = assign[(int64_t)q * S + s];
+                        if (a < 0 || a >= N || hazard[(int64_t)a * S + s]) continue;
+                        if (cnt[a]++ == 0) touched[nt++] = a;
+                    }
+                    int32_t t, m = 0;
+                    if (nt == 0) {
+                        t = zt[s];
+                        m = zm[s];
+                    } else {
+                        int32_t nbest = 0, only = -1;
+                        for (int32_t j = 0; j < nt; ++j) {
+                            const int32_t c = cnt[touched[j]];
+                            if (c > m) { m = c; nbest = 1; only = touched[j]; }
+                            else if (c == m) ++nbest;
+                        }
+                        if (nbest == 1) {
+                            t = only;
+                        } else {
+                            int64_t rmax = -1;
+                            t = TGT_NONE;
+                            for (int32_t j = 0; j < nt; ++j) {
+                                const int32_t n = touched[j];
+                                if (cnt[n] != m) continue;
+                                const int64_t rem = (int64_t)cap[n] - (int64_t)use[(int64_t)n * S + s];
+                                if (rem > rmax || (rem == rmax && t >= 0 && n < t)) { rmax = rem; t = n; }
+                            }
+                        }
+                        for (int32_t j = 0; j < nt; ++j) cnt[touched[j]] = 0;
+                    }
+                    out_target[i * S + s] = t;
+                    if (out_score) out_score[i * S + s] = m;
+                    if (t == TGT_NO_CANDIDATE) any_nc = 1;
+                }
+            }
+        }
+        free(touched);
+        free(cnt);
+    }
+    free(zt);
+    free(zm);
+    (void)nthreads;
+    return any_nc ? 1 : 0;
+}
+
+/* ------------------------------------------------------------------------
  * spread — rescheduling.py:89-101: min over non-hazard nodes of
  * (len(pods), nodename); ties -> smallest name in str order.  RuntimeError if
  * none (:98-99).  binpack — rescheduling.py:121-133: max of (cpu_pct, name).

@@ -1,9 +1,11 @@
 """GPU parity at the benchmark shapes (BASELINE.json configs 3-5).
 
-Each test runs librsk at the size bench.py times and checks it against the
-oracle (oracle/rsk_oracle.c, pinned by the reference's own fixtures) on every
-hard row plus a random sample, bit-exactly.  The kernels' template instances
-are the ones the bench runs: no score output, S >= 64 (64-scenario tiles).
+Each test runs librsk at the size bench.py times and checks EVERY cell
+against the oracle's sparse restatement (oracle_car_sparse, pinned to the
+literal per-cell oracle and to the reference's fixtures in
+tests/test_oracle_golden.py), bit-exactly; the literal oracle re-checks the
+hard rows.  The kernels' template instances are the ones the bench runs: no
+score output, S >= 64 (64-scenario tiles); config 2 at S = 1.
 """
 import os
 from types import SimpleNamespace
@@ -30,10 +32,38 @@ def _rows_to_check(c, n_sample, seed):
     return np.unique(np.concatenate([hard, sample])).astype(np.int32), hard
 
 
+def _all_cells(c, S, t, label):
+    """Every (row, scenario) cell of t [P, S] against oracle_car_sparse."""
+    from oracle import oracle as orc
+    exp, _ = orc.car_sparse(c.row_ptr, c.col_idx, c.assign, S, c.cap_cpu, c.use_cpu, c.hazard, c.N,
+                            threads=THREADS, want_score=False)
+    exp = exp.reshape(c.P, S)
+    bad = np.argwhere(t != exp)
+    assert bad.size == 0, f"{label}: {len(bad)} of {t.size} cells differ; first row {bad[0][0]} s {bad[0][1]}: " \
+                          f"gpu {t[bad[0][0], bad[0][1]]} oracle {exp[bad[0][0], bad[0][1]]}"
+    return t.size
+
+
+def test_config2_2k64_s1_all_rows(ctx, synth_golden):
+    """Config 2 exactly as bench.py runs it: 2k pods x 64 nodes, S = 1 (the
+    generic-tile instance), every row through CarPlan, plus the reference's
+    own decisions for scenario 0 of its golden 2k/64 batch."""
+    from rsk import api, synth
+    g = synth_golden["2k64"]
+    c = synth.make_cluster(2_000, 64, S=1, seed=0)
+    plan = api.CarPlan(c.row_ptr, c.col_idx, ctx=ctx)
+    tgt, _ = plan.execute(c.assign, 1, c.cap_cpu, c.use_cpu, c.hazard, c.N)
+    plan.close()
+    assert _all_cells(c, 1, tgt.reshape(c.P, 1), "config 2") == 2_000
+    g0 = [sc for sc in g["scenarios"] if sc["s"] == 0][0]
+    assert tgt[g0["pods"]].tolist() == g0["car_target"]
+
+
 def test_config3_headline_s4096(ctx, synth_golden):
-    """100k pods x 5k nodes x 4096 scenarios (the headline batch): every
-    mid / hub row and 1000 sampled rows against the oracle, and the reference's
-    own 66 golden pods in the unperturbed scenario 0."""
+    """100k pods x 5k nodes x 4096 scenarios (the headline batch): all
+    409.6 M cells against the sparse oracle, every row of degree > 16 plus
+    200 sampled rows against the literal one, and the reference's own 66
+    golden pods in the unperturbed scenario 0."""
     from oracle import oracle as orc
     from rsk import api, synth
     P, N, S = 100_000, 5_000, 4096
@@ -46,7 +76,8 @@ def test_config3_headline_s4096(ctx, synth_golden):
     t = tgt.reshape(P, S)
     g = synth_golden["100k5k"]["scenarios"][0]
     assert t[g["pods"], 0].tolist() == g["car_target"]
-    rows, hard = _rows_to_check(c, 1000, 7)
+    assert _all_cells(c, S, t, "config 3") == 409_600_000
+    rows, hard = _rows_to_check(c, 200, 7)
     assert hard.size == 640 and info["mid_rows"] + info["heavy_rows"] == 201
     assert info["side_rows"] == (640 if info["light_max"] == 16 else 201)
     assert info["sorted_rows"] == (0 if info["light_max"] == 16 else 439)
@@ -58,9 +89,10 @@ def test_config3_headline_s4096(ctx, synth_golden):
 
 
 def test_config4_1m50k_s64(ctx):
-    """1M pods x 50k nodes x 64 scenarios: all hub and mid rows (max degree
-    1,756) plus 1000 sampled rows; also the row-sharded plans of 2 ranks
-    (the rows each rank owns) give the same targets."""
+    """1M pods x 50k nodes x 64 scenarios: all 64 M cells against the sparse
+    oracle, all hub and mid rows (max degree 1,756) plus 200 sampled rows
+    against the literal one; also the row-sharded plans of 2 ranks (the rows
+    each rank owns) give the same targets."""
     from oracle import oracle as orc
     from rsk import api, synth
     from rsk import dist as rdist
@@ -70,7 +102,8 @@ def test_config4_1m50k_s64(ctx):
     tgt, _ = plan.execute(c.assign, S, c.cap_cpu, c.use_cpu, c.hazard, N)
     plan.close()
     t = tgt.reshape(P, S)
-    rows, hard = _rows_to_check(c, 1000, 8)
+    assert _all_cells(c, S, t, "config 4") == 64_000_000
+    rows, hard = _rows_to_check(c, 200, 8)
     assert hard.size > 1000 and int(np.diff(c.row_ptr).max()) > 1000
     exp, _ = orc.car(c.row_ptr, c.col_idx, c.assign, S, c.cap_cpu, c.use_cpu, c.hazard, N, rows=rows,
                      threads=THREADS)

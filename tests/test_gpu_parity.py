@@ -649,3 +649,116 @@ def test_car_row_single_launch_vs_oracle(ctx):
         assert t == int(ot[0]), f"trial {trial}: N={N} k={k} target {t} != {int(ot[0])}"
         if int(ot[0]) != -2:
             assert sc == int(osc[0]), f"trial {trial}: score {sc} != {int(osc[0])}"
+
+
+def _check_car_sparse(ctx, row_ptr, col_idx, assign, S, cap, use, haz, N, rows=None, label=""):
+    """_check_car against the sparse oracle (pinned to the literal one in
+    tests/test_oracle_golden.py), multi-threaded, for the big cases."""
+    from oracle import oracle as orc
+    from rsk import api
+    tgt, sc = api.car_place(row_ptr, col_idx, assign, S, cap, use, haz, N, rows=rows, ctx=ctx, want_score=True)
+    rp, ci = _dedup_csr(row_ptr, col_idx)
+    ot, osc = orc.car_sparse(rp, ci, assign, S, cap, use, haz, N, rows=rows, threads=min(16, os.cpu_count() or 1))
+    bad = np.nonzero(tgt != ot)[0]
+    assert bad.size == 0, f"{label}: {bad.size} targets differ, first cell {bad[0]}: gpu {tgt[bad[0]]} oracle {ot[bad[0]]}"
+    assert np.array_equal(sc, osc), f"{label}: scores differ"
+
+
+def test_car_many_global_table_rows_s768(ctx):
+    """80 rows of degree 22,000 over 30,000 nodes at S = 768 — 960
+    work items whose tables live in global memory, more than the capped grid
+    of resident work areas holds, so the workgroups stride over the items and
+    reuse their areas."""
+    rng = np.random.default_rng(2200)
+    P, N, S, deg, nbig = 30000, 30000, 768, 22000, 80
+    lens = rng.integers(0, 3, P)
+    lens[:nbig] = deg
+    rp = np.zeros(P + 1, np.int32)
+    rp[1:] = np.cumsum(lens)
+    ci = np.empty(int(rp[-1]), np.int32)
+    for p in range(P):
+        if lens[p] == deg:
+            ci[rp[p]:rp[p + 1]] = rng.choice(np.arange(nbig, P), deg, replace=False)
+        else:
+            ci[rp[p]:rp[p + 1]] = rng.integers(0, P, lens[p])
+    base = rng.permutation(P) % N
+    a = np.repeat(base[:, None], S, axis=1).astype(np.int32)
+    flip = rng.random((P, S)) < 0.01
+    a[flip] = rng.integers(-1, N, flip.sum())
+    cap = rng.choice([4000, 8000], N).astype(np.int32)
+    use = rng.integers(0, 8000, N * S).astype(np.int32)
+    haz = (rng.random(N * S) < 0.2).astype(np.uint8)
+    _check_car_sparse(ctx, rp, ci, a.reshape(-1), S, cap, use, haz, N, rows=np.arange(0, nbig + 40, dtype=np.int32),
+                      label="80 global-table rows, S=768")
+
+
+@pytest.mark.parametrize("S", [1, 3])
+def test_car_row_above_65535_neighbours(ctx, S):
+    """a row of degree 69,000 (beyond the side tables' 16-bit
+    counts) over a compact-sized node set: the plan is accepted and runs the
+    wide path (car_bigrow, 32-bit counts); a pile-up scenario puts every
+    neighbour on one node (count 69,000)."""
+    rng = np.random.default_rng(6900 + S)
+    P, N, deg = 70000, 50, 69000
+    lens = rng.integers(0, 3, P)
+    lens[0] = deg
+    rp = np.zeros(P + 1, np.int32)
+    rp[1:] = np.cumsum(lens)
+    ci = rng.integers(0, P, int(rp[-1])).astype(np.int32)
+    ci[:deg] = rng.choice(np.arange(1, P), deg, replace=False)
+    a = rng.integers(-1, N, (P, S)).astype(np.int32)
+    a[:, 0] = 7
+    cap = rng.choice([4000, 8000], N).astype(np.int32)
+    use = rng.integers(0, 8000, N * S).astype(np.int32)
+    haz = (rng.random(N * S) < 0.2).astype(np.uint8)
+    haz.reshape(N, S)[7, 0] = 0
+    from rsk import api
+    plan = api.CarPlan(rp, ci, ctx=ctx)
+    assert plan.info()["max_degree"] == deg
+    plan.close()
+    _check_car_sparse(ctx, rp, ci, a.reshape(-1), S, cap, use, haz, N, rows=np.arange(0, 64, dtype=np.int32),
+                      label=f"deg 69000 S={S}")
+
+
+@pytest.mark.parametrize("N", [1, 63, 1023, 1024, 1025, 4097, 70000])
+def test_random_candidates_order_and_count(ctx, N):
+    """rsk_random_candidates (the drop-in random's candidate list)
+    equals the reference's `[n for n in nodes_name if n not in hazard]`
+    (rescheduling.py:149-150) in order and count, across the multi-chunk
+    compaction (N > 1024) and the inputs above 64 KB, at several hazard
+    densities (none, some, all but one, all)."""
+    from rsk import api
+    rng = np.random.default_rng(N)
+    for p in (0.0, 0.1, 0.5, 0.97, 1.0):
+        h = (rng.random(N) < p).astype(np.uint8)
+        got = api.random_candidates(h, N, ctx=ctx)
+        assert np.array_equal(got, np.nonzero(h == 0)[0].astype(np.int32)), (N, p)
+    h = np.ones(N, np.uint8)
+    h[N - 1] = 0
+    assert api.random_candidates(h, N, ctx=ctx).tolist() == [N - 1]
+
+
+@pytest.mark.parametrize("seed", [0, 1, 7, 12345])
+def test_dropin_random_matches_reference_choice(ctx, seed):
+    """The drop-in random() picks what the reference's `rd.choice(candidates)`
+    (rescheduling.py:149-153, CPython's global Random) picks after the same
+    random.seed, on a 3,000-node cluster with hazards, and it leaves the global
+    state where the reference leaves it."""
+    import random as pyrandom
+
+    import rescheduling as R
+    from kubernetes import client
+    rng = np.random.default_rng(seed)
+    nodes = [f"node-{i:05d}" for i in range(3000)]
+    haz = [n for n in nodes if rng.random() < 0.3]
+    hs = set(haz)
+    pyrandom.seed(seed)
+    want = pyrandom.choice([n for n in nodes if n not in hs])
+    after = pyrandom.random()
+    info = {"metadata": {"name": "d0", "namespace": "default"},
+            "spec": {"template": {"spec": {"affinity": None}}}}
+    client.CREATED.clear()
+    pyrandom.seed(seed)
+    R.random(info, haz, nodes)
+    assert client.CREATED[-1][1]["spec"]["template"]["spec"]["nodeName"] == want
+    assert pyrandom.random() == after

@@ -252,3 +252,78 @@ def test_pick_max_pod_metric_edges_vs_reference():
         assert (pods[r][0] if r >= 0 else None) == pick_edge_expected(case), case
         raised += "raises" in case
     assert raised >= 10 and any(c.get("picked") and any(p[2] == 0 for p in c["pods"]) for c in cases)
+
+
+def _sparse_as_car(monkeypatch):
+    from oracle import oracle as orc
+    monkeypatch.setattr(orc, "car", orc.car_sparse)
+
+
+@pytest.mark.parametrize("fixture", ["wm", "edge"])
+def test_car_sparse_against_reference_fixtures(monkeypatch, wm_golden, edge_golden, fixture):
+    """The sparse CAR restatement (oracle_car_sparse, the full-batch checker of
+    tests/test_gpu_headline.py) decides the reference's own 256 workmodel
+    snapshots and 40 edge cases exactly as the reference did."""
+    _sparse_as_car(monkeypatch)
+    if fixture == "wm":
+        for k, snap in enumerate(wm_golden["snapshots"]):
+            assert oracle_decision("communication", snap, wm_golden["relation"]) == \
+                golden_decision(snap["results"]["communication"]), k
+    else:
+        for case in edge_golden["cases"]:
+            assert oracle_decision("communication", case, case["relations"]) == \
+                golden_decision(case["results"]["communication"]), case["name"]
+
+
+def test_car_sparse_synth_golden(synth_golden):
+    """... and the reference's 2k/64 (8 scenarios) and 100k/5k decisions."""
+    from oracle import oracle as orc
+    from rsk import synth
+    g = synth_golden["2k64"]
+    c = synth.make_cluster(g["P"], g["N"], S=g["S"], seed=g["seed"])
+    t, _ = orc.car_sparse(c.row_ptr, c.col_idx, c.assign, c.S, c.cap_cpu, c.use_cpu, c.hazard, c.N, threads=4)
+    t = t.reshape(c.P, c.S)
+    for sc in g["scenarios"]:
+        assert t[sc["pods"], sc["s"]].tolist() == sc["car_target"], sc["s"]
+    g = synth_golden["100k5k"]
+    c = synth.make_cluster(g["P"], g["N"], S=1, seed=0)
+    sc = g["scenarios"][0]
+    t, _ = orc.car_sparse(c.row_ptr, c.col_idx, c.assign, 1, c.cap_cpu, c.use_cpu, c.hazard, c.N, rows=sc["pods"])
+    assert t.tolist() == sc["car_target"]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_car_sparse_equals_car_one(seed):
+    """oracle_car_sparse == oracle_car (the literal per-cell restatement) on
+    random graphs built to hit every branch: duplicate entries and self edges
+    (the literal one counts entries as given), assignments outside [0, N),
+    hazard densities up to all-hazard, crowded ties with rem < 0 (None), a
+    single non-hazard node (the zero case's outright winner), empty rows, hubs,
+    row subsets and S not a multiple of the 16-scenario block."""
+    from oracle import oracle as orc
+    rng = np.random.default_rng(900 + seed)
+    seen = set()
+    for trial in range(12):
+        N = int(rng.choice([1, 2, 3, 7, 40, 300]))
+        P = int(rng.integers(2, 400))
+        S = int(rng.choice([1, 5, 16, 17, 40]))
+        lens = rng.integers(0, 7, P)
+        lens[rng.integers(0, P, 3)] = rng.integers(20, 120, 3)
+        rp = np.zeros(P + 1, np.int32)
+        rp[1:] = np.cumsum(lens)
+        ci = rng.integers(0, P, int(rp[-1])).astype(np.int32)
+        a = rng.integers(-2, N + 2, P * S).astype(np.int32)
+        cap = rng.choice([1000, 2000, 4000], N).astype(np.int32)
+        use = rng.choice([0, 999, 1000, 1001, 2000, 2500, 5000], N * S).astype(np.int32)
+        p_h = float(rng.choice([0.0, 0.3, 0.9, 1.0]))
+        h = (rng.random(N * S) < p_h).astype(np.uint8)
+        if trial % 4 == 3:            # exactly one non-hazard node in every scenario
+            h[:] = 1
+            h.reshape(N, S)[rng.integers(0, N), :] = 0
+        rows = None if trial % 2 else np.sort(rng.choice(P, min(P, 50), replace=False)).astype(np.int32)
+        et, es = orc.car(rp, ci, a, S, cap, use, h, N, rows=rows)
+        gt, gs = orc.car_sparse(rp, ci, a, S, cap, use, h, N, rows=rows, threads=3)
+        assert np.array_equal(gt, et), (seed, trial, int((gt != et).sum()))
+        assert np.array_equal(gs, es), (seed, trial)
+        seen.update(np.unique(np.minimum(et, 0)).tolist())
+    assert seen == {-2, -1, 0}, seen    # no candidate, None and real targets all occurred

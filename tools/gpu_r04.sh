@@ -1,0 +1,37 @@
+#!/bin/bash
+# Round-4 GPU session on one box.  usage: tools/gpu_r04.sh OUTDIR [steps...]
+# steps: test (pytest -m gpu), smoke, bench (headline), b2k (config 2),
+#        b1m (config 4), brounds (config 5), prof (rocprof trace + PMC of headline
+#        and 1m50k), profh / prof1m (one config), dropin
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+out=gpurun_out/${1:-r04}; shift
+mkdir -p "$out"
+export TMPDIR=/tmp
+step() {  # step <name> <seconds> <cmd...>
+    local name=$1 secs=$2; shift 2
+    timeout -k 10 "$secs" "$@" > "$out/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc $(date +%T) $(grep -o '"ms_per_step": [0-9.]*' "$out/$name.log" | head -1) $(grep -o '"parity_sample_ok": [a-z]*' "$out/$name.log" | head -1) $(grep -E -o '[0-9]+ (passed|failed)[^=]*' "$out/$name.log" | tail -1)"
+    [ $rc -ne 0 ] && { tail -25 "$out/$name.log"; exit $rc; }
+    return 0
+}
+for s in "${@:-test smoke bench}"; do
+  for w in $s; do
+    case $w in
+      test) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
+      test:*) step "pytest_${w#test:}" 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${w#test:}" ;;
+      smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+      bench) step bench_headline 600 python -u bench.py ;;
+      b2k) step bench_2k64 300 python -u bench.py --config 2k64 --no-cpu-baseline ;;
+      b1m) step bench_1m50k 600 python -u bench.py --config 1m50k --no-cpu-baseline ;;
+      brounds) step bench_rounds 300 python -u bench.py --config rounds --no-cpu-baseline ;;
+      dropin) step dropin 400 python -u tools/dropin_latency.py --calls 40 --out "$out/dropin.json" ;;
+      prof) for c in headline 1m50k; do
+              ./tools/gpu_prof.sh $c "$out/prof_$c" > "$out/prof_$c.log" 2>&1 || { tail -5 "$out/prof_$c.log"; exit 1; }
+              echo "== prof $c done $(date +%T)"; done ;;
+      profh) ./tools/gpu_prof.sh headline "$out/prof_headline" > "$out/prof_headline.log" 2>&1 || { tail -5 "$out/prof_headline.log"; exit 1; } ;;
+      prof1m) ./tools/gpu_prof.sh 1m50k "$out/prof_1m50k" > "$out/prof_1m50k.log" 2>&1 || { tail -5 "$out/prof_1m50k.log"; exit 1; } ;;
+      *) echo "unknown step $w"; exit 2 ;;
+    esac
+  done
+done
