@@ -315,7 +315,7 @@ def main():
                     help="multi-GPU layout (SURVEY §8e): scenario sharding (default; 1m50k: rows)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--row-rounds", type=int, default=20,
+    ap.add_argument("--row-rounds", type=int, default=256,
                     help="pod-row sharding: rounds of the row-sharded multi-round loop to time (0: skip)")
     ap.add_argument("--no-kernel-events", action="store_true", default=os.environ.get("RSK_BENCH_NO_EVENTS") == "1",
                     help="time the steps without per-kernel HIP events")
@@ -509,21 +509,32 @@ def main():
             rr2 = rdist.RowShardedRounds(rshard, be2)
             rr2.run(a3, T["use_cpu"], T["cap_cpu"], pc, pm, N, S, 1, threshold=thr)
             a3.copy_(T["assign"])
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        t2 = time.perf_counter()
-        with torch.cuda.stream(s2):
-            res2 = rr2.run(a3, T["use_cpu"], T["cap_cpu"], pc, pm, N, S, R, threshold=thr)
-        torch.cuda.synchronize(dev)
-        el2 = time.perf_counter() - t2
-        if world > 1:
-            e = torch.tensor([el2], dtype=torch.float64, device=dev)
-            dist.all_reduce(e, op=dist.ReduceOp.MAX)
-            el2 = float(e.item())
+        def timed_run(nr):
+            torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
+            t2 = time.perf_counter()
+            with torch.cuda.stream(s2):
+                out = rr2.run(a3, T["use_cpu"], T["cap_cpu"], pc, pm, N, S, nr, threshold=thr)
+            torch.cuda.synchronize(dev)
+            el2 = time.perf_counter() - t2
+            if world > 1:
+                e = torch.tensor([el2], dtype=torch.float64, device=dev)
+                dist.all_reduce(e, op=dist.ReduceOp.MAX)
+                el2 = float(e.item())
+            return out, el2
+
+        # the setup alone (R = 0: the rank's partials, the full cut count, the
+        # u16 shadow, the final all-reduce), then the timed R rounds from the
+        # generated state; steady state = (R rounds - setup) / R
+        _, el0 = timed_run(0)
+        a3.copy_(T["assign"])
+        res2, el2 = timed_run(R)
         same = bool(torch.equal(res2["target"], res["target"]) and torch.equal(res2["cut"], res["cut"]))
         be2.close()
         rounds_leg = {"rounds": R, "threshold_pct": thr, "ms_per_round": round(el2 * 1e3 / R, 4),
+                      "setup_ms": round(el0 * 1e3, 4),
+                      "steady_ms_per_round": round((el2 - el0) * 1e3 / R, 4),
                       "stream_ordered_matches_synced": same,
                       "ms_per_round_phase_synced": round(el * 1e3 / R, 4),
                       "phase_ms_per_round": {k: round(v / R, 4) for k, v in res["ms"].items()},
@@ -532,6 +543,58 @@ def main():
                       "collectives": "int64 all-reduce N*S cpu + mem partials, int64 MAX all-reduce S, "
                                      "all-gather S changed slices, int64 all-reduce S cut cost"}
         be.close()
+
+    k3_leg = None
+    if by_rows:
+        # north-star kernel 3 over the whole batch (all P rows, device pointers):
+        # per-node count / CPU / memory sums (rsk_node_reduce), the load std and the
+        # cut cost, each its own launch timed with HIP events on the context's stream
+        from rsk._lib import RSK_F_DEVICE, check
+        pc = torch.from_numpy(c.pod_cpu).to(dev)
+        pm = torch.from_numpy(c.pod_mem.astype(np.int64)).to(dev)
+        cnt = torch.empty(N * S, dtype=torch.int32, device=dev)
+        cs = torch.empty(N * S, dtype=torch.int64, device=dev)
+        ms_ = torch.empty(N * S, dtype=torch.int64, device=dev)
+        std = torch.empty(S, dtype=torch.float64, device=dev)
+        cut = torch.empty(S, dtype=torch.int64, device=dev)
+        rp_d = torch.from_numpy(c.row_ptr).to(dev)
+        ci_d = torch.from_numpy(c.col_idx).to(dev)
+        L, h = ctx.lib, ctx.handle
+
+        def k3():
+            check(L.rsk_node_reduce(h, T["assign"].data_ptr(), P, S, pc.data_ptr(), pm.data_ptr(), N, cnt.data_ptr(),
+                                    cs.data_ptr(), ms_.data_ptr(), RSK_F_DEVICE))
+            check(L.rsk_load_std(h, T["use_cpu"].data_ptr(), T["cap_cpu"].data_ptr(), N, S, std.data_ptr(),
+                                 RSK_F_DEVICE))
+            check(L.rsk_cut_cost(h, rp_d.data_ptr(), ci_d.data_ptr(), P, T["assign"].data_ptr(), S, None,
+                                 cut.data_ptr(), RSK_F_DEVICE))
+        k3()
+        ctx.reset_profiling()
+        ctx.set_profiling(True)
+        reps = 10
+        for _ in range(reps):
+            k3()
+        torch.cuda.synchronize(dev)
+        ctx.set_profiling(False)
+        k3_leg = {}
+        alg3 = {"node_reduce": 4 * P * S + 12 * P + 20 * N * S, "load_std": 8 * N * S + 4 * N,
+                "cut_cost": 4 * (P + 1) + 4 * c.nnz + 4 * P * S + 4 * c.nnz * S}
+        for name in ("node_reduce", "load_std", "cut_cost"):
+            tms, n = ctx.kernel_time(name)
+            if n:
+                k3_leg[name] = {"avg_ms": round(tms / n, 4), "launches_per_call": n // reps,
+                                "algorithmic_bytes": alg3[name],
+                                "algorithmic_GBps": round(alg3[name] / (tms / n / 1e3) / 1e9, 1)}
+        # parity of kernel 3 on a few scenarios' worth of rows: the oracle's sums
+        from oracle import oracle as orc
+        k = 4
+        sub = np.ascontiguousarray(c.assign.reshape(P, S)[:, :k]).reshape(-1)
+        ecnt, ecpu, emem = orc.node_reduce(sub, P, k, c.pod_cpu, c.pod_mem.astype(np.int64), N)
+        gsl = lambda t: t.view(N, S)[:, :k].cpu().numpy().reshape(-1)  # noqa: E731
+        k3_leg["parity_sample_ok"] = bool(np.array_equal(gsl(cnt), ecnt) and np.array_equal(gsl(cs), ecpu)
+                                          and np.array_equal(gsl(ms_), emem))
+        k3_leg["note"] = ("algorithmic bytes: node_reduce reads assign + pod cpu/mem and writes the N*S count/cpu/mem"
+                          " words; load_std reads use (+ pct temp); cut_cost reads CSR + assign + one gather per edge")
 
     alg = {k: alg_bytes(k, P, N, S, info) for k in kernels}
     B = algorithmic_bytes(P, N, S, c.nnz)
@@ -602,6 +665,7 @@ def main():
             line["roofline_scope"] = ("rank 0's rows: the plan's distinct neighbour pods of its row range "
                                       "(SURVEY §8e per-rank distinct-column roofline)")
             line["row_sharded_rounds"] = rounds_leg
+            line["kernel3"] = k3_leg
             line["allgather_ms_per_step"] = None if gather_ms is None else round(gather_ms, 4)
             line["end_to_end_ms_per_step"] = round(ms_step + (gather_ms or 0.0), 4)
         print(json.dumps(line), flush=True)

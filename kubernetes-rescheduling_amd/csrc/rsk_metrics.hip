@@ -402,6 +402,125 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(const int *__restrict_
     if (mem) atomicAdd(&mem[o], (unsigned long long)pod_mem[p]);
 }
 
+// The segmented form (S >= 32).  What-if scenarios perturb a common base, so a
+// pod sits on the same node in most scenarios.  The pods are bucketed by a key
+// node (the majority of three sampled scenarios; a counting sort: count, scan,
+// scatter), and a wave walks a run of consecutive bucketed pods with lane =
+// scenario: a lane whose pod sits on the key node adds it to a register
+// accumulator, flushed once per key (three coalesced atomics per 64 scenarios
+// per node instead of per pod); a lane whose pod sits elsewhere adds it
+// directly.  The sums are integers, so the result is the atomic kernel's,
+// whatever the order.  podmonitor.py:104-121 (pods grouped by node),
+// nodemonitor.py:24-46 (per-node sums).
+__device__ __forceinline__ int nr_key(const int *__restrict__ assign, int p, int S, int N) {
+    const size_t b = (size_t)p * S;
+    const int x = assign[b], y = assign[b + S / 3], z = assign[b + (2 * S) / 3];
+    const int k = (x == y || x == z) ? x : y;
+    return (unsigned)k < (unsigned)N ? k : N;
+}
+
+__global__ __launch_bounds__(256) void nr_count_kernel(const int *__restrict__ assign, int P, int S, int N,
+                                                       int *__restrict__ off) {
+    const int p = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (p < P) atomicAdd(&off[nr_key(assign, p, S, N)], 1);
+}
+
+// exclusive scan of off[0..n) in place (one workgroup), copied to cur
+__global__ __launch_bounds__(1024) void nr_scan_kernel(int *__restrict__ off, int *__restrict__ cur, int n) {
+    __shared__ int part[1024];
+    const int t = (int)threadIdx.x, per = (n + 1023) / 1024;
+    const int b = min(n, t * per), e = min(n, b + per);
+    int sum = 0;
+    for (int i = b; i < e; ++i) sum += off[i];
+    part[t] = sum;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
+        const int v = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int run = part[t] - sum;
+    for (int i = b; i < e; ++i) {
+        const int c = off[i];
+        off[i] = run;
+        cur[i] = run;
+        run += c;
+    }
+}
+
+__global__ __launch_bounds__(256) void nr_scatter_kernel(const int *__restrict__ assign, int P, int S, int N,
+                                                         int *__restrict__ cur, int *__restrict__ perm,
+                                                         int *__restrict__ keys) {
+    const int p = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (p >= P) return;
+    const int k = nr_key(assign, p, S, N);
+    const int pos = atomicAdd(&cur[k], 1);
+    perm[pos] = p;
+    keys[pos] = k;
+}
+
+constexpr int kNrRun = 128;  // bucketed pods per wave
+__global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restrict__ assign, int P, int S,
+                                                              const int *__restrict__ pod_cpu,
+                                                              const long long *__restrict__ pod_mem, int N,
+                                                              const int *__restrict__ perm,
+                                                              const int *__restrict__ keys, int runs,
+                                                              int *__restrict__ cnt,
+                                                              unsigned long long *__restrict__ cpu,
+                                                              unsigned long long *__restrict__ mem) {
+    const int w = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    const int chunk = w / runs, run = w - chunk * runs;
+    const int s = chunk * 64 + (int)(threadIdx.x & 63);
+    if (chunk * 64 >= S) return;
+    const bool live = s < S;
+    const int j0 = run * kNrRun, j1 = min(P, j0 + kNrRun);
+    const cint_ptr cperm = const_ptr(perm), ckeys = const_ptr(keys), ccpu = const_ptr(pod_cpu);
+    int rk = -1, rc = 0;
+    long long rcpu = 0, rmem = 0;
+    auto flush = [&]() {
+        if (live && rk >= 0 && rk < N && rc > 0) {
+            const size_t o = (size_t)rk * S + s;
+            atomicAdd(&cnt[o], rc);
+            atomicAdd(&cpu[o], (unsigned long long)rcpu);
+            if (mem) atomicAdd(&mem[o], (unsigned long long)rmem);
+        }
+        rc = 0;
+        rcpu = rmem = 0;
+    };
+    constexpr int kB = 8;
+    for (int j = j0; j < j1; j += kB) {
+        int a[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {  // the batch's assign rows in flight together
+            const int jj = min(j + u, j1 - 1);
+            a[u] = live ? __builtin_nontemporal_load(&assign[(size_t)cperm[jj] * S + s]) : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            if (j + u >= j1) break;
+            const int p = cperm[j + u], k = ckeys[j + u];
+            if (k != rk) {  // wave-uniform: a new key node
+                flush();
+                rk = k;
+            }
+            const int c = ccpu[p];
+            const long long m = mem ? pod_mem[p] : 0;
+            if (a[u] == k) {
+                ++rc;
+                rcpu += c;
+                rmem += m;
+            } else if ((unsigned)a[u] < (unsigned)N) {
+                const size_t o = (size_t)a[u] * S + s;
+                atomicAdd(&cnt[o], 1);
+                atomicAdd(&cpu[o], (unsigned long long)(long long)c);
+                if (mem) atomicAdd(&mem[o], (unsigned long long)m);
+            }
+        }
+    }
+    flush();
+}
+
 // get_resource_usage.py:37: int(round(u / c * 100)) — IEEE fp64 divide, then an
 // fp64 multiply (no FMA can form), then round-half-even (rint).
 __global__ __launch_bounds__(256) void cpu_pct_kernel(const int *__restrict__ use, const int *__restrict__ cap, int N,
@@ -952,7 +1071,25 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
     RSK_HIP(hipMemsetAsync(d_cnt, 0, NS * 4, ctx->stream));
     RSK_HIP(hipMemsetAsync(d_cs, 0, NS * 8, ctx->stream));
     if (d_ms) RSK_HIP(hipMemsetAsync(d_ms, 0, NS * 8, ctx->stream));
-    if (PS) {
+    if (PS && S >= 32) {  // segmented: bucket the pods by key node, then per-key register sums
+        const int runs = (int)ceil_div(P, kNrRun);
+        const int64_t waves = (int64_t)runs * ceil_div(S, 64);
+        RSK_CHECK(waves < (int64_t)INT32_MAX - 4, "node_reduce grid too large");
+        RSK_TRY(ctx->work[0].reserve((size_t)P * 8));
+        RSK_TRY(ctx->work[1].reserve((size_t)(N + 1) * 8));
+        int *perm = ctx->work[0].as<int>(), *keys = perm + P;
+        int *off = ctx->work[1].as<int>(), *cur = off + (N + 1);
+        ScopedTimer tm(ctx, "node_reduce");
+        RSK_HIP(hipMemsetAsync(off, 0, (size_t)(N + 1) * 4, ctx->stream));
+        const unsigned pb = (unsigned)ceil_div(P, 256);
+        nr_count_kernel<<<pb, 256, 0, ctx->stream>>>(d_assign, P, S, N, off);
+        nr_scan_kernel<<<1, 1024, 0, ctx->stream>>>(off, cur, N + 1);
+        nr_scatter_kernel<<<pb, 256, 0, ctx->stream>>>(d_assign, P, S, N, cur, perm, keys);
+        node_reduce_seg_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, ctx->stream>>>(
+            d_assign, P, S, d_cpu, reinterpret_cast<const long long *>(d_mem), N, perm, keys, runs, d_cnt,
+            reinterpret_cast<unsigned long long *>(d_cs), reinterpret_cast<unsigned long long *>(d_ms));
+        RSK_HIP(hipGetLastError());
+    } else if (PS) {
         ScopedTimer tm(ctx, "node_reduce");
         node_reduce_kernel<<<(unsigned)ceil_div(PS, 256), 256, 0, ctx->stream>>>(
             d_assign, P, S, d_cpu, reinterpret_cast<const long long *>(d_mem), N, d_cnt,

@@ -373,7 +373,9 @@ class RowShardedRounds:
         import torch
         dev = assign.device
         r0, r1 = self.shard.r0, self.shard.r1
-        t = {"monitor": 0.0, "detect": 0.0, "evict": 0.0, "place": 0.0, "exchange": 0.0, "update": 0.0, "cut": 0.0}
+        t = {"setup": 0.0, "monitor": 0.0, "detect": 0.0, "evict": 0.0, "place": 0.0, "exchange": 0.0, "update": 0.0,
+             "cut": 0.0}
+        c = time.perf_counter()
 
         def tick(name, t0):
             t[name] += (time.perf_counter() - t0) * 1e3
@@ -401,6 +403,7 @@ class RowShardedRounds:
             rows = assign[r0 * S:r1 * S]
             shadow = torch.where((rows >= 0) & (rows < N), rows, torch.full_like(rows, 65535)).to(torch.int16)
         evs, tgs, cuts = [], [], []
+        tick("setup", c)
         sidx = torch.arange(S, device=dev)
         pc64 = pod_cpu.to(torch.int64)
         mask32 = (1 << 32) - 1
@@ -484,7 +487,10 @@ class RowShardedRounds:
             evs.append(evict)
             tgs.append(target)
             cuts.append(cut)
-        cpu, _ = self._partials(assign, pod_cpu, pod_mem, N, S)
+        # the final usage from the partials kept exact round by round (no second
+        # pass over the rows)
+        cpu = lp_cpu.clone()
+        allreduce_(cpu, "sum", self.group)
         use_final = (base + cpu).to(torch.int32)
         empty = torch.empty(0, S, dtype=torch.int32, device=dev)
         return {"evict": torch.stack(evs) if evs else empty, "target": torch.stack(tgs) if tgs else empty,

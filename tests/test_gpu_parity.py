@@ -762,3 +762,28 @@ def test_dropin_random_matches_reference_choice(ctx, seed):
     R.random(info, haz, nodes)
     assert client.CREATED[-1][1]["spec"]["template"]["spec"]["nodeName"] == want
     assert pyrandom.random() == after
+
+
+@pytest.mark.parametrize("P,N,S,p_flip", [(3000, 97, 33, 0.01), (5000, 300, 64, 0.3), (20000, 2000, 130, 0.01),
+                                          (4000, 50, 1, 0.0), (1_000_000, 50_000, 64, 0.01)])
+def test_node_reduce_segmented_vs_oracle(ctx, P, N, S, p_flip):
+    """Kernel 3's per-node count / CPU / memory sums (podmonitor.py:104-121,
+    nodemonitor.py:24-46) against the oracle: the segmented kernel (S >= 32:
+    pods bucketed by key node, register sums per key) on perturbed batches,
+    heavily perturbed ones (30 % of placements redrawn: most lanes off the key),
+    a partial last chunk (S = 130), assignments outside [0, N) (skipped), and
+    the atomic kernel at S = 1; the last case is config 4's size."""
+    from oracle import oracle as orc
+    from rsk import api
+    rng = np.random.default_rng(P + S)
+    base = rng.integers(0, N, P)
+    a = np.repeat(base[:, None], S, axis=1).astype(np.int32)
+    flip = rng.random((P, S)) < p_flip
+    a[flip] = rng.integers(-2, N + 2, int(flip.sum()))
+    a[rng.integers(0, P, 50), :] = -1          # unscheduled pods
+    pod_cpu = rng.integers(50, 500, P).astype(np.int32)
+    pod_mem = rng.integers(1 << 20, 1 << 31, P).astype(np.int64)
+    got = api.node_reduce(a.reshape(-1), P, S, pod_cpu, pod_mem, N, ctx=ctx)
+    exp = orc.node_reduce(a.reshape(-1), P, S, pod_cpu, pod_mem, N)
+    for g, e, name in zip(got, exp, ("count", "cpu", "mem")):
+        assert np.array_equal(g, e), name
