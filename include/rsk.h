@@ -192,7 +192,9 @@ int rsk_cut_cost_rows(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_i
  *   out_evict[r*S+s]  = p, -1 when there is no hazard node or no pod on it
  *   out_target[r*S+s] = t: node, RSK_TARGET_NONE, RSK_TARGET_NO_CANDIDATE, or
  *                       RSK_TARGET_NO_EVICT (-3) when nothing was evicted.
- * assign[P*S] and use_cpu[N*S] are updated in place.  Row degree <= 4096.
+ * assign[P*S] and use_cpu[N*S] are updated in place.  Any row degree (the
+ * evicted pod's count table lives in the LDS, or in global work areas when its
+ * distinct nodes overflow it).
  * rsk_rounds_create deduplicates the CSR (self edges dropped, main.py:73) and
  * uploads it with pod_cpu[P] (millicores).                                   */
 #define RSK_TARGET_NO_EVICT (-3)

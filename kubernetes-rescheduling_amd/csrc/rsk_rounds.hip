@@ -29,7 +29,9 @@ struct rsk_rounds {
     rsk::DevBuf row_ptr, col, pod_cpu;
     rsk::DevBuf haz, most, evict, key_ws;
     rsk::DevBuf asg16;  // u16 shadow of assign for the eviction scan (N <= 65535, S % 8 == 0)
+    rsk::DevBuf gtab;   // global hash work areas (rows whose distinct nodes overflow the LDS)
     ~rsk_rounds() {
+        gtab.release();
         asg16.release();
         row_ptr.release();
         col.release();
@@ -45,35 +47,43 @@ namespace rsk {
 namespace {
 
 constexpr int kMoveThreads = 256;
-constexpr int kMoveMaxDeg = 4096;
 constexpr int kNoEvict = -3;
 
 __device__ __forceinline__ unsigned long long move_pack(int rem, int n) {  // (rem, -node), 0 = none
     return ((unsigned long long)((unsigned)rem ^ 0x80000000u) << 32) | (unsigned long long)(0x7fffffffu - (unsigned)n);
 }
 
-__global__ __launch_bounds__(kMoveThreads) void car_move_kernel(const int *__restrict__ row_ptr,
-                                                                const int *__restrict__ col,
-                                                                const int *__restrict__ pod_cpu, int *assign,
-                                                                int *use, const int *__restrict__ cap,
-                                                                const uint8_t *__restrict__ haz,
-                                                                const int *__restrict__ evict, int S, int N, int H,
-                                                                int update, int *__restrict__ out_target,
-                                                                unsigned short *__restrict__ asg16) {
-    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
-    unsigned *keys = lds, *cnts = lds + H;
-    unsigned long long *red64 = reinterpret_cast<unsigned long long *>(lds + 2 * H);  // best
-    unsigned *red = lds + 2 * H + 2;                                                   // M, n_at_M, n_free
-    const int s = blockIdx.x, tid = threadIdx.x;
+// One scenario s of car_move_kernel.  tab = the hash (keys[H] | cnts[H] | 8
+// reduction words): the workgroup's LDS, or (kGlobal: rows whose distinct
+// nodes overflow the LDS) its slot of a global work area, where every switch
+// from writing to reading goes through an agent-scope fence (plain loads may
+// hit stale L1 lines after atomics performed in L2).
+template <bool kGlobal>
+__device__ __forceinline__ void move_sync() {
+    if (kGlobal) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+    __syncthreads();
+}
+
+template <bool kGlobal>
+__device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, const int *__restrict__ col,
+                                             const int *__restrict__ pod_cpu, int *assign, int *use,
+                                             const int *__restrict__ cap, const uint8_t *__restrict__ haz,
+                                             const int *__restrict__ evict, int s, int S, int N, int H, int update,
+                                             int *__restrict__ out_target, unsigned short *__restrict__ asg16,
+                                             unsigned *tab) {
+    unsigned *keys = tab, *cnts = tab + H;
+    unsigned long long *red64 = reinterpret_cast<unsigned long long *>(tab + 2 * H);  // best
+    unsigned *red = tab + 2 * H + 2;                                                   // M, n_at_M, n_free
+    const int tid = threadIdx.x;
     const int p = evict[s];
     if (p < 0) {
         if (tid == 0) out_target[s] = kNoEvict;
         return;
     }
     const int b = row_ptr[p], d = row_ptr[p + 1] - b;
-    for (int k = tid; k < 2 * H; k += kMoveThreads) lds[k] = 0u;
-    if (tid < 8) lds[2 * H + tid] = 0u;
-    __syncthreads();
+    for (int k = tid; k < 2 * H; k += kMoveThreads) tab[k] = 0u;
+    if (tid < 8) tab[2 * H + tid] = 0u;
+    move_sync<kGlobal>();
     const unsigned mask = (unsigned)H - 1u;
     // A: count every neighbour on a non-hazard node
     for (int j = tid; j < d; j += kMoveThreads) {
@@ -88,12 +98,12 @@ __global__ __launch_bounds__(kMoveThreads) void car_move_kernel(const int *__res
         }
         atomicAdd(&cnts[h], 1u);
     }
-    __syncthreads();
+    move_sync<kGlobal>();
     // B: max count over the slots
     unsigned m = 0;
     for (int h = tid; h < H; h += kMoveThreads) m = max(m, cnts[h]);
     if (m) atomicMax(&red[0], m);
-    __syncthreads();
+    move_sync<kGlobal>();
     const unsigned M = red[0];
     if (M > 0) {  // C: nodes at the max count -> |best| and the best (rem, -node)
         unsigned long long best = 0;
@@ -123,7 +133,7 @@ __global__ __launch_bounds__(kMoveThreads) void car_move_kernel(const int *__res
             atomicMax(red64, best);
         }
     }
-    __syncthreads();
+    move_sync<kGlobal>();
     if (tid == 0) {
         const unsigned nbest = red[1];
         const unsigned long long best = *red64;
@@ -142,6 +152,27 @@ __global__ __launch_bounds__(kMoveThreads) void car_move_kernel(const int *__res
             assign[pc] = t;
             if (asg16) asg16[pc] = (unsigned short)t;
         }
+    }
+}
+
+// One workgroup per scenario (LDS hash), or kGlobal: a capped grid striding
+// over the scenarios, each workgroup with its own global work area.
+template <bool kGlobal>
+__global__ __launch_bounds__(kMoveThreads) void car_move_kernel(const int *__restrict__ row_ptr,
+                                                                const int *__restrict__ col,
+                                                                const int *__restrict__ pod_cpu, int *assign,
+                                                                int *use, const int *__restrict__ cap,
+                                                                const uint8_t *__restrict__ haz,
+                                                                const int *__restrict__ evict, int S, int N, int H,
+                                                                int update, int *__restrict__ out_target,
+                                                                unsigned short *__restrict__ asg16,
+                                                                unsigned *__restrict__ gtab) {
+    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
+    unsigned *tab = kGlobal ? gtab + (size_t)blockIdx.x * (size_t)(2 * H + 8) : lds;
+    for (int s = (int)blockIdx.x; s < S; s += (int)gridDim.x) {
+        car_move_one<kGlobal>(row_ptr, col, pod_cpu, assign, use, cap, haz, evict, s, S, N, H, update, out_target,
+                              asg16, tab);
+        if (kGlobal) move_sync<true>();  // the area is free before the next scenario clears it
     }
 }
 
@@ -199,23 +230,48 @@ __global__ __launch_bounds__(256) void pick16_kernel(const uint4 *__restrict__ a
 
 struct MoveGeom {
     int H;
-    size_t lds;
+    size_t lds;      // LDS bytes (0: the global work area)
+    int grid;        // workgroups (kGlobal: capped, striding over the scenarios)
     int rc;
 };
 
-MoveGeom move_geometry(const rsk_rounds *r) {
+// The hash holds the distinct candidate nodes of one row: at most min(dmax, N)
+// keys, load <= 1/2.  In the LDS while it fits (any degree when N <= ~10k);
+// beyond, in global work areas of at most 256 MiB together.
+MoveGeom move_geometry(rsk_rounds *r, int N, int S) {
     MoveGeom g;
-    g.H = next_pow2(std::max(2, 2 * r->dmax));
-    g.lds = ((size_t)2 * g.H + 8) * 4;
+    g.H = next_pow2(std::max(2, 2 * std::min(r->dmax, N)));
+    const size_t bytes = ((size_t)2 * g.H + 8) * 4;
     g.rc = RSK_OK;
-    if (g.lds > 160 * 1024) { set_error("rounds hash needs %zu B of LDS", g.lds); g.rc = RSK_EINVAL; return g; }
-    if (g.lds > 64 * 1024 &&
-        hipFuncSetAttribute(reinterpret_cast<const void *>(&car_move_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)g.lds) != hipSuccess) {
-        set_error("hipFuncSetAttribute failed");
-        g.rc = RSK_EHIP;
+    if (bytes <= 160 * 1024) {
+        g.lds = bytes;
+        g.grid = S;
+        if (g.lds > 64 * 1024 &&
+            hipFuncSetAttribute(reinterpret_cast<const void *>(&car_move_kernel<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds) != hipSuccess) {
+            set_error("hipFuncSetAttribute failed");
+            g.rc = RSK_EHIP;
+        }
+        return g;
     }
+    g.lds = 0;
+    g.grid = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)S, 1024, (int64_t)((256u << 20) / bytes)}));
+    g.rc = r->gtab.reserve((size_t)g.grid * bytes);
     return g;
+}
+
+int launch_move(rsk_rounds *r, hipStream_t st, const MoveGeom &g, int *assign, int *use, const int *cap,
+                const uint8_t *haz, const int *evict, int S, int N, int update, int *target, unsigned short *a16) {
+    if (g.lds)
+        car_move_kernel<false><<<dim3((unsigned)g.grid), dim3(kMoveThreads), g.lds, st>>>(
+            r->row_ptr.as<int>(), r->col.as<int>(), r->pod_cpu.as<int>(), assign, use, cap, haz, evict, S, N, g.H,
+            update, target, a16, nullptr);
+    else
+        car_move_kernel<true><<<dim3((unsigned)g.grid), dim3(kMoveThreads), 0, st>>>(
+            r->row_ptr.as<int>(), r->col.as<int>(), r->pod_cpu.as<int>(), assign, use, cap, haz, evict, S, N, g.H,
+            update, target, a16, r->gtab.as<unsigned>());
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
 }
 
 // Row-sharded loop glue: one thread per scenario.
@@ -329,7 +385,6 @@ int rsk_rounds_create(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_i
         dmax = std::max(dmax, (int)(ci.size() - r0));
         rp.push_back((int32_t)ci.size());
     }
-    RSK_CHECK(dmax <= kMoveMaxDeg, "row degree %d above %d", dmax, kMoveMaxDeg);
     auto *r = new rsk_rounds();
     r->ctx = ctx;
     r->P = P;
@@ -380,10 +435,8 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
     RSK_TRY(r->haz.reserve(NS));
     RSK_TRY(r->most.reserve((size_t)S * 4));
     RSK_TRY(r->key_ws.reserve((size_t)S * 8));
-    const MoveGeom g = move_geometry(r);
+    const MoveGeom g = move_geometry(r, N, S);
     RSK_TRY(g.rc);
-    const int H = g.H;
-    const size_t lds = g.lds;
     // the eviction scan reads a u16 shadow of assign when node ids fit (kept in
     // step by the move kernel); otherwise the int32 scan
     const bool s16 = N <= 65535 && S % 8 == 0 && PS > 0;
@@ -423,10 +476,8 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         }
         {
             ScopedTimer tm(ctx, "rounds_move");
-            car_move_kernel<<<dim3((unsigned)S), dim3(kMoveThreads), lds, st>>>(
-                r->row_ptr.as<int>(), r->col.as<int>(), r->pod_cpu.as<int>(), d_assign, d_use, d_cap,
-                r->haz.as<uint8_t>(), ev, S, N, H, 1, d_target + (size_t)round * S, a16);
-            RSK_HIP(hipGetLastError());
+            RSK_TRY(launch_move(r, st, g, d_assign, d_use, d_cap, r->haz.as<uint8_t>(), ev, S, N, 1,
+                                d_target + (size_t)round * S, a16));
         }
     }
     if (!dev) {
@@ -460,14 +511,12 @@ int rsk_rounds_place(rsk_rounds *r, const int32_t *assign, int32_t S, const int3
     RSK_TRY(stage_in(ctx, 3, hazard, NS, dev, reinterpret_cast<const void **>(&d_haz)));
     RSK_TRY(stage_in(ctx, 5, evict, (size_t)S * 4, dev, reinterpret_cast<const void **>(&d_evict)));
     RSK_TRY(stage_out(ctx, 4, out_target, (size_t)S * 4, dev, reinterpret_cast<void **>(&d_target)));
-    const MoveGeom g = move_geometry(r);
+    const MoveGeom g = move_geometry(r, N, S);
     RSK_TRY(g.rc);
     {
         ScopedTimer tm(ctx, "rounds_place");
-        car_move_kernel<<<dim3((unsigned)S), dim3(kMoveThreads), g.lds, ctx->stream>>>(
-            r->row_ptr.as<int>(), r->col.as<int>(), r->pod_cpu.as<int>(), const_cast<int *>(d_assign),
-            const_cast<int *>(d_use), d_cap, d_haz, d_evict, S, N, g.H, 0, d_target, nullptr);
-        RSK_HIP(hipGetLastError());
+        RSK_TRY(launch_move(r, ctx->stream, g, const_cast<int *>(d_assign), const_cast<int *>(d_use), d_cap, d_haz,
+                            d_evict, S, N, 0, d_target, nullptr));
     }
     if (!dev) {
         RSK_TRY(copy_back(ctx, out_target, d_target, (size_t)S * 4, false));

@@ -172,3 +172,38 @@ def test_rounds_none_and_no_candidate_mid_run(ctx):
                         use_cpu=use.astype(np.int32).reshape(-1))
     etg = _rounds_vs_oracle(ctx, c, S, R, S, threshold=120)
     assert (etg == -1).sum() > 100 and (etg == -2).sum() > 100 and (etg >= 0).sum() > 100
+
+
+@pytest.mark.parametrize("P,N,deg", [(12_000, 3_000, 5_000), (26_000, 30_000, 20_000)])
+def test_rounds_hub_above_4096_neighbours(ctx, P, N, deg):
+    """The loop takes any row CAR takes: a hub pod of degree 5,000
+    (its count table in the LDS) or 20,000 over 30,000 nodes (20,000 distinct
+    candidates: the table in global work areas).  The hub carries the largest
+    CPU, so every round evicts it from the hazard node it lands on and scores
+    it again; 24 rounds x 16 scenarios against oracle_rounds."""
+    rng = np.random.default_rng(deg)
+    S, R = 16, 24
+    lens = rng.integers(0, 3, P)
+    lens[5] = deg
+    rp = np.zeros(P + 1, np.int32)
+    rp[1:] = np.cumsum(lens)
+    ci = rng.integers(0, P, int(rp[-1])).astype(np.int32)
+    ci[rp[5]:rp[6]] = rng.choice(np.delete(np.arange(P), 5), deg, replace=False)
+    pod_cpu = rng.integers(50, 500, P).astype(np.int32)
+    pod_cpu[5] = 900_000
+    base = rng.integers(0, N, P)
+    a = np.repeat(base[:, None], S, axis=1)
+    flip = rng.random((P, S)) < 0.05
+    a[flip] = rng.integers(0, N, int(flip.sum()))
+    a = a.astype(np.int32)
+    cap = np.full(N, 2_000_000, np.int32)
+    use = np.zeros((N, S), np.int64)
+    for s in range(S):
+        use[:, s] = np.bincount(a[:, s], weights=pod_cpu, minlength=N) + rng.integers(0, 200_000, N)
+    c = SimpleNamespace(P=P, N=N, row_ptr=rp, col_idx=ci, pod_cpu=pod_cpu, assign=a.reshape(-1), cap_cpu=cap,
+                        use_cpu=use.astype(np.int32).reshape(-1))
+    from oracle import oracle as orc
+    _, _, eev, _ = orc.rounds(rp, ci, pod_cpu, c.assign, S, cap, c.use_cpu, N, R)
+    assert (eev == 5).sum() > R * S // 2      # the hub is the evicted pod in most rounds
+    etg = _rounds_vs_oracle(ctx, c, S, R, S)
+    assert (etg >= 0).sum() > R * S // 2
