@@ -85,7 +85,18 @@ __global__ __launch_bounds__(kPrep0Threads) void car_prep0_kernel(const int *__r
     for (int i = (int)threadIdx.x; i < zc_words; i += kPrep0Threads) zc[i] = 0u;
     if (!capmax) return;
     int mc = 0;
-    for (int n = (int)threadIdx.x; n < N; n += kPrep0Threads) mc = max(mc, cap[n]);
+    // 16-B loads, 8 in flight per thread (one workgroup: the latency of the
+    // chain of loads is the kernel's time; N = 50k in 2 rounds instead of 49)
+    const int N4 = ((uintptr_t)cap % 16) == 0 ? N / 4 : 0;
+    const int4 *cap4 = reinterpret_cast<const int4 *>(cap);
+    for (int i0 = (int)threadIdx.x; i0 < N4; i0 += 8 * kPrep0Threads) {
+        int4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = cap4[min(i0 + u * kPrep0Threads, N4 - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) mc = max(mc, max(max(v[u].x, v[u].y), max(v[u].z, v[u].w)));
+    }
+    for (int n = 4 * N4 + (int)threadIdx.x; n < N; n += kPrep0Threads) mc = max(mc, cap[n]);
     mc = dpp_max(mc);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mc;
     __syncthreads();
