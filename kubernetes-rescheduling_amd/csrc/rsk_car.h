@@ -256,6 +256,19 @@ __device__ __forceinline__ bool code_inexact(unsigned c) { return (c >= 8194u &&
 
 constexpr unsigned kCodeHaz = 0u;
 constexpr unsigned kCodeNeg = 1u;
+
+// The code of remaining CPU rem (hazard: 0) with the exact window at B (above).
+__device__ __forceinline__ unsigned code16(int rem, bool haz, int B) {
+    if (haz) return kCodeHaz;
+    if (rem < 0) return kCodeNeg;
+    if (rem >= B) return 32769u + (unsigned)min(rem - B, 32766);
+    const unsigned x = (unsigned)rem;
+    if (x < 8192u) return 2u + x;
+    const int e = 31 - __clz((int)x);  // 13..30
+    if (e > 18) return 32768u;          // one bucket from 2^19 to B (exact ties resolve it)
+    return 2u + 8192u + (unsigned)(e - 13) * 4096u + ((x >> (e - 12)) & 0xfffu);
+}
+
 constexpr int kMaxNodes16 = 65535;  // node ids fit 16 bits, 0xffff stays free as the pad node
 
 struct Prep16Args {
@@ -311,6 +324,11 @@ struct SideArgs {
     int xcd_per;              // workgroups per XCD run (set by launch_side16)
     int ablate;               // profiling only (results wrong): 1 no exact recounts, 2 pass 1 only, 4 no (1), 8 no (2)
     unsigned *gscratch;       // teams whose table exceeds the LDS: lds_team bytes per block in global memory
+    // on-the-fly node state (kOTF launches, code == null): codes from cap / use /
+    // haz with B from *capmax, the zero case scanned per scenario when needed, so
+    // the launch depends on car_prep0 only and runs beside car_prep
+    const uint8_t *haz;
+    const int *capmax;
 };
 struct SideGeom {
     int dmax, Dc, H, hshift, K, T, W, kB;
@@ -330,8 +348,13 @@ int launch_fused16(hipStream_t stream, const Tile16Args &a, const SideArgs &sa, 
                    bool score, bool off32, unsigned tile_blocks, size_t lds);
 // scratch: device memory for rows whose table exceeds the LDS (grown on demand)
 int launch_side16(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch);
+// the same rows with node state computed on the fly (a.code null, a.haz / a.capmax set)
+int launch_side16_otf(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch);
 
 int launch_prep(hipStream_t stream, const Prep16Args &a);
+// launch_prep in two halves: car_prep0 (zero-case reset, max(cap)), then car_prep
+int launch_prep0(hipStream_t stream, const Prep16Args &a);
+int launch_prep_main(hipStream_t stream, const Prep16Args &a);
 int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off32, bool heavy, unsigned blocks,
                   size_t lds);
 size_t tile16_lds_bytes(int rmax, int lsl, int rec_cap);

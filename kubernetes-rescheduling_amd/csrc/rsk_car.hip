@@ -1331,6 +1331,8 @@ struct SideBufs {
     const unsigned short *code;
     const unsigned long long *zkey;
     int *target, *score;
+    const uint8_t *haz;   // on-the-fly launches (launch_side16_otf)
+    const int *capmax;
 };
 
 // car_side16 launches of classes [c0, c1) on `stream`, the longest rows first.
@@ -1365,17 +1367,24 @@ SideArgs side16_class_args(const rsk_car_plan *plan, int c, const SideBufs &b, i
 
 // classes [c0, c1) except `skip` (fused into the tile launch)
 int launch_side16_classes(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, const SideBufs &b, int S, int N,
-                          int c0, int c1, int skip = -1) {
+                          int c0, int c1, int skip = -1, bool otf = false) {
     const bool off32 = (int64_t)std::max(plan->P, plan->Q) * S * 4 < ((int64_t)1 << 32);
     static const bool per_class = RSK_KNOB(RSK_SIDE_TIMERS, 0) != 0;
     static const char *const kNames[kNumSide] = {"car_side32", "car_side128", "car_side512",
                                                  "car_side2048", "car_side8192", "car_side65535"};
     for (int c = c1 - 1; c >= c0; --c) {
         if (c == skip || plan->side_end[c] == plan->side_beg[c]) continue;
-        const SideArgs a = side16_class_args(plan, c, b, S, N);
+        SideArgs a = side16_class_args(plan, c, b, S, N);
         const SideGeom g = side16_geometry(plan->side_dmax[c], N);
         ScopedTimer tm(ctx, per_class ? kNames[c] : "car_side", stream);
-        RSK_TRY(launch_side16(stream, a, g, off32, &plan->side_scratch));
+        if (otf) {
+            a.code = nullptr;
+            a.haz = b.haz;
+            a.capmax = b.capmax;
+            RSK_TRY(launch_side16_otf(stream, a, g, off32, &plan->side_scratch));
+        } else {
+            RSK_TRY(launch_side16(stream, a, g, off32, &plan->side_scratch));
+        }
     }
     return RSK_OK;
 }
@@ -1592,21 +1601,18 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     int *d_zcnt = reinterpret_cast<int *>(d_zkey + S);
     // zc_key[S] u64, zc_cnt[S], the capmax word: zeroed / written by launch_prep
 
-    {   // K0: node state (codes and / or exact keys) + the zero case
-        Prep16Args pa;
-        pa.cap = d_cap;
-        pa.use = d_use;
-        pa.haz = d_haz;
-        pa.N = N;
-        pa.S = S;
-        pa.code = d_code;
-        pa.nodekey = d_key;
-        pa.zc_cnt = d_zcnt;
-        pa.zc_key = d_zkey;
-        pa.capmax = d_zcnt + S;  // the zc buffer's spare words
-        ScopedTimer tm(ctx, "car_prep");
-        RSK_TRY(launch_prep(ctx->stream, pa));
-    }
+    // K0: node state (codes and / or exact keys) + the zero case, launched below
+    Prep16Args pa;
+    pa.cap = d_cap;
+    pa.use = d_use;
+    pa.haz = d_haz;
+    pa.N = N;
+    pa.S = S;
+    pa.code = d_code;
+    pa.nodekey = d_key;
+    pa.zc_cnt = d_zcnt;
+    pa.zc_key = d_zkey;
+    pa.capmax = d_zcnt + S;  // the zc buffer's spare words
     SideBufs sb;
     sb.assign = d_assign;
     sb.key = d_key;
@@ -1617,6 +1623,8 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     sb.zkey = d_zkey;
     sb.target = d_target;
     sb.score = d_score;
+    sb.haz = d_haz;
+    sb.capmax = pa.capmax;
     static const int ablate = RSK_ABLATION(RSK_ABLATE_TILE);
     static const int order = RSK_KNOB(RSK_TILE_ORDER, 2);
     static const int sl_max = [] { int v = RSK_KNOB(RSK_TILE_SL, 64); return v >= 1 && v <= 64 ? v : 64; }();
@@ -1675,9 +1683,27 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     // (S < 64: the tiles are short, the fork's events would cost more than the overlap)
     const bool big_fork = compact && big_left && big_aux && plan->T > 0 && S >= 64;
     const int nfork = big_fork ? 1 : 0;
-    if (nfork) RSK_TRY(aux_fork(ctx, nfork));
-    if (compact && big_left)
-        RSK_TRY(launch_side16_classes(plan, ctx, big_fork ? ctx->aux[0] : ctx->stream, sb, S, N, big_hi, kNumSide));
+    if (big_fork) {
+        // The rows too big for the fused grid run on a side stream from the
+        // start: their node codes computed on the fly (they need car_prep0's
+        // max(cap) only), so their workgroups take CUs beside car_prep, before
+        // the fused grid fills every slot and starves them.
+        {
+            ScopedTimer tm(ctx, "car_prep");
+            RSK_TRY(launch_prep0(ctx->stream, pa));
+        }
+        RSK_TRY(aux_fork(ctx, nfork));
+        RSK_TRY(launch_side16_classes(plan, ctx, ctx->aux[0], sb, S, N, big_hi, kNumSide, -1, true));
+        ScopedTimer tm(ctx, "car_prep");
+        RSK_TRY(launch_prep_main(ctx->stream, pa));
+    } else {
+        {
+            ScopedTimer tm(ctx, "car_prep");
+            RSK_TRY(launch_prep(ctx->stream, pa));
+        }
+        if (compact && big_left)
+            RSK_TRY(launch_side16_classes(plan, ctx, ctx->stream, sb, S, N, big_hi, kNumSide));
+    }
     RSK_TRY(launch_side(plan, ctx, ctx->stream, sb, S, N, compact, fuse_c));
     const bool off32 = (int64_t)std::max(plan->P, plan->Q) * S * 4 < ((int64_t)1 << 32);
     if (plan->T > 0 && compact) {   // K1 tiles, 32-bit {code, node} cells

@@ -41,17 +41,6 @@ __device__ __forceinline__ unsigned dbg16(unsigned idx, unsigned lim, unsigned c
 // ---------------------------------------------------------------------------
 // node state
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ unsigned code16(int rem, bool haz, int B) {
-    if (haz) return kCodeHaz;
-    if (rem < 0) return kCodeNeg;
-    if (rem >= B) return 32769u + (unsigned)min(rem - B, 32766);
-    const unsigned x = (unsigned)rem;
-    if (x < 8192u) return 2u + x;
-    const int e = 31 - __clz((int)x);  // 13..30
-    if (e > 18) return 32768u;          // one bucket from 2^19 to B (exact ties resolve it)
-    return 2u + 8192u + (unsigned)(e - 13) * 4096u + ((x >> (e - 12)) & 0xfffu);
-}
-
 template <int V>
 struct VecT;
 template <> struct VecT<1> { typedef int I; typedef uint8_t H; typedef unsigned short C; };
@@ -194,11 +183,20 @@ static int prep_launch(hipStream_t stream, const Prep16Args &a, int SV, int npb,
 }
 
 int launch_prep(hipStream_t stream, const Prep16Args &a) {
+    RSK_TRY(launch_prep0(stream, a));
+    return launch_prep_main(stream, a);
+}
+
+int launch_prep0(hipStream_t stream, const Prep16Args &a) {
     RSK_CHECK(a.code || a.nodekey, "prep: nothing to write");
     RSK_CHECK(!a.code || a.capmax, "prep: codes need the capmax scratch");
     car_prep0_kernel<<<1, kPrep0Threads, 0, stream>>>(a.cap, a.N, reinterpret_cast<unsigned *>(a.zc_key), 3 * a.S,
                                                       a.code ? a.capmax : nullptr);
     RSK_HIP(hipGetLastError());
+    return RSK_OK;
+}
+
+int launch_prep_main(hipStream_t stream, const Prep16Args &a) {
     // 4 scenarios per thread when S % 4 == 0 (16-B use / key words, 8-B codes)
     const bool v4 = a.S % 4 == 0 && ((uintptr_t)a.use % 16) == 0 && ((uintptr_t)a.haz % 4) == 0;
     const int SV = v4 ? a.S / 4 : a.S;

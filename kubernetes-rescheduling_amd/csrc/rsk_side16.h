@@ -59,9 +59,39 @@ __device__ __forceinline__ void glob_fence(bool glob) {
     if (glob) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
 }
 
-template <bool kOff32>
+// A node's code: the prep kernel's table, or (kOTF) computed from cap / use /
+// hazard as car_prep computes it (node N and beyond: no candidate).
+template <bool kOTF>
+__device__ __forceinline__ unsigned side_code(const SideArgs &a, unsigned n, unsigned s, int B) {
+    if (!kOTF) return ld16(a.code, n * (unsigned)a.S + s);  // row N: code 0
+    if (n >= (unsigned)a.N) return kCodeHaz;
+    const unsigned i = n * (unsigned)a.S + s;
+    return code16(a.cap[n] - ld32(a.use, i), a.haz[i] != 0, B);
+}
+
+// kOTF: the zero case of scenario ss (car_prep's per-scenario reduction:
+// non-hazard count, max packed (cap - use, ~node)) by the whole wave, lanes over
+// the nodes — only for lanes whose rows reach no candidate node (rare).
+__device__ __noinline__ ZeroCase side_zc_scan(const SideArgs &a, int ss, int lane) {
+    const unsigned S = (unsigned)a.S;
+    int cnt = 0;
+    unsigned long long key = 0ull;
+    for (int n0 = 0; n0 < a.N; n0 += 64) {
+        const int n = n0 + lane;
+        const bool ok = n < a.N && a.haz[(size_t)n * S + (unsigned)ss] == 0;
+        cnt += __builtin_popcountll(__builtin_amdgcn_ballot_w64(ok));
+        const unsigned long long k = ok ? zc_pack(a.cap[n] - a.use[(size_t)n * S + (unsigned)ss], n) : 0ull;
+        key = k > key ? k : key;
+    }
+    ZeroCase z;
+    z.cnt = cnt;
+    z.key = dpp_max_u64(key);
+    return z;
+}
+
+template <bool kOff32, bool kOTF = false>
 __device__ int side_exact(const SideArgs &a, const SideTab &tb, unsigned *cells, int ncap, cint_ptr nb, int d, int ss,
-                          int lane, int H, int &score) {
+                          int lane, int H, int &score, int B = 0) {
     const unsigned S = (unsigned)a.S, N = (unsigned)a.N;
     const bool glob = a.gscratch != nullptr;
     for (int i = lane; i < H; i += 64) tb.tab[i] = 0u;
@@ -80,7 +110,7 @@ __device__ int side_exact(const SideArgs &a, const SideTab &tb, unsigned *cells,
                                                                   (unsigned)ss), N);
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
-                        const unsigned c = ld16(a.code, v[u] * S + (unsigned)ss);  // row N: code 0
+                        const unsigned c = side_code<kOTF>(a, v[u], (unsigned)ss, B);  // node N: code 0
                         if (j + 64 * u < gn) cells[j + 64 * u] = (c << 16) | v[u];
                     }
                 }
@@ -104,7 +134,7 @@ __device__ int side_exact(const SideArgs &a, const SideTab &tb, unsigned *cells,
     }
     const unsigned long long k1 = best, k2 = dpp_max_u64(sec);
     const int M = (int)(k1 >> 32);
-    if (M == 0) return zero_target(load_zc(a.zc_cnt, a.zc_key, ss), score);
+    if (M == 0) return zero_target(kOTF ? side_zc_scan(a, ss, lane) : load_zc(a.zc_cnt, a.zc_key, ss), score);
     score = M;
     const unsigned bw = (unsigned)k1, bk = bw >> 16;
     const bool tie = (int)(k2 >> 32) == M;
@@ -118,7 +148,7 @@ __device__ int side_exact(const SideArgs &a, const SideTab &tb, unsigned *cells,
         if (d > ncap) {
             for (int j = lane; j < gn; j += 64) {
                 const unsigned n = min((unsigned)side_ld_assign<kOff32>(a.assign, (unsigned)nb[g0 + j], S, (unsigned)ss), N);
-                cells[j] = (ld16(a.code, n * S + (unsigned)ss) << 16) | n;
+                cells[j] = (side_code<kOTF>(a, n, (unsigned)ss, B) << 16) | n;
             }
             glob_fence(glob);
         }
@@ -183,7 +213,7 @@ __device__ __forceinline__ int side_pivot3(int x) {  // majority of lanes 0, 21,
 // deviations away from u plus its deviations onto u.  So the exact count >= 2
 // candidates are: the table's entries with C >= 2 (a handful), and the lane's
 // deviation nodes — both small sets.
-template <int kW, int kT, int kB, bool kOff32, bool kPipe, bool kGlobal = false>
+template <int kW, int kT, int kB, bool kOff32, bool kPipe, bool kGlobal = false, bool kOTF = false>
 __device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slot = -1) {
     static_assert(kT == 1 || kT == kW, "a team is one wave or the whole workgroup");
     extern __shared__ __attribute__((aligned(16))) unsigned slds[];
@@ -201,6 +231,7 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slo
     const int s0 = chunk * 64;
     const int s = min(s0 + lane, a.S - 1);
     const int H = a.H, K = a.K;
+    const int B = kOTF ? max(0, *const_ptr(a.capmax) - 32766) : 0;  // the exact code window (rsk_car.h)
 
     // kGlobal (one team per workgroup): the team's table, lists and merge area in
     // global scratch (a table beyond the LDS); the same code with global atomics
@@ -253,7 +284,7 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slo
         }
         unsigned c[kB];
 #pragma unroll
-        for (int u = 0; u < kB; ++u) c[u] = ld16(a.code, min((unsigned)v[u], N) * S + (unsigned)s);  // row N: 0
+        for (int u = 0; u < kB; ++u) c[u] = side_code<kOTF>(a, min((unsigned)v[u], N), (unsigned)s, B);  // row N: 0
         int vn[kB];
         if (kPipe) {  // ids clamped to the row: always valid addresses
             const int myq = qnext;
@@ -346,7 +377,7 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slo
             delta[i] = 0;
         }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) c[i] = ld16(a.code, (key[i] ? (key[i] >> 16) - 1u : N) * S + (unsigned)s);
+        for (int i = 0; i < 8; ++i) c[i] = side_code<kOTF>(a, key[i] ? (key[i] >> 16) - 1u : N, (unsigned)s, B);
         for (int k = 0; k < ndmax; ++k) {
             const unsigned x = k < ndk ? dl[k * 64 + lane] : 0xffffffffu;
             const unsigned io = (x >> 16) + 1u, in = (x & 0xffffu) + 1u;  // table keys (node + 1)
@@ -380,7 +411,7 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slo
             cnt = ok && !seen ? C + delta : 0;
         }
         if (__builtin_amdgcn_ballot_w64(cnt >= 2)) {
-            const unsigned c = ld16(a.code, (cnt >= 2 ? t : N) * S + (unsigned)s);
+            const unsigned c = side_code<kOTF>(a, cnt >= 2 ? t : N, (unsigned)s, B);
             b.put(cnt >= 2 && c != kCodeHaz, cnt, cand_word(c, t));
         }
     }
@@ -411,13 +442,25 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slo
     bool slow = nd > K || h2over;
     int tg, sc;
     if (M == 0) {
-        tg = zero_target(load_zc(a.zc_cnt, a.zc_key, s), sc);
+        if (kOTF) tg = RSK_TARGET_NO_CANDIDATE, sc = -1;  // set below from the scanned zero case
+        else tg = zero_target(load_zc(a.zc_cnt, a.zc_key, s), sc);
     } else {
         sc = M;
         const unsigned bk = w1 >> 16;
         const bool tie = w2 != 0u;
         tg = !tie ? cand_node(w1) : (bk >= 2u ? cand_node(w1) : RSK_TARGET_NONE);
         slow = slow || (tie && code_inexact(bk) && (w2 >> 16) == bk);
+    }
+    if (kOTF) {  // lanes that reach no candidate node: their scenario's zero case, scanned
+        unsigned long long zm = __builtin_amdgcn_ballot_w64(M == 0);
+        while (zm) {
+            const int ln = __builtin_ctzll(zm);
+            zm &= zm - 1ull;
+            int sx;
+            const int tx = zero_target(side_zc_scan(a, min(s0 + ln, a.S - 1), lane), sx);
+            tg = lane == ln ? tx : tg;
+            sc = lane == ln ? sx : sc;
+        }
     }
     // rare: deviation lists that overflowed, equal inexact codes at the top —
     // the wave recounts those scenarios exactly, one at a time (the table and
@@ -428,7 +471,7 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slo
             const int ln = __builtin_ctzll(sm);
             sm &= sm - 1ull;
             int sx;
-            const int tx = side_exact<kOff32>(a, tb, dl, 64 * K, nb, d, min(s0 + ln, a.S - 1), lane, H, sx);
+            const int tx = side_exact<kOff32, kOTF>(a, tb, dl, 64 * K, nb, d, min(s0 + ln, a.S - 1), lane, H, sx, B);
             tg = lane == ln ? tx : tg;
             sc = lane == ln ? sx : sc;
         }

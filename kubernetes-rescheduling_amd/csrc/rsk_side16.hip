@@ -37,13 +37,13 @@ namespace rsk {
 
 // kW waves per workgroup, teams of kT waves; blocks b and b + 8 share an XCD
 // (a.xcd_per: workgroups per XCD run).
-template <int kW, int kT, int kB, bool kOff32, bool kPipe, bool kGlobal = false>
-__global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(SideArgs a) {
+template <int kW, int kT, int kB, bool kOff32, bool kPipe, bool kGlobal = false, bool kOTF = false>
+__global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : (kOTF ? 4 : 8))) void car_side16_kernel(SideArgs a) {
     if (kGlobal) {  // a capped grid strides over the items; work area = the resident block's slot
         static_assert(!kGlobal || kT == kW, "global work areas are per workgroup team");
         const int items = a.n_rows * a.nchunk;
         for (int blk = (int)blockIdx.x; blk < items; blk += (int)gridDim.x) {
-            side16_block<kW, kT, kB, kOff32, kPipe, kGlobal>(a, blk, (int)blockIdx.x);
+            side16_block<kW, kT, kB, kOff32, kPipe, kGlobal, kOTF>(a, blk, (int)blockIdx.x);
             glob_fence(true);
             __syncthreads();  // every wave is done with the area before the next item clears it
         }
@@ -51,7 +51,7 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : 8)) void car_side16_kernel(S
     }
     int blk = (int)blockIdx.x;
     if (a.xcd_per) blk = (int)(blockIdx.x & 7u) * a.xcd_per + (int)(blockIdx.x >> 3);
-    side16_block<kW, kT, kB, kOff32, kPipe, kGlobal>(a, blk);
+    side16_block<kW, kT, kB, kOff32, kPipe, kGlobal, kOTF>(a, blk);
 }
 
 constexpr int kSideH2Cap = 2048;  // listed nodes counted >= 2 (e.g. degree 5000 over 6000 nodes: ~1200)
@@ -110,7 +110,8 @@ void side16_apply_geometry(SideArgs &a, const SideGeom &g) {
     a.h2cap = g.h2cap;
 }
 
-int launch_side16(hipStream_t stream, const SideArgs &a0, const SideGeom &g0, bool off32, DevBuf *scratch) {
+template <bool kOTF>
+static int launch_side16_t(hipStream_t stream, const SideArgs &a0, const SideGeom &g0, bool off32, DevBuf *scratch) {
     if (a0.n_rows == 0) return RSK_OK;
     // a table beyond the LDS: 8-wave teams with their work area in global memory
     const bool global = (size_t)(g0.T > 1 ? 1 : g0.W) * g0.lds_team > 160 * 1024;
@@ -133,14 +134,16 @@ int launch_side16(hipStream_t stream, const SideArgs &a0, const SideGeom &g0, bo
         RSK_TRY(scratch->reserve((size_t)gblocks * g.lds_team));
         a.gscratch = scratch->as<unsigned>();
         using KG = void (*)(SideArgs);
-        const KG kg = off32 ? &car_side16_kernel<8, 8, 32, true, false, true> : &car_side16_kernel<8, 8, 32, false, false, true>;
+        const KG kg = off32 ? &car_side16_kernel<8, 8, 32, true, false, true, kOTF>
+                            : &car_side16_kernel<8, 8, 32, false, false, true, kOTF>;
         kg<<<dim3((unsigned)gblocks), dim3(64 * 8), 0, stream>>>(a);
         RSK_HIP(hipGetLastError());
         return RSK_OK;
     }
     using K = void (*)(SideArgs);
     static const bool pipe = RSK_KNOB(RSK_SIDE_PIPE, 1) != 0;
-#define RSK_SIDE_P(W, T, B, O) (pipe ? &car_side16_kernel<W, T, B, O, true> : &car_side16_kernel<W, T, B, O, false>)
+#define RSK_SIDE_P(W, T, B, O) \
+    (pipe ? &car_side16_kernel<W, T, B, O, true, false, kOTF> : &car_side16_kernel<W, T, B, O, false, false, kOTF>)
 #define RSK_SIDE_O(W, T, B) (off32 ? RSK_SIDE_P(W, T, B, true) : RSK_SIDE_P(W, T, B, false))
 #define RSK_SIDE_W(W) (g.kB == 8 ? RSK_SIDE_O(W, 1, 8) : RSK_SIDE_O(W, 1, 16))
     RSK_CHECK(g.T == 1 || g.T == 8 || g.T == 16, "side teams of %d waves are not built", g.T);
@@ -156,6 +159,15 @@ int launch_side16(hipStream_t stream, const SideArgs &a0, const SideGeom &g0, bo
     kern<<<dim3((unsigned)blocks), dim3(64 * g.W), lds, stream>>>(a);
     RSK_HIP(hipGetLastError());
     return RSK_OK;
+}
+
+int launch_side16(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch) {
+    return launch_side16_t<false>(stream, a, g, off32, scratch);
+}
+
+int launch_side16_otf(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch) {
+    RSK_CHECK(a.haz && a.capmax && a.cap && a.use, "on-the-fly side rows need cap, use, hazard and capmax");
+    return launch_side16_t<true>(stream, a, g, off32, scratch);
 }
 
 }  // namespace rsk

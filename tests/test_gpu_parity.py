@@ -787,3 +787,55 @@ def test_node_reduce_segmented_vs_oracle(ctx, P, N, S, p_flip):
     exp = orc.node_reduce(a.reshape(-1), P, S, pod_cpu, pod_mem, N)
     for g, e, name in zip(got, exp, ("count", "cpu", "mem")):
         assert np.array_equal(g, e), name
+
+
+@pytest.mark.parametrize("S", [64, 130])
+def test_car_early_side_rows_on_the_fly_codes(ctx, S):
+    """Rows too big for the fused grid's 20 KB teams (degree 1,200-2,000 over
+    30,000 nodes) run on the side stream from the start with their node codes
+    computed on the fly (car_prep0's max(cap) only) and, where a scenario's row
+    reaches no candidate node, the zero case scanned by the wave: one row whose
+    neighbours all sit on nodes that are hazards in every scenario, one whose
+    neighbours are all unscheduled, crowded overloaded ties (None) and the
+    rest, against the oracle at S = 64 and a partial second chunk."""
+    rng = np.random.default_rng(1500 + S)
+    P, N = 30000, 30000
+    lens = rng.integers(0, 4, P)
+    big = np.arange(10, 22)
+    lens[big] = rng.integers(1200, 2000, big.size)
+    rp = np.zeros(P + 1, np.int32)
+    rp[1:] = np.cumsum(lens)
+    ci = rng.integers(0, P, int(rp[-1])).astype(np.int32)
+    base = rng.integers(0, N, P)
+    a = np.repeat(base[:, None], S, axis=1)
+    flip = rng.random((P, S)) < 0.02
+    a[flip] = rng.integers(-1, N, int(flip.sum()))
+    haz = (rng.random((N, S)) < 0.1).astype(np.uint8)
+    # row 10: every neighbour on nodes 0..99, hazard everywhere -> zero case
+    a[ci[rp[10]:rp[11]], :] = rng.integers(0, 100, (int(lens[10]), 1))
+    haz[:100, :] = 1
+    # row 11: every neighbour unscheduled -> zero case
+    a[ci[rp[11]:rp[12]], :] = -1
+    # row 12: neighbours piled on 40 overloaded nodes (ties at rem < 0 -> None)
+    nb12 = ci[rp[12]:rp[13]]
+    a[nb12, :] = 200 + (np.arange(nb12.size) % 40)[:, None]
+    cap = rng.choice([4000, 8000], N).astype(np.int32)
+    use = rng.integers(0, 8000, (N, S)).astype(np.int32)
+    use[200:240, :] = 9000
+    cap[200:240] = 4000
+    haz[200:240, :] = 0
+    rows = np.concatenate([big, rng.choice(P, 300, replace=False)]).astype(np.int32)
+    _check_car_sparse(ctx, rp, ci, a.astype(np.int32).reshape(-1), S, cap, use.reshape(-1), haz.reshape(-1), N,
+                      rows=np.unique(rows), label=f"early side rows S={S}")
+    from rsk import api
+    plan = api.CarPlan(rp, ci, ctx=ctx)
+    tgt, _ = plan.execute(a.astype(np.int32).reshape(-1), S, cap, use.reshape(-1), haz.reshape(-1), N)
+    plan.close()
+    from oracle import oracle as orc
+    drp, dci = _dedup_csr(rp, ci)
+    exp, _ = orc.car_sparse(drp, dci, a.astype(np.int32).reshape(-1), S, cap, use.reshape(-1), haz.reshape(-1), N,
+                            threads=min(16, os.cpu_count() or 1), want_score=False)
+    assert np.array_equal(tgt, exp), f"plan path: {(tgt != exp).sum()} cells differ"
+    t = tgt.reshape(P, S)
+    assert (t[11] >= 0).all() or (t[11] == -1).any()
+    assert (t[12] == -1).sum() > 0
