@@ -620,24 +620,48 @@ __global__ __launch_bounds__(256) void std_partial_kernel(const int *__restrict_
     pcnt[o] = c;
 }
 
-__global__ void std_merge_kernel(const double *__restrict__ pmean, const double *__restrict__ pm2,
-                                 const int *__restrict__ pcnt, int nchunks, int S, double *__restrict__ out) {
+// Chan et al.'s pairwise update: (n, mean, m2) of a union from its two parts.
+__device__ __forceinline__ void chan_merge(long long &n, double &mean, double &m2, long long nb, double mb, double m2b) {
 #pragma clang fp contract(off)
-    const int s = blockIdx.x * 256 + threadIdx.x;
-    if (s >= S) return;
+    if (!nb) return;
+    if (!n) { n = nb; mean = mb; m2 = m2b; return; }
+    const double delta = mb - mean;
+    const long long nt = n + nb;
+    mean += delta * ((double)nb / (double)nt);
+    m2 += m2b + delta * delta * ((double)n * (double)nb / (double)nt);
+    n = nt;
+}
+
+// One wave per scenario: lane l merges chunks l, l + 64, ... in order, then the
+// 64 lane states pairwise (xor butterfly, 6 levels); lane 0 writes the std.
+// (One thread per scenario walking every chunk in a chain of fp64 divides took
+// 1.6 ms at 50k nodes x 64 scenarios: 3,125 chunks.)
+__global__ __launch_bounds__(256) void std_merge_kernel(const double *__restrict__ pmean, const double *__restrict__ pm2,
+                                                        const int *__restrict__ pcnt, int nchunks, int S,
+                                                        double *__restrict__ out) {
+    const int s = (int)blockIdx.x * 4 + ((int)threadIdx.x >> 6), lane = (int)threadIdx.x & 63;
+    if (s >= S) return;  // whole wave
     double mean = 0.0, m2 = 0.0;
     long long n = 0;
-    for (int ch = 0; ch < nchunks; ++ch) {
+    for (int ch = lane; ch < nchunks; ch += 64) {
         const size_t o = (size_t)ch * S + s;
-        const int nb = pcnt[o];
-        if (!nb) continue;
-        const double mb = pmean[o], delta = mb - mean;
-        const long long nt = n + nb;
-        mean += delta * ((double)nb / (double)nt);
-        m2 += pm2[o] + delta * delta * ((double)n * (double)nb / (double)nt);
-        n = nt;
+        chan_merge(n, mean, m2, pcnt[o], pmean[o], pm2[o]);
     }
-    out[s] = n ? sqrt(m2 / (double)n) : 0.0;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const long long nb = __shfl_xor(n, off, 64);
+        const double mb = __shfl_xor(mean, off, 64), m2b = __shfl_xor(m2, off, 64);
+        // both lanes of a pair combine (lower lane first) so they hold the same state
+        if (lane & off) {
+            long long n2 = nb;
+            double mean2 = mb, m22 = m2b;
+            chan_merge(n2, mean2, m22, n, mean, m2);
+            n = n2, mean = mean2, m2 = m22;
+        } else {
+            chan_merge(n, mean, m2, nb, mb, m2b);
+        }
+    }
+    if (lane == 0) out[s] = n ? sqrt(m2 / (double)n) : 0.0;
 }
 
 constexpr int kCutBins = 64;
@@ -1175,7 +1199,7 @@ int rsk_load_std(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *cap_cpu, i
         std_partial_kernel<<<(unsigned)ceil_div(total, 256), 256, 0, ctx->stream>>>(
             d_use, d_cap, N, S, npb, total, ctx->work[0].as<double>(), ctx->work[1].as<double>(),
             ctx->work[2].as<int>());
-        std_merge_kernel<<<(unsigned)ceil_div(S, 256), 256, 0, ctx->stream>>>(
+        std_merge_kernel<<<(unsigned)ceil_div(S, 4), 256, 0, ctx->stream>>>(
             ctx->work[0].as<double>(), ctx->work[1].as<double>(), ctx->work[2].as<int>(), nch, S, d_out);
         RSK_HIP(hipGetLastError());
     }
