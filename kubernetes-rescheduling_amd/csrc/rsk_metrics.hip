@@ -404,7 +404,7 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(const int *__restrict_
 
 // The segmented form (S >= 32).  What-if scenarios perturb a common base, so a
 // pod sits on the same node in most scenarios.  The pods are bucketed by a key
-// node (the majority of three sampled scenarios; a counting sort: count, scan,
+// node (its node in scenario 0; a counting sort: count, scan,
 // scatter), and a wave walks a run of consecutive bucketed pods with lane =
 // scenario: a lane whose pod sits on the key node adds it to a register
 // accumulator, flushed once per key (three coalesced atomics per 64 scenarios
@@ -412,49 +412,77 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(const int *__restrict_
 // directly.  The sums are integers, so the result is the atomic kernel's,
 // whatever the order.  podmonitor.py:104-121 (pods grouped by node),
 // nodemonitor.py:24-46 (per-node sums).
-__device__ __forceinline__ int nr_key(const int *__restrict__ assign, int p, int S, int N) {
-    const size_t b = (size_t)p * S;
-    const int x = assign[b], y = assign[b + S / 3], z = assign[b + (2 * S) / 3];
-    const int k = (x == y || x == z) ? x : y;
-    return (unsigned)k < (unsigned)N ? k : N;
-}
-
+// The key node of pod p: its node in scenario 0, or N when it has none.  (A
+// majority of three sampled scenarios cost two more scattered lines per pod
+// for the 1 % of pods whose scenario-0 node is itself perturbed.)
 __global__ __launch_bounds__(256) void nr_count_kernel(const int *__restrict__ assign, int P, int S, int N,
-                                                       int *__restrict__ off) {
-    const int p = (int)(blockIdx.x * 256 + threadIdx.x);
-    if (p < P) atomicAdd(&off[nr_key(assign, p, S, N)], 1);
-}
-
-// exclusive scan of off[0..n) in place (one workgroup), copied to cur
-__global__ __launch_bounds__(1024) void nr_scan_kernel(int *__restrict__ off, int *__restrict__ cur, int n) {
-    __shared__ int part[1024];
-    const int t = (int)threadIdx.x, per = (n + 1023) / 1024;
-    const int b = min(n, t * per), e = min(n, b + per);
-    int sum = 0;
-    for (int i = b; i < e; ++i) sum += off[i];
-    part[t] = sum;
-    __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
-        const int v = t >= d ? part[t - d] : 0;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    int run = part[t] - sum;
-    for (int i = b; i < e; ++i) {
-        const int c = off[i];
-        off[i] = run;
-        cur[i] = run;
-        run += c;
-    }
-}
-
-__global__ __launch_bounds__(256) void nr_scatter_kernel(const int *__restrict__ assign, int P, int S, int N,
-                                                         int *__restrict__ cur, int *__restrict__ perm,
-                                                         int *__restrict__ keys) {
+                                                       int *__restrict__ off, int *__restrict__ pkey) {
     const int p = (int)(blockIdx.x * 256 + threadIdx.x);
     if (p >= P) return;
-    const int k = nr_key(assign, p, S, N);
+    const int a = assign[(size_t)p * S];
+    const int k = (unsigned)a < (unsigned)N ? a : N;
+    pkey[p] = k;
+    atomicAdd(&off[k], 1);
+}
+
+// Exclusive scan of off[0..n) in two launches of 1024-element blocks: the block
+// sums, then each block's scan plus the sum of the blocks before it.
+constexpr int kNrScanB = 1024;
+__device__ __forceinline__ int nr_block_incl_scan(int v, int *lds) {
+    const int t = (int)threadIdx.x;
+    lds[t] = v;
+    __syncthreads();
+    for (int d = 1; d < kNrScanB; d <<= 1) {  // Hillis-Steele
+        const int x = t >= d ? lds[t - d] : 0;
+        __syncthreads();
+        lds[t] += x;
+        __syncthreads();
+    }
+    return lds[t];
+}
+
+__global__ __launch_bounds__(kNrScanB) void nr_blocksum_kernel(const int *__restrict__ off, int n,
+                                                               int *__restrict__ bsum) {
+    __shared__ int red[kNrScanB / 64];
+    const int i = (int)blockIdx.x * kNrScanB + (int)threadIdx.x;
+    int v = i < n ? off[i] : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int w = 0; w < kNrScanB / 64; ++w) t += red[w];
+        bsum[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(kNrScanB) void nr_blockscan_kernel(int *__restrict__ off, int *__restrict__ cur, int n,
+                                                                const int *__restrict__ bsum) {
+    __shared__ int lds[kNrScanB];
+    __shared__ int base;
+    if (threadIdx.x < 64) {  // the blocks before this one
+        int b = 0;
+        for (int j = (int)threadIdx.x; j < (int)blockIdx.x; j += 64) b += bsum[j];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) b += __shfl_xor(b, o, 64);
+        if (threadIdx.x == 0) base = b;
+    }
+    const int i = (int)blockIdx.x * kNrScanB + (int)threadIdx.x;
+    const int v = i < n ? off[i] : 0;
+    const int incl = nr_block_incl_scan(v, lds);  // (its barriers also publish `base`)
+    if (i < n) {
+        const int e = base + incl - v;
+        off[i] = e;
+        cur[i] = e;
+    }
+}
+
+__global__ __launch_bounds__(256) void nr_scatter_kernel(const int *__restrict__ pkey, int P, int *__restrict__ cur,
+                                                         int *__restrict__ perm, int *__restrict__ keys) {
+    const int p = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (p >= P) return;
+    const int k = pkey[p];
     const int pos = atomicAdd(&cur[k], 1);
     perm[pos] = p;
     keys[pos] = k;
@@ -1099,16 +1127,18 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
         const int runs = (int)ceil_div(P, kNrRun);
         const int64_t waves = (int64_t)runs * ceil_div(S, 64);
         RSK_CHECK(waves < (int64_t)INT32_MAX - 4, "node_reduce grid too large");
-        RSK_TRY(ctx->work[0].reserve((size_t)P * 8));
-        RSK_TRY(ctx->work[1].reserve((size_t)(N + 1) * 8));
-        int *perm = ctx->work[0].as<int>(), *keys = perm + P;
-        int *off = ctx->work[1].as<int>(), *cur = off + (N + 1);
+        const int nb = (int)ceil_div(N + 1, kNrScanB);
+        RSK_TRY(ctx->work[0].reserve((size_t)P * 12));
+        RSK_TRY(ctx->work[1].reserve(((size_t)(N + 1) * 2 + nb) * 4));
+        int *perm = ctx->work[0].as<int>(), *keys = perm + P, *pkey = keys + P;
+        int *off = ctx->work[1].as<int>(), *cur = off + (N + 1), *bsum = cur + (N + 1);
         ScopedTimer tm(ctx, "node_reduce");
         RSK_HIP(hipMemsetAsync(off, 0, (size_t)(N + 1) * 4, ctx->stream));
         const unsigned pb = (unsigned)ceil_div(P, 256);
-        nr_count_kernel<<<pb, 256, 0, ctx->stream>>>(d_assign, P, S, N, off);
-        nr_scan_kernel<<<1, 1024, 0, ctx->stream>>>(off, cur, N + 1);
-        nr_scatter_kernel<<<pb, 256, 0, ctx->stream>>>(d_assign, P, S, N, cur, perm, keys);
+        nr_count_kernel<<<pb, 256, 0, ctx->stream>>>(d_assign, P, S, N, off, pkey);
+        nr_blocksum_kernel<<<nb, kNrScanB, 0, ctx->stream>>>(off, N + 1, bsum);
+        nr_blockscan_kernel<<<nb, kNrScanB, 0, ctx->stream>>>(off, cur, N + 1, bsum);
+        nr_scatter_kernel<<<pb, 256, 0, ctx->stream>>>(pkey, P, cur, perm, keys);
         node_reduce_seg_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, ctx->stream>>>(
             d_assign, P, S, d_cpu, reinterpret_cast<const long long *>(d_mem), N, perm, keys, runs, d_cnt,
             reinterpret_cast<unsigned long long *>(d_cs), reinterpret_cast<unsigned long long *>(d_ms));
