@@ -348,10 +348,6 @@ int launch_fused16(hipStream_t stream, const Tile16Args &a, const SideArgs &sa, 
                    bool score, bool off32, unsigned tile_blocks, size_t lds);
 // scratch: device memory for rows whose table exceeds the LDS (grown on demand)
 int launch_side16(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch);
-// rows of >= 768 neighbours as split teams (G workgroups of 16 waves per item,
-// areas in `area`, kept zeroed); *done = false: not taken, nothing launched
-int launch_side16_split(hipStream_t stream, const SideArgs &a, int dmax, bool off32, bool otf, DevBuf *area,
-                        bool *done);
 // the same rows with node state computed on the fly (a.code null, a.haz / a.capmax set)
 int launch_side16_otf(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch);
 

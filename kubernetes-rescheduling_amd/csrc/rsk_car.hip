@@ -862,7 +862,6 @@ struct rsk_car_plan {
     // descending, split into the kSideMax classes (neighbours in pcol)
     DevBuf side_items, pcol;
     DevBuf side_scratch;  // work areas of side rows whose table exceeds the LDS
-    DevBuf split_area;    // split teams' per-item areas (kept zeroed between launches)
     // wide path: rows above kHubMax neighbours (car_bigrow_kernel), neighbours in pcol
     DevBuf big_items;
     int n_big = 0, big_dmax = 0;
@@ -890,7 +889,6 @@ struct rsk_car_plan {
         hcol.release();
         side_items.release();
         side_scratch.release();
-        split_area.release();
         big_items.release();
         pcol.release();
         nodekey.release();
@@ -1383,10 +1381,7 @@ int launch_side16_classes(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, 
             a.code = nullptr;
             a.haz = b.haz;
             a.capmax = b.capmax;
-            static const bool split = RSK_KNOB(RSK_SIDE_SPLIT, 1) != 0;
-            bool done = false;
-            if (split) RSK_TRY(launch_side16_split(stream, a, plan->side_dmax[c], off32, true, &plan->split_area, &done));
-            if (!done) RSK_TRY(launch_side16_otf(stream, a, g, off32, &plan->side_scratch));
+            RSK_TRY(launch_side16_otf(stream, a, g, off32, &plan->side_scratch));
         } else {
             RSK_TRY(launch_side16(stream, a, g, off32, &plan->side_scratch));
         }

@@ -213,26 +213,13 @@ __device__ __forceinline__ int side_pivot3(int x) {  // majority of lanes 0, 21,
 // deviations away from u plus its deviations onto u.  So the exact count >= 2
 // candidates are: the table's entries with C >= 2 (a handful), and the lane's
 // deviation nodes — both small sets.
-//
-// kG > 1 (split teams, global work areas only): an item's team spans kG
-// workgroups — its pass 1 is split over kG * kT waves (virtual wave vw) that
-// share the item's global area; the last workgroup to finish pass 1 (an
-// arrival counter, release / acquire fences at agent scope: nothing waits)
-// does the rest with its kT waves and then zeroes the table, the list
-// counters and the arrival counter, so every area starts the next launch
-// zeroed (launch_side16_split zeroes it when it allocates).
-template <int kW, int kT, int kB, bool kOff32, bool kPipe, bool kGlobal = false, bool kOTF = false, int kG = 1>
+template <int kW, int kT, int kB, bool kOff32, bool kPipe, bool kGlobal = false, bool kOTF = false>
 __device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slot = -1) {
     static_assert(kT == 1 || kT == kW, "a team is one wave or the whole workgroup");
-    static_assert(kG == 1 || (kGlobal && kT == kW && kT > 1), "split teams are whole workgroups with global areas");
     extern __shared__ __attribute__((aligned(16))) unsigned slds[];
     const int lane = (int)threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     const int team = wave / kT, tw = wave % kT;
-    const int part = kG > 1 ? blk % kG : 0;
-    if (kG > 1) blk /= kG, slot = blk;  // the item's own area
-    const int vw = part * kT + tw;      // virtual wave of the split team
-    constexpr int kVT = kT * kG;        // waves splitting pass 1
     const int item = blk * (kW / kT) + team;
     if (item >= a.n_rows * a.nchunk) return;  // the whole team (kT > 1: the whole workgroup)
     const int chunk = item / a.n_rows, r = item - chunk * a.n_rows;
@@ -261,17 +248,14 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slo
     unsigned *h2 = base + a.off_h2;                        // [1 + n2] counter, table words counted >= 2
     unsigned *bx = h2;                                     // teams, after the list: [kT][3][64] the waves' bests
 
-    unsigned *ctr = dummy;  // kG > 1: the arrival counter (teams never write the sink)
-    if (kG == 1) {  // split teams find their area zeroed
-        for (int i = tw * 64 + lane; i < H; i += 64 * kT) tb.tab[i] = 0u;
-        if (kT > 1) {
-            if (tw == 0) {
-                ndl[lane] = 0;
-                if (lane == 0) h2[0] = 0u;
-            }
-            glob_fence(kGlobal);
-            __syncthreads();
+    for (int i = tw * 64 + lane; i < H; i += 64 * kT) tb.tab[i] = 0u;
+    if (kT > 1) {
+        if (tw == 0) {
+            ndl[lane] = 0;
+            if (lane == 0) h2[0] = 0u;
         }
+        glob_fence(kGlobal);
+        __syncthreads();
     }
 
     // ---- pass 1: the lane's top-2 words, pivots counted, deviations listed ----
@@ -281,22 +265,22 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slo
     // each batch's neighbour ids in one vector load (lane u: entry j0 + u),
     // broadcast by readlane; kPipe: the next batch's assign rows are loaded
     // before this batch is scored (its code gathers wait only for its own rows)
-    int qnext = nbv[min(vw * kB + lane, d - 1)];
+    int qnext = nbv[min(tw * kB + lane, d - 1)];
     int v[kB];
     if (kPipe) {
         const int myq = qnext;
 #pragma unroll
         for (int u = 0; u < kB; ++u)
             v[u] = side_ld_assign<kOff32>(a.assign, (unsigned)__builtin_amdgcn_readlane(myq, u), S, (unsigned)s);
-        qnext = nbv[min(vw * kB + kB * kVT + lane, d - 1)];
+        qnext = nbv[min(tw * kB + kB * kT + lane, d - 1)];
     }
-    for (int j0 = vw * kB; j0 < d; j0 += kB * kVT) {
+    for (int j0 = tw * kB; j0 < d; j0 += kB * kT) {
         if (!kPipe) {
             const int myq = qnext;
 #pragma unroll
             for (int u = 0; u < kB; ++u)
                 v[u] = side_ld_assign<kOff32>(a.assign, (unsigned)__builtin_amdgcn_readlane(myq, u), S, (unsigned)s);
-            qnext = nbv[min(j0 + kB * kVT + lane, d - 1)];
+            qnext = nbv[min(j0 + kB * kT + lane, d - 1)];
         }
         unsigned c[kB];
 #pragma unroll
@@ -307,7 +291,7 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slo
 #pragma unroll
             for (int u = 0; u < kB; ++u)
                 vn[u] = side_ld_assign<kOff32>(a.assign, (unsigned)__builtin_amdgcn_readlane(myq, u), S, (unsigned)s);
-            qnext = nbv[min(j0 + 2 * kB * kVT + lane, d - 1)];
+            qnext = nbv[min(j0 + 2 * kB * kT + lane, d - 1)];
         }
         const int nu = min(kB, d - j0);
         unsigned mine = 0u;  // lane u: key of entry j0 + u's pivot
@@ -339,16 +323,10 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slo
         }
     }
     if (kT > 1) {
-        fx[(2 * vw) * 64 + lane] = f.w1;
-        fx[(2 * vw + 1) * 64 + lane] = f.w2;
+        fx[(2 * tw) * 64 + lane] = f.w1;
+        fx[(2 * tw + 1) * 64 + lane] = f.w2;
         glob_fence(kGlobal);
         __syncthreads();
-        if (kG > 1) {  // the last part to arrive goes on; the others are done
-            __shared__ int s_last;
-            if (threadIdx.x == 0) s_last = atomicAdd(ctr, 1u) == (unsigned)(kG - 1);
-            __syncthreads();
-            if (!s_last) return;
-        }
         glob_fence(kGlobal);
         nd = ndl[lane];
     }
@@ -452,10 +430,6 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slo
             const unsigned w2w = bx[(3 * w + 2) * 64 + lane];
             b.put(Mw > 0, Mw, bx[(3 * w + 1) * 64 + lane]);
             b.put(Mw > 0 && w2w != 0u, Mw, w2w);
-        }
-        // every virtual wave's pass-1 top-2 (this wave's own words again: put is idempotent)
-#pragma unroll 1
-        for (int w = kG > 1 ? 0 : 1; w < kVT; ++w) {
             f.put(fx[(2 * w) * 64 + lane]);
             f.put(fx[(2 * w + 1) * 64 + lane]);
         }
@@ -508,8 +482,6 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slo
         a.out_target[o] = tg;
         if (a.out_score) a.out_score[o] = sc;
     }
-    if (kG > 1)  // leave the whole area zeroed for the next launch (this wave alone is left)
-        for (unsigned i = (unsigned)lane; i < (a.lds_team >> 2); i += 64u) base[i] = 0u;
 }
 
 }  // namespace rsk

@@ -54,13 +54,6 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : (kOTF ? 4 : 8))) void car_si
     side16_block<kW, kT, kB, kOff32, kPipe, kGlobal, kOTF>(a, blk);
 }
 
-// Split teams (side16_block kG > 1): kG workgroups of 16 waves per item, the
-// item's area in global memory, zeroed between launches.
-template <int kB, bool kOff32, bool kOTF, int kG>
-__global__ __launch_bounds__(1024, 1) void car_side16_split_kernel(SideArgs a) {
-    side16_block<16, 16, kB, kOff32, true, true, kOTF, kG>(a, (int)blockIdx.x);
-}
-
 constexpr int kSideH2Cap = 2048;  // listed nodes counted >= 2 (e.g. degree 5000 over 6000 nodes: ~1200)
 
 SideGeom side16_geometry(int dmax, int N, int T) {
@@ -170,42 +163,6 @@ static int launch_side16_t(hipStream_t stream, const SideArgs &a0, const SideGeo
 
 int launch_side16(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch) {
     return launch_side16_t<false>(stream, a, g, off32, scratch);
-}
-
-// Long rows as split teams: pass 1 over G x 16 waves (G workgroups, one
-// neighbour batch of 16 per wave every 16 G), so its chain of dependent loads
-// is G times shorter; returns RSK_OK with *done = false when the rows do not
-// qualify (short rows, or areas beyond 64 MiB) and nothing was launched.
-int launch_side16_split(hipStream_t stream, const SideArgs &a0, int dmax, bool off32, bool otf, DevBuf *area,
-                        bool *done) {
-    *done = false;
-    if (a0.n_rows == 0 || dmax < 768) return RSK_OK;
-    const int G = dmax <= 1024 ? 2 : (dmax <= 2048 ? 4 : 8);
-    const SideGeom g = side16_geometry(dmax, a0.N, 16 * G);  // merge areas for 16 G waves
-    const int64_t items = (int64_t)a0.n_rows * a0.nchunk;
-    const size_t bytes = (size_t)items * g.lds_team;
-    if (bytes > ((size_t)64 << 20) || items * G >= INT32_MAX) return RSK_OK;
-    SideArgs a = a0;
-    side16_apply_geometry(a, g);
-    a.xcd_per = 0;
-    void *const old = area->ptr;
-    const size_t old_bytes = area->bytes;
-    RSK_TRY(area->reserve(bytes));
-    if (area->ptr != old || area->bytes != old_bytes || !old)  // a new buffer: zeroed once, kept zeroed
-        RSK_HIP(hipMemsetAsync(area->ptr, 0, area->bytes, stream));
-    a.gscratch = area->as<unsigned>();
-    using K = void (*)(SideArgs);
-#define RSK_SPLIT_K(O, T) \
-    (G == 2 ? &car_side16_split_kernel<16, O, T, 2> : G == 4 ? &car_side16_split_kernel<16, O, T, 4> \
-                                                          : &car_side16_split_kernel<16, O, T, 8>)
-    const K k = off32 ? (otf ? RSK_SPLIT_K(true, true) : RSK_SPLIT_K(true, false))
-                      : (otf ? RSK_SPLIT_K(false, true) : RSK_SPLIT_K(false, false));
-#undef RSK_SPLIT_K
-    RSK_CHECK(!otf || (a.haz && a.capmax && a.cap && a.use), "on-the-fly side rows need cap, use, hazard and capmax");
-    k<<<dim3((unsigned)(items * G)), dim3(1024), 0, stream>>>(a);
-    RSK_HIP(hipGetLastError());
-    *done = true;
-    return RSK_OK;
 }
 
 int launch_side16_otf(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch) {
