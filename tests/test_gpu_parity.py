@@ -839,3 +839,44 @@ def test_car_early_side_rows_on_the_fly_codes(ctx, S):
     t = tgt.reshape(P, S)
     assert (t[11] >= 0).all() or (t[11] == -1).any()
     assert (t[12] == -1).sum() > 0
+
+
+def test_car_big_side_rows_plan_reuse(ctx):
+    """Side rows of degree 800 to 9,000 over 40,000 nodes (beyond the fused
+    grid's teams: on the side stream from the start, codes on the fly), one
+    plan executed four times — two batches at S = 128 (two chunks), one at S =
+    64, the first batch again — each against the oracle, so state a launch
+    leaves behind in the plan's work areas would show in the next."""
+    from oracle import oracle as orc
+    from rsk import api
+    rng = np.random.default_rng(9000)
+    P, N = 20000, 40000
+    lens = rng.integers(0, 4, P)
+    lens[:6] = [800, 1500, 3000, 5000, 7000, 9000]
+    rp = np.zeros(P + 1, np.int32)
+    rp[1:] = np.cumsum(lens)
+    ci = rng.integers(0, P, int(rp[-1])).astype(np.int32)
+    for r in range(6):
+        ci[rp[r]:rp[r + 1]] = rng.choice(np.arange(6, P), lens[r], replace=False)
+    drp, dci = _dedup_csr(rp, ci)
+    plan = api.CarPlan(rp, ci, ctx=ctx)
+
+    def batch(seed, S):
+        g = np.random.default_rng(seed)
+        base = g.integers(0, N, P)
+        a = np.repeat(base[:, None], S, axis=1)
+        flip = g.random((P, S)) < 0.03
+        a[flip] = g.integers(-1, N, int(flip.sum()))
+        cap = g.choice([4000, 8000], N).astype(np.int32)
+        use = g.integers(0, 8000, N * S).astype(np.int32)
+        haz = (g.random(N * S) < 0.2).astype(np.uint8)
+        return a.astype(np.int32).reshape(-1), cap, use, haz
+
+    for k, (seed, S) in enumerate([(1, 128), (2, 128), (3, 64), (1, 128)]):
+        a, cap, use, haz = batch(seed, S)
+        tgt, _ = plan.execute(a, S, cap, use, haz, N)
+        exp, _ = orc.car_sparse(drp, dci, a, S, cap, use, haz, N, threads=min(16, os.cpu_count() or 1),
+                                want_score=False)
+        bad = np.nonzero(tgt != exp)[0]
+        assert bad.size == 0, f"execute {k}: {bad.size} cells differ, first row {bad[0] // S}"
+    plan.close()
