@@ -412,17 +412,79 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(const int *__restrict_
 // directly.  The sums are integers, so the result is the atomic kernel's,
 // whatever the order.  podmonitor.py:104-121 (pods grouped by node),
 // nodemonitor.py:24-46 (per-node sums).
-// The key node of pod p: its node in scenario 0, or N when it has none.  (A
-// majority of three sampled scenarios cost two more scattered lines per pod
-// for the 1 % of pods whose scenario-0 node is itself perturbed.)
-__global__ __launch_bounds__(256) void nr_count_kernel(const int *__restrict__ assign, int P, int S, int N,
-                                                       int *__restrict__ off, int *__restrict__ pkey) {
-    const int p = (int)(blockIdx.x * 256 + threadIdx.x);
-    if (p >= P) return;
+// Grouping the pods by key node (its node in scenario 0, N when it has none) is
+// a two-level counting sort that keeps every counter in LDS: level 1 buckets
+// by key >> 8 (per-block histograms, a scan over them, a block-local scatter),
+// level 2 sorts each bucket by key & 255 in one workgroup.  (Global atomics
+// on the N key counters, one per pod for the count and again for the scatter,
+// took 55 + 68 us at 1M pods over 50k nodes.)
+constexpr int kNrChunk = 4096;     // pods per level-1 workgroup
+constexpr int kNrMaxBuckets = 16384;  // key >> 8 buckets held in LDS (N < 2^22)
+__device__ __forceinline__ int nr_key(const int *__restrict__ assign, int p, int S, int N) {
     const int a = assign[(size_t)p * S];
-    const int k = (unsigned)a < (unsigned)N ? a : N;
-    pkey[p] = k;
-    atomicAdd(&off[k], 1);
+    return (unsigned)a < (unsigned)N ? a : N;
+}
+
+// level 1a: keys (kept in pkey) and this block's bucket counts -> bh[j * nblk + b]
+__global__ __launch_bounds__(256) void nr_hist_kernel(const int *__restrict__ assign, int P, int S, int N, int nbk,
+                                                      int *__restrict__ pkey, int *__restrict__ bh) {
+    extern __shared__ int hist[];
+    for (int j = (int)threadIdx.x; j < nbk; j += 256) hist[j] = 0;
+    __syncthreads();
+    const int p0 = (int)blockIdx.x * kNrChunk, p1 = min(P, p0 + kNrChunk);
+    for (int p = p0 + (int)threadIdx.x; p < p1; p += 256) {
+        const int k = nr_key(assign, p, S, N);
+        pkey[p] = k;
+        atomicAdd(&hist[k >> 8], 1);
+    }
+    __syncthreads();
+    for (int j = (int)threadIdx.x; j < nbk; j += 256) bh[(size_t)j * gridDim.x + blockIdx.x] = hist[j];
+}
+
+// level 1b: each block's pods to its slice of every bucket (bh scanned: offsets)
+__global__ __launch_bounds__(256) void nr_part_kernel(const int *__restrict__ pkey, int P, int nbk,
+                                                      const int *__restrict__ boff, int *__restrict__ perm1,
+                                                      int *__restrict__ keys1) {
+    extern __shared__ int cur[];
+    for (int j = (int)threadIdx.x; j < nbk; j += 256) cur[j] = boff[(size_t)j * gridDim.x + blockIdx.x];
+    __syncthreads();
+    const int p0 = (int)blockIdx.x * kNrChunk, p1 = min(P, p0 + kNrChunk);
+    for (int p = p0 + (int)threadIdx.x; p < p1; p += 256) {
+        const int k = pkey[p];
+        const int pos = atomicAdd(&cur[k >> 8], 1);
+        perm1[pos] = p;
+        keys1[pos] = k;
+    }
+}
+
+// level 2: bucket j (one workgroup, any size) sorted by key & 255
+__global__ __launch_bounds__(256) void nr_sub_kernel(const int *__restrict__ perm1, const int *__restrict__ keys1,
+                                                     const int *__restrict__ boff, int nblk1, int nbk, int P,
+                                                     int *__restrict__ perm, int *__restrict__ keys) {
+    __shared__ int cnt[256], pre[256];
+    const int j = (int)blockIdx.x, t = (int)threadIdx.x;
+    const int lo = boff[(size_t)j * nblk1], hi = j + 1 < nbk ? boff[(size_t)(j + 1) * nblk1] : P;
+    cnt[t] = 0;
+    __syncthreads();
+    for (int i = lo + t; i < hi; i += 256) atomicAdd(&cnt[keys1[i] & 255], 1);
+    __syncthreads();
+    const int c = cnt[t];
+    pre[t] = c;
+    __syncthreads();
+    for (int d = 1; d < 256; d <<= 1) {
+        const int x = t >= d ? pre[t - d] : 0;
+        __syncthreads();
+        pre[t] += x;
+        __syncthreads();
+    }
+    cnt[t] = lo + pre[t] - c;  // the sub-bucket's first slot, then its cursor
+    __syncthreads();
+    for (int i = lo + t; i < hi; i += 256) {
+        const int k = keys1[i];
+        const int pos = atomicAdd(&cnt[k & 255], 1);
+        perm[pos] = perm1[i];
+        keys[pos] = k;
+    }
 }
 
 // Exclusive scan of off[0..n) in two launches of 1024-element blocks: the block
@@ -457,7 +519,7 @@ __global__ __launch_bounds__(kNrScanB) void nr_blocksum_kernel(const int *__rest
     }
 }
 
-__global__ __launch_bounds__(kNrScanB) void nr_blockscan_kernel(int *__restrict__ off, int *__restrict__ cur, int n,
+__global__ __launch_bounds__(kNrScanB) void nr_blockscan_kernel(int *__restrict__ off, int n,
                                                                 const int *__restrict__ bsum) {
     __shared__ int lds[kNrScanB];
     __shared__ int base;
@@ -471,21 +533,7 @@ __global__ __launch_bounds__(kNrScanB) void nr_blockscan_kernel(int *__restrict_
     const int i = (int)blockIdx.x * kNrScanB + (int)threadIdx.x;
     const int v = i < n ? off[i] : 0;
     const int incl = nr_block_incl_scan(v, lds);  // (its barriers also publish `base`)
-    if (i < n) {
-        const int e = base + incl - v;
-        off[i] = e;
-        cur[i] = e;
-    }
-}
-
-__global__ __launch_bounds__(256) void nr_scatter_kernel(const int *__restrict__ pkey, int P, int *__restrict__ cur,
-                                                         int *__restrict__ perm, int *__restrict__ keys) {
-    const int p = (int)(blockIdx.x * 256 + threadIdx.x);
-    if (p >= P) return;
-    const int k = pkey[p];
-    const int pos = atomicAdd(&cur[k], 1);
-    perm[pos] = p;
-    keys[pos] = k;
+    if (i < n) off[i] = base + incl - v;
 }
 
 constexpr int kNrRun = 128;  // bucketed pods per wave
@@ -1123,22 +1171,26 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
     RSK_HIP(hipMemsetAsync(d_cnt, 0, NS * 4, ctx->stream));
     RSK_HIP(hipMemsetAsync(d_cs, 0, NS * 8, ctx->stream));
     if (d_ms) RSK_HIP(hipMemsetAsync(d_ms, 0, NS * 8, ctx->stream));
-    if (PS && S >= 32) {  // segmented: bucket the pods by key node, then per-key register sums
+    const int nbk = (N >> 8) + 1;  // key >> 8 buckets (keys 0..N)
+    if (PS && S >= 32 && nbk <= kNrMaxBuckets) {  // segmented: group the pods by key node, per-key register sums
         const int runs = (int)ceil_div(P, kNrRun);
         const int64_t waves = (int64_t)runs * ceil_div(S, 64);
         RSK_CHECK(waves < (int64_t)INT32_MAX - 4, "node_reduce grid too large");
-        const int nb = (int)ceil_div(N + 1, kNrScanB);
-        RSK_TRY(ctx->work[0].reserve((size_t)P * 12));
-        RSK_TRY(ctx->work[1].reserve(((size_t)(N + 1) * 2 + nb) * 4));
-        int *perm = ctx->work[0].as<int>(), *keys = perm + P, *pkey = keys + P;
-        int *off = ctx->work[1].as<int>(), *cur = off + (N + 1), *bsum = cur + (N + 1);
+        const int nblk1 = (int)ceil_div(P, kNrChunk);
+        const int64_t nbh = (int64_t)nbk * nblk1;
+        RSK_CHECK(nbh < INT32_MAX / 2, "node_reduce grouping too large");
+        const int nsb = (int)ceil_div(nbh, kNrScanB);
+        RSK_TRY(ctx->work[0].reserve((size_t)P * 20));
+        RSK_TRY(ctx->work[1].reserve(((size_t)nbh + nsb) * 4));
+        int *perm = ctx->work[0].as<int>(), *keys = perm + P, *pkey = keys + P, *perm1 = pkey + P, *keys1 = perm1 + P;
+        int *bh = ctx->work[1].as<int>(), *bsum = bh + nbh;
         ScopedTimer tm(ctx, "node_reduce");
-        RSK_HIP(hipMemsetAsync(off, 0, (size_t)(N + 1) * 4, ctx->stream));
-        const unsigned pb = (unsigned)ceil_div(P, 256);
-        nr_count_kernel<<<pb, 256, 0, ctx->stream>>>(d_assign, P, S, N, off, pkey);
-        nr_blocksum_kernel<<<nb, kNrScanB, 0, ctx->stream>>>(off, N + 1, bsum);
-        nr_blockscan_kernel<<<nb, kNrScanB, 0, ctx->stream>>>(off, cur, N + 1, bsum);
-        nr_scatter_kernel<<<pb, 256, 0, ctx->stream>>>(pkey, P, cur, perm, keys);
+        const size_t hl = (size_t)nbk * 4;
+        nr_hist_kernel<<<nblk1, 256, hl, ctx->stream>>>(d_assign, P, S, N, nbk, pkey, bh);
+        nr_blocksum_kernel<<<nsb, kNrScanB, 0, ctx->stream>>>(bh, (int)nbh, bsum);
+        nr_blockscan_kernel<<<nsb, kNrScanB, 0, ctx->stream>>>(bh, (int)nbh, bsum);
+        nr_part_kernel<<<nblk1, 256, hl, ctx->stream>>>(pkey, P, nbk, bh, perm1, keys1);
+        nr_sub_kernel<<<nbk, 256, 0, ctx->stream>>>(perm1, keys1, bh, nblk1, nbk, P, perm, keys);
         node_reduce_seg_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, ctx->stream>>>(
             d_assign, P, S, d_cpu, reinterpret_cast<const long long *>(d_mem), N, perm, keys, runs, d_cnt,
             reinterpret_cast<unsigned long long *>(d_cs), reinterpret_cast<unsigned long long *>(d_ms));
