@@ -537,18 +537,14 @@ __global__ __launch_bounds__(kNrScanB) void nr_blockscan_kernel(int *__restrict_
 }
 
 constexpr int kNrRun = 128;  // bucketed pods per wave
-// The sums of a (node, scenario) cell are staged interleaved — count, CPU[,
-// memory] as adjacent u64 words — so the three atomics a pod adds land in one
-// cache line (the first brings it to the L2, the others hit); nr_unstage_kernel
-// writes the ABI's three arrays from the staging.  (Three separate arrays: each
-// off-key pod cost three random lines, 0.21 ms at 1M x 50k x 64.)
-template <int kW>
 __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restrict__ assign, int P, int S,
                                                               const int *__restrict__ pod_cpu,
                                                               const long long *__restrict__ pod_mem, int N,
                                                               const int *__restrict__ perm,
                                                               const int *__restrict__ keys, int runs,
-                                                              unsigned long long *__restrict__ stage) {
+                                                              int *__restrict__ cnt,
+                                                              unsigned long long *__restrict__ cpu,
+                                                              unsigned long long *__restrict__ mem) {
     const int w = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
     const int chunk = w / runs, run = w - chunk * runs;
     const int s = chunk * 64 + (int)(threadIdx.x & 63);
@@ -558,14 +554,13 @@ __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restr
     const cint_ptr cperm = const_ptr(perm), ckeys = const_ptr(keys), ccpu = const_ptr(pod_cpu);
     int rk = -1, rc = 0;
     long long rcpu = 0, rmem = 0;
-    auto add = [&](int node, unsigned long long c, unsigned long long cpu, unsigned long long mem) {
-        unsigned long long *o = stage + ((size_t)node * S + s) * kW;
-        atomicAdd(o, c);
-        atomicAdd(o + 1, cpu);
-        if (kW == 3) atomicAdd(o + 2, mem);
-    };
     auto flush = [&]() {
-        if (live && rk >= 0 && rk < N && rc > 0) add(rk, (unsigned long long)rc, (unsigned long long)rcpu, (unsigned long long)rmem);
+        if (live && rk >= 0 && rk < N && rc > 0) {
+            const size_t o = (size_t)rk * S + s;
+            atomicAdd(&cnt[o], rc);
+            atomicAdd(&cpu[o], (unsigned long long)rcpu);
+            if (mem) atomicAdd(&mem[o], (unsigned long long)rmem);
+        }
         rc = 0;
         rcpu = rmem = 0;
     };
@@ -586,29 +581,20 @@ __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restr
                 rk = k;
             }
             const int c = ccpu[p];
-            const long long m = kW == 3 ? pod_mem[p] : 0;
+            const long long m = mem ? pod_mem[p] : 0;
             if (a[u] == k) {
                 ++rc;
                 rcpu += c;
                 rmem += m;
             } else if ((unsigned)a[u] < (unsigned)N) {
-                add(a[u], 1ull, (unsigned long long)(long long)c, (unsigned long long)m);
+                const size_t o = (size_t)a[u] * S + s;
+                atomicAdd(&cnt[o], 1);
+                atomicAdd(&cpu[o], (unsigned long long)(long long)c);
+                if (mem) atomicAdd(&mem[o], (unsigned long long)m);
             }
         }
     }
     flush();
-}
-
-template <int kW>
-__global__ __launch_bounds__(256) void nr_unstage_kernel(const unsigned long long *__restrict__ stage, size_t n,
-                                                         int *__restrict__ cnt, long long *__restrict__ cpu,
-                                                         long long *__restrict__ mem) {
-    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const unsigned long long *x = stage + i * kW;
-    cnt[i] = (int)x[0];
-    cpu[i] = (long long)x[1];
-    if (kW == 3) mem[i] = (long long)x[2];
 }
 
 // get_resource_usage.py:37: int(round(u / c * 100)) — IEEE fp64 divide, then an
@@ -1182,14 +1168,11 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
     RSK_TRY(stage_out(ctx, 3, pod_count, NS * 4, dev, reinterpret_cast<void **>(&d_cnt)));
     RSK_TRY(stage_out(ctx, 4, cpu_sum, NS * 8, dev, reinterpret_cast<void **>(&d_cs)));
     if (mem_sum) RSK_TRY(stage_out(ctx, 5, mem_sum, NS * 8, dev, reinterpret_cast<void **>(&d_ms)));
+    RSK_HIP(hipMemsetAsync(d_cnt, 0, NS * 4, ctx->stream));
+    RSK_HIP(hipMemsetAsync(d_cs, 0, NS * 8, ctx->stream));
+    if (d_ms) RSK_HIP(hipMemsetAsync(d_ms, 0, NS * 8, ctx->stream));
     const int nbk = (N >> 8) + 1;  // key >> 8 buckets (keys 0..N)
-    const bool seg = PS && S >= 32 && nbk <= kNrMaxBuckets;
-    if (!seg) {
-        RSK_HIP(hipMemsetAsync(d_cnt, 0, NS * 4, ctx->stream));
-        RSK_HIP(hipMemsetAsync(d_cs, 0, NS * 8, ctx->stream));
-        if (d_ms) RSK_HIP(hipMemsetAsync(d_ms, 0, NS * 8, ctx->stream));
-    }
-    if (seg) {  // segmented: group the pods by key node, per-key register sums
+    if (PS && S >= 32 && nbk <= kNrMaxBuckets) {  // segmented: group the pods by key node, per-key register sums
         const int runs = (int)ceil_div(P, kNrRun);
         const int64_t waves = (int64_t)runs * ceil_div(S, 64);
         RSK_CHECK(waves < (int64_t)INT32_MAX - 4, "node_reduce grid too large");
@@ -1208,20 +1191,9 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
         nr_blockscan_kernel<<<nsb, kNrScanB, 0, ctx->stream>>>(bh, (int)nbh, bsum);
         nr_part_kernel<<<nblk1, 256, hl, ctx->stream>>>(pkey, P, nbk, bh, perm1, keys1);
         nr_sub_kernel<<<nbk, 256, 0, ctx->stream>>>(perm1, keys1, bh, nblk1, nbk, P, perm, keys);
-        const int W = d_ms ? 3 : 2;
-        RSK_TRY(ctx->work[2].reserve(NS * W * 8));
-        auto *stage = ctx->work[2].as<unsigned long long>();
-        RSK_HIP(hipMemsetAsync(stage, 0, NS * W * 8, ctx->stream));
-        const unsigned gb = (unsigned)ceil_div(waves, 4), ub = (unsigned)ceil_div((int64_t)NS, 256);
-        const auto *pm = reinterpret_cast<const long long *>(d_mem);
-        auto *cs = reinterpret_cast<long long *>(d_cs), *ms = reinterpret_cast<long long *>(d_ms);
-        if (W == 3) {
-            node_reduce_seg_kernel<3><<<gb, 256, 0, ctx->stream>>>(d_assign, P, S, d_cpu, pm, N, perm, keys, runs, stage);
-            nr_unstage_kernel<3><<<ub, 256, 0, ctx->stream>>>(stage, NS, d_cnt, cs, ms);
-        } else {
-            node_reduce_seg_kernel<2><<<gb, 256, 0, ctx->stream>>>(d_assign, P, S, d_cpu, pm, N, perm, keys, runs, stage);
-            nr_unstage_kernel<2><<<ub, 256, 0, ctx->stream>>>(stage, NS, d_cnt, cs, nullptr);
-        }
+        node_reduce_seg_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, ctx->stream>>>(
+            d_assign, P, S, d_cpu, reinterpret_cast<const long long *>(d_mem), N, perm, keys, runs, d_cnt,
+            reinterpret_cast<unsigned long long *>(d_cs), reinterpret_cast<unsigned long long *>(d_ms));
         RSK_HIP(hipGetLastError());
     } else if (PS) {
         ScopedTimer tm(ctx, "node_reduce");
