@@ -537,12 +537,6 @@ __global__ __launch_bounds__(kNrScanB) void nr_blockscan_kernel(int *__restrict_
 }
 
 constexpr int kNrRun = 128;  // bucketed pods per wave
-// Off-key pods (a lane whose pod is not on the run's key node, ~2 % of cells)
-// are listed per lane in LDS and added in rounds, every lane one entry per
-// atomic instruction: a handful of full-wave atomics per run instead of three
-// nearly empty ones per pod slot with any off-key lane (which bounded the
-// kernel: 0.21 ms at 1M x 50k x 64).
-constexpr int kNrDev = 16;  // listed entries per lane; rounds run before a batch could overflow it
 __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restrict__ assign, int P, int S,
                                                               const int *__restrict__ pod_cpu,
                                                               const long long *__restrict__ pod_mem, int N,
@@ -551,16 +545,14 @@ __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restr
                                                               int *__restrict__ cnt,
                                                               unsigned long long *__restrict__ cpu,
                                                               unsigned long long *__restrict__ mem) {
-    __shared__ uint2 dev[4][kNrDev][64];  // (node, pod) per listed entry
-    const int wv = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
-    const int w = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + wv);
+    const int w = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
     const int chunk = w / runs, run = w - chunk * runs;
-    const int s = chunk * 64 + lane;
+    const int s = chunk * 64 + (int)(threadIdx.x & 63);
     if (chunk * 64 >= S) return;
     const bool live = s < S;
     const int j0 = run * kNrRun, j1 = min(P, j0 + kNrRun);
     const cint_ptr cperm = const_ptr(perm), ckeys = const_ptr(keys), ccpu = const_ptr(pod_cpu);
-    int rk = -1, rc = 0, nd = 0;
+    int rk = -1, rc = 0;
     long long rcpu = 0, rmem = 0;
     auto flush = [&]() {
         if (live && rk >= 0 && rk < N && rc > 0) {
@@ -572,21 +564,7 @@ __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restr
         rc = 0;
         rcpu = rmem = 0;
     };
-    auto flush_dev = [&]() {  // the listed off-key pods, one per lane per round
-        const int m = dpp_max(nd);
-        for (int r = 0; r < m; ++r) {
-            if (r < nd) {
-                const uint2 e = dev[wv][r][lane];
-                const size_t o = (size_t)e.x * S + s;
-                atomicAdd(&cnt[o], 1);
-                atomicAdd(&cpu[o], (unsigned long long)(long long)pod_cpu[e.y]);
-                if (mem) atomicAdd(&mem[o], (unsigned long long)pod_mem[e.y]);
-            }
-        }
-        nd = 0;
-    };
     constexpr int kB = 8;
-    static_assert(kNrDev >= 2 * kB, "a batch adds at most kB entries per lane");
     for (int j = j0; j < j1; j += kB) {
         int a[kB];
 #pragma unroll
@@ -602,19 +580,21 @@ __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restr
                 flush();
                 rk = k;
             }
+            const int c = ccpu[p];
+            const long long m = mem ? pod_mem[p] : 0;
             if (a[u] == k) {
                 ++rc;
-                rcpu += ccpu[p];
-                rmem += mem ? pod_mem[p] : 0;
+                rcpu += c;
+                rmem += m;
             } else if ((unsigned)a[u] < (unsigned)N) {
-                dev[wv][nd][lane] = make_uint2((unsigned)a[u], (unsigned)p);
-                ++nd;
+                const size_t o = (size_t)a[u] * S + s;
+                atomicAdd(&cnt[o], 1);
+                atomicAdd(&cpu[o], (unsigned long long)(long long)c);
+                if (mem) atomicAdd(&mem[o], (unsigned long long)m);
             }
         }
-        if (dpp_max(nd) > kNrDev - kB) flush_dev();
     }
     flush();
-    flush_dev();
 }
 
 // get_resource_usage.py:37: int(round(u / c * 100)) — IEEE fp64 divide, then an
