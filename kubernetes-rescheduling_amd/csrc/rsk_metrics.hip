@@ -566,22 +566,33 @@ __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restr
     };
     constexpr int kB = 8;
     for (int j = j0; j < j1; j += kB) {
-        int a[kB];
+        // every load of the batch issued before its first use: the assign rows,
+        // and the pods' CPU / memory (scattered pod ids: each a cache miss that,
+        // loaded per pod behind the previous pod's atomics, serialised the run)
+        int a[kB], pp[kB], kk[kB], cc[kB];
+        long long mm[kB];
 #pragma unroll
-        for (int u = 0; u < kB; ++u) {  // the batch's assign rows in flight together
+        for (int u = 0; u < kB; ++u) {
             const int jj = min(j + u, j1 - 1);
-            a[u] = live ? __builtin_nontemporal_load(&assign[(size_t)cperm[jj] * S + s]) : -1;
+            pp[u] = cperm[jj];
+            kk[u] = ckeys[jj];
+        }
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            a[u] = live ? __builtin_nontemporal_load(&assign[(size_t)pp[u] * S + s]) : -1;
+            cc[u] = ccpu[pp[u]];
+            mm[u] = mem ? pod_mem[pp[u]] : 0;
         }
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
             if (j + u >= j1) break;
-            const int p = cperm[j + u], k = ckeys[j + u];
+            const int k = kk[u];
             if (k != rk) {  // wave-uniform: a new key node
                 flush();
                 rk = k;
             }
-            const int c = ccpu[p];
-            const long long m = mem ? pod_mem[p] : 0;
+            const int c = cc[u];
+            const long long m = mm[u];
             if (a[u] == k) {
                 ++rc;
                 rcpu += c;
