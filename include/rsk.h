@@ -57,8 +57,12 @@ int rsk_ctx_destroy(rsk_ctx *ctx);
 /* Run subsequent work on `hip_stream` (a hipStream_t; NULL = the context's own). */
 int rsk_ctx_set_stream(rsk_ctx *ctx, void *hip_stream);
 int rsk_ctx_synchronize(rsk_ctx *ctx);
-/* Kernel timing with HIP events recorded on the context's stream around every
- * launch of the named kernel ("car_prep", "car_tile", "car_mid", "car_heavy" = the hub rows). */
+/* Kernel timing with HIP events recorded on the stream of every launch of the
+ * named kernel group: "car_prep" (prep0 and prep), "car_tile" (the fused lean
+ * tile + side launch and the heavy tile launch), "car_side" (side rows launched
+ * on their own, e.g. config 4's rows beyond the fused grid on the side stream),
+ * "car_mid" / "car_heavy" (the wide path's 33..64 and hub rows, N > 65535),
+ * "node_reduce", "load_std", "cut_cost", "rounds_*", ... */
 int rsk_ctx_set_profiling(rsk_ctx *ctx, int on);
 /* Restrict the timing events to launches of one kernel name (NULL or "" = all):
  * fewer events inside a timed region. */
@@ -88,7 +92,9 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
                          int32_t *out_target, int32_t *out_score, uint32_t flags);
 /* Plan layout statistics (host, no GPU work): how the rows were routed.
  * out[0] rows scored in tiles (deg <= 32)   out[1] (unused, 0)
- * out[2] mid rows (33..64)   out[3] hub rows (> 64)   out[4] tiles
+ * out[2] rows of degree 33..64, out[3] rows of degree 65..4096 (the wide
+ *        path's car_mid / car_hub classes; the compact path scores both with
+ *        car_side16 and counts them in out[15])   out[4] tiles
  * out[5] max image rows per tile   out[6] max owner rows per tile
  * out[7] tile plan bytes   out[8] (unused, 0)   out[9] mid record bytes
  * out[10] hub item + CSR bytes   out[11] max row degree
