@@ -849,14 +849,19 @@ __global__ __launch_bounds__(256) void cut_cost_wave_kernel(const int *__restric
             for (int i = 0; i < kW; ++i) o[i] = rp[min(p + 1 + i, r1)];
             const int kend = min(min(kb, k0 + kW), o[kW - 1]);
             if (kend <= k0) { p += kW; continue; }  // kW rows without edges here
-            int aq[kW], am[kW], last = 0;
+            // the row of edge k0 + j is p + #{i : o[i] <= k0 + j}: lane j counts it
+            // for its edge (31 VALU for the window, not 31 per edge), and every
+            // edge's count is read back as a scalar
+            const int kl = min(k0 + (lane & (kW - 1)), kend - 1);
+            int rl = 0;
+#pragma unroll
+            for (int i = 0; i < kW - 1; ++i) rl += o[i] <= kl ? 1 : 0;
+            const int last = __builtin_amdgcn_readlane(rl, kend - 1 - k0);
+            int aq[kW], am[kW];
 #pragma unroll
             for (int j = 0; j < kW; ++j) {
                 const int k = min(k0 + j, kend - 1);
-                int r = 0;
-#pragma unroll
-                for (int i = 0; i < kW - 1; ++i) r += o[i] <= k ? 1 : 0;
-                if (k0 + j < kend) last = r;
+                const int r = __builtin_amdgcn_readlane(rl, j);
                 aq[j] = assign[(size_t)cl[k] * S + s];
                 am[j] = assign[(size_t)(p + r) * S + s];
             }
@@ -1281,7 +1286,9 @@ int rsk_load_std(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *cap_cpu, i
     RSK_TRY(stage_in(ctx, 0, use_cpu, NS * 4, dev, reinterpret_cast<const void **>(&d_use)));
     RSK_TRY(stage_in(ctx, 1, cap_cpu, (size_t)N * 4, dev, reinterpret_cast<const void **>(&d_cap)));
     RSK_TRY(stage_out(ctx, 2, out_std, (size_t)S * 8, dev, reinterpret_cast<void **>(&d_out)));
-    const int npb = std::max(chunk_for(N, S), 16);
+    // nodes per thread: at least 16, and at most 1,024 chunks for the merge
+    // waves to walk (50k nodes x 64 scenarios: 49 nodes, 1,021 chunks)
+    const int npb = std::max({chunk_for(N, S), 16, (int)ceil_div(N, 1024)});
     const int nch = (int)ceil_div(N, npb);
     RSK_TRY(ctx->work[0].reserve((size_t)nch * S * 8));
     RSK_TRY(ctx->work[1].reserve((size_t)nch * S * 8));
