@@ -1196,12 +1196,15 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
     TileBuilder tl, th;
     tl.owners_cap = th.owners_cap = plan->owners_cap;
     tl.rows_cap = th.rows_cap = plan->rows_cap;
+    // RSK_LEAN32 (default): the 17..32 rows stay in the lean tiles (w64_ds_lean);
+    // 0: they and the d + 1 rows after each go to heavy tiles (w64_ds)
+    static const bool lean32 = RSK_KNOB(RSK_LEAN32, 1) != 0;
     int heavy_left = 0;
     for (int i : light) {
         const int p = rows ? rows[i] : i;
         const int d = rp[p + 1] - rp[p];
         const int *nbp = ci.data() + rp[p];
-        if (light_class(d) == 5) heavy_left = std::max(heavy_left, d + 1);
+        if (!lean32 && light_class(d) == 5) heavy_left = std::max(heavy_left, d + 1);
         TileBuilder &tb = heavy_left > 0 ? th : tl;
         if (heavy_left > 0) --heavy_left;
         if (!tb.fits(nbp, d)) tb.close();

@@ -866,6 +866,68 @@ __device__ __forceinline__ void w64_ds(const Tile16Args &a, const W64 &w, cint_p
     emit64<kScore, kOff32>(a, r[0], s0, w, M == 0 ? w.zt : t, M == 0 ? w.zs : M);
 }
 
+// 17 <= d <= 32 in the lean tiles, record j at R[20 * j] (as w64_ds): the
+// counting walk of w64_dm with only the first 16 cells in registers.  Entry
+// e's count c = #{earlier entries equal to it}: for e < 16 against the
+// registers; for e >= 16 (cell read from the LDS image) against the 16
+// registers plus the earlier entries >= 16, re-read from the LDS one at a time
+// (<= 120 extra ds_read_b32 per record).  About 30 VGPRs instead of the sort
+// network's 32 cells + state, so the class fits the lean kernel's 64 and runs
+// at 8 workgroups per CU instead of in heavy tiles at 6.
+template <bool kScore, bool kOff32>
+__device__ __forceinline__ void w64_ds_lean(const Tile16Args &a, const W64 &w, cint_ptr R, int j, int s0) {
+    const cint_ptr r = R + 20 * j;
+    const int d = r[1];
+    auto row_of = [&](int i) -> int {
+        const unsigned pr = (unsigned)r[4 + i / 2];
+        return (i & 1) ? (int)(pr >> 16) : (int)(pr & 0xffffu);
+    };
+    unsigned x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = w.cell(row_of(i));  // d >= 17: all real cells
+    int M = -1, Rn = 0, namb = 0;
+    unsigned bw = 0u;
+    auto put = [&](unsigned xe, int c) {
+        const bool cand = cell_code(xe) != kCodeHaz;
+        const unsigned wv = cell_cand(xe);
+        const bool gt = cand && c > M, eq = cand && c == M;
+        const unsigned kw = cell_code(wv), kb = cell_code(bw);
+        namb = gt ? 1 : (eq ? (kw > kb ? 1 : (kw == kb ? namb + 1 : namb)) : namb);
+        bw = gt ? wv : (eq ? max(bw, wv) : bw);
+        Rn = gt ? 1 : (eq ? Rn + 1 : Rn);
+        M = gt ? c : M;
+    };
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        if (e % 8 == 0) __builtin_amdgcn_sched_barrier(0);
+        int c = 0;
+#pragma unroll
+        for (int h = 0; h < e; ++h) c += x[h] == x[e];
+        put(x[e], c);
+    }
+#pragma unroll 1
+    for (int e = 16; e < d; ++e) {  // wave-uniform bound
+        const unsigned xe = w.cell(row_of(e));
+        int c = 0;
+#pragma unroll
+        for (int h = 0; h < 16; ++h) c += x[h] == xe;
+#pragma unroll 1
+        for (int h = 16; h < e; ++h) c += w.cell(row_of(h)) == xe;
+        put(xe, c);
+    }
+    const unsigned bk = cell_code(bw);
+    int t = Rn == 1 ? cand_node(bw) : (bk >= 2u ? cand_node(bw) : RSK_TARGET_NONE);
+    const bool need = Rn > 1 && code_inexact(bk) && namb > 1;
+    if (__builtin_amdgcn_ballot_w64(need)) {  // rare: wave-uniform branch
+        Img16 im;
+        im.w = reinterpret_cast<const unsigned *>(w.img);
+        im.lsl = 6;
+        const int te = t16_exact_scan(a, im, (const int *)(uintptr_t)(r + 4), d, (int)(w.col4 >> 2), M + 1, bk, w.s);
+        t = need ? te : t;
+    }
+    emit64<kScore, kOff32>(a, r[0], s0, w, M < 0 ? w.zt : t, M < 0 ? w.zs : M + 1);
+}
+
 // kL64 phase 2, part 1: the multi-neighbour classes (d >= 3), most expensive
 // first.  Record j of a class goes to wave (rot + j) % 4, rot carried from
 // class to class (and into part 2), so a tile's few records of each class do
@@ -874,9 +936,14 @@ template <bool kScore, bool kOff32, bool kHeavy>
 __device__ __forceinline__ int w64_score_heavy(const Tile16Args &a, const W64 &w, cint_ptr m, cint_ptr R, int wave,
                                                int s0) {
     int rot = 0;
-    if (kHeavy) {  // d = 17..32: heavy tiles only (own instantiation, registers for 32 cells)
+    {   // d = 17..32: the sort network in heavy tiles (own instantiation, registers
+        // for 32 cells); the register-light walk in lean tiles (plans built with
+        // RSK_LEAN32, the default)
         const cint_ptr Rc = R + m[15];
-        for (int j = (wave - rot) & 3; j < m[9]; j += 4) w64_ds<kScore, kOff32>(a, w, Rc, j, s0);
+        for (int j = (wave - rot) & 3; j < m[9]; j += 4) {
+            if (kHeavy) w64_ds<kScore, kOff32>(a, w, Rc, j, s0);
+            else w64_ds_lean<kScore, kOff32>(a, w, Rc, j, s0);
+        }
         rot = (rot + m[9]) & 3;
     }
     {
