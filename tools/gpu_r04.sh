@@ -25,6 +25,8 @@ for s in "${@:-test smoke bench}"; do
       b2k) step bench_2k64 300 python -u bench.py --config 2k64 --no-cpu-baseline ;;
       b1m) step bench_1m50k 600 python -u bench.py --config 1m50k --no-cpu-baseline ;;
       brounds) step bench_rounds 300 python -u bench.py --config rounds --no-cpu-baseline ;;
+      ab:*) kv=${w#ab:}; step "ab_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u bench.py --no-cpu-baseline ;;
+      ab1m:*) kv=${w#ab1m:}; step "ab1m_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u bench.py --config 1m50k --no-cpu-baseline --row-rounds 0 ;;
       dropin) step dropin 400 python -u tools/dropin_latency.py --calls 40 --out "$out/dropin.json" ;;
       prof) for c in headline 1m50k; do
               ./tools/gpu_prof.sh $c "$out/prof_$c" > "$out/prof_$c.log" 2>&1 || { tail -5 "$out/prof_$c.log"; exit 1; }
