@@ -95,6 +95,54 @@ __global__ __launch_bounds__(kPrep0Threads) void car_prep0_kernel(const int *__r
     }
 }
 
+// Small batches (N * S <= kPrepSmallCells, S <= kPrepSmallS; config 2 is
+// 64 cells): prep0 and prep in one workgroup, one launch instead of two.
+constexpr int kPrepSmallCells = 32768, kPrepSmallS = 256;
+__global__ __launch_bounds__(kPrep0Threads) void car_prep_small_kernel(const int *__restrict__ cap,
+                                                                      const int *__restrict__ use,
+                                                                      const uint8_t *__restrict__ haz, int N, int S,
+                                                                      unsigned short *__restrict__ code,
+                                                                      int *__restrict__ nodekey,
+                                                                      int *__restrict__ zc_cnt,
+                                                                      unsigned long long *__restrict__ zc_key,
+                                                                      int *__restrict__ capmax) {
+    __shared__ int red[kPrep0Threads / 64];
+    __shared__ int lcnt[kPrepSmallS];
+    __shared__ unsigned long long lkey[kPrepSmallS];
+    const int t = (int)threadIdx.x;
+    int mc = 0;
+    for (int n = t; n < N; n += kPrep0Threads) mc = max(mc, cap[n]);
+    mc = dpp_max(mc);
+    if ((t & 63) == 0) red[t >> 6] = mc;
+    for (int i = t; i < S; i += kPrep0Threads) {
+        lcnt[i] = 0;
+        lkey[i] = 0ull;
+    }
+    __syncthreads();
+    mc = red[0];
+    for (int w = 1; w < kPrep0Threads / 64; ++w) mc = max(mc, red[w]);
+    const int B = max(0, mc - 32766);  // the exact code window (rsk_car.h)
+    if (t == 0 && capmax) *capmax = mc;
+    if (code)
+        for (int i = t; i < S; i += kPrep0Threads) code[(size_t)N * S + i] = 0;  // row N: no candidate
+    for (int i = t; i < N * S; i += kPrep0Threads) {
+        const int n = i / S, sc = i - n * S;
+        const int rem = cap[n] - use[i];
+        const bool h = haz[i] != 0;
+        if (code) code[i] = (unsigned short)code16(rem, h, B);
+        if (nodekey) nodekey[i] = h ? kKeyHaz : rem;
+        if (!h) {
+            atomicAdd(&lcnt[sc], 1);
+            atomicMax(&lkey[sc], zc_pack(rem, n));
+        }
+    }
+    __syncthreads();
+    for (int i = t; i < S; i += kPrep0Threads) {
+        zc_cnt[i] = lcnt[i];
+        zc_key[i] = lkey[i];
+    }
+}
+
 template <int V, bool kCode, bool kKey>
 __global__ __launch_bounds__(256) void car_prep_kernel(const int *__restrict__ cap, const typename VecT<V>::I *__restrict__ use,
                                                        const typename VecT<V>::H *__restrict__ haz, int N, int SV,
@@ -183,6 +231,13 @@ static int prep_launch(hipStream_t stream, const Prep16Args &a, int SV, int npb,
 }
 
 int launch_prep(hipStream_t stream, const Prep16Args &a) {
+    if ((int64_t)a.N * a.S <= kPrepSmallCells && a.S <= kPrepSmallS) {
+        RSK_CHECK(a.code || a.nodekey, "prep: nothing to write");
+        car_prep_small_kernel<<<1, kPrep0Threads, 0, stream>>>(a.cap, a.use, a.haz, a.N, a.S, a.code, a.nodekey,
+                                                               a.zc_cnt, a.zc_key, a.code ? a.capmax : nullptr);
+        RSK_HIP(hipGetLastError());
+        return RSK_OK;
+    }
     RSK_TRY(launch_prep0(stream, a));
     return launch_prep_main(stream, a);
 }
