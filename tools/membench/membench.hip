@@ -35,6 +35,34 @@ __global__ __launch_bounds__(256) void k_tile(const int *__restrict__ src, int *
     if (MODE == 1 && acc == 0x7fffffff) sink[0] = acc;
 }
 
+// CH consecutive 256-B segments of a row per work item (chunk of 64 * CH
+// scenarios): a wave moves one row's CH segments back to back, so the
+// requests of one row reach DRAM together (512 B / 1 KB per row visit).
+template <int CH, int MODE>
+__global__ __launch_bounds__(256) void k_tile_wide(const int *__restrict__ src, int *__restrict__ dst, int P, int S,
+                                                   int nblk, int chunk_major, const int *__restrict__ perm,
+                                                   int *__restrict__ sink) {
+    const int nchunk = S / (64 * CH);
+    const int bid = blockIdx.x;
+    const int blk = chunk_major ? bid % nblk : bid / nchunk;
+    const int c = chunk_major ? bid / nblk : bid % nchunk;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int acc = 0;
+#pragma unroll 2
+    for (int r = wave; r < 128; r += 4) {
+        const int row = blk * 128 + r;
+        const int q = perm[min(row, P - 1)];
+        const size_t o = (size_t)q * S + (size_t)c * 64 * CH + lane;
+#pragma unroll
+        for (int h = 0; h < CH; ++h) {
+            if (MODE == 0) dst[o + 64 * h] = src[o + 64 * h];
+            else if (MODE == 1) acc += src[o + 64 * h];
+            else dst[o + 64 * h] = row;
+        }
+    }
+    if (MODE == 1 && acc == 0x7fffffff) sink[0] = acc;
+}
+
 int main(int argc, char **argv) {
     const int P = 100000, S = 4096;
     const size_t n = (size_t)P * S;
@@ -68,6 +96,13 @@ int main(int argc, char **argv) {
         printf("%-6s seg=%2d %s perm=%d: %.3f ms  %.2f TB/s\n", name, seg, cm ? "chunk-major" : "pod-major  ", (int)shuffle, ms,
                bytes_mult * n * 4 / (ms * 1e-3) / 1e12);
     };
+    run(k_tile_wide<1, 0>, 64, "copyW1", 1, 2);
+    run(k_tile_wide<2, 0>, 128, "copyW2", 1, 2);
+    run(k_tile_wide<4, 0>, 256, "copyW4", 1, 2);
+    run(k_tile_wide<1, 1>, 64, "readW1", 1, 1);
+    run(k_tile_wide<2, 1>, 128, "readW2", 1, 1);
+    run(k_tile_wide<1, 2>, 64, "writW1", 1, 1);
+    run(k_tile_wide<2, 2>, 128, "writW2", 1, 1);
     for (int cm = 1; cm >= 0; --cm) {
         run(k_tile<16, 0>, 16, "copy", cm, 2);
         run(k_tile<32, 0>, 32, "copy", cm, 2);
