@@ -933,6 +933,32 @@ int launch_detect_use(hipStream_t stream, const int *use, const int *cap, int N,
     return RSK_OK;
 }
 
+// The multi-round loop's halves without memsets or decode launches: the keys
+// arrive zeroed (the move kernel clears its scenario's words after use).
+int launch_detect_use_keys(hipStream_t stream, const int *use, const int *cap, int N, int S, int threshold,
+                           uint8_t *hazard, unsigned long long *key) {
+    const int npb = chunk_for(N, S);
+    const unsigned total = (unsigned)(ceil_div(N, npb) * S);
+    detect_use_kernel<<<(unsigned)ceil_div(total, 256), 256, 0, stream>>>(use, cap, N, S, threshold, npb, total, hazard,
+                                                                           key);
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
+}
+
+int launch_pick_keys(hipStream_t stream, const int *assign, const int *pod_cpu, int P, int S,
+                     const unsigned long long *kdet, int *most_ws, unsigned long long *kpick) {
+    decode_first_max<<<(unsigned)ceil_div(S, 256), 256, 0, stream>>>(kdet, S, most_ws);
+    if (P > 0) {
+        const int ppt = chunk_for(P, S);
+        const int64_t tot = ceil_div(P, ppt) * S;
+        RSK_CHECK(tot < INT32_MAX, "grid too large");
+        pick_pod_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, stream>>>(assign, pod_cpu, P, S, most_ws, ppt,
+                                                                          (unsigned)tot, kpick);
+    }
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
+}
+
 int launch_decode_first_max(hipStream_t stream, const unsigned long long *key, int S, int *out_pod) {
     decode_first_max<<<(unsigned)ceil_div(S, 256), 256, 0, stream>>>(key, S, out_pod);
     RSK_HIP(hipGetLastError());

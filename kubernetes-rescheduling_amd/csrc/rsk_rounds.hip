@@ -70,14 +70,25 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
                                              const int *__restrict__ cap, const uint8_t *__restrict__ haz,
                                              const int *__restrict__ evict, int s, int S, int N, int H, int update,
                                              int *__restrict__ out_target, unsigned short *__restrict__ asg16,
-                                             unsigned *tab) {
+                                             unsigned *tab, unsigned long long *__restrict__ kpick,
+                                             unsigned long long *__restrict__ kdet, int *__restrict__ ev_out) {
     unsigned *keys = tab, *cnts = tab + H;
     unsigned long long *red64 = reinterpret_cast<unsigned long long *>(tab + 2 * H);  // best
     unsigned *red = tab + 2 * H + 2;                                                   // M, n_at_M, n_free
     const int tid = threadIdx.x;
-    const int p = evict[s];
+    int p;
+    if (kpick) {  // the loop: the pick kernel's packed (cpu, ~pod) key, decoded here
+        const unsigned long long k = kpick[s];
+        p = k ? (int)(~(unsigned)(k & 0xffffffffull)) : -1;
+    } else {
+        p = evict[s];
+    }
+    if (kpick && tid == 0) ev_out[s] = p;
     if (p < 0) {
-        if (tid == 0) out_target[s] = kNoEvict;
+        if (tid == 0) {
+            out_target[s] = kNoEvict;
+            if (kpick) kpick[s] = kdet[s] = 0ull;  // zeroed for the next round's atomics
+        }
         return;
     }
     const int b = row_ptr[p], d = row_ptr[p + 1] - b;
@@ -144,6 +155,7 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
         else if (nbest == 1) t = node;                // the single best, even if overloaded
         else t = rem >= 0 ? node : RSK_TARGET_NONE;   // largest remaining CPU, None if < 0
         out_target[s] = t;
+        if (kpick) kpick[s] = kdet[s] = 0ull;  // every thread read p long before the last barrier
         if (update && t >= 0) {  // build-defined update: the pod's CPU moves with it
             const size_t pc = (size_t)p * S + s;
             const int old = assign[pc], c = pod_cpu[p];
@@ -166,12 +178,15 @@ __global__ __launch_bounds__(kMoveThreads) void car_move_kernel(const int *__res
                                                                 const int *__restrict__ evict, int S, int N, int H,
                                                                 int update, int *__restrict__ out_target,
                                                                 unsigned short *__restrict__ asg16,
-                                                                unsigned *__restrict__ gtab) {
+                                                                unsigned *__restrict__ gtab,
+                                                                unsigned long long *__restrict__ kpick,
+                                                                unsigned long long *__restrict__ kdet,
+                                                                int *__restrict__ ev_out) {
     extern __shared__ __attribute__((aligned(16))) unsigned lds[];
     unsigned *tab = kGlobal ? gtab + (size_t)blockIdx.x * (size_t)(2 * H + 8) : lds;
     for (int s = (int)blockIdx.x; s < S; s += (int)gridDim.x) {
         car_move_one<kGlobal>(row_ptr, col, pod_cpu, assign, use, cap, haz, evict, s, S, N, H, update, out_target,
-                              asg16, tab);
+                              asg16, tab, kpick, kdet, ev_out);
         if (kGlobal) move_sync<true>();  // the area is free before the next scenario clears it
     }
 }
@@ -194,8 +209,11 @@ __global__ __launch_bounds__(256) void asg16_kernel(const int *__restrict__ assi
 // 8 consecutive scenarios), one 16-B load per pod; the first max (cpu, -pod)
 // among pods on most[s] with cpu > -1, packed as pick_pod_kernel packs it.  Half
 // the bytes of the int32 scan (rsk_metrics.hip pick_pod_kernel).
+// kKeys (the loop): most[s] decoded from the detect kernel's packed key.
+template <bool kKeys>
 __global__ __launch_bounds__(256) void pick16_kernel(const uint4 *__restrict__ asg, const int *__restrict__ pod_cpu,
-                                                      int P, int S8, const int *__restrict__ most, int ppt,
+                                                      int P, int S8, const int *__restrict__ most,
+                                                      const unsigned long long *__restrict__ kdet, int ppt,
                                                       unsigned total, unsigned long long *__restrict__ best) {
     const unsigned t = blockIdx.x * 256u + threadIdx.x;
     if (t >= total) return;
@@ -205,7 +223,13 @@ __global__ __launch_bounds__(256) void pick16_kernel(const uint4 *__restrict__ a
     bool any = false;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const int v = most[s8 * 8 + j];
+        int v;
+        if (kKeys) {
+            const unsigned long long k = kdet[s8 * 8 + j];
+            v = k ? (int)(~(unsigned)(k & 0xffffffffull)) : -1;
+        } else {
+            v = most[s8 * 8 + j];
+        }
         m[j] = v < 0 ? 0x10000u : (unsigned)v;  // no hazard node: matches nothing
         any |= v >= 0;
     }
@@ -261,15 +285,16 @@ MoveGeom move_geometry(rsk_rounds *r, int N, int S) {
 }
 
 int launch_move(rsk_rounds *r, hipStream_t st, const MoveGeom &g, int *assign, int *use, const int *cap,
-                const uint8_t *haz, const int *evict, int S, int N, int update, int *target, unsigned short *a16) {
+                const uint8_t *haz, const int *evict, int S, int N, int update, int *target, unsigned short *a16,
+                unsigned long long *kpick = nullptr, unsigned long long *kdet = nullptr, int *ev_out = nullptr) {
     if (g.lds)
         car_move_kernel<false><<<dim3((unsigned)g.grid), dim3(kMoveThreads), g.lds, st>>>(
             r->row_ptr.as<int>(), r->col.as<int>(), r->pod_cpu.as<int>(), assign, use, cap, haz, evict, S, N, g.H,
-            update, target, a16, nullptr);
+            update, target, a16, nullptr, kpick, kdet, ev_out);
     else
         car_move_kernel<true><<<dim3((unsigned)g.grid), dim3(kMoveThreads), 0, st>>>(
             r->row_ptr.as<int>(), r->col.as<int>(), r->pod_cpu.as<int>(), assign, use, cap, haz, evict, S, N, g.H,
-            update, target, a16, r->gtab.as<unsigned>());
+            update, target, a16, r->gtab.as<unsigned>(), kpick, kdet, ev_out);
     RSK_HIP(hipGetLastError());
     return RSK_OK;
 }
@@ -434,7 +459,7 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
     }
     RSK_TRY(r->haz.reserve(NS));
     RSK_TRY(r->most.reserve((size_t)S * 4));
-    RSK_TRY(r->key_ws.reserve((size_t)S * 8));
+    RSK_TRY(r->key_ws.reserve((size_t)S * 16));  // the detect and pick keys
     const MoveGeom g = move_geometry(r, N, S);
     RSK_TRY(g.rc);
     // the eviction scan reads a u16 shadow of assign when node ids fit (kept in
@@ -448,36 +473,36 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         asg16_kernel<<<(unsigned)ceil_div((int64_t)PS, 256), 256, 0, st>>>(d_assign, PS, N, a16);
         RSK_HIP(hipGetLastError());
     }
+    // Three launches per round: detect -> (packed key) -> pick -> (packed key) ->
+    // move, which decodes the eviction, writes it out and zeroes both keys for
+    // the next round (no memsets, no decode launches; zeroed once here).
+    unsigned long long *kdet = r->key_ws.as<unsigned long long>(), *kpick = kdet + S;
+    RSK_HIP(hipMemsetAsync(kdet, 0, (size_t)S * 16, st));
     for (int round = 0; round < R; ++round) {
         int *ev = d_evict + (size_t)round * S;
         {
             ScopedTimer tm(ctx, "rounds_detect");
-            RSK_TRY(launch_detect_use(st, d_use, d_cap, N, S, threshold, r->haz.as<uint8_t>(),
-                                      r->key_ws.as<unsigned long long>(), r->most.as<int>()));
+            RSK_TRY(launch_detect_use_keys(st, d_use, d_cap, N, S, threshold, r->haz.as<uint8_t>(), kdet));
         }
         {
             ScopedTimer tm(ctx, "rounds_pick");
             if (s16) {
-                unsigned long long *key = r->key_ws.as<unsigned long long>();
-                RSK_HIP(hipMemsetAsync(key, 0, (size_t)S * 8, st));
                 const int S8 = S / 8;
                 const int ppt = (int)std::max<int64_t>(1, ceil_div((int64_t)r->P * S8, (int64_t)256 * 4096));
                 const int64_t tot = ceil_div(r->P, ppt) * S8;
                 RSK_CHECK(tot < INT32_MAX, "grid too large");
-                pick16_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, st>>>(
-                    reinterpret_cast<const uint4 *>(a16), r->pod_cpu.as<int>(), r->P, S8, r->most.as<int>(), ppt,
-                    (unsigned)tot, key);
+                pick16_kernel<true><<<(unsigned)ceil_div(tot, 256), 256, 0, st>>>(
+                    reinterpret_cast<const uint4 *>(a16), r->pod_cpu.as<int>(), r->P, S8, nullptr, kdet, ppt,
+                    (unsigned)tot, kpick);
                 RSK_HIP(hipGetLastError());
-                RSK_TRY(launch_decode_first_max(st, key, S, ev));
             } else {
-                RSK_TRY(launch_pick_max_pod(st, d_assign, r->pod_cpu.as<int>(), r->P, S, r->most.as<int>(),
-                                            r->key_ws.as<unsigned long long>(), ev));
+                RSK_TRY(launch_pick_keys(st, d_assign, r->pod_cpu.as<int>(), r->P, S, kdet, r->most.as<int>(), kpick));
             }
         }
         {
             ScopedTimer tm(ctx, "rounds_move");
-            RSK_TRY(launch_move(r, st, g, d_assign, d_use, d_cap, r->haz.as<uint8_t>(), ev, S, N, 1,
-                                d_target + (size_t)round * S, a16));
+            RSK_TRY(launch_move(r, st, g, d_assign, d_use, d_cap, r->haz.as<uint8_t>(), nullptr, S, N, 1,
+                                d_target + (size_t)round * S, a16, kpick, kdet, ev));
         }
     }
     if (!dev) {
@@ -590,8 +615,8 @@ int rsk_pick_max_pod16(rsk_ctx *ctx, const uint16_t *assign16, const int32_t *po
         const int ppt = (int)std::max<int64_t>(1, ceil_div((int64_t)P * S8, (int64_t)256 * 4096));
         const int64_t tot = ceil_div(P, ppt) * S8;
         RSK_CHECK(tot < INT32_MAX, "grid too large");
-        pick16_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, ctx->stream>>>(
-            reinterpret_cast<const uint4 *>(assign16), pod_cpu, P, S8, most, ppt, (unsigned)tot, key);
+        pick16_kernel<false><<<(unsigned)ceil_div(tot, 256), 256, 0, ctx->stream>>>(
+            reinterpret_cast<const uint4 *>(assign16), pod_cpu, P, S8, most, nullptr, ppt, (unsigned)tot, key);
         RSK_HIP(hipGetLastError());
     }
     return launch_decode_first_max(ctx->stream, key, S, out_pod);
