@@ -199,10 +199,14 @@ int next_pow2(int x) {
 
 // u16 shadow of assign: node ids < N <= 65535, anything outside [0, N) -> 0xffff
 // (never a hazard node)
-__global__ __launch_bounds__(256) void asg16_kernel(const int *__restrict__ assign, size_t n, int N,
-                                                     unsigned short *__restrict__ out) {
+// (8 values per thread: two 16-B loads, one 16-B store; n % 8 == 0 since S % 8 == 0)
+__global__ __launch_bounds__(256) void asg16_kernel(const int4 *__restrict__ assign, size_t n8, int N,
+                                                     uint4 *__restrict__ out) {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < n) out[i] = (unsigned)assign[i] < (unsigned)N ? (unsigned short)assign[i] : (unsigned short)0xffff;
+    if (i >= n8) return;
+    const int4 a = assign[2 * i], b = assign[2 * i + 1];
+    auto c = [N](int v) { return (unsigned)v < (unsigned)N ? (unsigned)v : 0xffffu; };
+    out[i] = make_uint4(c(a.x) | c(a.y) << 16, c(a.z) | c(a.w) << 16, c(b.x) | c(b.y) << 16, c(b.z) | c(b.w) << 16);
 }
 
 // delete_replaced_pod.py:41-61 over the u16 shadow: thread = (chunk of ppt pods,
@@ -464,13 +468,14 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
     RSK_TRY(g.rc);
     // the eviction scan reads a u16 shadow of assign when node ids fit (kept in
     // step by the move kernel); otherwise the int32 scan
-    const bool s16 = N <= 65535 && S % 8 == 0 && PS > 0;
+    const bool s16 = N <= 65535 && S % 8 == 0 && PS > 0 && ((uintptr_t)d_assign % 16) == 0;
     unsigned short *a16 = nullptr;
     if (s16) {
         RSK_TRY(r->asg16.reserve(PS * 2));
         a16 = r->asg16.as<unsigned short>();
         ScopedTimer tm(ctx, "rounds_shadow");
-        asg16_kernel<<<(unsigned)ceil_div((int64_t)PS, 256), 256, 0, st>>>(d_assign, PS, N, a16);
+        asg16_kernel<<<(unsigned)ceil_div((int64_t)(PS / 8), 256), 256, 0, st>>>(
+            reinterpret_cast<const int4 *>(d_assign), PS / 8, N, reinterpret_cast<uint4 *>(a16));
         RSK_HIP(hipGetLastError());
     }
     // Three launches per round: detect -> (packed key) -> pick -> (packed key) ->
