@@ -147,7 +147,7 @@ int launch_decode_first_max(hipStream_t stream, const unsigned long long *key, i
 // launch (the next kernel decodes); launch_pick_keys decodes kdet into most_ws
 // for the int32 scan
 int launch_detect_use_keys(hipStream_t stream, const int *use, const int *cap, int N, int S, int threshold,
-                           uint8_t *hazard, unsigned long long *key);
+                           uint8_t *hazard, unsigned long long *key, int *zc_cnt, unsigned long long *zc_key);
 int launch_pick_keys(hipStream_t stream, const int *assign, const int *pod_cpu, int P, int S,
                      const unsigned long long *kdet, int *most_ws, unsigned long long *kpick);
 

@@ -646,26 +646,40 @@ __global__ __launch_bounds__(256) void detect_kernel(const int *__restrict__ pct
 // detect_kernel with cpu_pct computed in place (get_resource_usage.py:37, the
 // same fp64 divide, multiply and rint as cpu_pct_kernel): the multi-round loop
 // needs only the hazard flags and the most hazardous node, not the pct array.
+// zc_cnt / zc_key (may be null): the round's zero case per scenario as
+// car_prep reduces it (non-hazard nodes, max packed (cap - use, ~node)), for
+// the move kernel's rows that reach no candidate node.
 __global__ __launch_bounds__(256) void detect_use_kernel(const int *__restrict__ use, const int *__restrict__ cap, int N,
                                                          int S, int thr, int npb, unsigned total,
-                                                         uint8_t *__restrict__ haz, unsigned long long *__restrict__ most) {
+                                                         uint8_t *__restrict__ haz, unsigned long long *__restrict__ most,
+                                                         int *__restrict__ zc_cnt = nullptr,
+                                                         unsigned long long *__restrict__ zc_key = nullptr) {
     const unsigned t = blockIdx.x * 256u + threadIdx.x;
     if (t >= total) return;
     const int s = (int)(t % (unsigned)S);
     const int n0 = (int)(t / (unsigned)S) * npb, n1 = min(N, n0 + npb);
-    unsigned long long b = 0;
+    unsigned long long b = 0, bz = 0;
+    int nz = 0;
     for (int n = n0; n < n1; ++n) {
         const size_t idx = (size_t)n * S + s;
-        const int c = cap[n];
-        const int v = c == 0 ? -1 : (int)rint((double)use[idx] / (double)c * 100.0);
+        const int c = cap[n], u = use[idx];
+        const int v = c == 0 ? -1 : (int)rint((double)u / (double)c * 100.0);
         const bool h = v >= thr;
         haz[idx] = h;
         if (h) {
             const unsigned long long k = pack_hi_lo(v, ~(unsigned)n);
             b = k > b ? k : b;
+        } else {
+            ++nz;
+            const unsigned long long k = zc_pack(c - u, n);
+            bz = k > bz ? k : bz;
         }
     }
     if (b) atomicMax(&most[s], b);
+    if (zc_cnt && nz) {
+        atomicAdd(&zc_cnt[s], nz);
+        atomicMax(&zc_key[s], bz);
+    }
 }
 
 __global__ void decode_first_max(const unsigned long long *__restrict__ key, int S, int *__restrict__ out) {
@@ -936,11 +950,11 @@ int launch_detect_use(hipStream_t stream, const int *use, const int *cap, int N,
 // The multi-round loop's halves without memsets or decode launches: the keys
 // arrive zeroed (the move kernel clears its scenario's words after use).
 int launch_detect_use_keys(hipStream_t stream, const int *use, const int *cap, int N, int S, int threshold,
-                           uint8_t *hazard, unsigned long long *key) {
+                           uint8_t *hazard, unsigned long long *key, int *zc_cnt, unsigned long long *zc_key) {
     const int npb = chunk_for(N, S);
     const unsigned total = (unsigned)(ceil_div(N, npb) * S);
     detect_use_kernel<<<(unsigned)ceil_div(total, 256), 256, 0, stream>>>(use, cap, N, S, threshold, npb, total, hazard,
-                                                                           key);
+                                                                           key, zc_cnt, zc_key);
     RSK_HIP(hipGetLastError());
     return RSK_OK;
 }

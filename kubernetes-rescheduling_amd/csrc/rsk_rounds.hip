@@ -71,7 +71,8 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
                                              const int *__restrict__ evict, int s, int S, int N, int H, int update,
                                              int *__restrict__ out_target, unsigned short *__restrict__ asg16,
                                              unsigned *tab, unsigned long long *__restrict__ kpick,
-                                             unsigned long long *__restrict__ kdet, int *__restrict__ ev_out) {
+                                             unsigned long long *__restrict__ kdet, int *__restrict__ ev_out,
+                                             int *__restrict__ zc_cnt, unsigned long long *__restrict__ zc_key) {
     unsigned *keys = tab, *cnts = tab + H;
     unsigned long long *red64 = reinterpret_cast<unsigned long long *>(tab + 2 * H);  // best
     unsigned *red = tab + 2 * H + 2;                                                   // M, n_at_M, n_free
@@ -88,6 +89,7 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
         if (tid == 0) {
             out_target[s] = kNoEvict;
             if (kpick) kpick[s] = kdet[s] = 0ull;  // zeroed for the next round's atomics
+            if (zc_cnt) zc_cnt[s] = 0, zc_key[s] = 0ull;
         }
         return;
     }
@@ -130,6 +132,12 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
             atomicAdd(&red[1], nb);
             atomicMax(red64, best);
         }
+    } else if (zc_cnt) {  // max score 0: the detect kernel's zero case of the scenario
+        if (tid == 0) {
+            const unsigned long long z = zc_key[s];
+            red[1] = (unsigned)zc_cnt[s];
+            *red64 = red[1] ? move_pack((int)((unsigned)(z >> 32) ^ 0x80000000u), (int)~(unsigned)(z & 0xffffffffull)) : 0ull;
+        }
     } else {  // max score 0: every non-hazard node ties
         unsigned long long best = 0;
         unsigned nb = 0;
@@ -156,6 +164,7 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
         else t = rem >= 0 ? node : RSK_TARGET_NONE;   // largest remaining CPU, None if < 0
         out_target[s] = t;
         if (kpick) kpick[s] = kdet[s] = 0ull;  // every thread read p long before the last barrier
+        if (zc_cnt) zc_cnt[s] = 0, zc_key[s] = 0ull;
         if (update && t >= 0) {  // build-defined update: the pod's CPU moves with it
             const size_t pc = (size_t)p * S + s;
             const int old = assign[pc], c = pod_cpu[p];
@@ -181,12 +190,13 @@ __global__ __launch_bounds__(kMoveThreads) void car_move_kernel(const int *__res
                                                                 unsigned *__restrict__ gtab,
                                                                 unsigned long long *__restrict__ kpick,
                                                                 unsigned long long *__restrict__ kdet,
-                                                                int *__restrict__ ev_out) {
+                                                                int *__restrict__ ev_out, int *__restrict__ zc_cnt,
+                                                                unsigned long long *__restrict__ zc_key) {
     extern __shared__ __attribute__((aligned(16))) unsigned lds[];
     unsigned *tab = kGlobal ? gtab + (size_t)blockIdx.x * (size_t)(2 * H + 8) : lds;
     for (int s = (int)blockIdx.x; s < S; s += (int)gridDim.x) {
         car_move_one<kGlobal>(row_ptr, col, pod_cpu, assign, use, cap, haz, evict, s, S, N, H, update, out_target,
-                              asg16, tab, kpick, kdet, ev_out);
+                              asg16, tab, kpick, kdet, ev_out, zc_cnt, zc_key);
         if (kGlobal) move_sync<true>();  // the area is free before the next scenario clears it
     }
 }
@@ -290,15 +300,16 @@ MoveGeom move_geometry(rsk_rounds *r, int N, int S) {
 
 int launch_move(rsk_rounds *r, hipStream_t st, const MoveGeom &g, int *assign, int *use, const int *cap,
                 const uint8_t *haz, const int *evict, int S, int N, int update, int *target, unsigned short *a16,
-                unsigned long long *kpick = nullptr, unsigned long long *kdet = nullptr, int *ev_out = nullptr) {
+                unsigned long long *kpick = nullptr, unsigned long long *kdet = nullptr, int *ev_out = nullptr,
+                int *zc_cnt = nullptr, unsigned long long *zc_key = nullptr) {
     if (g.lds)
         car_move_kernel<false><<<dim3((unsigned)g.grid), dim3(kMoveThreads), g.lds, st>>>(
             r->row_ptr.as<int>(), r->col.as<int>(), r->pod_cpu.as<int>(), assign, use, cap, haz, evict, S, N, g.H,
-            update, target, a16, nullptr, kpick, kdet, ev_out);
+            update, target, a16, nullptr, kpick, kdet, ev_out, zc_cnt, zc_key);
     else
         car_move_kernel<true><<<dim3((unsigned)g.grid), dim3(kMoveThreads), 0, st>>>(
             r->row_ptr.as<int>(), r->col.as<int>(), r->pod_cpu.as<int>(), assign, use, cap, haz, evict, S, N, g.H,
-            update, target, a16, r->gtab.as<unsigned>(), kpick, kdet, ev_out);
+            update, target, a16, r->gtab.as<unsigned>(), kpick, kdet, ev_out, zc_cnt, zc_key);
     RSK_HIP(hipGetLastError());
     return RSK_OK;
 }
@@ -463,7 +474,7 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
     }
     RSK_TRY(r->haz.reserve(NS));
     RSK_TRY(r->most.reserve((size_t)S * 4));
-    RSK_TRY(r->key_ws.reserve((size_t)S * 16));  // the detect and pick keys
+    RSK_TRY(r->key_ws.reserve((size_t)S * 28));  // the detect and pick keys, the zero case
     const MoveGeom g = move_geometry(r, N, S);
     RSK_TRY(g.rc);
     // the eviction scan reads a u16 shadow of assign when node ids fit (kept in
@@ -481,13 +492,14 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
     // Three launches per round: detect -> (packed key) -> pick -> (packed key) ->
     // move, which decodes the eviction, writes it out and zeroes both keys for
     // the next round (no memsets, no decode launches; zeroed once here).
-    unsigned long long *kdet = r->key_ws.as<unsigned long long>(), *kpick = kdet + S;
-    RSK_HIP(hipMemsetAsync(kdet, 0, (size_t)S * 16, st));
+    unsigned long long *kdet = r->key_ws.as<unsigned long long>(), *kpick = kdet + S, *zkey = kpick + S;
+    int *zcnt = reinterpret_cast<int *>(zkey + S);
+    RSK_HIP(hipMemsetAsync(kdet, 0, (size_t)S * 28, st));
     for (int round = 0; round < R; ++round) {
         int *ev = d_evict + (size_t)round * S;
         {
             ScopedTimer tm(ctx, "rounds_detect");
-            RSK_TRY(launch_detect_use_keys(st, d_use, d_cap, N, S, threshold, r->haz.as<uint8_t>(), kdet));
+            RSK_TRY(launch_detect_use_keys(st, d_use, d_cap, N, S, threshold, r->haz.as<uint8_t>(), kdet, zcnt, zkey));
         }
         {
             ScopedTimer tm(ctx, "rounds_pick");
@@ -507,7 +519,7 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         {
             ScopedTimer tm(ctx, "rounds_move");
             RSK_TRY(launch_move(r, st, g, d_assign, d_use, d_cap, r->haz.as<uint8_t>(), nullptr, S, N, 1,
-                                d_target + (size_t)round * S, a16, kpick, kdet, ev));
+                                d_target + (size_t)round * S, a16, kpick, kdet, ev, zcnt, zkey));
         }
     }
     if (!dev) {
