@@ -134,9 +134,6 @@ constexpr int kBlock = 256;
 // by the public entry points and the multi-round loop (rsk_rounds.hip).
 // `key_ws` is S u64 of scratch; every call queues on `stream` only.
 int launch_cpu_pct(hipStream_t stream, const int *use, const int *cap, int N, int S, int *pct);
-// cpu_pct + detect in one pass (no pct array)
-int launch_detect_use(hipStream_t stream, const int *use, const int *cap, int N, int S, int threshold, uint8_t *hazard,
-                      unsigned long long *key_ws, int *most);
 int launch_detect(hipStream_t stream, const int *pct, int N, int S, int threshold, uint8_t *hazard,
                   unsigned long long *key_ws, int *most);
 int launch_pick_max_pod(hipStream_t stream, const int *assign, const int *pod_cpu, int P, int S, const int *most,

@@ -648,32 +648,50 @@ __global__ __launch_bounds__(256) void detect_kernel(const int *__restrict__ pct
 // needs only the hazard flags and the most hazardous node, not the pct array.
 // zc_cnt / zc_key (may be null): the round's zero case per scenario as
 // car_prep reduces it (non-hazard nodes, max packed (cap - use, ~node)), for
-// the move kernel's rows that reach no candidate node.
+// the move kernel's rows that reach no candidate node.  A workgroup = 64
+// scenarios (lane) x 4 waves over consecutive node ranges of npw nodes; the
+// waves' results meet in LDS, so a scenario's words take one atomic per
+// workgroup (125 per round at 5k nodes x 1024 scenarios, not 512).
 __global__ __launch_bounds__(256) void detect_use_kernel(const int *__restrict__ use, const int *__restrict__ cap, int N,
-                                                         int S, int thr, int npb, unsigned total,
-                                                         uint8_t *__restrict__ haz, unsigned long long *__restrict__ most,
-                                                         int *__restrict__ zc_cnt = nullptr,
-                                                         unsigned long long *__restrict__ zc_key = nullptr) {
-    const unsigned t = blockIdx.x * 256u + threadIdx.x;
-    if (t >= total) return;
-    const int s = (int)(t % (unsigned)S);
-    const int n0 = (int)(t / (unsigned)S) * npb, n1 = min(N, n0 + npb);
+                                                         int S, int thr, int npw, uint8_t *__restrict__ haz,
+                                                         unsigned long long *__restrict__ most,
+                                                         int *__restrict__ zc_cnt,
+                                                         unsigned long long *__restrict__ zc_key) {
+    __shared__ unsigned long long lb[4][64], lz[4][64];
+    __shared__ int ln[4][64];
+    const int lane = (int)threadIdx.x & 63, wv = (int)threadIdx.x >> 6;
+    const int nsc = (S + 63) >> 6;
+    const int sc = (int)blockIdx.x % nsc, nb = (int)blockIdx.x / nsc;
+    const int s = sc * 64 + lane;
+    const int n0 = (nb * 4 + wv) * npw, n1 = min(N, n0 + npw);
     unsigned long long b = 0, bz = 0;
     int nz = 0;
-    for (int n = n0; n < n1; ++n) {
-        const size_t idx = (size_t)n * S + s;
-        const int c = cap[n], u = use[idx];
-        const int v = c == 0 ? -1 : (int)rint((double)u / (double)c * 100.0);
-        const bool h = v >= thr;
-        haz[idx] = h;
-        if (h) {
-            const unsigned long long k = pack_hi_lo(v, ~(unsigned)n);
-            b = k > b ? k : b;
-        } else {
-            ++nz;
-            const unsigned long long k = zc_pack(c - u, n);
-            bz = k > bz ? k : bz;
+    if (s < S)
+        for (int n = n0; n < n1; ++n) {
+            const size_t idx = (size_t)n * S + s;
+            const int c = cap[n], u = use[idx];
+            const int v = c == 0 ? -1 : (int)rint((double)u / (double)c * 100.0);
+            const bool h = v >= thr;
+            haz[idx] = h;
+            if (h) {
+                const unsigned long long k = pack_hi_lo(v, ~(unsigned)n);
+                b = k > b ? k : b;
+            } else {
+                ++nz;
+                const unsigned long long k = zc_pack(c - u, n);
+                bz = k > bz ? k : bz;
+            }
         }
+    lb[wv][lane] = b;
+    lz[wv][lane] = bz;
+    ln[wv][lane] = nz;
+    __syncthreads();
+    if (wv != 0 || s >= S) return;
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+        b = max(b, lb[w][lane]);
+        bz = max(bz, lz[w][lane]);
+        nz += ln[w][lane];
     }
     if (b) atomicMax(&most[s], b);
     if (zc_cnt && nz) {
@@ -935,26 +953,16 @@ int launch_detect(hipStream_t stream, const int *pct, int N, int S, int threshol
     return RSK_OK;
 }
 
-int launch_detect_use(hipStream_t stream, const int *use, const int *cap, int N, int S, int threshold, uint8_t *hazard,
-                      unsigned long long *key_ws, int *most) {
-    RSK_HIP(hipMemsetAsync(key_ws, 0, (size_t)S * 8, stream));
-    const int npb = chunk_for(N, S);
-    const unsigned total = (unsigned)(ceil_div(N, npb) * S);
-    detect_use_kernel<<<(unsigned)ceil_div(total, 256), 256, 0, stream>>>(use, cap, N, S, threshold, npb, total, hazard,
-                                                                           key_ws);
-    decode_first_max<<<(unsigned)ceil_div(S, 256), 256, 0, stream>>>(key_ws, S, most);
-    RSK_HIP(hipGetLastError());
-    return RSK_OK;
-}
-
 // The multi-round loop's halves without memsets or decode launches: the keys
 // arrive zeroed (the move kernel clears its scenario's words after use).
 int launch_detect_use_keys(hipStream_t stream, const int *use, const int *cap, int N, int S, int threshold,
                            uint8_t *hazard, unsigned long long *key, int *zc_cnt, unsigned long long *zc_key) {
-    const int npb = chunk_for(N, S);
-    const unsigned total = (unsigned)(ceil_div(N, npb) * S);
-    detect_use_kernel<<<(unsigned)ceil_div(total, 256), 256, 0, stream>>>(use, cap, N, S, threshold, npb, total, hazard,
-                                                                           key, zc_cnt, zc_key);
+    const int64_t nsc = ceil_div(S, 64);
+    const int npw = (int)std::max<int64_t>(4, ceil_div((int64_t)N * nsc, 8192));  // ~8k waves
+    const int64_t blocks = nsc * ceil_div(N, 4 * npw);
+    RSK_CHECK(blocks < INT32_MAX, "grid too large");
+    detect_use_kernel<<<(unsigned)blocks, 256, 0, stream>>>(use, cap, N, S, threshold, npw, hazard, key, zc_cnt,
+                                                            zc_key);
     RSK_HIP(hipGetLastError());
     return RSK_OK;
 }
