@@ -414,12 +414,13 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(const int *__restrict_
 // nodemonitor.py:24-46 (per-node sums).
 // Grouping the pods by key node (its node in scenario 0, N when it has none) is
 // a two-level counting sort that keeps every counter in LDS: level 1 buckets
-// by key >> 8 (per-block histograms, a scan over them, a block-local scatter),
-// level 2 sorts each bucket by key & 255 in one workgroup.  (Global atomics
+// by key >> 6 (per-block histograms, a scan over them, a block-local scatter),
+// level 2 sorts each bucket by key & 63 in one workgroup.  (Global atomics
 // on the N key counters, one per pod for the count and again for the scatter,
 // took 55 + 68 us at 1M pods over 50k nodes.)
 constexpr int kNrChunk = 4096;     // pods per level-1 workgroup
-constexpr int kNrMaxBuckets = 16384;  // key >> 8 buckets held in LDS (N < 2^22)
+constexpr int kNrSubBits = 6, kNrSub = 1 << kNrSubBits;  // level-2 sub-buckets
+constexpr int kNrMaxBuckets = 16384;  // key >> kNrSubBits buckets held in LDS (N < 2^20)
 __device__ __forceinline__ int nr_key(const int *__restrict__ assign, int p, int S, int N) {
     const int a = assign[(size_t)p * S];
     return (unsigned)a < (unsigned)N ? a : N;
@@ -435,7 +436,7 @@ __global__ __launch_bounds__(256) void nr_hist_kernel(const int *__restrict__ as
     for (int p = p0 + (int)threadIdx.x; p < p1; p += 256) {
         const int k = nr_key(assign, p, S, N);
         pkey[p] = k;
-        atomicAdd(&hist[k >> 8], 1);
+        atomicAdd(&hist[k >> kNrSubBits], 1);
     }
     __syncthreads();
     for (int j = (int)threadIdx.x; j < nbk; j += 256) bh[(size_t)j * gridDim.x + blockIdx.x] = hist[j];
@@ -451,37 +452,38 @@ __global__ __launch_bounds__(256) void nr_part_kernel(const int *__restrict__ pk
     const int p0 = (int)blockIdx.x * kNrChunk, p1 = min(P, p0 + kNrChunk);
     for (int p = p0 + (int)threadIdx.x; p < p1; p += 256) {
         const int k = pkey[p];
-        const int pos = atomicAdd(&cur[k >> 8], 1);
+        const int pos = atomicAdd(&cur[k >> kNrSubBits], 1);
         perm1[pos] = p;
         keys1[pos] = k;
     }
 }
 
-// level 2: bucket j (one workgroup, any size) sorted by key & 255
+// level 2: bucket j (one workgroup, any size) sorted by key & (kNrSub - 1)
 __global__ __launch_bounds__(256) void nr_sub_kernel(const int *__restrict__ perm1, const int *__restrict__ keys1,
                                                      const int *__restrict__ boff, int nblk1, int nbk, int P,
                                                      int *__restrict__ perm, int *__restrict__ keys) {
-    __shared__ int cnt[256], pre[256];
+    __shared__ int cnt[kNrSub];
     const int j = (int)blockIdx.x, t = (int)threadIdx.x;
     const int lo = boff[(size_t)j * nblk1], hi = j + 1 < nbk ? boff[(size_t)(j + 1) * nblk1] : P;
-    cnt[t] = 0;
+    if (t < kNrSub) cnt[t] = 0;
     __syncthreads();
-    for (int i = lo + t; i < hi; i += 256) atomicAdd(&cnt[keys1[i] & 255], 1);
+    for (int i = lo + t; i < hi; i += 256) atomicAdd(&cnt[keys1[i] & (kNrSub - 1)], 1);
     __syncthreads();
-    const int c = cnt[t];
-    pre[t] = c;
-    __syncthreads();
-    for (int d = 1; d < 256; d <<= 1) {
-        const int x = t >= d ? pre[t - d] : 0;
-        __syncthreads();
-        pre[t] += x;
-        __syncthreads();
+    if (t < 64) {  // one wave scans the kNrSub (<= 64) counts
+        static_assert(kNrSub <= 64, "one wave scans the sub-buckets");
+        const int c = t < kNrSub ? cnt[t] : 0;
+        int x = c;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(x, d, 64);
+            x += t >= d ? y : 0;
+        }
+        if (t < kNrSub) cnt[t] = lo + x - c;  // the sub-bucket's first slot, then its cursor
     }
-    cnt[t] = lo + pre[t] - c;  // the sub-bucket's first slot, then its cursor
     __syncthreads();
     for (int i = lo + t; i < hi; i += 256) {
         const int k = keys1[i];
-        const int pos = atomicAdd(&cnt[k & 255], 1);
+        const int pos = atomicAdd(&cnt[k & (kNrSub - 1)], 1);
         perm[pos] = perm1[i];
         keys[pos] = k;
     }
@@ -1235,7 +1237,7 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
     RSK_HIP(hipMemsetAsync(d_cnt, 0, NS * 4, ctx->stream));
     RSK_HIP(hipMemsetAsync(d_cs, 0, NS * 8, ctx->stream));
     if (d_ms) RSK_HIP(hipMemsetAsync(d_ms, 0, NS * 8, ctx->stream));
-    const int nbk = (N >> 8) + 1;  // key >> 8 buckets (keys 0..N)
+    const int nbk = (N >> kNrSubBits) + 1;  // key >> kNrSubBits buckets (keys 0..N)
     if (PS && S >= 32 && nbk <= kNrMaxBuckets) {  // segmented: group the pods by key node, per-key register sums
         const int runs = (int)ceil_div(P, kNrRun);
         const int64_t waves = (int64_t)runs * ceil_div(S, 64);
