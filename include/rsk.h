@@ -252,6 +252,35 @@ int rsk_rows_cut_delta(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_
                        const int32_t *evict, const int32_t *target, int32_t N, int64_t *cut_inout, uint32_t flags);
 int rsk_pick_max_pod16(rsk_ctx *ctx, const uint16_t *assign16, const int32_t *pod_cpu, int32_t P, int32_t S,
                        const int32_t *most, int32_t *out_pod, uint32_t flags);
+/* The row-sharded round fused into four launches (device pointers, RSK_F_DEVICE
+ * required).  key_most / key_evict / zc_cnt / zc_key [S] are zero before the
+ * first round; rsk_rows_place leaves them zero for the next one.
+ * rsk_rows_detect: the monitor's usage out_use = (int32)(base + cpu) (the
+ *   summed per-node partials, nodemonitor.py's read-back), get_resource_usage.py:
+ *   37's pct, harzard_detect.py:3-27's hazard flags, key_most[s] = the packed
+ *   (pct, ~node) max (the most hazardous node, first on ties) and the zero
+ *   case per scenario (non-hazard count, max (cap - use, ~node)).
+ * rsk_rows_pick: delete_replaced_pod.py:41-61 over this rank's q rows (int32
+ *   assign rows or the u16 shadow, elem_bytes 4 / 2; pod r0 + p): key_evict[s]
+ *   = atomic max of pod_cpu[g] << 32 | (2^32 - 1 - g) over its pods on the
+ *   most hazardous node (0: none) -- the MAX all-reduce key.
+ * rsk_rows_place: the CAR target (rescheduling.py:174-218) of the reduced key's
+ *   pod when it is in rows [r0, r1), else RSK_TARGET_NO_EVICT; out_evict[s] =
+ *   the decoded pod (-1 none) on every rank.  The zero case comes from
+ *   rsk_rows_detect's words.
+ * rsk_rows_move: rsk_rows_cut_delta then rsk_rows_apply in one launch.        */
+int rsk_rows_detect(rsk_ctx *ctx, const int64_t *base, const int64_t *cpu, const int32_t *cap_cpu, int32_t N, int32_t S,
+                    int32_t threshold, int32_t *out_use, uint8_t *out_hazard, int64_t *key_most, int32_t *zc_cnt,
+                    int64_t *zc_key, uint32_t flags);
+int rsk_rows_pick(rsk_ctx *ctx, const void *rows, int32_t elem_bytes, int32_t q, int32_t S, int32_t r0,
+                  const int32_t *pod_cpu, const int64_t *key_most, int64_t *key_evict, uint32_t flags);
+int rsk_rows_place(rsk_rounds *r, const int32_t *assign, int32_t S, const int32_t *cap_cpu, const int32_t *use_cpu,
+                   const uint8_t *hazard, int32_t N, int32_t r0, int32_t r1, int64_t *key_most, int64_t *key_evict,
+                   int32_t *zc_cnt, int64_t *zc_key, int32_t *out_evict, int32_t *out_target, uint32_t flags);
+int rsk_rows_move(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, const int32_t *rev_ptr,
+                  const int32_t *rev_idx, int32_t P, int32_t r0, int32_t r1, int32_t *assign, int32_t S,
+                  const int32_t *evict, const int32_t *target, int32_t N, const int32_t *pod_cpu, const int64_t *pod_mem,
+                  int64_t *cpu_part, int64_t *mem_part, uint16_t *shadow16, int64_t *cut_inout, uint32_t flags);
 
 /* ---- µBench workmodel -> relation CSR (host only, no device) -----------------
  * The caller's on-disk format (workmodelC.json).  One

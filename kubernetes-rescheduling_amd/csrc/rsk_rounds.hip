@@ -72,7 +72,8 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
                                              int *__restrict__ out_target, unsigned short *__restrict__ asg16,
                                              unsigned *tab, unsigned long long *__restrict__ kpick,
                                              unsigned long long *__restrict__ kdet, int *__restrict__ ev_out,
-                                             int *__restrict__ zc_cnt, unsigned long long *__restrict__ zc_key) {
+                                             int *__restrict__ zc_cnt, unsigned long long *__restrict__ zc_key,
+                                             int own0, int own1) {
     unsigned *keys = tab, *cnts = tab + H;
     unsigned long long *red64 = reinterpret_cast<unsigned long long *>(tab + 2 * H);  // best
     unsigned *red = tab + 2 * H + 2;                                                   // M, n_at_M, n_free
@@ -85,7 +86,7 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
         p = evict[s];
     }
     if (kpick && tid == 0) ev_out[s] = p;
-    if (p < 0) {
+    if (p < own0 || p >= own1) {  // no eviction, or (row-sharded) another rank's pod
         if (tid == 0) {
             out_target[s] = kNoEvict;
             if (kpick) kpick[s] = kdet[s] = 0ull;  // zeroed for the next round's atomics
@@ -191,12 +192,13 @@ __global__ __launch_bounds__(kMoveThreads) void car_move_kernel(const int *__res
                                                                 unsigned long long *__restrict__ kpick,
                                                                 unsigned long long *__restrict__ kdet,
                                                                 int *__restrict__ ev_out, int *__restrict__ zc_cnt,
-                                                                unsigned long long *__restrict__ zc_key) {
+                                                                unsigned long long *__restrict__ zc_key, int own0,
+                                                                int own1) {
     extern __shared__ __attribute__((aligned(16))) unsigned lds[];
     unsigned *tab = kGlobal ? gtab + (size_t)blockIdx.x * (size_t)(2 * H + 8) : lds;
     for (int s = (int)blockIdx.x; s < S; s += (int)gridDim.x) {
         car_move_one<kGlobal>(row_ptr, col, pod_cpu, assign, use, cap, haz, evict, s, S, N, H, update, out_target,
-                              asg16, tab, kpick, kdet, ev_out, zc_cnt, zc_key);
+                              asg16, tab, kpick, kdet, ev_out, zc_cnt, zc_key, own0, own1);
         if (kGlobal) move_sync<true>();  // the area is free before the next scenario clears it
     }
 }
@@ -301,15 +303,15 @@ MoveGeom move_geometry(rsk_rounds *r, int N, int S) {
 int launch_move(rsk_rounds *r, hipStream_t st, const MoveGeom &g, int *assign, int *use, const int *cap,
                 const uint8_t *haz, const int *evict, int S, int N, int update, int *target, unsigned short *a16,
                 unsigned long long *kpick = nullptr, unsigned long long *kdet = nullptr, int *ev_out = nullptr,
-                int *zc_cnt = nullptr, unsigned long long *zc_key = nullptr) {
+                int *zc_cnt = nullptr, unsigned long long *zc_key = nullptr, int own0 = 0, int own1 = INT_MAX) {
     if (g.lds)
         car_move_kernel<false><<<dim3((unsigned)g.grid), dim3(kMoveThreads), g.lds, st>>>(
             r->row_ptr.as<int>(), r->col.as<int>(), r->pod_cpu.as<int>(), assign, use, cap, haz, evict, S, N, g.H,
-            update, target, a16, nullptr, kpick, kdet, ev_out, zc_cnt, zc_key);
+            update, target, a16, nullptr, kpick, kdet, ev_out, zc_cnt, zc_key, own0, own1);
     else
         car_move_kernel<true><<<dim3((unsigned)g.grid), dim3(kMoveThreads), 0, st>>>(
             r->row_ptr.as<int>(), r->col.as<int>(), r->pod_cpu.as<int>(), assign, use, cap, haz, evict, S, N, g.H,
-            update, target, a16, r->gtab.as<unsigned>(), kpick, kdet, ev_out, zc_cnt, zc_key);
+            update, target, a16, r->gtab.as<unsigned>(), kpick, kdet, ev_out, zc_cnt, zc_key, own0, own1);
     RSK_HIP(hipGetLastError());
     return RSK_OK;
 }
@@ -396,6 +398,136 @@ __global__ __launch_bounds__(256) void rows_cut_delta_kernel(const int *__restri
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
     if (lane == 0 && d) cut[s] += d;
+}
+
+// ---- the row-sharded loop, fused (rsk_rows_detect / _pick / _place / _move) ----
+// The monitor's usage (base + the ranks' summed CPU partials, truncated to int32
+// as the torch path does) and detect_use_kernel's pass in one: hazard flags,
+// the packed (pct, ~node) maxima, the zero case; the usage is written out for
+// the placement's exact ties.
+__global__ __launch_bounds__(256) void rows_detect_kernel(const long long *__restrict__ base,
+                                                          const long long *__restrict__ cpu, const int *__restrict__ cap,
+                                                          int N, int S, int thr, int npw, int *__restrict__ use_out,
+                                                          uint8_t *__restrict__ haz, unsigned long long *__restrict__ most,
+                                                          int *__restrict__ zc_cnt, unsigned long long *__restrict__ zc_key) {
+    __shared__ unsigned long long lb[4][64], lz[4][64];
+    __shared__ int ln[4][64];
+    const int lane = (int)threadIdx.x & 63, wv = (int)threadIdx.x >> 6;
+    const int nsc = (S + 63) >> 6;
+    const int sc = (int)blockIdx.x % nsc, nb = (int)blockIdx.x / nsc;
+    const int s = sc * 64 + lane;
+    const int n0 = (nb * 4 + wv) * npw, n1 = min(N, n0 + npw);
+    unsigned long long b = 0, bz = 0;
+    int nz = 0;
+    if (s < S)
+        for (int n = n0; n < n1; ++n) {
+            const size_t idx = (size_t)n * S + s;
+            const int c = cap[n], u = (int)(base[idx] + cpu[idx]);
+            use_out[idx] = u;
+            const int v = c == 0 ? -1 : (int)rint((double)u / (double)c * 100.0);
+            const bool h = v >= thr;
+            haz[idx] = h;
+            if (h) {
+                const unsigned long long k = ((unsigned long long)((unsigned)v ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)n);
+                b = k > b ? k : b;
+            } else {
+                ++nz;
+                const unsigned long long k = ((unsigned long long)((unsigned)(c - u) ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)n);
+                bz = k > bz ? k : bz;
+            }
+        }
+    lb[wv][lane] = b;
+    lz[wv][lane] = bz;
+    ln[wv][lane] = nz;
+    __syncthreads();
+    if (wv != 0 || s >= S) return;
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+        b = max(b, lb[w][lane]);
+        bz = max(bz, lz[w][lane]);
+        nz += ln[w][lane];
+    }
+    if (b) atomicMax(&most[s], b);
+    if (nz) {
+        atomicAdd(&zc_cnt[s], nz);
+        atomicMax(&zc_key[s], bz);
+    }
+}
+
+// delete_replaced_pod.py:41-61 over this rank's rows (T = u16 shadow or int32
+// rows): the first max-CPU pod on most[s] (decoded from the detect key), as the
+// all-reduce MAX key pod_cpu << 32 | (2^32 - 1 - global pod); 0 = none.
+template <typename T>
+__global__ __launch_bounds__(256) void rows_pick_kernel(const T *__restrict__ rows, const int *__restrict__ pod_cpu,
+                                                        int q, int S, int r0, int ppt, unsigned total,
+                                                        const unsigned long long *__restrict__ most,
+                                                        unsigned long long *__restrict__ key) {
+    const unsigned t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= total) return;
+    const int s = (int)(t % (unsigned)S);
+    const unsigned long long mk = most[s];
+    if (!mk) return;
+    const int m = (int)~(unsigned)(mk & 0xffffffffull);
+    const int p0 = (int)(t / (unsigned)S) * ppt, p1 = min(q, p0 + ppt);
+    unsigned long long b = 0;
+    for (int p = p0; p < p1; ++p) {
+        if ((int)rows[(size_t)p * S + s] != m) continue;
+        const long long g = (long long)r0 + p;
+        const int c = pod_cpu[g];
+        if (c < 0) continue;
+        const unsigned long long k = ((unsigned long long)(unsigned)c << 32) | (0xffffffffull - (unsigned long long)g);
+        b = k > b ? k : b;
+    }
+    if (b) atomicMax(&key[s], b);
+}
+
+// The round's move for rows [r0, r1): the cut delta of rows_cut_delta_kernel
+// (lanes over the moved pod's edges, read before the move), then lane 0 applies
+// it as rows_apply_kernel does.  One wave per scenario: scenario s owns
+// assign[:, s] and the partials' column s.
+__global__ __launch_bounds__(256) void rows_move_kernel(const int *__restrict__ rp, const int *__restrict__ ci,
+                                                        const int *__restrict__ rvp, const int *__restrict__ rvi, int P,
+                                                        int r0, int r1, int *__restrict__ assign, int S,
+                                                        const int *__restrict__ evict, const int *__restrict__ target,
+                                                        int N, const int *__restrict__ pod_cpu,
+                                                        const long long *__restrict__ pod_mem,
+                                                        long long *__restrict__ cpu_part, long long *__restrict__ mem_part,
+                                                        unsigned short *__restrict__ shadow, long long *__restrict__ cut) {
+    const int lane = threadIdx.x & 63;
+    const int s = (int)blockIdx.x * 4 + ((int)threadIdx.x >> 6);
+    if (s >= S) return;  // whole wave
+    const int e = evict[s], t = target[s];
+    if (e < 0 || e >= P || t < 0 || t >= N) return;  // no move (rows_apply's rule)
+    int *ae = assign + (size_t)e * S + s;
+    const int o = *ae;
+    int d = 0;
+    if (e >= r0 && e < r1)
+        for (int k = rp[e] + lane; k < rp[e + 1]; k += 64) {
+            const int q = ci[k];
+            if (q == e) continue;
+            const int a = assign[(size_t)q * S + s];
+            d += (int)(t != a) - (int)(o != a);
+        }
+    for (int k = rvp[e] + lane; k < rvp[e + 1]; k += 64) {
+        const int q = rvi[k];
+        if (q == e || q < r0 || q >= r1) continue;
+        const int a = assign[(size_t)q * S + s];
+        d += (int)(a != t) - (int)(a != o);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
+    if (lane != 0) return;
+    if (d) cut[s] += d;
+    *ae = t;
+    if (e < r0 || e >= r1) return;
+    if (shadow) shadow[(size_t)(e - r0) * S + s] = (unsigned short)t;
+    const long long c = pod_cpu[e], m = pod_mem[e];
+    if ((unsigned)o < (unsigned)N) {
+        cpu_part[(size_t)o * S + s] -= c;
+        mem_part[(size_t)o * S + s] -= m;
+    }
+    cpu_part[(size_t)t * S + s] += c;
+    mem_part[(size_t)t * S + s] += m;
 }
 
 }  // namespace
@@ -637,6 +769,86 @@ int rsk_pick_max_pod16(rsk_ctx *ctx, const uint16_t *assign16, const int32_t *po
         RSK_HIP(hipGetLastError());
     }
     return launch_decode_first_max(ctx->stream, key, S, out_pod);
+}
+
+// ---- the row-sharded loop, fused (device pointers; keys zeroed on entry) ----
+int rsk_rows_detect(rsk_ctx *ctx, const int64_t *base, const int64_t *cpu, const int32_t *cap_cpu, int32_t N, int32_t S,
+                    int32_t threshold, int32_t *out_use, uint8_t *out_hazard, int64_t *key_most, int32_t *zc_cnt,
+                    int64_t *zc_key, uint32_t flags) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK((flags & RSK_F_DEVICE) && base && cpu && cap_cpu && out_use && out_hazard && key_most && zc_cnt && zc_key &&
+                  N > 0 && S > 0 && (int64_t)N * S < INT32_MAX,
+              "rsk_rows_detect: device pointers and N, S > 0 required");
+    const int64_t nsc = ceil_div(S, 64);
+    const int npw = (int)std::max<int64_t>(4, ceil_div((int64_t)N * nsc, 8192));
+    const int64_t blocks = nsc * ceil_div(N, 4 * npw);
+    ScopedTimer tm(ctx, "rows_detect");
+    rows_detect_kernel<<<(unsigned)blocks, 256, 0, ctx->stream>>>(
+        reinterpret_cast<const long long *>(base), reinterpret_cast<const long long *>(cpu), cap_cpu, N, S, threshold,
+        npw, out_use, out_hazard, reinterpret_cast<unsigned long long *>(key_most), zc_cnt,
+        reinterpret_cast<unsigned long long *>(zc_key));
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
+}
+
+int rsk_rows_pick(rsk_ctx *ctx, const void *rows, int32_t elem_bytes, int32_t q, int32_t S, int32_t r0,
+                  const int32_t *pod_cpu, const int64_t *key_most, int64_t *key_evict, uint32_t flags) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK((flags & RSK_F_DEVICE) && pod_cpu && key_most && key_evict && (elem_bytes == 2 || elem_bytes == 4) &&
+                  q >= 0 && S > 0 && r0 >= 0 && (q == 0 || rows),
+              "rsk_rows_pick: device pointers, 2- or 4-byte rows required");
+    if (q == 0) return RSK_OK;
+    const int ppt = (int)std::max<int64_t>(1, ceil_div((int64_t)q * S, (int64_t)256 * 2048));
+    const int64_t tot = ceil_div(q, ppt) * S;
+    RSK_CHECK(tot < INT32_MAX, "grid too large");
+    ScopedTimer tm(ctx, "rows_pick");
+    const auto *mk = reinterpret_cast<const unsigned long long *>(key_most);
+    auto *ke = reinterpret_cast<unsigned long long *>(key_evict);
+    if (elem_bytes == 2)
+        rows_pick_kernel<unsigned short><<<(unsigned)ceil_div(tot, 256), 256, 0, ctx->stream>>>(
+            static_cast<const unsigned short *>(rows), pod_cpu, q, S, r0, ppt, (unsigned)tot, mk, ke);
+    else
+        rows_pick_kernel<int><<<(unsigned)ceil_div(tot, 256), 256, 0, ctx->stream>>>(
+            static_cast<const int *>(rows), pod_cpu, q, S, r0, ppt, (unsigned)tot, mk, ke);
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
+}
+
+int rsk_rows_place(rsk_rounds *r, const int32_t *assign, int32_t S, const int32_t *cap_cpu, const int32_t *use_cpu,
+                   const uint8_t *hazard, int32_t N, int32_t r0, int32_t r1, int64_t *key_most, int64_t *key_evict,
+                   int32_t *zc_cnt, int64_t *zc_key, int32_t *out_evict, int32_t *out_target, uint32_t flags) {
+    RSK_CHECK(r, "null rounds object");
+    rsk_ctx *ctx = r->ctx;
+    RSK_TRY(activate(ctx));
+    RSK_CHECK((flags & RSK_F_DEVICE) && assign && cap_cpu && use_cpu && hazard && key_most && key_evict && zc_cnt &&
+                  zc_key && out_evict && out_target && S > 0 && N > 0 && 0 <= r0 && r0 <= r1 && r1 <= r->P &&
+                  (int64_t)N * S < INT32_MAX && (int64_t)r->P * S < INT32_MAX,
+              "rsk_rows_place: device pointers and rows [%d, %d) of P=%d required", r0, r1, r->P);
+    const MoveGeom g = move_geometry(r, N, S);
+    RSK_TRY(g.rc);
+    ScopedTimer tm(ctx, "rows_place");
+    return launch_move(r, ctx->stream, g, const_cast<int *>(assign), const_cast<int *>(use_cpu), cap_cpu, hazard,
+                       nullptr, S, N, 0, out_target, nullptr, reinterpret_cast<unsigned long long *>(key_evict),
+                       reinterpret_cast<unsigned long long *>(key_most), out_evict, zc_cnt,
+                       reinterpret_cast<unsigned long long *>(zc_key), r0, r1);
+}
+
+int rsk_rows_move(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, const int32_t *rev_ptr,
+                  const int32_t *rev_idx, int32_t P, int32_t r0, int32_t r1, int32_t *assign, int32_t S,
+                  const int32_t *evict, const int32_t *target, int32_t N, const int32_t *pod_cpu, const int64_t *pod_mem,
+                  int64_t *cpu_part, int64_t *mem_part, uint16_t *shadow16, int64_t *cut_inout, uint32_t flags) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK((flags & RSK_F_DEVICE) && row_ptr && col_idx && rev_ptr && rev_idx && assign && evict && target && pod_cpu &&
+                  pod_mem && cpu_part && mem_part && cut_inout && P > 0 && S > 0 && N > 0 && 0 <= r0 && r0 <= r1 &&
+                  r1 <= P,
+              "rsk_rows_move: device pointers and rows [%d, %d) of P=%d required", r0, r1, P);
+    ScopedTimer tm(ctx, "rows_move");
+    rows_move_kernel<<<(unsigned)ceil_div(S, 4), 256, 0, ctx->stream>>>(
+        row_ptr, col_idx, rev_ptr, rev_idx, P, r0, r1, assign, S, evict, target, N, pod_cpu,
+        reinterpret_cast<const long long *>(pod_mem), reinterpret_cast<long long *>(cpu_part),
+        reinterpret_cast<long long *>(mem_part), shadow16, reinterpret_cast<long long *>(cut_inout));
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
 }
 
 }  // extern "C"

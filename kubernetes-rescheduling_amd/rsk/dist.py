@@ -203,7 +203,7 @@ class LibrskRoundsBackend:
     rank's GPU; every call is asynchronous on the context's stream, which is the
     current torch stream's device)."""
 
-    def __init__(self, row_ptr, col_idx, pod_cpu, ctx=None, device=None, stream_ordered=False):
+    def __init__(self, row_ptr, col_idx, pod_cpu, ctx=None, device=None, stream_ordered=False, fused=True):
         import numpy as np
         import torch
         from . import api
@@ -236,6 +236,9 @@ class LibrskRoundsBackend:
         self.rev_ptr = torch.from_numpy(rvp).to(self.dev)
         self.rev_idx = torch.from_numpy(np.ascontiguousarray(src[order] if nnz else np.zeros(1, np.int32))).to(self.dev)
         self._F, self._check = RSK_F_DEVICE, check
+        # fused: the round as rsk_rows_detect / _pick / _place / _move (four
+        # launches around the collectives); else the per-phase calls below
+        self.fused = fused
 
     def _sync(self):
         import torch
@@ -340,6 +343,52 @@ class LibrskRoundsBackend:
         self._sync()
         return out
 
+    # ---- the fused round (RowShardedRounds.run when self.fused) ----
+    def round_buffers(self, N, S):
+        """Per-run device buffers of the fused round.  The packed keys start at
+        zero and rows_place leaves them zero for the next round."""
+        import torch
+        z = lambda n, dt: torch.zeros(n, dtype=dt, device=self.dev)  # noqa: E731
+        return {"use": z(N * S, torch.int32), "haz": z(N * S, torch.uint8), "most": z(S, torch.int64),
+                "key": z(S, torch.int64), "zc_cnt": z(S, torch.int32), "zc_key": z(S, torch.int64)}
+
+    def rows_detect(self, base, cpu, cap, N, S, threshold, b):
+        self._sync()
+        self._check(self.ctx.lib.rsk_rows_detect(self.ctx.handle, base.data_ptr(), cpu.data_ptr(), cap.data_ptr(), N,
+                                                 S, threshold, b["use"].data_ptr(), b["haz"].data_ptr(),
+                                                 b["most"].data_ptr(), b["zc_cnt"].data_ptr(),
+                                                 b["zc_key"].data_ptr(), self._F))
+        self._sync()
+
+    def rows_pick(self, rows, q, S, r0, pod_cpu, b):
+        self._sync()
+        self._check(self.ctx.lib.rsk_rows_pick(self.ctx.handle, rows.data_ptr() if q else None, rows.element_size(),
+                                               q, S, r0, pod_cpu.data_ptr(), b["most"].data_ptr(),
+                                               b["key"].data_ptr(), self._F))
+        self._sync()
+
+    def rows_place(self, assign, S, cap, N, r0, r1, b):
+        import torch
+        self._sync()
+        ev = torch.empty(S, dtype=torch.int32, device=self.dev)
+        tg = torch.empty(S, dtype=torch.int32, device=self.dev)
+        self._check(self.ctx.lib.rsk_rows_place(self.rounds.handle, assign.data_ptr(), S, cap.data_ptr(),
+                                                b["use"].data_ptr(), b["haz"].data_ptr(), N, r0, r1,
+                                                b["most"].data_ptr(), b["key"].data_ptr(), b["zc_cnt"].data_ptr(),
+                                                b["zc_key"].data_ptr(), ev.data_ptr(), tg.data_ptr(), self._F))
+        self._sync()
+        return ev, tg
+
+    def rows_move(self, assign, S, evict, target, r0, r1, N, pod_cpu, pod_mem, cpu_part, mem_part, shadow, cut):
+        self._sync()
+        self._check(self.ctx.lib.rsk_rows_move(self.ctx.handle, self.row_ptr.data_ptr(), self.col_idx.data_ptr(),
+                                               self.rev_ptr.data_ptr(), self.rev_idx.data_ptr(), self.P, r0, r1,
+                                               assign.data_ptr(), S, evict.data_ptr(), target.data_ptr(), N,
+                                               pod_cpu.data_ptr(), pod_mem.data_ptr(), cpu_part.data_ptr(),
+                                               mem_part.data_ptr(), None if shadow is None else shadow.data_ptr(),
+                                               cut.data_ptr(), self._F))
+        self._sync()
+
     def close(self):
         self.rounds.close()
         if self.stream_ordered:
@@ -408,6 +457,9 @@ class RowShardedRounds:
         pc64 = pod_cpu.to(torch.int64)
         mask32 = (1 << 32) - 1
         trace = os.environ.get("RSK_DIST_TRACE")
+        if getattr(self.be, "fused", False) and delta:
+            return self._run_fused(assign, base, cap, pc32, pm64c, lp_cpu, lp_mem, cut_local, shadow, N, S, R,
+                                   threshold, t)
         for rnd in range(R):
             if trace:
                 print(f"[rank {self.shard.rank}] round {rnd}", file=sys.stderr, flush=True)
@@ -487,6 +539,10 @@ class RowShardedRounds:
             evs.append(evict)
             tgs.append(target)
             cuts.append(cut)
+        return self._finish(base, lp_cpu, evs, tgs, cuts, S, dev, t)
+
+    def _finish(self, base, lp_cpu, evs, tgs, cuts, S, dev, t):
+        import torch
         # the final usage from the partials kept exact round by round (no second
         # pass over the rows)
         cpu = lp_cpu.clone()
@@ -495,3 +551,52 @@ class RowShardedRounds:
         empty = torch.empty(0, S, dtype=torch.int32, device=dev)
         return {"evict": torch.stack(evs) if evs else empty, "target": torch.stack(tgs) if tgs else empty,
                 "cut": torch.stack(cuts) if cuts else empty.to(torch.int64), "use": use_final, "ms": t}
+
+    def _run_fused(self, assign, base, cap, pc32, pm64, lp_cpu, lp_mem, cut_local, shadow, N, S, R, threshold, t):
+        """The rounds of ``run`` with the backend's fused launches: detect (usage
+        = base + the summed partials, hazards, the most-loaded node and the zero
+        case in one pass), the eviction scan straight to the packed all-reduce
+        key, CAR of this rank's evicted pods (the key decoded in the kernel; the
+        keys left zero for the next round), then cut delta + move in one launch.
+        Same collectives and results as the unfused loop."""
+        import time
+        be, dev = self.be, assign.device
+        r0, r1 = self.shard.r0, self.shard.r1
+        b = be.round_buffers(N, S)
+        rows = shadow if shadow is not None else assign[r0 * S:r1 * S]
+        multi = _multi_rank()
+        evs, tgs, cuts = [], [], []
+        for _ in range(R):
+            c = time.perf_counter()
+            if multi:
+                cpu, mem = lp_cpu.clone(), lp_mem.clone()
+                allreduce_(cpu, "sum", self.group)
+                allreduce_(mem, "sum", self.group)
+            else:
+                cpu = lp_cpu
+            t["monitor"] += (time.perf_counter() - c) * 1e3
+            c = time.perf_counter()
+            be.rows_detect(base, cpu, cap, N, S, threshold, b)
+            t["detect"] += (time.perf_counter() - c) * 1e3
+            c = time.perf_counter()
+            be.rows_pick(rows, r1 - r0, S, r0, pc32, b)
+            allreduce_(b["key"], "max", self.group)
+            t["evict"] += (time.perf_counter() - c) * 1e3
+            c = time.perf_counter()
+            evict, target = be.rows_place(assign, S, cap, N, r0, r1, b)
+            t["place"] += (time.perf_counter() - c) * 1e3
+            c = time.perf_counter()
+            if multi:
+                target = allgather(target, self.group).max(dim=0).values.contiguous()
+            t["exchange"] += (time.perf_counter() - c) * 1e3
+            c = time.perf_counter()
+            be.rows_move(assign, S, evict, target, r0, r1, N, pc32, pm64, lp_cpu, lp_mem, shadow, cut_local)
+            t["update"] += (time.perf_counter() - c) * 1e3
+            c = time.perf_counter()
+            cut = cut_local.clone()
+            allreduce_(cut, "sum", self.group)
+            t["cut"] += (time.perf_counter() - c) * 1e3
+            evs.append(evict)
+            tgs.append(target)
+            cuts.append(cut)
+        return self._finish(base, lp_cpu, evs, tgs, cuts, S, dev, t)

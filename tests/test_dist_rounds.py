@@ -124,7 +124,7 @@ def _expected(c, pod_cpu, R):
     return np.array(ev), np.array(tg), np.array(cut), a, u
 
 
-def _worker(rank, world, port, R, out_q, use_gpu, pg="gloo", ordered=False):
+def _worker(rank, world, port, R, out_q, use_gpu, pg="gloo", ordered=False, fused=True):
     import sys
     sys.path[:0] = [PKG, REPO]
     import torch
@@ -153,7 +153,8 @@ def _worker(rank, world, port, R, out_q, use_gpu, pg="gloo", ordered=False):
         if st is not None:
             st.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(st) if st is not None else contextlib.nullcontext():
-            be = (rdist.LibrskRoundsBackend(c.row_ptr, c.col_idx, pod_cpu, device=dev, stream_ordered=ordered)
+            be = (rdist.LibrskRoundsBackend(c.row_ptr, c.col_idx, pod_cpu, device=dev, stream_ordered=ordered,
+                                            fused=fused)
                   if use_gpu else OracleRoundsBackend(c.row_ptr, c.col_idx))
             res = rdist.RowShardedRounds(sh, be).run(assign, *args)
         if use_gpu:
@@ -170,11 +171,11 @@ def _worker(rank, world, port, R, out_q, use_gpu, pg="gloo", ordered=False):
         dist.destroy_process_group()
 
 
-def _run(world, R, use_gpu=False, pg="gloo", ordered=False):
+def _run(world, R, use_gpu=False, pg="gloo", ordered=False, fused=True):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, R, q, use_gpu, pg, ordered)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, R, q, use_gpu, pg, ordered, fused)) for r in range(world)]
     for p in procs:
         p.start()
     outs = []
@@ -264,5 +265,19 @@ def test_row_sharded_rounds_stream_ordered_gloo_world2():
     c, pod_cpu, _ = _case()
     ev, tg, cut, a, u = _expected(c, pod_cpu, R)
     for rank, e, t, k, a_r, u_r in _run(2, R, use_gpu=True, ordered=True):
+        assert np.array_equal(e, ev) and np.array_equal(t, tg), f"rank {rank}"
+        assert np.array_equal(k, cut) and np.array_equal(a_r, a) and np.array_equal(u_r, u), f"rank {rank}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ordered", [False, True])
+def test_row_sharded_rounds_unfused_world2(ordered):
+    """The per-phase librsk calls (fused=False: detect, pick, evict key / decode,
+    place, cut delta, apply as separate launches) against oracle_rounds; the
+    tests above run the fused round (rsk_rows_detect / _pick / _place / _move)."""
+    R = 4
+    c, pod_cpu, _ = _case()
+    ev, tg, cut, a, u = _expected(c, pod_cpu, R)
+    for rank, e, t, k, a_r, u_r in _run(2, R, use_gpu=True, ordered=ordered, fused=False):
         assert np.array_equal(e, ev) and np.array_equal(t, tg), f"rank {rank}"
         assert np.array_equal(k, cut) and np.array_equal(a_r, a) and np.array_equal(u_r, u), f"rank {rank}"
