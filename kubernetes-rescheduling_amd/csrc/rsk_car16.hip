@@ -143,19 +143,20 @@ __global__ __launch_bounds__(kPrep0Threads) void car_prep_small_kernel(const int
     }
 }
 
-template <int V, bool kCode, bool kKey>
-__global__ __launch_bounds__(256) void car_prep_kernel(const int *__restrict__ cap, const typename VecT<V>::I *__restrict__ use,
+template <int V, bool kCode, bool kKey, int kBlock = 256>
+__global__ __launch_bounds__(kBlock) void car_prep_kernel(const int *__restrict__ cap, const typename VecT<V>::I *__restrict__ use,
                                                        const typename VecT<V>::H *__restrict__ haz, int N, int SV,
                                                        int npb, unsigned total, typename VecT<V>::C *__restrict__ code,
                                                        typename VecT<V>::I *__restrict__ nodekey,
                                                        int *__restrict__ zc_cnt, unsigned long long *__restrict__ zc_key,
                                                        const int *__restrict__ capmax) {
+    // kBlock 1024 only with SV <= 256: the slots never exceed 256
     __shared__ int lcnt[256 * V];
     __shared__ unsigned long long lkey[256 * V];
-    const unsigned t = blockIdx.x * 256u + threadIdx.x;
-    const unsigned base = (blockIdx.x * 256u) % (unsigned)SV;  // vector slot of thread 0
+    const unsigned t = blockIdx.x * (unsigned)kBlock + threadIdx.x;
+    const unsigned base = (blockIdx.x * (unsigned)kBlock) % (unsigned)SV;  // vector slot of thread 0
     const int nslot = min(256, SV);
-    for (int i = threadIdx.x; i < nslot * V; i += 256) { lcnt[i] = 0; lkey[i] = 0ull; }
+    for (int i = threadIdx.x; i < nslot * V; i += kBlock) { lcnt[i] = 0; lkey[i] = 0ull; }
     __syncthreads();
     const int B = kCode ? max(0, *capmax - 32766) : 0;  // the exact code window (rsk_car.h)
     if (kCode && t < (unsigned)SV) {  // code row N: code 0 for every scenario (clamped invalid assignments)
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(256) void car_prep_kernel(const int *__restrict__ c
             }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < nslot * V; i += 256)
+    for (int i = threadIdx.x; i < nslot * V; i += kBlock)
         if (lcnt[i]) {
             const int s = (int)(((base + (unsigned)(i / V)) % (unsigned)SV) * V + (unsigned)(i % V));
             atomicAdd(&zc_cnt[s], lcnt[i]);
@@ -207,24 +208,24 @@ __global__ __launch_bounds__(256) void car_prep_kernel(const int *__restrict__ c
         }
 }
 
-template <int V>
+template <int V, int kBlock = 256>
 static int prep_launch(hipStream_t stream, const Prep16Args &a, int SV, int npb, unsigned total) {
     typedef typename VecT<V>::I I;
     typedef typename VecT<V>::H H;
     typedef typename VecT<V>::C C;
-    const dim3 grid((unsigned)ceil_div(total, 256)), block(256);
+    const dim3 grid((unsigned)ceil_div(total, kBlock)), block(kBlock);
     const I *use = reinterpret_cast<const I *>(a.use);
     const H *haz = reinterpret_cast<const H *>(a.haz);
     C *code = reinterpret_cast<C *>(a.code);
     I *key = reinterpret_cast<I *>(a.nodekey);
     if (a.code && a.nodekey)
-        car_prep_kernel<V, true, true><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
+        car_prep_kernel<V, true, true, kBlock><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
                                                                  a.capmax);
     else if (a.code)
-        car_prep_kernel<V, true, false><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
+        car_prep_kernel<V, true, false, kBlock><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
                                                                  a.capmax);
     else
-        car_prep_kernel<V, false, true><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
+        car_prep_kernel<V, false, true, kBlock><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
                                                                  a.capmax);
     RSK_HIP(hipGetLastError());
     return RSK_OK;
@@ -261,6 +262,16 @@ int launch_prep_main(hipStream_t stream, const Prep16Args &a) {
     // 256 * max(SV, 256) threads within [2^16, 2^18] (config 3, SV = 1024:
     // 2^18; config 4, SV = 16: 2^16, prep 0.029 -> 0.024 ms).  RSK_PREP_THREADS
     // overrides (experiments).
+    // Few scenarios (SV <= 64, e.g. config 4: SV = 16): workgroups of 1024
+    // threads, 4 nodes per thread — a scenario's slot still takes one atomic per
+    // workgroup (N * SV / 4096 of them), with 4x the loads in flight of 256-thread
+    // workgroups at 13 nodes per thread (prep 17 us at 50k nodes x 64).
+    static const bool big = RSK_KNOB(RSK_PREP_BIG, 1) != 0;
+    if (big && v4 && SV <= 64) {
+        const int npb = 4;
+        const unsigned total = (unsigned)(ceil_div(a.N, npb) * SV);
+        return prep_launch<4, 1024>(stream, a, SV, npb, total);
+    }
     static const int env_threads = RSK_KNOB(RSK_PREP_THREADS, 0);
     const int target_threads = env_threads >= 1024 ? env_threads
                                                    : (int)std::min<int64_t>(256 * 1024, std::max<int64_t>(65536, 256LL * std::max(SV, 256)));
