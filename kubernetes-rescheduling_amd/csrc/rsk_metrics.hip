@@ -567,24 +567,31 @@ __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restr
         rcpu = rmem = 0;
     };
     constexpr int kB = 8;
-    for (int j = j0; j < j1; j += kB) {
-        // every load of the batch issued before its first use: the assign rows,
-        // and the pods' CPU / memory (scattered pod ids: each a cache miss that,
-        // loaded per pod behind the previous pod's atomics, serialised the run)
-        int a[kB], pp[kB], kk[kB], cc[kB];
-        long long mm[kB];
+    // software-pipelined: batch i + 1's loads are issued before batch i's
+    // atomics (gfx9 counts no-return atomics in vmcnt, in order with the loads:
+    // a load issued after the atomics would wait for them too)
+    int a[kB], kk[kB], cc[kB];
+    long long mm[kB];
+    auto load = [&](int jb, int *a_, int *k_, int *c_, long long *m_) {
+        int pp[kB];
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
-            const int jj = min(j + u, j1 - 1);
+            const int jj = min(jb + u, j1 - 1);
             pp[u] = cperm[jj];
-            kk[u] = ckeys[jj];
+            k_[u] = ckeys[jj];
         }
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
-            a[u] = live ? __builtin_nontemporal_load(&assign[(size_t)pp[u] * S + s]) : -1;
-            cc[u] = ccpu[pp[u]];
-            mm[u] = mem ? pod_mem[pp[u]] : 0;
+            a_[u] = live ? __builtin_nontemporal_load(&assign[(size_t)pp[u] * S + s]) : -1;
+            c_[u] = ccpu[pp[u]];
+            m_[u] = mem ? pod_mem[pp[u]] : 0;
         }
+    };
+    load(j0, a, kk, cc, mm);
+    for (int j = j0; j < j1; j += kB) {
+        int an[kB], kn[kB], cn[kB];
+        long long mn[kB];
+        if (j + kB < j1) load(j + kB, an, kn, cn, mn);  // wave-uniform
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
             if (j + u >= j1) break;
@@ -605,6 +612,13 @@ __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restr
                 atomicAdd(&cpu[o], (unsigned long long)(long long)c);
                 if (mem) atomicAdd(&mem[o], (unsigned long long)m);
             }
+        }
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            a[u] = an[u];
+            kk[u] = kn[u];
+            cc[u] = cn[u];
+            mm[u] = mn[u];
         }
     }
     flush();

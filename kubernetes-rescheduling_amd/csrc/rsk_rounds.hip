@@ -30,7 +30,15 @@ struct rsk_rounds {
     rsk::DevBuf haz, most, evict, key_ws;
     rsk::DevBuf asg16;  // u16 shadow of assign for the eviction scan (N <= 65535, S % 8 == 0)
     rsk::DevBuf gtab;   // global hash work areas (rows whose distinct nodes overflow the LDS)
+    // the eviction pick's pod lists (rsk_rounds_run): base node per pod, the
+    // pods of each base node (CSR), per scenario the pods off their base node
+    rsk::DevBuf lbase, loff, lpod, lcnt, llist;
     ~rsk_rounds() {
+        lbase.release();
+        loff.release();
+        lpod.release();
+        lcnt.release();
+        llist.release();
         gtab.release();
         asg16.release();
         row_ptr.release();
@@ -48,6 +56,15 @@ namespace {
 
 constexpr int kMoveThreads = 256;
 constexpr int kNoEvict = -3;
+
+// Per-scenario lists of the pods off their base node (base = scenario 0's
+// node): every pod p with assign[p, s] != base[p] is in list s (duplicates
+// allowed); cnt[s] > cap: the list overflowed, scenario s is scanned in full.
+struct DevLists {
+    const int *base = nullptr;
+    int *cnt = nullptr, *list = nullptr;
+    int cap = 0;
+};
 
 __device__ __forceinline__ unsigned long long move_pack(int rem, int n) {  // (rem, -node), 0 = none
     return ((unsigned long long)((unsigned)rem ^ 0x80000000u) << 32) | (unsigned long long)(0x7fffffffu - (unsigned)n);
@@ -73,7 +90,7 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
                                              unsigned *tab, unsigned long long *__restrict__ kpick,
                                              unsigned long long *__restrict__ kdet, int *__restrict__ ev_out,
                                              int *__restrict__ zc_cnt, unsigned long long *__restrict__ zc_key,
-                                             int own0, int own1) {
+                                             int own0, int own1, DevLists dl) {
     unsigned *keys = tab, *cnts = tab + H;
     unsigned long long *red64 = reinterpret_cast<unsigned long long *>(tab + 2 * H);  // best
     unsigned *red = tab + 2 * H + 2;                                                   // M, n_at_M, n_free
@@ -173,6 +190,11 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
             use[(size_t)t * S + s] += c;
             assign[pc] = t;
             if (asg16) asg16[pc] = (unsigned short)t;
+            if (dl.base && old == dl.base[p]) {  // leaves its base node: into the scenario's list
+                const int q = dl.cnt[s];
+                dl.cnt[s] = q + 1;
+                if (q < dl.cap) dl.list[(size_t)s * dl.cap + q] = p;
+            }
         }
     }
 }
@@ -193,12 +215,12 @@ __global__ __launch_bounds__(kMoveThreads) void car_move_kernel(const int *__res
                                                                 unsigned long long *__restrict__ kdet,
                                                                 int *__restrict__ ev_out, int *__restrict__ zc_cnt,
                                                                 unsigned long long *__restrict__ zc_key, int own0,
-                                                                int own1) {
+                                                                int own1, DevLists dl) {
     extern __shared__ __attribute__((aligned(16))) unsigned lds[];
     unsigned *tab = kGlobal ? gtab + (size_t)blockIdx.x * (size_t)(2 * H + 8) : lds;
     for (int s = (int)blockIdx.x; s < S; s += (int)gridDim.x) {
         car_move_one<kGlobal>(row_ptr, col, pod_cpu, assign, use, cap, haz, evict, s, S, N, H, update, out_target,
-                              asg16, tab, kpick, kdet, ev_out, zc_cnt, zc_key, own0, own1);
+                              asg16, tab, kpick, kdet, ev_out, zc_cnt, zc_key, own0, own1, dl);
         if (kGlobal) move_sync<true>();  // the area is free before the next scenario clears it
     }
 }
@@ -303,17 +325,114 @@ MoveGeom move_geometry(rsk_rounds *r, int N, int S) {
 int launch_move(rsk_rounds *r, hipStream_t st, const MoveGeom &g, int *assign, int *use, const int *cap,
                 const uint8_t *haz, const int *evict, int S, int N, int update, int *target, unsigned short *a16,
                 unsigned long long *kpick = nullptr, unsigned long long *kdet = nullptr, int *ev_out = nullptr,
-                int *zc_cnt = nullptr, unsigned long long *zc_key = nullptr, int own0 = 0, int own1 = INT_MAX) {
+                int *zc_cnt = nullptr, unsigned long long *zc_key = nullptr, int own0 = 0, int own1 = INT_MAX,
+                DevLists dl = DevLists()) {
     if (g.lds)
         car_move_kernel<false><<<dim3((unsigned)g.grid), dim3(kMoveThreads), g.lds, st>>>(
             r->row_ptr.as<int>(), r->col.as<int>(), r->pod_cpu.as<int>(), assign, use, cap, haz, evict, S, N, g.H,
-            update, target, a16, nullptr, kpick, kdet, ev_out, zc_cnt, zc_key, own0, own1);
+            update, target, a16, nullptr, kpick, kdet, ev_out, zc_cnt, zc_key, own0, own1, dl);
     else
         car_move_kernel<true><<<dim3((unsigned)g.grid), dim3(kMoveThreads), 0, st>>>(
             r->row_ptr.as<int>(), r->col.as<int>(), r->pod_cpu.as<int>(), assign, use, cap, haz, evict, S, N, g.H,
-            update, target, a16, r->gtab.as<unsigned>(), kpick, kdet, ev_out, zc_cnt, zc_key, own0, own1);
+            update, target, a16, r->gtab.as<unsigned>(), kpick, kdet, ev_out, zc_cnt, zc_key, own0, own1, dl);
     RSK_HIP(hipGetLastError());
     return RSK_OK;
+}
+
+// ---- the eviction pick over pod lists (rsk_rounds_run) ----
+// setup: base[p] = assign[p, 0] (clamped to N), the base nodes' pod counts
+__global__ __launch_bounds__(256) void list_base_kernel(const int *__restrict__ assign, int P, int S, int N,
+                                                        int *__restrict__ base, int *__restrict__ cnt) {
+    const int p = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (p >= P) return;
+    const int a = assign[(size_t)p * S];
+    const int b = (unsigned)a < (unsigned)N ? a : N;
+    base[p] = b;
+    atomicAdd(&cnt[b], 1);
+}
+
+// exclusive scan of cnt[0..n] into off (one workgroup: setup only)
+__global__ __launch_bounds__(1024) void list_scan_kernel(const int *__restrict__ cnt, int n, int *__restrict__ off) {
+    __shared__ int part[1024];
+    const int t = (int)threadIdx.x, per = (n + 1023) / 1024;
+    const int i0 = min(n, t * per), i1 = min(n, i0 + per);
+    int sum = 0;
+    for (int i = i0; i < i1; ++i) sum += cnt[i];
+    part[t] = sum;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int x = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += x;
+        __syncthreads();
+    }
+    int run = part[t] - sum;
+    for (int i = i0; i < i1; ++i) {
+        off[i] = run;
+        run += cnt[i];
+    }
+    if (t == 1023) off[n] = part[1023];
+}
+
+// the base nodes' pod lists (cursor = a copy of off) and the scenarios' lists
+// of pods off their base node: thread = (pod, 64-scenario lane)
+__global__ __launch_bounds__(256) void list_fill_kernel(const int *__restrict__ assign, int P, int S, int N,
+                                                        const int *__restrict__ base, int *__restrict__ cur,
+                                                        int *__restrict__ pod, int *__restrict__ dcnt,
+                                                        int *__restrict__ dlist, int cap) {
+    const int lane = (int)threadIdx.x & 63;
+    const int nsc = (S + 63) >> 6;
+    const int w = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int p = w / nsc, s = (w - p * nsc) * 64 + lane;
+    if (p >= P) return;
+    const int b = base[p];
+    if (s == 0) pod[atomicAdd(&cur[b], 1)] = p;
+    if (s >= S) return;
+    const int a = assign[(size_t)p * S + s];
+    if (((unsigned)a < (unsigned)N ? a : N) != b) {
+        const int q = atomicAdd(&dcnt[s], 1);
+        if (q < cap) dlist[(size_t)s * cap + q] = p;
+    }
+}
+
+// delete_replaced_pod.py:41-61 per scenario by one wave: the pods on the most
+// hazardous node m (kdet) are the base list of m plus the scenario's list of
+// pods off their base node, each checked against assign (T: the u16 shadow or
+// int32); an overflowed list scans every pod.  Same packed key as pick16.
+template <typename T>
+__global__ __launch_bounds__(256) void pick_list_kernel(const T *__restrict__ asg, const int *__restrict__ pod_cpu,
+                                                        int P, int S, const unsigned long long *__restrict__ kdet,
+                                                        const int *__restrict__ off, const int *__restrict__ pod,
+                                                        const int *__restrict__ dcnt, const int *__restrict__ dlist,
+                                                        int cap, unsigned long long *__restrict__ kpick) {
+    const int lane = (int)threadIdx.x & 63;
+    const int s = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (s >= S) return;  // whole wave
+    const unsigned long long kd = kdet[s];
+    if (!kd) return;  // no hazard node: kpick stays 0
+    const int m = (int)~(unsigned)(kd & 0xffffffffull);
+    unsigned long long best = 0ull;
+    auto look = [&](int p) {
+        if ((int)asg[(size_t)p * S + s] != m) return;
+        const int c = pod_cpu[p];
+        const unsigned long long k =
+            c >= 0 ? ((unsigned long long)((unsigned)c ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)p) : 0ull;
+        best = k > best ? k : best;
+    };
+    for (int i = off[m] + lane; i < off[m + 1]; i += 64) look(pod[i]);
+    const int n = dcnt[s];
+    if (n <= cap) {
+        const int *l = dlist + (size_t)s * cap;
+        for (int i = lane; i < n; i += 64) look(l[i]);
+    } else {
+        for (int p = lane; p < P; p += 64) look(p);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long x = __shfl_xor(best, o, 64);
+        best = x > best ? x : best;
+    }
+    if (lane == 0 && best) kpick[s] = best;
 }
 
 // Row-sharded loop glue: one thread per scenario.
@@ -648,6 +767,41 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
     unsigned long long *kdet = r->key_ws.as<unsigned long long>(), *kpick = kdet + S, *zkey = kpick + S;
     int *zcnt = reinterpret_cast<int *>(zkey + S);
     RSK_HIP(hipMemsetAsync(kdet, 0, (size_t)S * 28, st));
+    // The eviction pick over pod lists: the pods on a node in scenario s are the
+    // node's base pods (scenario 0's node) plus those of s's list of pods off
+    // their base node; the move kernel appends a pod that leaves its base node.
+    // Per round one wave per scenario reads ~(P/N + list) pods instead of the
+    // P x S scan (rsk_rounds.hip pick16: 205 MB at config 5).  Built per call
+    // from one read of assign.
+    static const bool lists_on = RSK_KNOB(RSK_ROUNDS_LISTS, 1) != 0;
+    DevLists dl;
+    if (lists_on && r->P > 0 && R > 0) {
+        const int P = r->P;
+        int cap = (int)std::max<int64_t>(256, P / 16);
+        cap = (int)std::max<int64_t>(64, std::min<int64_t>(cap, ((int64_t)64 << 20) / ((int64_t)S * 4)));
+        RSK_TRY(r->lbase.reserve((size_t)P * 4));
+        RSK_TRY(r->loff.reserve((size_t)(N + 2) * 4 * 2));
+        RSK_TRY(r->lpod.reserve((size_t)P * 4));
+        RSK_TRY(r->lcnt.reserve((size_t)S * 4));
+        RSK_TRY(r->llist.reserve((size_t)S * cap * 4));
+        int *cntb = r->loff.as<int>() + (N + 2);  // N + 1 counts, then the fill cursors
+        ScopedTimer tm(ctx, "rounds_lists");
+        RSK_HIP(hipMemsetAsync(cntb, 0, (size_t)(N + 1) * 4, st));
+        RSK_HIP(hipMemsetAsync(r->lcnt.ptr, 0, (size_t)S * 4, st));
+        list_base_kernel<<<(unsigned)ceil_div(P, 256), 256, 0, st>>>(d_assign, P, S, N, r->lbase.as<int>(), cntb);
+        list_scan_kernel<<<1, 1024, 0, st>>>(cntb, N + 1, r->loff.as<int>());
+        RSK_HIP(hipMemcpyAsync(cntb, r->loff.ptr, (size_t)(N + 1) * 4, hipMemcpyDeviceToDevice, st));
+        const int64_t waves = (int64_t)P * ceil_div(S, 64);
+        RSK_CHECK(waves < INT32_MAX, "list grid too large");
+        list_fill_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, st>>>(d_assign, P, S, N, r->lbase.as<int>(), cntb,
+                                                                        r->lpod.as<int>(), r->lcnt.as<int>(),
+                                                                        r->llist.as<int>(), cap);
+        RSK_HIP(hipGetLastError());
+        dl.base = r->lbase.as<int>();
+        dl.cnt = r->lcnt.as<int>();
+        dl.list = r->llist.as<int>();
+        dl.cap = cap;
+    }
     for (int round = 0; round < R; ++round) {
         int *ev = d_evict + (size_t)round * S;
         {
@@ -656,7 +810,18 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         }
         {
             ScopedTimer tm(ctx, "rounds_pick");
-            if (s16) {
+            if (dl.base) {
+                const unsigned blocks = (unsigned)ceil_div(S, 4);
+                if (s16)
+                    pick_list_kernel<unsigned short><<<blocks, 256, 0, st>>>(
+                        a16, r->pod_cpu.as<int>(), r->P, S, kdet, r->loff.as<int>(), r->lpod.as<int>(), dl.cnt, dl.list,
+                        dl.cap, kpick);
+                else
+                    pick_list_kernel<int><<<blocks, 256, 0, st>>>(d_assign, r->pod_cpu.as<int>(), r->P, S, kdet,
+                                                                  r->loff.as<int>(), r->lpod.as<int>(), dl.cnt,
+                                                                  dl.list, dl.cap, kpick);
+                RSK_HIP(hipGetLastError());
+            } else if (s16) {
                 const int S8 = S / 8;
                 const int ppt = (int)std::max<int64_t>(1, ceil_div((int64_t)r->P * S8, (int64_t)256 * 4096));
                 const int64_t tot = ceil_div(r->P, ppt) * S8;
@@ -672,7 +837,7 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         {
             ScopedTimer tm(ctx, "rounds_move");
             RSK_TRY(launch_move(r, st, g, d_assign, d_use, d_cap, r->haz.as<uint8_t>(), nullptr, S, N, 1,
-                                d_target + (size_t)round * S, a16, kpick, kdet, ev, zcnt, zkey));
+                                d_target + (size_t)round * S, a16, kpick, kdet, ev, zcnt, zkey, 0, INT_MAX, dl));
         }
     }
     if (!dev) {

@@ -116,3 +116,44 @@ def test_gpu_rounds_hub_rows_and_hash():
     assert (exp[2][:S] <= 2).all()  # the first round evicts a hub pod
     for g, e, name in zip((a, u, ev, tg), exp, ("assign", "use", "evict", "target")):
         assert np.array_equal(g, e), name
+
+
+@pytest.mark.gpu
+def test_gpu_rounds_pod_lists_overflow_mid_run():
+    """The eviction pick's pod lists (rsk_rounds_run): scenarios whose list of
+    pods off their base node (scenario 0's node) starts just under the list's
+    capacity (max(256, P/16) = 256 here) and overflows while pods move (the
+    full-scan fallback), one far beyond it from the start, and unassigned pods
+    (-1) in the base and in the scenarios."""
+    from oracle import oracle as orc
+    from rsk import _lib, api
+    rng = np.random.default_rng(21)
+    P, N, S, R = 4096, 64, 8, 24
+    rows = [rng.integers(0, P, int(rng.integers(0, 6))).tolist() for _ in range(P)]
+    rp = np.zeros(P + 1, np.int32)
+    rp[1:] = np.cumsum([len(r) for r in rows])
+    ci = np.array([q for r in rows for q in r], np.int32)
+    base = rng.integers(0, N, P).astype(np.int32)
+    base[rng.random(P) < 0.01] = -1
+    a = np.repeat(base[:, None], S, axis=1)
+    for s in range(1, S):
+        k = {1: 0, 2: 240, 3: 250, 4: 255, 5: 256, 6: 3000}.get(s, 100)
+        idx = rng.choice(P, k, replace=False)
+        a[idx, s] = (a[idx, s] + 1 + rng.integers(0, N - 1, k)) % N   # another node (or -1 -> a node)
+    a[rng.random((P, S)) < 0.002] = -1
+    assign = a.reshape(-1).astype(np.int32)
+    pod_cpu = rng.integers(1, 500, P).astype(np.int32)
+    pod_cpu[rng.random(P) < 0.03] = -1
+    load = np.stack([np.bincount(a[:, s][a[:, s] >= 0], weights=np.maximum(pod_cpu[a[:, s] >= 0], 0), minlength=N)
+                     for s in range(S)], axis=1)
+    cap = np.full(N, int(load.mean() * 100 / 30) + 1, np.int32)
+    use = (load + rng.integers(0, cap[0] // 10, (N, 1))).astype(np.int32).reshape(-1)
+    exp = orc.rounds(rp, ci, pod_cpu, assign, S, cap, use, N, R)
+    rounds = api.Rounds(rp, ci, pod_cpu, ctx=_lib.default_context())
+    g_a, g_u = assign.copy(), use.copy()
+    ev, tg = rounds.run(g_a, S, cap, g_u, N, R)
+    rounds.close()
+    assert (exp[3] >= 0).sum() > R * S // 2   # pods really move (lists grow)
+    for g, e, name in zip((g_a, g_u, ev, tg), exp, ("assign", "use", "evict", "target")):
+        bad = np.nonzero(g != e)[0]
+        assert bad.size == 0, f"{name}: {bad.size} differ, first {bad[0]}: gpu {g[bad[0]]} oracle {e[bad[0]]}"

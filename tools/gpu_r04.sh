@@ -27,6 +27,7 @@ for s in "${@:-test smoke bench}"; do
       brounds) step bench_rounds 300 python -u bench.py --config rounds --no-cpu-baseline ;;
       ab:*) kv=${w#ab:}; step "ab_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u bench.py --no-cpu-baseline ;;
       ab1m:*) kv=${w#ab1m:}; step "ab1m_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u bench.py --config 1m50k --no-cpu-baseline --row-rounds 0 ;;
+      abr:*) kv=${w#abr:}; step "abr_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u bench.py --config rounds --no-cpu-baseline ;;
       sb:*) kv=${w#sb:}; step "sb_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_abl.so ${kv//,/ } python -u tools/sidebench.py ;;
       dropin) step dropin 400 python -u tools/dropin_latency.py --calls 40 --out "$out/dropin.json" ;;
       prof) for c in headline 1m50k; do
