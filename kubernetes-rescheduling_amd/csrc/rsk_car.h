@@ -329,13 +329,7 @@ struct SideArgs {
     // the launch depends on car_prep0 only and runs beside car_prep
     const uint8_t *haz;
     const int *capmax;
-    // split teams (kSplit launches): each item's lanes' top-2 candidate words per
-    // slice of kSplitSL neighbours, written by car_side16_top2_kernel (one wave
-    // per slice, spread over the CUs) and merged by the team
-    unsigned *top2;
-    int nslice;
 };
-constexpr int kSplitSL = 64;  // neighbours per split wave
 struct SideGeom {
     int dmax, Dc, H, hshift, K, T, W, kB;
     int off_dl, off_ndl, off_dummy, off_fx, off_h2, h2cap;
@@ -353,12 +347,9 @@ struct FuseMap {
 int launch_fused16(hipStream_t stream, const Tile16Args &a, const SideArgs &sa, int side_blocks, const SideArgs &ba,
                    bool score, bool off32, unsigned tile_blocks, size_t lds);
 // scratch: device memory for rows whose table exceeds the LDS (grown on demand)
-// split: device memory of the split pass's top-2 words (T = 8 / 16 teams; null: no split)
-int launch_side16(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch,
-                  DevBuf *split = nullptr);
+int launch_side16(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch);
 // the same rows with node state computed on the fly (a.code null, a.haz / a.capmax set)
-int launch_side16_otf(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch,
-                      DevBuf *split = nullptr);
+int launch_side16_otf(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch);
 
 int launch_prep(hipStream_t stream, const Prep16Args &a);
 // launch_prep in two halves: car_prep0 (zero-case reset, max(cap)), then car_prep

@@ -862,7 +862,6 @@ struct rsk_car_plan {
     // descending, split into the kSideMax classes (neighbours in pcol)
     DevBuf side_items, pcol;
     DevBuf side_scratch;  // work areas of side rows whose table exceeds the LDS
-    DevBuf side_top2;     // the split pass's top-2 words of the team classes
     // wide path: rows above kHubMax neighbours (car_bigrow_kernel), neighbours in pcol
     DevBuf big_items;
     int n_big = 0, big_dmax = 0;
@@ -890,7 +889,6 @@ struct rsk_car_plan {
         hcol.release();
         side_items.release();
         side_scratch.release();
-        side_top2.release();
         big_items.release();
         pcol.release();
         nodekey.release();
@@ -1386,9 +1384,9 @@ int launch_side16_classes(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, 
             a.code = nullptr;
             a.haz = b.haz;
             a.capmax = b.capmax;
-            RSK_TRY(launch_side16_otf(stream, a, g, off32, &plan->side_scratch, &plan->side_top2));
+            RSK_TRY(launch_side16_otf(stream, a, g, off32, &plan->side_scratch));
         } else {
-            RSK_TRY(launch_side16(stream, a, g, off32, &plan->side_scratch, &plan->side_top2));
+            RSK_TRY(launch_side16(stream, a, g, off32, &plan->side_scratch));
         }
     }
     return RSK_OK;

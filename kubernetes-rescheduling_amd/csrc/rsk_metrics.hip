@@ -567,31 +567,24 @@ __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restr
         rcpu = rmem = 0;
     };
     constexpr int kB = 8;
-    // software-pipelined: batch i + 1's loads are issued before batch i's
-    // atomics (gfx9 counts no-return atomics in vmcnt, in order with the loads:
-    // a load issued after the atomics would wait for them too)
-    int a[kB], kk[kB], cc[kB];
-    long long mm[kB];
-    auto load = [&](int jb, int *a_, int *k_, int *c_, long long *m_) {
-        int pp[kB];
-#pragma unroll
-        for (int u = 0; u < kB; ++u) {
-            const int jj = min(jb + u, j1 - 1);
-            pp[u] = cperm[jj];
-            k_[u] = ckeys[jj];
-        }
-#pragma unroll
-        for (int u = 0; u < kB; ++u) {
-            a_[u] = live ? __builtin_nontemporal_load(&assign[(size_t)pp[u] * S + s]) : -1;
-            c_[u] = ccpu[pp[u]];
-            m_[u] = mem ? pod_mem[pp[u]] : 0;
-        }
-    };
-    load(j0, a, kk, cc, mm);
     for (int j = j0; j < j1; j += kB) {
-        int an[kB], kn[kB], cn[kB];
-        long long mn[kB];
-        if (j + kB < j1) load(j + kB, an, kn, cn, mn);  // wave-uniform
+        // every load of the batch issued before its first use: the assign rows,
+        // and the pods' CPU / memory (scattered pod ids: each a cache miss that,
+        // loaded per pod behind the previous pod's atomics, serialised the run)
+        int a[kB], pp[kB], kk[kB], cc[kB];
+        long long mm[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            const int jj = min(j + u, j1 - 1);
+            pp[u] = cperm[jj];
+            kk[u] = ckeys[jj];
+        }
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            a[u] = live ? __builtin_nontemporal_load(&assign[(size_t)pp[u] * S + s]) : -1;
+            cc[u] = ccpu[pp[u]];
+            mm[u] = mem ? pod_mem[pp[u]] : 0;
+        }
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
             if (j + u >= j1) break;
@@ -612,13 +605,6 @@ __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restr
                 atomicAdd(&cpu[o], (unsigned long long)(long long)c);
                 if (mem) atomicAdd(&mem[o], (unsigned long long)m);
             }
-        }
-#pragma unroll
-        for (int u = 0; u < kB; ++u) {
-            a[u] = an[u];
-            kk[u] = kn[u];
-            cc[u] = cn[u];
-            mm[u] = mn[u];
         }
     }
     flush();
@@ -668,43 +654,56 @@ __global__ __launch_bounds__(256) void detect_kernel(const int *__restrict__ pct
 // scenarios (lane) x 4 waves over consecutive node ranges of npw nodes; the
 // waves' results meet in LDS, so a scenario's words take one atomic per
 // workgroup (125 per round at 5k nodes x 1024 scenarios, not 512).
-__global__ __launch_bounds__(256) void detect_use_kernel(const int *__restrict__ use, const int *__restrict__ cap, int N,
-                                                         int S, int thr, int npw, uint8_t *__restrict__ haz,
-                                                         unsigned long long *__restrict__ most,
-                                                         int *__restrict__ zc_cnt,
-                                                         unsigned long long *__restrict__ zc_key) {
-    __shared__ unsigned long long lb[4][64], lz[4][64];
-    __shared__ int ln[4][64];
+template <int kW>
+__global__ __launch_bounds__(64 * kW) void detect_use_kernel(const int *__restrict__ use, const int *__restrict__ cap,
+                                                             int N, int S, int thr, int npw,
+                                                             uint8_t *__restrict__ haz,
+                                                             unsigned long long *__restrict__ most,
+                                                             int *__restrict__ zc_cnt,
+                                                             unsigned long long *__restrict__ zc_key) {
+    __shared__ unsigned long long lb[kW][64], lz[kW][64];
+    __shared__ int ln[kW][64];
+    constexpr int kU = 4;  // nodes per batch: their loads in flight together
     const int lane = (int)threadIdx.x & 63, wv = (int)threadIdx.x >> 6;
     const int nsc = (S + 63) >> 6;
     const int sc = (int)blockIdx.x % nsc, nb = (int)blockIdx.x / nsc;
-    const int s = sc * 64 + lane;
-    const int n0 = (nb * 4 + wv) * npw, n1 = min(N, n0 + npw);
+    const bool live = sc * 64 + lane < S;
+    const int s = min(sc * 64 + lane, S - 1);
+    const int n0 = (nb * kW + wv) * npw, n1 = min(N, n0 + npw);
     unsigned long long b = 0, bz = 0;
     int nz = 0;
-    if (s < S)
-        for (int n = n0; n < n1; ++n) {
-            const size_t idx = (size_t)n * S + s;
-            const int c = cap[n], u = use[idx];
-            const int v = c == 0 ? -1 : (int)rint((double)u / (double)c * 100.0);
+    for (int n = n0; n < n1; n += kU) {
+        int u[kU], c[kU];
+#pragma unroll
+        for (int k = 0; k < kU; ++k) {  // clamped, always-valid addresses
+            const int m = min(n + k, n1 - 1);
+            u[k] = use[(size_t)m * S + s];
+            c[k] = cap[m];
+        }
+#pragma unroll
+        for (int k = 0; k < kU; ++k) {
+            if (n + k >= n1) break;
+            const int m = n + k;
+            const int v = c[k] == 0 ? -1 : (int)rint((double)u[k] / (double)c[k] * 100.0);
             const bool h = v >= thr;
-            haz[idx] = h;
+            if (live) haz[(size_t)m * S + s] = h;
             if (h) {
-                const unsigned long long k = pack_hi_lo(v, ~(unsigned)n);
-                b = k > b ? k : b;
+                const unsigned long long kk = pack_hi_lo(v, ~(unsigned)m);
+                b = kk > b ? kk : b;
             } else {
                 ++nz;
-                const unsigned long long k = zc_pack(c - u, n);
-                bz = k > bz ? k : bz;
+                const unsigned long long kk = zc_pack(c[k] - u[k], m);
+                bz = kk > bz ? kk : bz;
             }
         }
+    }
     lb[wv][lane] = b;
     lz[wv][lane] = bz;
     ln[wv][lane] = nz;
     __syncthreads();
-    if (wv != 0 || s >= S) return;
+    if (wv != 0 || !live) return;
 #pragma unroll
-    for (int w = 1; w < 4; ++w) {
+    for (int w = 1; w < kW; ++w) {
         b = max(b, lb[w][lane]);
         bz = max(bz, lz[w][lane]);
         nz += ln[w][lane];
@@ -973,12 +972,18 @@ int launch_detect(hipStream_t stream, const int *pct, int N, int S, int threshol
 // arrive zeroed (the move kernel clears its scenario's words after use).
 int launch_detect_use_keys(hipStream_t stream, const int *use, const int *cap, int N, int S, int threshold,
                            uint8_t *hazard, unsigned long long *key, int *zc_cnt, unsigned long long *zc_key) {
+    // ~512 workgroups of 64 scenarios x 16 waves (rsk_rows_detect's geometry):
+    // one atomic per scenario word per workgroup
+    static const int w16 = RSK_KNOB(RSK_DET_W16, 1);
+    static const int target = std::max(1, RSK_KNOB(RSK_DET_BLOCKS, 512));
+    const int kW = w16 ? 16 : 4;
     const int64_t nsc = ceil_div(S, 64);
-    const int npw = (int)std::max<int64_t>(4, ceil_div((int64_t)N * nsc, 8192));  // ~8k waves
-    const int64_t blocks = nsc * ceil_div(N, 4 * npw);
+    const int64_t nbk = std::max<int64_t>(1, std::min<int64_t>(ceil_div(N, kW * 4), ceil_div(target, nsc)));
+    const int npw = (int)ceil_div(N, nbk * kW);
+    const int64_t blocks = nsc * ceil_div(N, (int64_t)kW * npw);
     RSK_CHECK(blocks < INT32_MAX, "grid too large");
-    detect_use_kernel<<<(unsigned)blocks, 256, 0, stream>>>(use, cap, N, S, threshold, npw, hazard, key, zc_cnt,
-                                                            zc_key);
+    auto *kern = w16 ? &detect_use_kernel<16> : &detect_use_kernel<4>;
+    kern<<<(unsigned)blocks, 64 * kW, 0, stream>>>(use, cap, N, S, threshold, npw, hazard, key, zc_cnt, zc_key);
     RSK_HIP(hipGetLastError());
     return RSK_OK;
 }

@@ -395,44 +395,64 @@ __global__ __launch_bounds__(256) void list_fill_kernel(const int *__restrict__ 
     }
 }
 
-// delete_replaced_pod.py:41-61 per scenario by one wave: the pods on the most
-// hazardous node m (kdet) are the base list of m plus the scenario's list of
-// pods off their base node, each checked against assign (T: the u16 shadow or
-// int32); an overflowed list scans every pod.  Same packed key as pick16.
+// delete_replaced_pod.py:41-61 per scenario by one workgroup: the pods on the
+// most hazardous node m (kdet) are the base list of m plus the scenario's list
+// of pods off their base node, each checked against assign (T: the u16 shadow
+// or int32); an overflowed list scans every pod.  Same packed key as pick16.
+// Latency-bound (a list entry, then its assign word and CPU): 4 waves per
+// scenario, kU entries per thread in flight at once.
 template <typename T>
 __global__ __launch_bounds__(256) void pick_list_kernel(const T *__restrict__ asg, const int *__restrict__ pod_cpu,
                                                         int P, int S, const unsigned long long *__restrict__ kdet,
                                                         const int *__restrict__ off, const int *__restrict__ pod,
                                                         const int *__restrict__ dcnt, const int *__restrict__ dlist,
                                                         int cap, unsigned long long *__restrict__ kpick) {
-    const int lane = (int)threadIdx.x & 63;
-    const int s = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
-    if (s >= S) return;  // whole wave
+    constexpr int kU = 8;
+    __shared__ unsigned long long red[4];
+    const int s = (int)blockIdx.x, t = (int)threadIdx.x;
     const unsigned long long kd = kdet[s];
-    if (!kd) return;  // no hazard node: kpick stays 0
+    if (!kd) return;  // no hazard node: kpick stays 0 (the whole workgroup)
     const int m = (int)~(unsigned)(kd & 0xffffffffull);
+    const int b0 = off[m], nb = off[m + 1] - b0;
+    const int nd = dcnt[s];
+    const bool full = nd > cap;
+    const int n = nb + (full ? P : nd);  // entries: the base list, then the scenario's list (or every pod)
+    const int *l = dlist + (size_t)s * cap;
     unsigned long long best = 0ull;
-    auto look = [&](int p) {
-        if ((int)asg[(size_t)p * S + s] != m) return;
-        const int c = pod_cpu[p];
-        const unsigned long long k =
-            c >= 0 ? ((unsigned long long)((unsigned)c ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)p) : 0ull;
-        best = k > best ? k : best;
-    };
-    for (int i = off[m] + lane; i < off[m + 1]; i += 64) look(pod[i]);
-    const int n = dcnt[s];
-    if (n <= cap) {
-        const int *l = dlist + (size_t)s * cap;
-        for (int i = lane; i < n; i += 64) look(l[i]);
-    } else {
-        for (int p = lane; p < P; p += 64) look(p);
+    for (int i0 = 0; i0 < n; i0 += 256 * kU) {
+        int p[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int i = min(i0 + u * 256 + t, n - 1);  // clamped: always a valid entry
+            p[u] = i < nb ? pod[b0 + i] : (full ? i - nb : l[i - nb]);
+        }
+        int a[kU], c[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            a[u] = (int)asg[(size_t)p[u] * S + s];
+            c[u] = pod_cpu[p[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const unsigned long long k = a[u] == m && c[u] >= 0
+                                             ? ((unsigned long long)((unsigned)c[u] ^ 0x80000000u) << 32) |
+                                                   (unsigned long long)(~(unsigned)p[u])
+                                             : 0ull;
+            best = k > best ? k : best;
+        }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const unsigned long long x = __shfl_xor(best, o, 64);
         best = x > best ? x : best;
     }
-    if (lane == 0 && best) kpick[s] = best;
+    if ((t & 63) == 0) red[t >> 6] = best;
+    __syncthreads();
+    if (t == 0) {
+        best = red[0];
+        for (int w = 1; w < 4; ++w) best = red[w] > best ? red[w] : best;
+        if (best) kpick[s] = best;
+    }
 }
 
 // Row-sharded loop glue: one thread per scenario.
@@ -811,7 +831,7 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         {
             ScopedTimer tm(ctx, "rounds_pick");
             if (dl.base) {
-                const unsigned blocks = (unsigned)ceil_div(S, 4);
+                const unsigned blocks = (unsigned)S;
                 if (s16)
                     pick_list_kernel<unsigned short><<<blocks, 256, 0, st>>>(
                         a16, r->pod_cpu.as<int>(), r->P, S, kdet, r->loff.as<int>(), r->lpod.as<int>(), dl.cnt, dl.list,

@@ -213,11 +213,7 @@ __device__ __forceinline__ int side_pivot3(int x) {  // majority of lanes 0, 21,
 // deviations away from u plus its deviations onto u.  So the exact count >= 2
 // candidates are: the table's entries with C >= 2 (a handful), and the lane's
 // deviation nodes — both small sets.
-// kSplit: the codes of pass 1 are not gathered here; the lanes' top-2 words come
-// from the split pass (a.top2, car_side16_top2_kernel), whose divergent code
-// gathers are spread over many CUs instead of one CU's memory pipeline.
-template <int kW, int kT, int kB, bool kOff32, bool kPipe, bool kGlobal = false, bool kOTF = false,
-          bool kSplit = false>
+template <int kW, int kT, int kB, bool kOff32, bool kPipe, bool kGlobal = false, bool kOTF = false>
 __device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slot = -1) {
     static_assert(kT == 1 || kT == kW, "a team is one wave or the whole workgroup");
     extern __shared__ __attribute__((aligned(16))) unsigned slds[];
@@ -287,10 +283,8 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slo
             qnext = nbv[min(j0 + kB * kT + lane, d - 1)];
         }
         unsigned c[kB];
-        if (!kSplit) {
 #pragma unroll
-            for (int u = 0; u < kB; ++u) c[u] = side_code<kOTF>(a, min((unsigned)v[u], N), (unsigned)s, B);  // row N: 0
-        }
+        for (int u = 0; u < kB; ++u) c[u] = side_code<kOTF>(a, min((unsigned)v[u], N), (unsigned)s, B);  // row N: 0
         int vn[kB];
         if (kPipe) {  // ids clamped to the row: always valid addresses
             const int myq = qnext;
@@ -319,21 +313,13 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slo
                     }
                 }
                 mine = lane == u ? (unsigned)p + 1u : mine;
-                if (!kSplit) f.put(c[u] != kCodeHaz ? cand_word(c[u], (unsigned)x) : 0u);
+                f.put(c[u] != kCodeHaz ? cand_word(c[u], (unsigned)x) : 0u);
             }
         }
         if (mine != 0u && mine <= N) tb.add(mine);  // pivot node < N (N: unassigned, never counted)
         if (kPipe) {
 #pragma unroll
             for (int u = 0; u < kB; ++u) v[u] = vn[u];
-        }
-    }
-    if (kSplit) {  // the split pass's top-2 words of this item's slices; the team's waves take turns
-        const unsigned *t2 = a.top2 + (size_t)item * a.nslice * 128;
-        const int nsl = (d + kSplitSL - 1) / kSplitSL;
-        for (int k = tw; k < nsl; k += kT) {
-            f.put(t2[k * 128 + lane]);
-            f.put(t2[k * 128 + 64 + lane]);
         }
     }
     if (kT > 1) {

@@ -37,8 +37,7 @@ namespace rsk {
 
 // kW waves per workgroup, teams of kT waves; blocks b and b + 8 share an XCD
 // (a.xcd_per: workgroups per XCD run).
-template <int kW, int kT, int kB, bool kOff32, bool kPipe, bool kGlobal = false, bool kOTF = false,
-          bool kSplit = false>
+template <int kW, int kT, int kB, bool kOff32, bool kPipe, bool kGlobal = false, bool kOTF = false>
 __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : (kOTF ? 4 : 8))) void car_side16_kernel(SideArgs a) {
     if (kGlobal) {  // a capped grid strides over the items; work area = the resident block's slot
         static_assert(!kGlobal || kT == kW, "global work areas are per workgroup team");
@@ -52,51 +51,7 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : (kOTF ? 4 : 8))) void car_si
     }
     int blk = (int)blockIdx.x;
     if (a.xcd_per) blk = (int)(blockIdx.x & 7u) * a.xcd_per + (int)(blockIdx.x >> 3);
-    side16_block<kW, kT, kB, kOff32, kPipe, kGlobal, kOTF, kSplit>(a, blk);
-}
-
-// The split pass of a team launch: one wave per (item, slice of kSplitSL
-// neighbours), lane = scenario — the neighbours' assign rows, the lane's codes
-// of those nodes and its two largest distinct candidate words (side16_block's
-// pass-1 Top2), written to a.top2.  A team of 8-16 waves on one CU would issue
-// all of a row's divergent code gathers (64 lines per neighbour per array)
-// through that CU's memory pipeline; one wave per workgroup spreads them.
-template <bool kOff32, bool kOTF>
-__global__ __launch_bounds__(64) void car_side16_top2_kernel(SideArgs a) {
-    constexpr int kB = 32;
-    const int w = (int)blockIdx.x;
-    const int item = w / a.nslice, k = w - item * a.nslice;
-    if (item >= a.n_rows * a.nchunk) return;
-    const int chunk = item / a.n_rows, r = item - chunk * a.n_rows;
-    const cint_ptr itp = const_ptr(a.items) + 4 * r;
-    const int d = itp[2];
-    const int j0 = k * kSplitSL;
-    if (j0 >= d) return;
-    const int j1 = min(d, j0 + kSplitSL);
-    const int *__restrict__ nbv = a.col + itp[1];
-    const int lane = (int)threadIdx.x;
-    const unsigned S = (unsigned)a.S, N = (unsigned)a.N;
-    const int s = min(chunk * 64 + lane, a.S - 1);
-    const int B = kOTF ? max(0, *const_ptr(a.capmax) - 32766) : 0;
-    Top2 f;
-    f.init();
-    for (int jb = j0; jb < j1; jb += kB) {
-        const int myq = nbv[min(jb + lane, j1 - 1)];  // ids clamped to the slice: always valid addresses
-        int v[kB];
-#pragma unroll
-        for (int u = 0; u < kB; ++u)
-            v[u] = side_ld_assign<kOff32>(a.assign, (unsigned)__builtin_amdgcn_readlane(myq, u), S, (unsigned)s);
-        unsigned c[kB];
-#pragma unroll
-        for (int u = 0; u < kB; ++u) c[u] = side_code<kOTF>(a, min((unsigned)v[u], N), (unsigned)s, B);
-        const int nu = min(kB, j1 - jb);
-#pragma unroll
-        for (int u = 0; u < kB; ++u)
-            if (u < nu) f.put(c[u] != kCodeHaz ? cand_word(c[u], min((unsigned)v[u], N)) : 0u);
-    }
-    unsigned *t2 = a.top2 + ((size_t)item * a.nslice + k) * 128;
-    t2[lane] = f.w1;
-    t2[64 + lane] = f.w2;
+    side16_block<kW, kT, kB, kOff32, kPipe, kGlobal, kOTF>(a, blk);
 }
 
 constexpr int kSideH2Cap = 2048;  // listed nodes counted >= 2 (e.g. degree 5000 over 6000 nodes: ~1200)
@@ -156,8 +111,7 @@ void side16_apply_geometry(SideArgs &a, const SideGeom &g) {
 }
 
 template <bool kOTF>
-static int launch_side16_t(hipStream_t stream, const SideArgs &a0, const SideGeom &g0, bool off32, DevBuf *scratch,
-                           DevBuf *split) {
+static int launch_side16_t(hipStream_t stream, const SideArgs &a0, const SideGeom &g0, bool off32, DevBuf *scratch) {
     if (a0.n_rows == 0) return RSK_OK;
     // a table beyond the LDS: 8-wave teams with their work area in global memory
     const bool global = (size_t)(g0.T > 1 ? 1 : g0.W) * g0.lds_team > 160 * 1024;
@@ -187,27 +141,6 @@ static int launch_side16_t(hipStream_t stream, const SideArgs &a0, const SideGeo
         return RSK_OK;
     }
     using K = void (*)(SideArgs);
-    static const bool split_on = RSK_KNOB(RSK_SIDE_SPLIT, 1) != 0;
-    if (split && split_on && (g.T == 8 || g.T == 16)) {  // teams: the split pass, then the team kernel
-        a.nslice = (int)ceil_div(g.dmax, kSplitSL);
-        const int64_t waves = items * a.nslice;
-        RSK_CHECK(waves < INT32_MAX, "split grid too large");
-        RSK_TRY(split->reserve((size_t)waves * 128 * 4));
-        a.top2 = split->as<unsigned>();
-        (off32 ? &car_side16_top2_kernel<true, kOTF> : &car_side16_top2_kernel<false, kOTF>)
-            <<<dim3((unsigned)waves), dim3(64), 0, stream>>>(a);
-        RSK_HIP(hipGetLastError());
-        const K kern = g.T == 16 ? (off32 ? &car_side16_kernel<16, 16, 16, true, true, false, kOTF, true>
-                                          : &car_side16_kernel<16, 16, 16, false, true, false, kOTF, true>)
-                                 : (off32 ? &car_side16_kernel<8, 8, 32, true, true, false, kOTF, true>
-                                          : &car_side16_kernel<8, 8, 32, false, true, false, kOTF, true>);
-        if (lds > 64 * 1024)
-            RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        kern<<<dim3((unsigned)blocks), dim3(64 * g.W), lds, stream>>>(a);
-        RSK_HIP(hipGetLastError());
-        return RSK_OK;
-    }
     static const bool pipe = RSK_KNOB(RSK_SIDE_PIPE, 1) != 0;
 #define RSK_SIDE_P(W, T, B, O) \
     (pipe ? &car_side16_kernel<W, T, B, O, true, false, kOTF> : &car_side16_kernel<W, T, B, O, false, false, kOTF>)
@@ -228,15 +161,13 @@ static int launch_side16_t(hipStream_t stream, const SideArgs &a0, const SideGeo
     return RSK_OK;
 }
 
-int launch_side16(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch,
-                  DevBuf *split) {
-    return launch_side16_t<false>(stream, a, g, off32, scratch, split);
+int launch_side16(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch) {
+    return launch_side16_t<false>(stream, a, g, off32, scratch);
 }
 
-int launch_side16_otf(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch,
-                      DevBuf *split) {
+int launch_side16_otf(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch) {
     RSK_CHECK(a.haz && a.capmax && a.cap && a.use, "on-the-fly side rows need cap, use, hazard and capmax");
-    return launch_side16_t<true>(stream, a, g, off32, scratch, split);
+    return launch_side16_t<true>(stream, a, g, off32, scratch);
 }
 
 }  // namespace rsk
