@@ -663,7 +663,7 @@ __global__ __launch_bounds__(64 * kW) void detect_use_kernel(const int *__restri
                                                              unsigned long long *__restrict__ zc_key) {
     __shared__ unsigned long long lb[kW][64], lz[kW][64];
     __shared__ int ln[kW][64];
-    constexpr int kU = 4;  // nodes per batch: their loads in flight together
+    constexpr int kU = 8;  // nodes per batch: their loads in flight together
     const int lane = (int)threadIdx.x & 63, wv = (int)threadIdx.x >> 6;
     const int nsc = (S + 63) >> 6;
     const int sc = (int)blockIdx.x % nsc, nb = (int)blockIdx.x / nsc;

@@ -58,11 +58,16 @@ constexpr int kMoveThreads = 256;
 constexpr int kNoEvict = -3;
 
 // Per-scenario lists of the pods off their base node (base = scenario 0's
-// node): every pod p with assign[p, s] != base[p] is in list s (duplicates
-// allowed); cnt[s] > cap: the list overflowed, scenario s is scanned in full.
+// node), as (pod, its current node) entries: every pod that has left its base
+// node in scenario s has exactly one entry in list s, holding the node it is
+// on now (the move kernel updates it in place, or appends the pod when it
+// first leaves its base node).  src[s]: the entry the round's pick came from
+// (-1: the base list).  cnt[s] > cap: the list overflowed, scenario s is
+// scanned in full from then on.
 struct DevLists {
     const int *base = nullptr;
-    int *cnt = nullptr, *list = nullptr;
+    int *cnt = nullptr, *src = nullptr;
+    int2 *list = nullptr;
     int cap = 0;
 };
 
@@ -190,10 +195,18 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
             use[(size_t)t * S + s] += c;
             assign[pc] = t;
             if (asg16) asg16[pc] = (unsigned short)t;
-            if (dl.base && old == dl.base[p]) {  // leaves its base node: into the scenario's list
-                const int q = dl.cnt[s];
-                dl.cnt[s] = q + 1;
-                if (q < dl.cap) dl.list[(size_t)s * dl.cap + q] = p;
+            if (dl.base) {  // the pod's entry follows it (one entry per pod off its base node)
+                const int j = dl.src[s], q = dl.cnt[s];
+                if (q <= dl.cap) {
+                    if (j >= 0) {
+                        dl.list[(size_t)s * dl.cap + j].y = t;
+                    } else if (q < dl.cap) {
+                        dl.list[(size_t)s * dl.cap + q] = make_int2(p, t);
+                        dl.cnt[s] = q + 1;
+                    } else {
+                        dl.cnt[s] = dl.cap + 1;  // overflow: full scans from now on
+                    }
+                }
             }
         }
     }
@@ -379,7 +392,7 @@ __global__ __launch_bounds__(1024) void list_scan_kernel(const int *__restrict__
 __global__ __launch_bounds__(256) void list_fill_kernel(const int *__restrict__ assign, int P, int S, int N,
                                                         const int *__restrict__ base, int *__restrict__ cur,
                                                         int *__restrict__ pod, int *__restrict__ dcnt,
-                                                        int *__restrict__ dlist, int cap) {
+                                                        int2 *__restrict__ dlist, int cap) {
     const int lane = (int)threadIdx.x & 63;
     const int nsc = (S + 63) >> 6;
     const int w = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
@@ -389,26 +402,29 @@ __global__ __launch_bounds__(256) void list_fill_kernel(const int *__restrict__ 
     if (s == 0) pod[atomicAdd(&cur[b], 1)] = p;
     if (s >= S) return;
     const int a = assign[(size_t)p * S + s];
-    if (((unsigned)a < (unsigned)N ? a : N) != b) {
+    const int x = (unsigned)a < (unsigned)N ? a : N;
+    if (x != b) {
         const int q = atomicAdd(&dcnt[s], 1);
-        if (q < cap) dlist[(size_t)s * cap + q] = p;
+        if (q < cap) dlist[(size_t)s * cap + q] = make_int2(p, x);
     }
 }
 
 // delete_replaced_pod.py:41-61 per scenario by one workgroup: the pods on the
-// most hazardous node m (kdet) are the base list of m plus the scenario's list
-// of pods off their base node, each checked against assign (T: the u16 shadow
-// or int32); an overflowed list scans every pod.  Same packed key as pick16.
-// Latency-bound (a list entry, then its assign word and CPU): 4 waves per
-// scenario, kU entries per thread in flight at once.
+// most hazardous node m (kdet) are the base pods of m still on m (their
+// assign word checked: ~P/N gathers) and the list entries whose node is m
+// (read in order, no gather); an overflowed list scans every pod's assign
+// word (T: the u16 shadow or int32).  Same packed key as pick16; src[s] = the
+// winning list entry (-1: a base pod), for the move kernel's entry update.
 template <typename T>
 __global__ __launch_bounds__(256) void pick_list_kernel(const T *__restrict__ asg, const int *__restrict__ pod_cpu,
                                                         int P, int S, const unsigned long long *__restrict__ kdet,
                                                         const int *__restrict__ off, const int *__restrict__ pod,
-                                                        const int *__restrict__ dcnt, const int *__restrict__ dlist,
-                                                        int cap, unsigned long long *__restrict__ kpick) {
+                                                        const int *__restrict__ dcnt, const int2 *__restrict__ dlist,
+                                                        int cap, unsigned long long *__restrict__ kpick,
+                                                        int *__restrict__ src) {
     constexpr int kU = 8;
     __shared__ unsigned long long red[4];
+    __shared__ int lsrc;
     const int s = (int)blockIdx.x, t = (int)threadIdx.x;
     const unsigned long long kd = kdet[s];
     if (!kd) return;  // no hazard node: kpick stays 0 (the whole workgroup)
@@ -416,15 +432,20 @@ __global__ __launch_bounds__(256) void pick_list_kernel(const T *__restrict__ as
     const int b0 = off[m], nb = off[m + 1] - b0;
     const int nd = dcnt[s];
     const bool full = nd > cap;
-    const int n = nb + (full ? P : nd);  // entries: the base list, then the scenario's list (or every pod)
-    const int *l = dlist + (size_t)s * cap;
+    const int2 *l = dlist + (size_t)s * cap;
+    auto key = [](int p, int c) {
+        return c >= 0 ? ((unsigned long long)((unsigned)c ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)p)
+                      : 0ull;
+    };
     unsigned long long best = 0ull;
-    for (int i0 = 0; i0 < n; i0 += 256 * kU) {
+    // the base pods of m (or, overflowed, every pod): assign word checked
+    const int ng = full ? P : nb;
+    for (int i0 = 0; i0 < ng; i0 += 256 * kU) {
         int p[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-            const int i = min(i0 + u * 256 + t, n - 1);  // clamped: always a valid entry
-            p[u] = i < nb ? pod[b0 + i] : (full ? i - nb : l[i - nb]);
+            const int i = min(i0 + u * 256 + t, ng - 1);  // clamped: always a valid entry
+            p[u] = full ? i : pod[b0 + i];
         }
         int a[kU], c[kU];
 #pragma unroll
@@ -434,10 +455,22 @@ __global__ __launch_bounds__(256) void pick_list_kernel(const T *__restrict__ as
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-            const unsigned long long k = a[u] == m && c[u] >= 0
-                                             ? ((unsigned long long)((unsigned)c[u] ^ 0x80000000u) << 32) |
-                                                   (unsigned long long)(~(unsigned)p[u])
-                                             : 0ull;
+            const unsigned long long k = a[u] == m ? key(p[u], c[u]) : 0ull;
+            best = k > best ? k : best;
+        }
+    }
+    // the list entries on m
+    const int nl = full ? 0 : nd;
+    for (int i0 = 0; i0 < nl; i0 += 256 * kU) {
+        int2 e[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) e[u] = l[min(i0 + u * 256 + t, nl - 1)];
+        int c[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) c[u] = pod_cpu[e[u].x];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const unsigned long long k = e[u].y == m ? key(e[u].x, c[u]) : 0ull;
             best = k > best ? k : best;
         }
     }
@@ -447,11 +480,19 @@ __global__ __launch_bounds__(256) void pick_list_kernel(const T *__restrict__ as
         best = x > best ? x : best;
     }
     if ((t & 63) == 0) red[t >> 6] = best;
+    if (t == 0) lsrc = -1;
+    __syncthreads();
+    best = red[0];
+    for (int w = 1; w < 4; ++w) best = red[w] > best ? red[w] : best;
+    if (!best) return;  // no pod on m with CPU >= 0 (the whole workgroup)
+    // the winner's list entry, if it has one (it then has exactly one, on m)
+    const int pw = (int)~(unsigned)(best & 0xffffffffull);
+    for (int i = t; i < nl; i += 256)
+        if (l[i].x == pw) lsrc = i;
     __syncthreads();
     if (t == 0) {
-        best = red[0];
-        for (int w = 1; w < 4; ++w) best = red[w] > best ? red[w] : best;
-        if (best) kpick[s] = best;
+        kpick[s] = best;
+        src[s] = lsrc;
     }
 }
 
@@ -555,7 +596,7 @@ __global__ __launch_bounds__(64 * kW) void rows_detect_kernel(const long long *_
                                                               unsigned long long *__restrict__ zc_key) {
     __shared__ unsigned long long lb[kW][64], lz[kW][64];
     __shared__ int ln[kW][64];
-    constexpr int kU = 4;  // nodes per batch: their loads in flight together
+    constexpr int kU = 8;  // nodes per batch: their loads in flight together
     const int lane = (int)threadIdx.x & 63, wv = (int)threadIdx.x >> 6;
     const int nsc = (S + 63) >> 6;
     const int sc = (int)blockIdx.x % nsc, nb = (int)blockIdx.x / nsc;
@@ -798,12 +839,12 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
     if (lists_on && r->P > 0 && R > 0) {
         const int P = r->P;
         int cap = (int)std::max<int64_t>(256, P / 16);
-        cap = (int)std::max<int64_t>(64, std::min<int64_t>(cap, ((int64_t)64 << 20) / ((int64_t)S * 4)));
+        cap = (int)std::max<int64_t>(64, std::min<int64_t>(cap, ((int64_t)128 << 20) / ((int64_t)S * 8)));
         RSK_TRY(r->lbase.reserve((size_t)P * 4));
         RSK_TRY(r->loff.reserve((size_t)(N + 2) * 4 * 2));
         RSK_TRY(r->lpod.reserve((size_t)P * 4));
-        RSK_TRY(r->lcnt.reserve((size_t)S * 4));
-        RSK_TRY(r->llist.reserve((size_t)S * cap * 4));
+        RSK_TRY(r->lcnt.reserve((size_t)S * 8));  // counts, then the picks' source entries
+        RSK_TRY(r->llist.reserve((size_t)S * cap * 8));
         int *cntb = r->loff.as<int>() + (N + 2);  // N + 1 counts, then the fill cursors
         ScopedTimer tm(ctx, "rounds_lists");
         RSK_HIP(hipMemsetAsync(cntb, 0, (size_t)(N + 1) * 4, st));
@@ -815,11 +856,12 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         RSK_CHECK(waves < INT32_MAX, "list grid too large");
         list_fill_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, st>>>(d_assign, P, S, N, r->lbase.as<int>(), cntb,
                                                                         r->lpod.as<int>(), r->lcnt.as<int>(),
-                                                                        r->llist.as<int>(), cap);
+                                                                        r->llist.as<int2>(), cap);
         RSK_HIP(hipGetLastError());
         dl.base = r->lbase.as<int>();
         dl.cnt = r->lcnt.as<int>();
-        dl.list = r->llist.as<int>();
+        dl.src = dl.cnt + S;
+        dl.list = r->llist.as<int2>();
         dl.cap = cap;
     }
     for (int round = 0; round < R; ++round) {
@@ -835,11 +877,11 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
                 if (s16)
                     pick_list_kernel<unsigned short><<<blocks, 256, 0, st>>>(
                         a16, r->pod_cpu.as<int>(), r->P, S, kdet, r->loff.as<int>(), r->lpod.as<int>(), dl.cnt, dl.list,
-                        dl.cap, kpick);
+                        dl.cap, kpick, dl.src);
                 else
                     pick_list_kernel<int><<<blocks, 256, 0, st>>>(d_assign, r->pod_cpu.as<int>(), r->P, S, kdet,
                                                                   r->loff.as<int>(), r->lpod.as<int>(), dl.cnt,
-                                                                  dl.list, dl.cap, kpick);
+                                                                  dl.list, dl.cap, kpick, dl.src);
                 RSK_HIP(hipGetLastError());
             } else if (s16) {
                 const int S8 = S / 8;

@@ -29,6 +29,8 @@ for s in "${@:-test smoke bench}"; do
       ab1m:*) kv=${w#ab1m:}; step "ab1m_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u bench.py --config 1m50k --no-cpu-baseline --row-rounds 0 ;;
       abr:*) kv=${w#abr:}; step "abr_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u bench.py --config rounds --no-cpu-baseline ;;
       sb:*) kv=${w#sb:}; step "sb_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_abl.so ${kv//,/ } python -u tools/sidebench.py ;;
+      hp:*) step "hostprobe_${w#hp:}" 300 python -u tools/hostprobe.py "${w#hp:}" ;;
+      bnoev) step bench_noevents 600 python -u bench.py --no-cpu-baseline --no-kernel-events ;;
       dropin) step dropin 400 python -u tools/dropin_latency.py --calls 40 --out "$out/dropin.json" ;;
       prof) for c in headline 1m50k; do
               ./tools/gpu_prof.sh $c "$out/prof_$c" > "$out/prof_$c.log" 2>&1 || { tail -5 "$out/prof_$c.log"; exit 1; }
