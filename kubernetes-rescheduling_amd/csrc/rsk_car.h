@@ -299,6 +299,7 @@ struct Tile16Args {
     int img_cells;         // LDS cells of the largest image (rmax * SL); the records follow
     int rec_cap;           // record ints reserved in LDS; the unit counter follows
     int order, xcd_per;    // grid order (RSK_TILE_ORDER) as in the wide kernel
+    int group;             // order 2: > 1 = groups of this many chunks walked tile-major (RSK_TILE_GROUP)
     int ablate;            // profiling only (RSK_ABLATE_TILE): 1 skip image load, 2 skip scoring
     unsigned n_assign, n_out, n_pods, n_recs, n_key;  // element counts (debug bounds build)
 };

@@ -1735,6 +1735,8 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         a.lsl = 0;
         while ((1 << a.lsl) < SL) ++a.lsl;
         a.order = order;
+        static const int group = RSK_KNOB(RSK_TILE_GROUP, 0);
+        a.group = group;
         a.ablate = ablate;
         a.rec_cap = (plan->recmax + 3) & ~3;
         a.img_cells = (plan->rmax * SL + 3) & ~3;

@@ -1076,8 +1076,25 @@ __device__ __forceinline__ void tile16_block(const Tile16Args &a, unsigned bid) 
         unit = (int)(bid & 7u) * a.xcd_per + (int)(bid >> 3);
         if (unit >= nchunk * a.T) return;  // whole workgroup, before any barrier
     }
-    const int tile = a.tile0 + (a.order == 1 ? unit / nchunk : unit % a.T);
-    const int chunk = a.order == 1 ? unit % nchunk : unit / a.T;
+    int tile, chunk;
+    if (a.order == 2 && a.group > 1) {
+        // groups of `group` chunks, each walked tile-major: the workgroups an XCD
+        // runs together read adjacent 256-B segments of the same pod rows
+        const int G = a.group, full = nchunk / G;
+        if (unit < full * a.T * G) {
+            const int cg = unit / (a.T * G), r = unit - cg * a.T * G;
+            tile = r / G;
+            chunk = cg * G + (r - tile * G);
+        } else {
+            const int g = nchunk - full * G, r = unit - full * a.T * G;
+            tile = r / g;
+            chunk = full * G + (r - tile * g);
+        }
+        tile += a.tile0;
+    } else {
+        tile = a.tile0 + (a.order == 1 ? unit / nchunk : unit % a.T);
+        chunk = a.order == 1 ? unit % nchunk : unit / a.T;
+    }
     const int lane = threadIdx.x & 63;
     const int s0 = chunk * SL;
     unsigned *img = reinterpret_cast<unsigned *>(lds);
