@@ -286,7 +286,7 @@ def bench_rounds(args, cfg, world, rank, local, dev):
         ctx.set_profiling(False)
         T["assign"].copy_(a_keep)
         T["use_cpu"].copy_(u_keep)
-        for name in ("rounds_lists", "rounds_shadow", "rounds_detect", "rounds_pick", "rounds_move"):
+        for name in ("rounds_lists", "rounds_shadow", "rounds_detect", "rounds_pick", "rounds_move", "rounds_persist"):
             ms, n = ctx.kernel_time(name)
             if n:
                 kernels[name] = {"avg_ms": ms / n, "launches": n, "per_step_ms": ms / args.steps}

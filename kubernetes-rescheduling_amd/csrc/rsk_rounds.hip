@@ -33,7 +33,9 @@ struct rsk_rounds {
     // the eviction pick's pod lists (rsk_rounds_run): base node per pod, the
     // pods of each base node (CSR), per scenario the pods off their base node
     rsk::DevBuf lbase, loff, lpod, lcnt, llist;
+    rsk::DevBuf blk;   // the persistent loop's per-(scenario, 64-node block) detect maxima
     ~rsk_rounds() {
+        blk.release();
         lbase.release();
         loff.release();
         lpod.release();
@@ -496,6 +498,280 @@ __global__ __launch_bounds__(256) void pick_list_kernel(const T *__restrict__ as
     }
 }
 
+// ---- the persistent loop (rsk_rounds_run): every round of a scenario in one workgroup ----
+// Scenarios never touch each other's state, so a workgroup can run all R rounds
+// of its scenario without a grid-wide step: detect kept incrementally (a move
+// changes the CPU of two nodes; their 64-node blocks' maxima are recomputed and
+// the scenario's maxima re-reduced over the blocks), the pick over the pod
+// lists, CAR and the update by car_move_one.
+constexpr int kBlkNodes = 64;
+struct BlkArgs {
+    unsigned long long *bm;  // [S][NB] packed (pct, ~node) max over the block's hazard nodes (0: none)
+    unsigned long long *bz;  // [S][NB] packed (cap - use, ~node) max over its non-hazard nodes
+    int *bc;                 // [S][NB] its non-hazard nodes
+    int NB;
+};
+
+__device__ __forceinline__ int pct_of(int u, int c) {  // get_resource_usage.py:37 (cpu_pct_kernel)
+    return c == 0 ? -1 : (int)rint((double)u / (double)c * 100.0);
+}
+
+// setup: hazard flags and every (scenario, block) entry; lane = scenario,
+// wave = (64-scenario chunk, block)
+__global__ __launch_bounds__(256) void blk_detect_kernel(const int *__restrict__ use, const int *__restrict__ cap,
+                                                         int N, int S, int thr, uint8_t *__restrict__ haz,
+                                                         BlkArgs ba) {
+    const int lane = (int)threadIdx.x & 63;
+    const int nsc = (S + 63) >> 6;
+    const int w = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int b = w / nsc, sc = w - b * nsc;
+    if (b >= ba.NB) return;
+    const int s = sc * 64 + lane;
+    if (s >= S) return;
+    const int n0 = b * kBlkNodes, n1 = min(N, n0 + kBlkNodes);
+    unsigned long long m = 0ull, z = 0ull;
+    int cnt = 0;
+    for (int n = n0; n < n1; ++n) {
+        const size_t i = (size_t)n * S + s;
+        const int c = cap[n], u = use[i], v = pct_of(u, c);
+        const bool h = v >= thr;
+        haz[i] = h;
+        if (h) {
+            const unsigned long long k = ((unsigned long long)((unsigned)v ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)n);
+            m = k > m ? k : m;
+        } else {
+            ++cnt;
+            const unsigned long long k = ((unsigned long long)((unsigned)(c - u) ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)n);
+            z = k > z ? k : z;
+        }
+    }
+    const size_t o = (size_t)s * ba.NB + b;
+    ba.bm[o] = m;
+    ba.bz[o] = z;
+    ba.bc[o] = cnt;
+}
+
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long y = __shfl_xor(x, o, 64);
+        x = y > x ? y : x;
+    }
+    return x;
+}
+
+__device__ __forceinline__ int wave_sum(int x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+
+struct ScnState {  // the scenario's detect maxima (LDS)
+    unsigned long long most, zkey;
+    int zcnt;
+};
+
+// the scenario's maxima over its NB block entries (every thread; ends with a barrier)
+__device__ __forceinline__ void scn_reduce(const BlkArgs &ba, int s, ScnState *st, unsigned long long *r64, int *r32) {
+    const int t = (int)threadIdx.x;
+    const size_t o = (size_t)s * ba.NB;
+    unsigned long long m = 0ull, z = 0ull;
+    int c = 0;
+    for (int b = t; b < ba.NB; b += 256) {
+        const unsigned long long x = ba.bm[o + b], y = ba.bz[o + b];
+        m = x > m ? x : m;
+        z = y > z ? y : z;
+        c += ba.bc[o + b];
+    }
+    m = wave_max_u64(m);
+    z = wave_max_u64(z);
+    c = wave_sum(c);
+    if ((t & 63) == 0) {
+        r64[t >> 6] = m;
+        r64[4 + (t >> 6)] = z;
+        r32[t >> 6] = c;
+    }
+    __syncthreads();
+    if (t == 0) {
+        for (int w = 1; w < 4; ++w) {
+            m = r64[w] > m ? r64[w] : m;
+            z = r64[4 + w] > z ? r64[4 + w] : z;
+            c += r32[w];
+        }
+        st->most = m;
+        st->zkey = z;
+        st->zcnt = c;
+    }
+    __syncthreads();
+}
+
+// block b of scenario s re-reduced after a move, by one wave (lane = node)
+__device__ __forceinline__ void blk_update(const int *__restrict__ use, const int *__restrict__ cap, int N, int S,
+                                           int thr, uint8_t *__restrict__ haz, const BlkArgs &ba, int s, int b, int o,
+                                           int t) {
+    const int lane = (int)threadIdx.x & 63;
+    const int n = b * kBlkNodes + lane;
+    unsigned long long m = 0ull, z = 0ull;
+    int cnt = 0;
+    if (n < N) {
+        const size_t i = (size_t)n * S + s;
+        const int c = cap[n], u = use[i], v = pct_of(u, c);
+        const bool h = v >= thr;
+        if (n == o || n == t) haz[i] = h;
+        if (h) m = ((unsigned long long)((unsigned)v ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)n);
+        else {
+            cnt = 1;
+            z = ((unsigned long long)((unsigned)(c - u) ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)n);
+        }
+    }
+    m = wave_max_u64(m);
+    z = wave_max_u64(z);
+    cnt = wave_sum(cnt);
+    if (lane == 0) {
+        const size_t x = (size_t)s * ba.NB + b;
+        ba.bm[x] = m;
+        ba.bz[x] = z;
+        ba.bc[x] = cnt;
+    }
+}
+
+// delete_replaced_pod.py:41-61 for scenario s by the workgroup (pick_list_kernel's
+// rule); returns the pod (-1 none) to every thread, the winning entry in *src
+template <typename T>
+__device__ __forceinline__ int scn_pick(const T *__restrict__ asg, const int *__restrict__ pod_cpu, int P, int S,
+                                        int s, unsigned long long kd, const int *__restrict__ off,
+                                        const int *__restrict__ pod, const DevLists &dl, unsigned long long *r64,
+                                        int *lsrc) {
+    constexpr int kU = 4;
+    const int t = (int)threadIdx.x;
+    if (!kd) return -1;  // uniform
+    const int m = (int)~(unsigned)(kd & 0xffffffffull);
+    const int b0 = off[m], nb = off[m + 1] - b0;
+    const int nd = dl.cnt[s];
+    const bool full = nd > dl.cap;
+    const int2 *l = dl.list + (size_t)s * dl.cap;
+    auto key = [](int p, int c) {
+        return c >= 0 ? ((unsigned long long)((unsigned)c ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)p)
+                      : 0ull;
+    };
+    unsigned long long best = 0ull;
+    const int ng = full ? P : nb;
+    for (int i0 = 0; i0 < ng; i0 += 256 * kU) {
+        int p[kU], a[kU], c[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int i = min(i0 + u * 256 + t, ng - 1);
+            p[u] = full ? i : pod[b0 + i];
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            a[u] = (int)asg[(size_t)p[u] * S + s];
+            c[u] = pod_cpu[p[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const unsigned long long k = a[u] == m ? key(p[u], c[u]) : 0ull;
+            best = k > best ? k : best;
+        }
+    }
+    const int nl = full ? 0 : nd;
+    for (int i0 = 0; i0 < nl; i0 += 256 * kU) {
+        int2 e[kU];
+        int c[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) e[u] = l[min(i0 + u * 256 + t, nl - 1)];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) c[u] = pod_cpu[e[u].x];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const unsigned long long k = e[u].y == m ? key(e[u].x, c[u]) : 0ull;
+            best = k > best ? k : best;
+        }
+    }
+    best = wave_max_u64(best);
+    if ((t & 63) == 0) r64[t >> 6] = best;
+    if (t == 0) *lsrc = -1;
+    __syncthreads();
+    best = r64[0];
+    for (int w = 1; w < 4; ++w) best = r64[w] > best ? r64[w] : best;
+    if (!best) {
+        __syncthreads();  // r64 is reused by the caller
+        return -1;
+    }
+    const int pw = (int)~(unsigned)(best & 0xffffffffull);
+    for (int i = t; i < nl; i += 256)
+        if (l[i].x == pw) *lsrc = i;
+    __syncthreads();
+    return pw;
+}
+
+struct PersistArgs {
+    const int *row_ptr, *col, *pod_cpu, *cap;
+    int *assign, *use;
+    uint8_t *haz;
+    int *ev_cur;                      // [S] the round's eviction (car_move_one reads evict[s])
+    int *zc_cnt;                      // [S] the scenario's zero case, as car_move_one reads it
+    unsigned long long *zc_key;
+    const int *off, *pod;             // the base nodes' pod lists
+    DevLists dl;
+    BlkArgs ba;
+    int *out_evict, *out_target;      // [R][S]
+    int P, N, S, H, R, thr;
+};
+
+template <bool kGlobal>
+__global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArgs a, unsigned *__restrict__ gtab) {
+    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
+    __shared__ unsigned long long r64[8];
+    __shared__ int r32[4];
+    __shared__ int lsrc;
+    __shared__ ScnState st;
+    unsigned *tab = kGlobal ? gtab + (size_t)blockIdx.x * (size_t)(2 * a.H + 8) : lds;
+    const int t = (int)threadIdx.x;
+    for (int s = (int)blockIdx.x; s < a.S; s += (int)gridDim.x) {
+        scn_reduce(a.ba, s, &st, r64, r32);
+        if (t == 0) {
+            a.zc_cnt[s] = st.zcnt;
+            a.zc_key[s] = st.zkey;
+        }
+        for (int r = 0; r < a.R; ++r) {
+            const unsigned long long kd = st.most;
+            const int p = scn_pick<int>(a.assign, a.pod_cpu, a.P, a.S, s, kd, a.off, a.pod, a.dl, r64, &lsrc);
+            int *tg_row = a.out_target + (size_t)r * a.S;
+            if (t == 0) {
+                a.out_evict[(size_t)r * a.S + s] = p;
+                a.ev_cur[s] = p;
+                if (p >= 0) a.dl.src[s] = lsrc;
+            }
+            if (p < 0) {
+                if (t == 0) tg_row[s] = kNoEvict;
+                continue;  // uniform: the state is unchanged
+            }
+            const int o = a.assign[(size_t)p * a.S + s];  // its node before the move
+            __syncthreads();                              // ev_cur / src visible to the workgroup
+            car_move_one<kGlobal>(a.row_ptr, a.col, a.pod_cpu, a.assign, a.use, a.cap, a.haz, a.ev_cur, s, a.S, a.N,
+                                  a.H, 1, tg_row, nullptr, tab, nullptr, nullptr, nullptr, a.zc_cnt, a.zc_key, 0,
+                                  INT_MAX, a.dl);
+            move_sync<kGlobal>();  // the move's state update (thread 0) before it is read
+            const int tt = tg_row[s];
+            if (tt >= 0) {  // two nodes' CPU changed: their blocks, then the scenario's maxima
+                const int bo = (unsigned)o < (unsigned)a.N ? o / kBlkNodes : -1, bt = tt / kBlkNodes;
+                const int w = t >> 6;
+                if (w == 0) blk_update(a.use, a.cap, a.N, a.S, a.thr, a.haz, a.ba, s, bt, o, tt);
+                if (w == 1 && bo >= 0 && bo != bt) blk_update(a.use, a.cap, a.N, a.S, a.thr, a.haz, a.ba, s, bo, o, tt);
+                __syncthreads();
+                scn_reduce(a.ba, s, &st, r64, r32);
+            }
+            if (t == 0) {  // car_move_one zeroes the zero-case words (the launch loop's atomics)
+                a.zc_cnt[s] = st.zcnt;
+                a.zc_key[s] = st.zkey;
+            }
+            if (kGlobal) move_sync<true>();  // the area is free before the next round clears it
+            else __syncthreads();
+        }
+    }
+}
+
 // Row-sharded loop glue: one thread per scenario.
 __global__ void rows_evict_key_kernel(const int *__restrict__ local_pod, int S, int r0, const int *__restrict__ pod_cpu,
                                       long long *__restrict__ key) {
@@ -812,7 +1088,10 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
     RSK_TRY(g.rc);
     // the eviction scan reads a u16 shadow of assign when node ids fit (kept in
     // step by the move kernel); otherwise the int32 scan
-    const bool s16 = N <= 65535 && S % 8 == 0 && PS > 0 && ((uintptr_t)d_assign % 16) == 0;
+    static const bool lists_on = RSK_KNOB(RSK_ROUNDS_LISTS, 1) != 0;
+    static const bool persist_on = RSK_KNOB(RSK_ROUNDS_PERSIST, 1) != 0;
+    const bool persist = lists_on && persist_on && r->P > 0 && R > 0;  // one launch, no shadow
+    const bool s16 = !persist && N <= 65535 && S % 8 == 0 && PS > 0 && ((uintptr_t)d_assign % 16) == 0;
     unsigned short *a16 = nullptr;
     if (s16) {
         RSK_TRY(r->asg16.reserve(PS * 2));
@@ -834,7 +1113,6 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
     // Per round one wave per scenario reads ~(P/N + list) pods instead of the
     // P x S scan (rsk_rounds.hip pick16: 205 MB at config 5).  Built per call
     // from one read of assign.
-    static const bool lists_on = RSK_KNOB(RSK_ROUNDS_LISTS, 1) != 0;
     DevLists dl;
     if (lists_on && r->P > 0 && R > 0) {
         const int P = r->P;
@@ -863,6 +1141,56 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         dl.src = dl.cnt + S;
         dl.list = r->llist.as<int2>();
         dl.cap = cap;
+    }
+    if (persist) {
+        // one launch for all R rounds: the hazard flags and the block maxima
+        // once, then a workgroup per scenario walks its rounds
+        PersistArgs pa;
+        pa.ba.NB = (int)ceil_div(N, kBlkNodes);
+        const size_t nbs = (size_t)S * pa.ba.NB;
+        RSK_TRY(r->blk.reserve(nbs * 20 + (size_t)S * 4));
+        pa.ba.bm = r->blk.as<unsigned long long>();
+        pa.ba.bz = pa.ba.bm + nbs;
+        pa.ba.bc = reinterpret_cast<int *>(pa.ba.bz + nbs);
+        pa.ev_cur = pa.ba.bc + nbs;
+        pa.row_ptr = r->row_ptr.as<int>();
+        pa.col = r->col.as<int>();
+        pa.pod_cpu = r->pod_cpu.as<int>();
+        pa.cap = d_cap;
+        pa.assign = d_assign;
+        pa.use = d_use;
+        pa.haz = r->haz.as<uint8_t>();
+        pa.zc_cnt = zcnt;
+        pa.zc_key = zkey;
+        pa.off = r->loff.as<int>();
+        pa.pod = r->lpod.as<int>();
+        pa.dl = dl;
+        pa.out_evict = d_evict;
+        pa.out_target = d_target;
+        pa.P = r->P;
+        pa.N = N;
+        pa.S = S;
+        pa.H = g.H;
+        pa.R = R;
+        pa.thr = threshold;
+        {
+            ScopedTimer tm(ctx, "rounds_detect");
+            const int64_t waves = (int64_t)pa.ba.NB * ceil_div(S, 64);
+            blk_detect_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, st>>>(d_use, d_cap, N, S, threshold,
+                                                                           r->haz.as<uint8_t>(), pa.ba);
+            RSK_HIP(hipGetLastError());
+        }
+        ScopedTimer tm(ctx, "rounds_persist");
+        if (g.lds) {
+            if (g.lds > 64 * 1024)
+                RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&rounds_persist_kernel<false>),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds));
+            rounds_persist_kernel<false><<<dim3((unsigned)g.grid), dim3(kMoveThreads), g.lds, st>>>(pa, nullptr);
+        } else {
+            rounds_persist_kernel<true><<<dim3((unsigned)g.grid), dim3(kMoveThreads), 0, st>>>(pa, r->gtab.as<unsigned>());
+        }
+        RSK_HIP(hipGetLastError());
+        R = 0;  // every round done
     }
     for (int round = 0; round < R; ++round) {
         int *ev = d_evict + (size_t)round * S;
