@@ -97,7 +97,7 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
                                              unsigned *tab, unsigned long long *__restrict__ kpick,
                                              unsigned long long *__restrict__ kdet, int *__restrict__ ev_out,
                                              int *__restrict__ zc_cnt, unsigned long long *__restrict__ zc_key,
-                                             int own0, int own1, DevLists dl) {
+                                             int own0, int own1, DevLists dl, int p_direct = -1) {
     unsigned *keys = tab, *cnts = tab + H;
     unsigned long long *red64 = reinterpret_cast<unsigned long long *>(tab + 2 * H);  // best
     unsigned *red = tab + 2 * H + 2;                                                   // M, n_at_M, n_free
@@ -107,7 +107,7 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
         const unsigned long long k = kpick[s];
         p = k ? (int)(~(unsigned)(k & 0xffffffffull)) : -1;
     } else {
-        p = evict[s];
+        p = evict ? evict[s] : p_direct;  // (the persistent loop: its pick, in registers)
     }
     if (kpick && tid == 0) ev_out[s] = p;
     if (p < own0 || p >= own1) {  // no eviction, or (row-sharded) another rank's pod
@@ -188,6 +188,7 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
         else if (nbest == 1) t = node;                // the single best, even if overloaded
         else t = rem >= 0 ? node : RSK_TARGET_NONE;   // largest remaining CPU, None if < 0
         out_target[s] = t;
+        red[5] = (unsigned)t;  // for the workgroup (the persistent loop), after its next barrier
         if (kpick) kpick[s] = kdet[s] = 0ull;  // every thread read p long before the last barrier
         if (zc_cnt) zc_cnt[s] = 0, zc_key[s] = 0ull;
         if (update && t >= 0) {  // build-defined update: the pod's CPU moves with it
@@ -390,24 +391,82 @@ __global__ __launch_bounds__(1024) void list_scan_kernel(const int *__restrict__
 }
 
 // the base nodes' pod lists (cursor = a copy of off) and the scenarios' lists
-// of pods off their base node: thread = (pod, 64-scenario lane)
+// of pods off their base node.  Workgroup = (64-scenario chunk, kLF pods), lane
+// = scenario, each wave a quarter of the pods: the lanes count their deviating
+// pods, one atomic per scenario and workgroup reserves the list slots, then
+// the pods (their rows now in L2) are walked again to write the entries.
+constexpr int kLF = 1024;
 __global__ __launch_bounds__(256) void list_fill_kernel(const int *__restrict__ assign, int P, int S, int N,
                                                         const int *__restrict__ base, int *__restrict__ cur,
                                                         int *__restrict__ pod, int *__restrict__ dcnt,
                                                         int2 *__restrict__ dlist, int cap) {
-    const int lane = (int)threadIdx.x & 63;
+    constexpr int kK = 16;  // deviations kept per (wave, lane) in LDS; more: the rows are walked again
+    __shared__ int wc[4][64];
+    __shared__ int2 keep[4][kK][64];
+    const int lane = (int)threadIdx.x & 63, wv = (int)threadIdx.x >> 6;
     const int nsc = (S + 63) >> 6;
-    const int w = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
-    const int p = w / nsc, s = (w - p * nsc) * 64 + lane;
-    if (p >= P) return;
-    const int b = base[p];
-    if (s == 0) pod[atomicAdd(&cur[b], 1)] = p;
-    if (s >= S) return;
-    const int a = assign[(size_t)p * S + s];
-    const int x = (unsigned)a < (unsigned)N ? a : N;
-    if (x != b) {
-        const int q = atomicAdd(&dcnt[s], 1);
-        if (q < cap) dlist[(size_t)s * cap + q] = make_int2(p, x);
+    const int pg = (int)blockIdx.x / nsc, s = ((int)blockIdx.x - pg * nsc) * 64 + lane;
+    const int q0 = pg * kLF + wv * (kLF / 4), q1 = min(P, q0 + kLF / 4);
+    const int ss = min(s, S - 1);
+    if (s < 64) {  // the base lists: the first scenario chunk's lanes, a pod each
+#pragma unroll 4
+        for (int p = q0 + lane; p < q1; p += 64) pod[atomicAdd(&cur[base[p]], 1)] = p;
+    }
+    constexpr int kB = 16;
+    int n = 0;
+    for (int p0 = q0; p0 < q1; p0 += kB) {
+        int a[kB], b[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            const int p = min(p0 + u, q1 - 1);  // clamped: always a valid row
+            a[u] = assign[(size_t)p * S + ss];
+            b[u] = base[p];
+        }
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            const int x = (unsigned)a[u] < (unsigned)N ? a[u] : N;
+            if (p0 + u < q1 && x != b[u]) {
+                if (n < kK) keep[wv][n][lane] = make_int2(p0 + u, x);
+                ++n;
+            }
+        }
+    }
+    wc[wv][lane] = n;
+    __syncthreads();
+    if (wv == 0) {
+        const int tot = wc[0][lane] + wc[1][lane] + wc[2][lane] + wc[3][lane];
+        int at = (s < S && tot) ? atomicAdd(&dcnt[s], tot) : 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const int c = wc[w][lane];
+            wc[w][lane] = at;
+            at += c;
+        }
+    }
+    __syncthreads();
+    if (s >= S || n == 0) return;
+    int q = wc[wv][lane];
+    if (n <= kK) {  // the kept entries
+        for (int k = 0; k < n; ++k, ++q)
+            if (q < cap) dlist[(size_t)s * cap + q] = keep[wv][k][lane];
+        return;
+    }
+    for (int p0 = q0; p0 < q1; p0 += kB) {
+        int a[kB], b[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            const int p = min(p0 + u, q1 - 1);
+            a[u] = assign[(size_t)p * S + ss];
+            b[u] = base[p];
+        }
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            const int x = (unsigned)a[u] < (unsigned)N ? a[u] : N;
+            if (p0 + u < q1 && x != b[u]) {
+                if (q < cap) dlist[(size_t)s * cap + q] = make_int2(p0 + u, x);
+                ++q;
+            }
+        }
     }
 }
 
@@ -572,9 +631,11 @@ struct ScnState {  // the scenario's detect maxima (LDS)
 };
 
 // the scenario's maxima over its NB block entries (every thread; ends with a barrier)
-__device__ __forceinline__ void scn_reduce(const BlkArgs &ba, int s, ScnState *st, unsigned long long *r64, int *r32) {
+// (sb: the scenario's row of the block arrays, in LDS or global memory)
+__device__ __forceinline__ void scn_reduce(const BlkArgs &sb, ScnState *st, unsigned long long *r64, int *r32) {
     const int t = (int)threadIdx.x;
-    const size_t o = (size_t)s * ba.NB;
+    const BlkArgs &ba = sb;
+    const size_t o = 0;
     unsigned long long m = 0ull, z = 0ull;
     int c = 0;
     for (int b = t; b < ba.NB; b += 256) {
@@ -607,7 +668,7 @@ __device__ __forceinline__ void scn_reduce(const BlkArgs &ba, int s, ScnState *s
 
 // block b of scenario s re-reduced after a move, by one wave (lane = node)
 __device__ __forceinline__ void blk_update(const int *__restrict__ use, const int *__restrict__ cap, int N, int S,
-                                           int thr, uint8_t *__restrict__ haz, const BlkArgs &ba, int s, int b, int o,
+                                           int thr, uint8_t *__restrict__ haz, const BlkArgs &sb, int s, int b, int o,
                                            int t) {
     const int lane = (int)threadIdx.x & 63;
     const int n = b * kBlkNodes + lane;
@@ -628,10 +689,9 @@ __device__ __forceinline__ void blk_update(const int *__restrict__ use, const in
     z = wave_max_u64(z);
     cnt = wave_sum(cnt);
     if (lane == 0) {
-        const size_t x = (size_t)s * ba.NB + b;
-        ba.bm[x] = m;
-        ba.bz[x] = z;
-        ba.bc[x] = cnt;
+        sb.bm[b] = m;
+        sb.bz[b] = z;
+        sb.bc[b] = cnt;
     }
 }
 
@@ -655,6 +715,7 @@ __device__ __forceinline__ int scn_pick(const T *__restrict__ asg, const int *__
                       : 0ull;
     };
     unsigned long long best = 0ull;
+    int bsrc = -1;  // the list entry of this thread's best (-1: a base pod)
     const int ng = full ? P : nb;
     for (int i0 = 0; i0 < ng; i0 += 256 * kU) {
         int p[kU], a[kU], c[kU];
@@ -685,24 +746,21 @@ __device__ __forceinline__ int scn_pick(const T *__restrict__ asg, const int *__
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const unsigned long long k = e[u].y == m ? key(e[u].x, c[u]) : 0ull;
+            // >=: an entry of the same pod as a base hit carries the pod's entry index
+            if (k && k >= best) bsrc = min(i0 + u * 256 + t, nl - 1);
             best = k > best ? k : best;
         }
     }
+    const unsigned long long mine = best;
     best = wave_max_u64(best);
     if ((t & 63) == 0) r64[t >> 6] = best;
     if (t == 0) *lsrc = -1;
     __syncthreads();
     best = r64[0];
     for (int w = 1; w < 4; ++w) best = r64[w] > best ? r64[w] : best;
-    if (!best) {
-        __syncthreads();  // r64 is reused by the caller
-        return -1;
-    }
-    const int pw = (int)~(unsigned)(best & 0xffffffffull);
-    for (int i = t; i < nl; i += 256)
-        if (l[i].x == pw) *lsrc = i;
+    if (best && mine == best && bsrc >= 0) *lsrc = bsrc;  // the winner's entry (at most one per pod)
     __syncthreads();
-    return pw;
+    return best ? (int)~(unsigned)(best & 0xffffffffull) : -1;
 }
 
 struct PersistArgs {
@@ -717,6 +775,8 @@ struct PersistArgs {
     BlkArgs ba;
     int *out_evict, *out_target;      // [R][S]
     int P, N, S, H, R, thr;
+    int blk_lds;                      // the scenario's block row kept in LDS (after the hash when it is there)
+    unsigned hash_bytes;              // dynamic LDS of the hash (0: global work areas)
 };
 
 template <bool kGlobal>
@@ -729,7 +789,26 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
     unsigned *tab = kGlobal ? gtab + (size_t)blockIdx.x * (size_t)(2 * a.H + 8) : lds;
     const int t = (int)threadIdx.x;
     for (int s = (int)blockIdx.x; s < a.S; s += (int)gridDim.x) {
-        scn_reduce(a.ba, s, &st, r64, r32);
+        BlkArgs sb;
+        sb.NB = a.ba.NB;
+        const size_t row = (size_t)s * a.ba.NB;
+        if (a.blk_lds) {  // the row in LDS for the scenario's rounds (written back never: per call)
+            char *base = reinterpret_cast<char *>(lds) + a.hash_bytes;
+            sb.bm = reinterpret_cast<unsigned long long *>(base);
+            sb.bz = sb.bm + sb.NB;
+            sb.bc = reinterpret_cast<int *>(sb.bz + sb.NB);
+            for (int b = t; b < sb.NB; b += kMoveThreads) {
+                sb.bm[b] = a.ba.bm[row + b];
+                sb.bz[b] = a.ba.bz[row + b];
+                sb.bc[b] = a.ba.bc[row + b];
+            }
+            __syncthreads();
+        } else {
+            sb.bm = a.ba.bm + row;
+            sb.bz = a.ba.bz + row;
+            sb.bc = a.ba.bc + row;
+        }
+        scn_reduce(sb, &st, r64, r32);
         if (t == 0) {
             a.zc_cnt[s] = st.zcnt;
             a.zc_key[s] = st.zkey;
@@ -740,27 +819,25 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
             int *tg_row = a.out_target + (size_t)r * a.S;
             if (t == 0) {
                 a.out_evict[(size_t)r * a.S + s] = p;
-                a.ev_cur[s] = p;
-                if (p >= 0) a.dl.src[s] = lsrc;
+                if (p >= 0) a.dl.src[s] = lsrc;  // read by car_move_one's thread 0
             }
             if (p < 0) {
                 if (t == 0) tg_row[s] = kNoEvict;
                 continue;  // uniform: the state is unchanged
             }
-            const int o = a.assign[(size_t)p * a.S + s];  // its node before the move
-            __syncthreads();                              // ev_cur / src visible to the workgroup
-            car_move_one<kGlobal>(a.row_ptr, a.col, a.pod_cpu, a.assign, a.use, a.cap, a.haz, a.ev_cur, s, a.S, a.N,
+            const int o = (int)~(unsigned)(kd & 0xffffffffull);  // the picked pod sits on the hazard node
+            car_move_one<kGlobal>(a.row_ptr, a.col, a.pod_cpu, a.assign, a.use, a.cap, a.haz, nullptr, s, a.S, a.N,
                                   a.H, 1, tg_row, nullptr, tab, nullptr, nullptr, nullptr, a.zc_cnt, a.zc_key, 0,
-                                  INT_MAX, a.dl);
+                                  INT_MAX, a.dl, p);
             move_sync<kGlobal>();  // the move's state update (thread 0) before it is read
-            const int tt = tg_row[s];
+            const int tt = (int)tab[2 * a.H + 7];  // car_move_one's target (red[5])
             if (tt >= 0) {  // two nodes' CPU changed: their blocks, then the scenario's maxima
                 const int bo = (unsigned)o < (unsigned)a.N ? o / kBlkNodes : -1, bt = tt / kBlkNodes;
                 const int w = t >> 6;
-                if (w == 0) blk_update(a.use, a.cap, a.N, a.S, a.thr, a.haz, a.ba, s, bt, o, tt);
-                if (w == 1 && bo >= 0 && bo != bt) blk_update(a.use, a.cap, a.N, a.S, a.thr, a.haz, a.ba, s, bo, o, tt);
+                if (w == 0) blk_update(a.use, a.cap, a.N, a.S, a.thr, a.haz, sb, s, bt, o, tt);
+                if (w == 1 && bo >= 0 && bo != bt) blk_update(a.use, a.cap, a.N, a.S, a.thr, a.haz, sb, s, bo, o, tt);
                 __syncthreads();
-                scn_reduce(a.ba, s, &st, r64, r32);
+                scn_reduce(sb, &st, r64, r32);
             }
             if (t == 0) {  // car_move_one zeroes the zero-case words (the launch loop's atomics)
                 a.zc_cnt[s] = st.zcnt;
@@ -1130,9 +1207,9 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         list_base_kernel<<<(unsigned)ceil_div(P, 256), 256, 0, st>>>(d_assign, P, S, N, r->lbase.as<int>(), cntb);
         list_scan_kernel<<<1, 1024, 0, st>>>(cntb, N + 1, r->loff.as<int>());
         RSK_HIP(hipMemcpyAsync(cntb, r->loff.ptr, (size_t)(N + 1) * 4, hipMemcpyDeviceToDevice, st));
-        const int64_t waves = (int64_t)P * ceil_div(S, 64);
-        RSK_CHECK(waves < INT32_MAX, "list grid too large");
-        list_fill_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, st>>>(d_assign, P, S, N, r->lbase.as<int>(), cntb,
+        const int64_t blocks = ceil_div(P, kLF) * ceil_div(S, 64);
+        RSK_CHECK(blocks < INT32_MAX, "list grid too large");
+        list_fill_kernel<<<(unsigned)blocks, 256, 0, st>>>(d_assign, P, S, N, r->lbase.as<int>(), cntb,
                                                                         r->lpod.as<int>(), r->lcnt.as<int>(),
                                                                         r->llist.as<int2>(), cap);
         RSK_HIP(hipGetLastError());
@@ -1180,15 +1257,17 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
                                                                            r->haz.as<uint8_t>(), pa.ba);
             RSK_HIP(hipGetLastError());
         }
+        // the scenario's block row in LDS while it fits beside the hash
+        const size_t blk_bytes = (size_t)pa.ba.NB * 20;
+        pa.hash_bytes = (unsigned)g.lds;
+        pa.blk_lds = blk_bytes <= 32 * 1024 && g.lds + blk_bytes <= 160 * 1024;
+        const size_t lds = g.lds + (pa.blk_lds ? blk_bytes : 0);
         ScopedTimer tm(ctx, "rounds_persist");
-        if (g.lds) {
-            if (g.lds > 64 * 1024)
-                RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&rounds_persist_kernel<false>),
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds));
-            rounds_persist_kernel<false><<<dim3((unsigned)g.grid), dim3(kMoveThreads), g.lds, st>>>(pa, nullptr);
-        } else {
-            rounds_persist_kernel<true><<<dim3((unsigned)g.grid), dim3(kMoveThreads), 0, st>>>(pa, r->gtab.as<unsigned>());
-        }
+        auto *kern = g.lds ? &rounds_persist_kernel<false> : &rounds_persist_kernel<true>;
+        if (lds > 64 * 1024)
+            RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)lds));
+        kern<<<dim3((unsigned)g.grid), dim3(kMoveThreads), lds, st>>>(pa, g.lds ? nullptr : r->gtab.as<unsigned>());
         RSK_HIP(hipGetLastError());
         R = 0;  // every round done
     }
