@@ -433,10 +433,20 @@ __global__ __launch_bounds__(256) void nr_hist_kernel(const int *__restrict__ as
     for (int j = (int)threadIdx.x; j < nbk; j += 256) hist[j] = 0;
     __syncthreads();
     const int p0 = (int)blockIdx.x * kNrChunk, p1 = min(P, p0 + kNrChunk);
-    for (int p = p0 + (int)threadIdx.x; p < p1; p += 256) {
-        const int k = nr_key(assign, p, S, N);
-        pkey[p] = k;
-        atomicAdd(&hist[k >> kNrSubBits], 1);
+    constexpr int kU = kNrChunk / 256;  // the thread's pods: their (strided) key loads issued together
+    int k[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        const int p = min(p0 + u * 256 + (int)threadIdx.x, P - 1);
+        k[u] = nr_key(assign, p, S, N);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        const int p = p0 + u * 256 + (int)threadIdx.x;
+        if (p < p1) {
+            pkey[p] = k[u];
+            atomicAdd(&hist[k[u] >> kNrSubBits], 1);
+        }
     }
     __syncthreads();
     for (int j = (int)threadIdx.x; j < nbk; j += 256) bh[(size_t)j * gridDim.x + blockIdx.x] = hist[j];
@@ -450,11 +460,18 @@ __global__ __launch_bounds__(256) void nr_part_kernel(const int *__restrict__ pk
     for (int j = (int)threadIdx.x; j < nbk; j += 256) cur[j] = boff[(size_t)j * gridDim.x + blockIdx.x];
     __syncthreads();
     const int p0 = (int)blockIdx.x * kNrChunk, p1 = min(P, p0 + kNrChunk);
-    for (int p = p0 + (int)threadIdx.x; p < p1; p += 256) {
-        const int k = pkey[p];
-        const int pos = atomicAdd(&cur[k >> kNrSubBits], 1);
-        perm1[pos] = p;
-        keys1[pos] = k;
+    constexpr int kU = kNrChunk / 256;
+    int k[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) k[u] = pkey[min(p0 + u * 256 + (int)threadIdx.x, P - 1)];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        const int p = p0 + u * 256 + (int)threadIdx.x;
+        if (p < p1) {
+            const int pos = atomicAdd(&cur[k[u] >> kNrSubBits], 1);
+            perm1[pos] = p;
+            keys1[pos] = k[u];
+        }
     }
 }
 
@@ -546,7 +563,10 @@ __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restr
                                                               const int *__restrict__ keys, int runs,
                                                               int *__restrict__ cnt,
                                                               unsigned long long *__restrict__ cpu,
-                                                              unsigned long long *__restrict__ mem) {
+                                                              unsigned long long *__restrict__ mem, int ablate) {
+#ifndef RSK_ABLATIONS
+    ablate = 0;  // profiling switches exist only in ablation builds
+#endif
     const int w = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
     const int chunk = w / runs, run = w - chunk * runs;
     const int s = chunk * 64 + (int)(threadIdx.x & 63);
@@ -557,7 +577,7 @@ __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restr
     int rk = -1, rc = 0;
     long long rcpu = 0, rmem = 0;
     auto flush = [&]() {
-        if (live && rk >= 0 && rk < N && rc > 0) {
+        if (live && rk >= 0 && rk < N && rc > 0 && !(ablate & 2)) {  // ablate 2: no run flushes
             const size_t o = (size_t)rk * S + s;
             atomicAdd(&cnt[o], rc);
             atomicAdd(&cpu[o], (unsigned long long)rcpu);
@@ -599,7 +619,7 @@ __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restr
                 ++rc;
                 rcpu += c;
                 rmem += m;
-            } else if ((unsigned)a[u] < (unsigned)N) {
+            } else if ((unsigned)a[u] < (unsigned)N && !(ablate & 1)) {  // ablate 1: no off-key atomics
                 const size_t o = (size_t)a[u] * S + s;
                 atomicAdd(&cnt[o], 1);
                 atomicAdd(&cpu[o], (unsigned long long)(long long)c);
@@ -1271,6 +1291,7 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
         int *bh = ctx->work[1].as<int>(), *bsum = bh + nbh;
         ScopedTimer tm(ctx, "node_reduce");
         const size_t hl = (size_t)nbk * 4;
+        static const int nr_ablate = RSK_ABLATION(RSK_ABLATE_NR);
         nr_hist_kernel<<<nblk1, 256, hl, ctx->stream>>>(d_assign, P, S, N, nbk, pkey, bh);
         nr_blocksum_kernel<<<nsb, kNrScanB, 0, ctx->stream>>>(bh, (int)nbh, bsum);
         nr_blockscan_kernel<<<nsb, kNrScanB, 0, ctx->stream>>>(bh, (int)nbh, bsum);
@@ -1278,7 +1299,7 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
         nr_sub_kernel<<<nbk, 256, 0, ctx->stream>>>(perm1, keys1, bh, nblk1, nbk, P, perm, keys);
         node_reduce_seg_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, ctx->stream>>>(
             d_assign, P, S, d_cpu, reinterpret_cast<const long long *>(d_mem), N, perm, keys, runs, d_cnt,
-            reinterpret_cast<unsigned long long *>(d_cs), reinterpret_cast<unsigned long long *>(d_ms));
+            reinterpret_cast<unsigned long long *>(d_cs), reinterpret_cast<unsigned long long *>(d_ms), nr_ablate);
         RSK_HIP(hipGetLastError());
     } else if (PS) {
         ScopedTimer tm(ctx, "node_reduce");
