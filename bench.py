@@ -551,8 +551,9 @@ def main():
                       "phase_ms_per_round": {k: round(v / R, 4) for k, v in res["ms"].items()},
                       "scoring_only_ms_per_round": round(res["ms"]["place"] / R, 4),
                       "moves": int((res["target"] >= 0).sum().item()),
-                      "collectives": "int64 all-reduce N*S cpu + mem partials, int64 MAX all-reduce S, "
-                                     "all-gather S changed slices, int64 all-reduce S cut cost"}
+                      "collectives": "setup: int64 all-reduce of the N*S cpu partials; per round: int64 MAX "
+                                     "all-reduce S, all-gather S changed slices, int64 all-reduce S cut cost; "
+                                     "end: int64 all-reduce of the N*S cpu partials"}
         be.close()
 
     k3_leg = None

@@ -268,7 +268,16 @@ int rsk_pick_max_pod16(rsk_ctx *ctx, const uint16_t *assign16, const int32_t *po
  *   pod when it is in rows [r0, r1), else RSK_TARGET_NO_EVICT; out_evict[s] =
  *   the decoded pod (-1 none) on every rank.  The zero case comes from
  *   rsk_rows_detect's words.
- * rsk_rows_move: rsk_rows_cut_delta then rsk_rows_apply in one launch.        */
+ * rsk_rows_move: rsk_rows_cut_delta then rsk_rows_apply in one launch.  With
+ *   blk (rsk_rows_blk_bytes(N, S) bytes of device memory) it also keeps the
+ *   round's state in step on every rank (the moves are known to all ranks
+ *   after the target all-gather): use_cpu (the usage replica) -= / += the
+ *   pod's CPU, the two changed nodes' hazard flags, the per-(scenario,
+ *   64-node block) maxima in blk, and key_most / zc_cnt / zc_key for the next
+ *   round (rsk_rows_place zeroes them) — no per-round detect pass and no
+ *   all-reduce of the usage partials.
+ * rsk_rows_detect_setup: the blk state, hazard flags, key_most and the zero
+ *   case from a usage array (the loop's round 0).                           */
 int rsk_rows_detect(rsk_ctx *ctx, const int64_t *base, const int64_t *cpu, const int32_t *cap_cpu, int32_t N, int32_t S,
                     int32_t threshold, int32_t *out_use, uint8_t *out_hazard, int64_t *key_most, int32_t *zc_cnt,
                     int64_t *zc_key, uint32_t flags);
@@ -280,7 +289,13 @@ int rsk_rows_place(rsk_rounds *r, const int32_t *assign, int32_t S, const int32_
 int rsk_rows_move(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, const int32_t *rev_ptr,
                   const int32_t *rev_idx, int32_t P, int32_t r0, int32_t r1, int32_t *assign, int32_t S,
                   const int32_t *evict, const int32_t *target, int32_t N, const int32_t *pod_cpu, const int64_t *pod_mem,
-                  int64_t *cpu_part, int64_t *mem_part, uint16_t *shadow16, int64_t *cut_inout, uint32_t flags);
+                  int64_t *cpu_part, int64_t *mem_part, uint16_t *shadow16, int64_t *cut_inout, int32_t *use_cpu,
+                  const int32_t *cap_cpu, int32_t threshold, uint8_t *hazard, void *blk, int64_t *key_most,
+                  int32_t *zc_cnt, int64_t *zc_key, uint32_t flags);
+int64_t rsk_rows_blk_bytes(int32_t N, int32_t S);
+int rsk_rows_detect_setup(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *cap_cpu, int32_t N, int32_t S,
+                          int32_t threshold, uint8_t *out_hazard, void *blk, int64_t *key_most, int32_t *zc_cnt,
+                          int64_t *zc_key, uint32_t flags);
 
 /* ---- µBench workmodel -> relation CSR (host only, no device) -----------------
  * The caller's on-disk format (workmodelC.json).  One

@@ -1084,6 +1084,108 @@ __global__ __launch_bounds__(256) void rows_move_kernel(const int *__restrict__ 
     mem_part[(size_t)t * S + s] += m;
 }
 
+// rows_move_kernel with the usage replica and the detection kept in step (one
+// workgroup per scenario): wave 0 moves the pod (cut delta, assign, the owner's
+// partials and shadow, every rank's usage replica: the round's moves are known
+// to all ranks after the target all-gather), waves 0 / 1 re-reduce the two
+// changed 64-node blocks, then the workgroup re-reduces the scenario's blocks
+// into the next round's most-hazardous key and zero case (rsk_rows_place zeroed
+// them).  Same results as a full detect pass over the updated usage.
+__global__ __launch_bounds__(256) void rows_move_detect_kernel(
+    const int *__restrict__ rp, const int *__restrict__ ci, const int *__restrict__ rvp, const int *__restrict__ rvi,
+    int P, int r0, int r1, int *__restrict__ assign, int S, const int *__restrict__ evict,
+    const int *__restrict__ target, int N, const int *__restrict__ pod_cpu, const long long *__restrict__ pod_mem,
+    long long *__restrict__ cpu_part, long long *__restrict__ mem_part, unsigned short *__restrict__ shadow,
+    long long *__restrict__ cut, int *__restrict__ use, const int *__restrict__ cap, int thr,
+    uint8_t *__restrict__ haz, BlkArgs ba, unsigned long long *__restrict__ most, int *__restrict__ zc_cnt,
+    unsigned long long *__restrict__ zc_key) {
+    __shared__ unsigned long long r64[8];
+    __shared__ int r32[4];
+    __shared__ ScnState st;
+    const int lane = (int)threadIdx.x & 63, w = (int)threadIdx.x >> 6;
+    const int s = (int)blockIdx.x;
+    const int e = evict[s], t = target[s];
+    const bool moved = e >= 0 && e < P && t >= 0 && t < N;  // rows_apply's rule (uniform)
+    int o = -1;
+    if (moved) {
+        int *ae = assign + (size_t)e * S + s;
+        o = *ae;
+        if (w == 0) {
+            int d = 0;
+            if (e >= r0 && e < r1)
+                for (int k = rp[e] + lane; k < rp[e + 1]; k += 64) {
+                    const int q = ci[k];
+                    if (q == e) continue;
+                    const int a = assign[(size_t)q * S + s];
+                    d += (int)(t != a) - (int)(o != a);
+                }
+            for (int k = rvp[e] + lane; k < rvp[e + 1]; k += 64) {
+                const int q = rvi[k];
+                if (q == e || q < r0 || q >= r1) continue;
+                const int a = assign[(size_t)q * S + s];
+                d += (int)(a != t) - (int)(a != o);
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
+            if (lane == 0) {
+                if (d) cut[s] += d;
+                *ae = t;
+                const int c = pod_cpu[e];
+                if ((unsigned)o < (unsigned)N) use[(size_t)o * S + s] -= c;
+                use[(size_t)t * S + s] += c;
+                if (e >= r0 && e < r1) {
+                    if (shadow) shadow[(size_t)(e - r0) * S + s] = (unsigned short)t;
+                    const long long m = pod_mem[e];
+                    if ((unsigned)o < (unsigned)N) {
+                        cpu_part[(size_t)o * S + s] -= c;
+                        mem_part[(size_t)o * S + s] -= m;
+                    }
+                    cpu_part[(size_t)t * S + s] += c;
+                    mem_part[(size_t)t * S + s] += m;
+                }
+            }
+        }
+        __syncthreads();  // the usage update before the blocks read it
+        BlkArgs sb = ba;
+        sb.bm = ba.bm + (size_t)s * ba.NB;
+        sb.bz = ba.bz + (size_t)s * ba.NB;
+        sb.bc = ba.bc + (size_t)s * ba.NB;
+        const int bo = (unsigned)o < (unsigned)N ? o / kBlkNodes : -1, bt = t / kBlkNodes;
+        if (w == 0) blk_update(use, cap, N, S, thr, haz, sb, s, bt, o, t);
+        if (w == 1 && bo >= 0 && bo != bt) blk_update(use, cap, N, S, thr, haz, sb, s, bo, o, t);
+        __syncthreads();
+    }
+    BlkArgs sb = ba;
+    sb.bm = ba.bm + (size_t)s * ba.NB;
+    sb.bz = ba.bz + (size_t)s * ba.NB;
+    sb.bc = ba.bc + (size_t)s * ba.NB;
+    scn_reduce(sb, &st, r64, r32);
+    if (threadIdx.x == 0) {
+        most[s] = st.most;
+        zc_cnt[s] = st.zcnt;
+        zc_key[s] = st.zkey;
+    }
+}
+
+// the scenario maxima from the block arrays (setup), one workgroup per scenario
+__global__ __launch_bounds__(256) void blk_scn_kernel(BlkArgs ba, unsigned long long *__restrict__ most,
+                                                      int *__restrict__ zc_cnt, unsigned long long *__restrict__ zc_key) {
+    __shared__ unsigned long long r64[8];
+    __shared__ int r32[4];
+    __shared__ ScnState st;
+    const int s = (int)blockIdx.x;
+    BlkArgs sb = ba;
+    sb.bm = ba.bm + (size_t)s * ba.NB;
+    sb.bz = ba.bz + (size_t)s * ba.NB;
+    sb.bc = ba.bc + (size_t)s * ba.NB;
+    scn_reduce(sb, &st, r64, r32);
+    if (threadIdx.x == 0) {
+        most[s] = st.most;
+        zc_cnt[s] = st.zcnt;
+        zc_key[s] = st.zkey;
+    }
+}
+
 }  // namespace
 }  // namespace rsk
 
@@ -1496,20 +1598,66 @@ int rsk_rows_place(rsk_rounds *r, const int32_t *assign, int32_t S, const int32_
                        reinterpret_cast<unsigned long long *>(zc_key), r0, r1);
 }
 
+int64_t rsk_rows_blk_bytes(int32_t N, int32_t S) {
+    if (N <= 0 || S <= 0) return 0;
+    return (int64_t)S * ceil_div(N, kBlkNodes) * 20;
+}
+
+static BlkArgs blk_args(void *blk, int N, int S) {
+    BlkArgs ba;
+    ba.NB = (int)ceil_div(N, kBlkNodes);
+    const size_t nbs = (size_t)S * ba.NB;
+    ba.bm = static_cast<unsigned long long *>(blk);
+    ba.bz = ba.bm + nbs;
+    ba.bc = reinterpret_cast<int *>(ba.bz + nbs);
+    return ba;
+}
+
+int rsk_rows_detect_setup(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *cap_cpu, int32_t N, int32_t S,
+                          int32_t threshold, uint8_t *out_hazard, void *blk, int64_t *key_most, int32_t *zc_cnt,
+                          int64_t *zc_key, uint32_t flags) {
+    RSK_TRY(activate(ctx));
+    RSK_CHECK((flags & RSK_F_DEVICE) && use_cpu && cap_cpu && out_hazard && blk && key_most && zc_cnt && zc_key &&
+                  N > 0 && S > 0 && (int64_t)N * S < INT32_MAX,
+              "rsk_rows_detect_setup: device pointers and N, S > 0 required");
+    const BlkArgs ba = blk_args(blk, N, S);
+    ScopedTimer tm(ctx, "rows_detect");
+    const int64_t waves = (int64_t)ba.NB * ceil_div(S, 64);
+    blk_detect_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, ctx->stream>>>(use_cpu, cap_cpu, N, S, threshold,
+                                                                            out_hazard, ba);
+    blk_scn_kernel<<<(unsigned)S, 256, 0, ctx->stream>>>(ba, reinterpret_cast<unsigned long long *>(key_most), zc_cnt,
+                                                         reinterpret_cast<unsigned long long *>(zc_key));
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
+}
+
 int rsk_rows_move(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, const int32_t *rev_ptr,
                   const int32_t *rev_idx, int32_t P, int32_t r0, int32_t r1, int32_t *assign, int32_t S,
                   const int32_t *evict, const int32_t *target, int32_t N, const int32_t *pod_cpu, const int64_t *pod_mem,
-                  int64_t *cpu_part, int64_t *mem_part, uint16_t *shadow16, int64_t *cut_inout, uint32_t flags) {
+                  int64_t *cpu_part, int64_t *mem_part, uint16_t *shadow16, int64_t *cut_inout, int32_t *use_cpu,
+                  const int32_t *cap_cpu, int32_t threshold, uint8_t *hazard, void *blk, int64_t *key_most,
+                  int32_t *zc_cnt, int64_t *zc_key, uint32_t flags) {
     RSK_TRY(activate(ctx));
     RSK_CHECK((flags & RSK_F_DEVICE) && row_ptr && col_idx && rev_ptr && rev_idx && assign && evict && target && pod_cpu &&
                   pod_mem && cpu_part && mem_part && cut_inout && P > 0 && S > 0 && N > 0 && 0 <= r0 && r0 <= r1 &&
                   r1 <= P,
               "rsk_rows_move: device pointers and rows [%d, %d) of P=%d required", r0, r1, P);
     ScopedTimer tm(ctx, "rows_move");
-    rows_move_kernel<<<(unsigned)ceil_div(S, 4), 256, 0, ctx->stream>>>(
-        row_ptr, col_idx, rev_ptr, rev_idx, P, r0, r1, assign, S, evict, target, N, pod_cpu,
-        reinterpret_cast<const long long *>(pod_mem), reinterpret_cast<long long *>(cpu_part),
-        reinterpret_cast<long long *>(mem_part), shadow16, reinterpret_cast<long long *>(cut_inout));
+    if (blk) {  // the usage replica and the detection kept in step
+        RSK_CHECK(use_cpu && cap_cpu && hazard && key_most && zc_cnt && zc_key,
+                  "rsk_rows_move: the detect state (use, cap, hazard, keys) is required with blk");
+        rows_move_detect_kernel<<<(unsigned)S, 256, 0, ctx->stream>>>(
+            row_ptr, col_idx, rev_ptr, rev_idx, P, r0, r1, assign, S, evict, target, N, pod_cpu,
+            reinterpret_cast<const long long *>(pod_mem), reinterpret_cast<long long *>(cpu_part),
+            reinterpret_cast<long long *>(mem_part), shadow16, reinterpret_cast<long long *>(cut_inout), use_cpu,
+            cap_cpu, threshold, hazard, blk_args(blk, N, S), reinterpret_cast<unsigned long long *>(key_most), zc_cnt,
+            reinterpret_cast<unsigned long long *>(zc_key));
+    } else {
+        rows_move_kernel<<<(unsigned)ceil_div(S, 4), 256, 0, ctx->stream>>>(
+            row_ptr, col_idx, rev_ptr, rev_idx, P, r0, r1, assign, S, evict, target, N, pod_cpu,
+            reinterpret_cast<const long long *>(pod_mem), reinterpret_cast<long long *>(cpu_part),
+            reinterpret_cast<long long *>(mem_part), shadow16, reinterpret_cast<long long *>(cut_inout));
+    }
     RSK_HIP(hipGetLastError());
     return RSK_OK;
 }

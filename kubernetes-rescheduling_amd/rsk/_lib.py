@@ -81,7 +81,11 @@ SIGNATURES = {
     "rsk_rows_place": (C.c_int, [_vp, _vp, C.c_int32, _vp, _vp, _vp, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, _vp,
                                  _vp, _vp, _vp, C.c_uint32]),
     "rsk_rows_move": (C.c_int, [_vp, _vp, _vp, _vp, _vp, C.c_int32, C.c_int32, C.c_int32, _vp, C.c_int32, _vp, _vp,
-                                C.c_int32, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint32]),
+                                C.c_int32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int32, _vp, _vp, _vp, _vp, _vp,
+                                C.c_uint32]),
+    "rsk_rows_blk_bytes": (C.c_int64, [C.c_int32, C.c_int32]),
+    "rsk_rows_detect_setup": (C.c_int, [_vp, _vp, _vp, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, _vp, _vp, _vp,
+                                        C.c_uint32]),
     "rsk_workmodel_parse": (C.c_int, [C.c_char_p, C.c_int64, C.POINTER(_vp)]),
     "rsk_workmodel_load": (C.c_int, [C.c_char_p, C.POINTER(_vp)]),
     "rsk_workmodel_sizes": (C.c_int, [_vp, _i32p, _i64p, _i64p]),

@@ -345,19 +345,25 @@ class LibrskRoundsBackend:
 
     # ---- the fused round (RowShardedRounds.run when self.fused) ----
     def round_buffers(self, N, S):
-        """Per-run device buffers of the fused round.  The packed keys start at
-        zero and rows_place leaves them zero for the next round."""
+        """Per-run device buffers of the fused round.  The eviction key starts at
+        zero and rows_place leaves it zero for the next round; the detect state
+        (usage replica, hazard flags, block maxima, most-hazardous key, zero
+        case) is set up once and kept in step by rows_move."""
         import torch
         z = lambda n, dt: torch.zeros(n, dtype=dt, device=self.dev)  # noqa: E731
+        nb = int(self.ctx.lib.rsk_rows_blk_bytes(N, S))
         return {"use": z(N * S, torch.int32), "haz": z(N * S, torch.uint8), "most": z(S, torch.int64),
-                "key": z(S, torch.int64), "zc_cnt": z(S, torch.int32), "zc_key": z(S, torch.int64)}
+                "key": z(S, torch.int64), "zc_cnt": z(S, torch.int32), "zc_key": z(S, torch.int64),
+                "blk": z(max(nb, 8), torch.uint8)}
 
-    def rows_detect(self, base, cpu, cap, N, S, threshold, b):
+    def rows_detect_setup(self, use, cap, N, S, threshold, b):
+        """b["use"] = use (the replica), and the detect state from it."""
         self._sync()
-        self._check(self.ctx.lib.rsk_rows_detect(self.ctx.handle, base.data_ptr(), cpu.data_ptr(), cap.data_ptr(), N,
-                                                 S, threshold, b["use"].data_ptr(), b["haz"].data_ptr(),
-                                                 b["most"].data_ptr(), b["zc_cnt"].data_ptr(),
-                                                 b["zc_key"].data_ptr(), self._F))
+        b["use"].copy_(use)
+        self._check(self.ctx.lib.rsk_rows_detect_setup(self.ctx.handle, b["use"].data_ptr(), cap.data_ptr(), N, S,
+                                                       threshold, b["haz"].data_ptr(), b["blk"].data_ptr(),
+                                                       b["most"].data_ptr(), b["zc_cnt"].data_ptr(),
+                                                       b["zc_key"].data_ptr(), self._F))
         self._sync()
 
     def rows_pick(self, rows, q, S, r0, pod_cpu, b):
@@ -379,14 +385,17 @@ class LibrskRoundsBackend:
         self._sync()
         return ev, tg
 
-    def rows_move(self, assign, S, evict, target, r0, r1, N, pod_cpu, pod_mem, cpu_part, mem_part, shadow, cut):
+    def rows_move(self, assign, S, evict, target, r0, r1, N, pod_cpu, pod_mem, cpu_part, mem_part, shadow, cut,
+                  cap, threshold, b):
         self._sync()
         self._check(self.ctx.lib.rsk_rows_move(self.ctx.handle, self.row_ptr.data_ptr(), self.col_idx.data_ptr(),
                                                self.rev_ptr.data_ptr(), self.rev_idx.data_ptr(), self.P, r0, r1,
                                                assign.data_ptr(), S, evict.data_ptr(), target.data_ptr(), N,
                                                pod_cpu.data_ptr(), pod_mem.data_ptr(), cpu_part.data_ptr(),
                                                mem_part.data_ptr(), None if shadow is None else shadow.data_ptr(),
-                                               cut.data_ptr(), self._F))
+                                               cut.data_ptr(), b["use"].data_ptr(), cap.data_ptr(), threshold,
+                                               b["haz"].data_ptr(), b["blk"].data_ptr(), b["most"].data_ptr(),
+                                               b["zc_cnt"].data_ptr(), b["zc_key"].data_ptr(), self._F))
         self._sync()
 
     def close(self):
@@ -553,31 +562,30 @@ class RowShardedRounds:
                 "cut": torch.stack(cuts) if cuts else empty.to(torch.int64), "use": use_final, "ms": t}
 
     def _run_fused(self, assign, base, cap, pc32, pm64, lp_cpu, lp_mem, cut_local, shadow, N, S, R, threshold, t):
-        """The rounds of ``run`` with the backend's fused launches: detect (usage
-        = base + the summed partials, hazards, the most-loaded node and the zero
-        case in one pass), the eviction scan straight to the packed all-reduce
-        key, CAR of this rank's evicted pods (the key decoded in the kernel; the
-        keys left zero for the next round), then cut delta + move in one launch.
-        Same collectives and results as the unfused loop."""
+        """The rounds of ``run`` with the backend's fused launches.  Round 0's
+        usage (base + the all-reduced partials) seeds a usage replica on every
+        rank with its hazard flags, per-(scenario, 64-node block) maxima, most
+        hazardous node and zero case (``rsk_rows_detect_setup``); every round
+        then: the eviction scan straight to the packed all-reduce key, CAR of
+        this rank's evicted pods (the key decoded in the kernel), the target
+        all-gather, and the move, which updates the replica and re-reduces the
+        two changed blocks on every rank (the moves are known to all ranks), so
+        no round re-reads the N x S usage or all-reduces the partials.  Same
+        results as the unfused loop."""
         import time
+        import torch
         be, dev = self.be, assign.device
         r0, r1 = self.shard.r0, self.shard.r1
         b = be.round_buffers(N, S)
         rows = shadow if shadow is not None else assign[r0 * S:r1 * S]
         multi = _multi_rank()
+        c = time.perf_counter()
+        cpu0 = lp_cpu.clone()
+        allreduce_(cpu0, "sum", self.group)
+        be.rows_detect_setup((base + cpu0).to(torch.int32), cap, N, S, threshold, b)
+        t["setup"] += (time.perf_counter() - c) * 1e3
         evs, tgs, cuts = [], [], []
         for _ in range(R):
-            c = time.perf_counter()
-            if multi:
-                cpu, mem = lp_cpu.clone(), lp_mem.clone()
-                allreduce_(cpu, "sum", self.group)
-                allreduce_(mem, "sum", self.group)
-            else:
-                cpu = lp_cpu
-            t["monitor"] += (time.perf_counter() - c) * 1e3
-            c = time.perf_counter()
-            be.rows_detect(base, cpu, cap, N, S, threshold, b)
-            t["detect"] += (time.perf_counter() - c) * 1e3
             c = time.perf_counter()
             be.rows_pick(rows, r1 - r0, S, r0, pc32, b)
             allreduce_(b["key"], "max", self.group)
@@ -590,7 +598,8 @@ class RowShardedRounds:
                 target = allgather(target, self.group).max(dim=0).values.contiguous()
             t["exchange"] += (time.perf_counter() - c) * 1e3
             c = time.perf_counter()
-            be.rows_move(assign, S, evict, target, r0, r1, N, pc32, pm64, lp_cpu, lp_mem, shadow, cut_local)
+            be.rows_move(assign, S, evict, target, r0, r1, N, pc32, pm64, lp_cpu, lp_mem, shadow, cut_local, cap,
+                         threshold, b)
             t["update"] += (time.perf_counter() - c) * 1e3
             c = time.perf_counter()
             cut = cut_local.clone()
