@@ -767,7 +767,6 @@ struct PersistArgs {
     const int *row_ptr, *col, *pod_cpu, *cap;
     int *assign, *use;
     uint8_t *haz;
-    int *ev_cur;                      // [S] the round's eviction (car_move_one reads evict[s])
     int *zc_cnt;                      // [S] the scenario's zero case, as car_move_one reads it
     unsigned long long *zc_key;
     const int *off, *pod;             // the base nodes' pod lists
@@ -1327,11 +1326,10 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         PersistArgs pa;
         pa.ba.NB = (int)ceil_div(N, kBlkNodes);
         const size_t nbs = (size_t)S * pa.ba.NB;
-        RSK_TRY(r->blk.reserve(nbs * 20 + (size_t)S * 4));
+        RSK_TRY(r->blk.reserve(nbs * 20));
         pa.ba.bm = r->blk.as<unsigned long long>();
         pa.ba.bz = pa.ba.bm + nbs;
         pa.ba.bc = reinterpret_cast<int *>(pa.ba.bz + nbs);
-        pa.ev_cur = pa.ba.bc + nbs;
         pa.row_ptr = r->row_ptr.as<int>();
         pa.col = r->col.as<int>();
         pa.pod_cpu = r->pod_cpu.as<int>();
