@@ -200,7 +200,9 @@ int rsk_cut_cost_rows(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_i
  *                       RSK_TARGET_NO_EVICT (-3) when nothing was evicted.
  * assign[P*S] and use_cpu[N*S] are updated in place.  Any row degree (the
  * evicted pod's count table lives in the LDS, or in global work areas when its
- * distinct nodes overflow it).
+ * distinct nodes overflow it).  Scenarios are independent: after a per-call
+ * setup (pod lists, hazard flags, per-64-node-block maxima) one launch runs
+ * every round, a workgroup per scenario.
  * rsk_rounds_create deduplicates the CSR (self edges dropped, main.py:73) and
  * uploads it with pod_cpu[P] (millicores).                                   */
 #define RSK_TARGET_NO_EVICT (-3)
