@@ -41,6 +41,8 @@ extern "C" {
 #define RSK_ERCCL 4        /* reserved: collective error */
 
 #define RSK_F_DEVICE 1u    /* all array pointers are device pointers; async */
+#define RSK_F_TILED 4u     /* rsk_car_plan_execute: the tile / side kernels even for a small batch
+                              (S <= 4, Q*S <= 65536, no scores), which otherwise runs in one launch */
 
 #define RSK_TARGET_NONE (-1)
 #define RSK_TARGET_NO_CANDIDATE (-2)

@@ -875,6 +875,9 @@ struct rsk_car_plan {
     int side_dmax[kNumSide] = {};
     // per-execute workspace
     DevBuf nodekey, code, zc;
+    // the deduplicated CSR and the row map on the device (the one-launch path of small batches)
+    DevBuf drp, dci, drows;
+    int ddmax = 0;
     // the inputs, kept for the N >= kPackMaxN variant (built on first use)
     std::vector<int32_t> h_row_ptr, h_col_idx, h_rows;
     bool has_rows = false;
@@ -889,6 +892,9 @@ struct rsk_car_plan {
         hcol.release();
         side_items.release();
         side_scratch.release();
+        drp.release();
+        dci.release();
+        drows.release();
         big_items.release();
         pcol.release();
         nodekey.release();
@@ -1148,6 +1154,17 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
         nb.erase(std::remove(nb.begin(), nb.end(), p), nb.end());
         ci.insert(ci.end(), nb.begin(), nb.end());
         rp[p + 1] = (int)ci.size();
+    }
+    {  // the deduplicated CSR for the one-launch path (rsk_rounds.hip car_direct_kernel)
+        RSK_TRY(plan->drp.reserve(rp.size() * 4));
+        RSK_TRY(plan->dci.reserve(std::max<size_t>(1, ci.size()) * 4));
+        RSK_HIP(hipMemcpy(plan->drp.ptr, rp.data(), rp.size() * 4, hipMemcpyHostToDevice));
+        if (!ci.empty()) RSK_HIP(hipMemcpy(plan->dci.ptr, ci.data(), ci.size() * 4, hipMemcpyHostToDevice));
+        if (rows && Q > 0) {
+            RSK_TRY(plan->drows.reserve((size_t)Q * 4));
+            RSK_HIP(hipMemcpy(plan->drows.ptr, rows, (size_t)Q * 4, hipMemcpyHostToDevice));
+        }
+        for (int p = 0; p < P; ++p) plan->ddmax = std::max(plan->ddmax, rp[p + 1] - rp[p]);
     }
     const std::vector<int> order = locality_order(P, rp, ci);
     std::vector<int> pos(P);
@@ -1589,6 +1606,24 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     RSK_TRY(stage_out(ctx, 4, out_target, QS * 4, dev, reinterpret_cast<void **>(&d_target)));
     if (out_score) RSK_TRY(stage_out(ctx, 5, out_score, QS * 4, dev, reinterpret_cast<void **>(&d_score)));
 
+    // small batches: one launch (a workgroup per (row, scenario), exact rem from
+    // cap / use, no node codes); the latency-bound case, config 2
+    static const bool direct_on = RSK_KNOB(RSK_CAR_DIRECT, 1) != 0;
+    if (direct_on && !(flags & RSK_F_TILED) && S <= 4 && QS <= 65536 && !d_score) {
+        {
+            ScopedTimer tm(ctx, "car_direct");
+            RSK_TRY(launch_car_direct(ctx->stream, plan->drp.as<int>(), plan->dci.as<int>(),
+                                      plan->drows.ptr ? plan->drows.as<int>() : nullptr, plan->Q, d_assign, d_use,
+                                      d_cap, d_haz, S, N, plan->ddmax, d_target, &plan->side_scratch));
+        }
+        if (!dev) {
+            RSK_TRY(copy_back(ctx, out_target, d_target, QS * 4, false));
+            RSK_HIP(hipStreamSynchronize(ctx->stream));
+            for (size_t k = 0; k < QS; ++k)
+                if (out_target[k] == RSK_TARGET_NO_CANDIDATE) return RSK_NO_CANDIDATE;
+        }
+        return RSK_OK;
+    }
     int *d_key = nullptr;
     unsigned short *d_code = nullptr;
     if (!compact) {

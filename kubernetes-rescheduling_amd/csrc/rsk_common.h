@@ -150,4 +150,10 @@ int launch_pick_keys(hipStream_t stream, const int *assign, const int *pod_cpu, 
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// One-launch CAR of a small batch (rsk_rounds.hip): rows [0, Q) of the
+// deduplicated CSR rp / ci (pods rows[i], or i), S scenarios; targets only.
+int launch_car_direct(hipStream_t st, const int *rp, const int *ci, const int *rows, int Q, const int *assign,
+                      const int *use, const int *cap, const uint8_t *haz, int S, int N, int dmax, int *out_target,
+                      DevBuf *scratch);
+
 }  // namespace rsk

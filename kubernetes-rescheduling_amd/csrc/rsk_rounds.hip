@@ -848,6 +848,34 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
     }
 }
 
+// ---- one-launch CAR for small batches (rsk_car_plan_execute, S <= 4) ----
+// A workgroup per (row, scenario) scores the row with car_move_one (lanes =
+// neighbours, the LDS hash of their nodes, exact remaining CPU from cap / use):
+// no node-code pass, no tiles, no side launch — the latency-bound case
+// (config 2: 2k rows x S = 1) in one launch.  Same rule as every CAR path
+// (rescheduling.py:183-214, the deduplicated rows without self edges).
+template <bool kGlobal>
+__global__ __launch_bounds__(kMoveThreads) void car_direct_kernel(const int *__restrict__ rp, const int *__restrict__ ci,
+                                                                  const int *__restrict__ rows, int Q,
+                                                                  const int *__restrict__ assign,
+                                                                  const int *__restrict__ use,
+                                                                  const int *__restrict__ cap,
+                                                                  const uint8_t *__restrict__ haz, int S, int N, int H,
+                                                                  int *__restrict__ out_target,
+                                                                  unsigned *__restrict__ gtab) {
+    extern __shared__ __attribute__((aligned(16))) unsigned lds[];
+    unsigned *tab = kGlobal ? gtab + (size_t)blockIdx.x * (size_t)(2 * H + 8) : lds;
+    const int units = Q * S;
+    for (int u = (int)blockIdx.x; u < units; u += (int)gridDim.x) {
+        const int i = u / S, s = u - i * S;
+        const int p = rows ? rows[i] : i;
+        car_move_one<kGlobal>(rp, ci, nullptr, const_cast<int *>(assign), const_cast<int *>(use), cap, haz, nullptr,
+                              s, S, N, H, 0, out_target + (size_t)i * S, nullptr, tab, nullptr, nullptr, nullptr,
+                              nullptr, nullptr, 0, INT_MAX, DevLists(), p);
+        move_sync<kGlobal>();  // the hash is free before the next unit clears it
+    }
+}
+
 // Row-sharded loop glue: one thread per scenario.
 __global__ void rows_evict_key_kernel(const int *__restrict__ local_pod, int S, int r0, const int *__restrict__ pod_cpu,
                                       long long *__restrict__ key) {
@@ -1186,6 +1214,34 @@ __global__ __launch_bounds__(256) void blk_scn_kernel(BlkArgs ba, unsigned long 
 }
 
 }  // namespace
+
+int launch_car_direct(hipStream_t st, const int *rp, const int *ci, const int *rows, int Q, const int *assign,
+                      const int *use, const int *cap, const uint8_t *haz, int S, int N, int dmax, int *out_target,
+                      DevBuf *scratch) {
+    if (Q <= 0) return RSK_OK;
+    int H = 1;
+    while (H < std::max(2, 2 * std::min(dmax, N))) H <<= 1;
+    const size_t bytes = ((size_t)2 * H + 8) * 4;
+    const int64_t units = (int64_t)Q * S;
+    RSK_CHECK(units < INT32_MAX, "direct grid too large");
+    if (bytes <= 160 * 1024) {
+        const int grid = (int)std::min<int64_t>(units, 65536);
+        if (bytes > 64 * 1024)
+            RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&car_direct_kernel<false>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+        car_direct_kernel<false><<<dim3((unsigned)grid), dim3(kMoveThreads), bytes, st>>>(
+            rp, ci, rows, Q, assign, use, cap, haz, S, N, H, out_target, nullptr);
+    } else {  // a table beyond the LDS: global work areas, one per resident workgroup
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>({units, 1024, (int64_t)((256u << 20) / bytes)}));
+        RSK_CHECK(scratch, "direct CAR: no scratch for a %zu-B table", bytes);
+        RSK_TRY(scratch->reserve((size_t)grid * bytes));
+        car_direct_kernel<true><<<dim3((unsigned)grid), dim3(kMoveThreads), 0, st>>>(
+            rp, ci, rows, Q, assign, use, cap, haz, S, N, H, out_target, scratch->as<unsigned>());
+    }
+    RSK_HIP(hipGetLastError());
+    return RSK_OK;
+}
+
 }  // namespace rsk
 
 using namespace rsk;

@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("RSK_LIB", os.path.join(HERE, "librsk.so"))
 
 RSK_OK, RSK_NO_CANDIDATE, RSK_EINVAL, RSK_EHIP, RSK_ERCCL = 0, 1, 2, 3, 4
 RSK_F_DEVICE = 1
+RSK_F_TILED = 4
 TARGET_NONE, TARGET_NO_CANDIDATE, TARGET_NO_EVICT = -1, -2, -3
 
 _i32p = C.POINTER(C.c_int32)

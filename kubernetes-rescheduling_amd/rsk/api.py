@@ -12,7 +12,7 @@ from typing import Optional
 
 import numpy as np
 
-from ._lib import (RSK_F_DEVICE, Context, check, default_context, load_library, ptr)
+from ._lib import (RSK_F_DEVICE, RSK_F_TILED, Context, check, default_context, load_library, ptr)
 
 _I32 = np.int32
 
@@ -69,11 +69,13 @@ class CarPlan:
             pass
 
     def execute(self, assign, S, cap_cpu, use_cpu, hazard, N, out_target=None, out_score=None,
-                device: bool = False, want_score: bool = False):
+                device: bool = False, want_score: bool = False, tiled: bool = False):
+        """tiled: the tile / side kernels even for a small batch (RSK_F_TILED)."""
+        fl = RSK_F_TILED if tiled else 0
         if device:
             check(self.ctx.lib.rsk_car_plan_execute(self.handle, ptr(assign), S, ptr(cap_cpu), ptr(use_cpu),
                                                     ptr(hazard), N, ptr(out_target), ptr(out_score),
-                                                    RSK_F_DEVICE))
+                                                    RSK_F_DEVICE | fl))
             return out_target, out_score
         assign, cap_cpu, use_cpu = _c(assign, _I32), _c(cap_cpu, _I32), _c(use_cpu, _I32)
         hazard = _c(hazard, np.uint8)
@@ -82,15 +84,16 @@ class CarPlan:
         tgt = np.empty(self.Q * S, _I32) if out_target is None else out_target
         sc = (np.empty(self.Q * S, _I32) if out_score is None else out_score) if (want_score or out_score is not None) else None
         check(self.ctx.lib.rsk_car_plan_execute(self.handle, ptr(assign), S, ptr(cap_cpu), ptr(use_cpu), ptr(hazard),
-                                                N, ptr(tgt), ptr(sc), 0), allow_no_candidate=True)
+                                                N, ptr(tgt), ptr(sc), fl), allow_no_candidate=True)
         return tgt, sc
 
 
-def car_place(row_ptr, col_idx, assign, S, cap_cpu, use_cpu, hazard, N, rows=None, ctx=None, want_score=False):
+def car_place(row_ptr, col_idx, assign, S, cap_cpu, use_cpu, hazard, N, rows=None, ctx=None, want_score=False,
+              tiled=False):
     """One-shot CAR scoring (host arrays): returns (target[Q*S], score or None)."""
     plan = CarPlan(row_ptr, col_idx, rows=rows, ctx=ctx)
     try:
-        return plan.execute(assign, S, cap_cpu, use_cpu, hazard, N, want_score=want_score)
+        return plan.execute(assign, S, cap_cpu, use_cpu, hazard, N, want_score=want_score, tiled=tiled)
     finally:
         plan.close()
 

@@ -52,11 +52,14 @@ def test_config2_2k64_s1_all_rows(ctx, synth_golden):
     g = synth_golden["2k64"]
     c = synth.make_cluster(2_000, 64, S=1, seed=0)
     plan = api.CarPlan(c.row_ptr, c.col_idx, ctx=ctx)
-    tgt, _ = plan.execute(c.assign, 1, c.cap_cpu, c.use_cpu, c.hazard, c.N)
+    tgt, _ = plan.execute(c.assign, 1, c.cap_cpu, c.use_cpu, c.hazard, c.N)   # one launch (small batch)
+    tt, _ = plan.execute(c.assign, 1, c.cap_cpu, c.use_cpu, c.hazard, c.N, tiled=True)   # tiles + side rows
     plan.close()
     assert _all_cells(c, 1, tgt.reshape(c.P, 1), "config 2") == 2_000
+    assert _all_cells(c, 1, tt.reshape(c.P, 1), "config 2 tiled") == 2_000
     g0 = [sc for sc in g["scenarios"] if sc["s"] == 0][0]
     assert tgt[g0["pods"]].tolist() == g0["car_target"]
+    assert tt[g0["pods"]].tolist() == g0["car_target"]
 
 
 def test_config3_headline_s4096(ctx, synth_golden):

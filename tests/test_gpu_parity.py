@@ -880,3 +880,37 @@ def test_car_big_side_rows_plan_reuse(ctx):
         bad = np.nonzero(tgt != exp)[0]
         assert bad.size == 0, f"execute {k}: {bad.size} cells differ, first row {bad[0] // S}"
     plan.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S", [1, 3, 4])
+def test_car_direct_small_batches(ctx, S):
+    """The one-launch path of small batches (S <= 4, Q*S <= 65536, no scores
+    requested: a workgroup per (row, scenario)) against the oracle: rows with
+    duplicates and a self edge, unassigned pods, an all-hazard scenario (no
+    candidate), a row subset in shuffled order, and a hub row whose distinct
+    nodes overflow an LDS table (global work areas)."""
+    from oracle import oracle as orc
+    from rsk import api
+    rng = np.random.default_rng(40 + S)
+    P, N = 12000, 10000
+    rows_l = [rng.integers(0, P, int(rng.integers(0, 6))).tolist() for _ in range(P)]
+    rows_l[0] = rng.choice(P, 9000, replace=False).tolist()   # ~5,900 distinct nodes: beyond the LDS
+    rows_l[1] = [1, 1, 2, 2, 3]                               # a self edge and duplicates
+    rp = np.zeros(P + 1, np.int32)
+    rp[1:] = np.cumsum([len(r) for r in rows_l])
+    ci = np.array([q for r in rows_l for q in r], np.int32)
+    assign = rng.integers(0, N, P * S).astype(np.int32)
+    assign[rng.random(P * S) < 0.01] = -1
+    cap = np.full(N, 50000, np.int32)
+    use = rng.integers(0, 60000, N * S).astype(np.int32)
+    haz = (rng.random(N * S) < 0.2).astype(np.uint8)
+    haz.reshape(N, S)[:, S - 1] = 1                           # the last scenario: every node hazardous
+    rpd, cid = _dedup_csr(rp, ci)
+    subset = rng.permutation(P)[:7000].astype(np.int32)
+    for rows in (None, subset):
+        tgt, _ = api.car_place(rp, ci, assign, S, cap, use, haz, N, rows=rows, ctx=ctx)
+        ot, _ = orc.car(rpd, cid, assign, S, cap, use, haz, N, rows=rows)
+        bad = np.nonzero(tgt != ot)[0]
+        assert bad.size == 0, f"S={S}: {bad.size} differ, first {bad[0]}: gpu {tgt[bad[0]]} oracle {ot[bad[0]]}"
+        assert (tgt.reshape(-1, S)[:, S - 1] == -2).all()     # no candidate anywhere in the last scenario
