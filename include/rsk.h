@@ -259,19 +259,14 @@ int rsk_pick_max_pod16(rsk_ctx *ctx, const uint16_t *assign16, const int32_t *po
 /* The row-sharded round fused into four launches (device pointers, RSK_F_DEVICE
  * required).  key_most / key_evict / zc_cnt / zc_key [S] are zero before the
  * first round; rsk_rows_place leaves them zero for the next one.
- * rsk_rows_detect: the monitor's usage out_use = (int32)(base + cpu) (the
- *   summed per-node partials, nodemonitor.py's read-back), get_resource_usage.py:
- *   37's pct, harzard_detect.py:3-27's hazard flags, key_most[s] = the packed
- *   (pct, ~node) max (the most hazardous node, first on ties) and the zero
- *   case per scenario (non-hazard count, max (cap - use, ~node)).
  * rsk_rows_pick: delete_replaced_pod.py:41-61 over this rank's q rows (int32
  *   assign rows or the u16 shadow, elem_bytes 4 / 2; pod r0 + p): key_evict[s]
  *   = atomic max of pod_cpu[g] << 32 | (2^32 - 1 - g) over its pods on the
  *   most hazardous node (0: none) -- the MAX all-reduce key.
  * rsk_rows_place: the CAR target (rescheduling.py:174-218) of the reduced key's
  *   pod when it is in rows [r0, r1), else RSK_TARGET_NO_EVICT; out_evict[s] =
- *   the decoded pod (-1 none) on every rank.  The zero case comes from
- *   rsk_rows_detect's words.
+ *   the decoded pod (-1 none) on every rank.  The zero case comes from the
+ *   detect words rsk_rows_detect_setup / rsk_rows_move keep.
  * rsk_rows_move: rsk_rows_cut_delta then rsk_rows_apply in one launch.  With
  *   blk (rsk_rows_blk_bytes(N, S) bytes of device memory) it also keeps the
  *   round's state in step on every rank (the moves are known to all ranks
@@ -282,9 +277,6 @@ int rsk_pick_max_pod16(rsk_ctx *ctx, const uint16_t *assign16, const int32_t *po
  *   all-reduce of the usage partials.
  * rsk_rows_detect_setup: the blk state, hazard flags, key_most and the zero
  *   case from a usage array (the loop's round 0).                           */
-int rsk_rows_detect(rsk_ctx *ctx, const int64_t *base, const int64_t *cpu, const int32_t *cap_cpu, int32_t N, int32_t S,
-                    int32_t threshold, int32_t *out_use, uint8_t *out_hazard, int64_t *key_most, int32_t *zc_cnt,
-                    int64_t *zc_key, uint32_t flags);
 int rsk_rows_pick(rsk_ctx *ctx, const void *rows, int32_t elem_bytes, int32_t q, int32_t S, int32_t r0,
                   const int32_t *pod_cpu, const int64_t *key_most, int64_t *key_evict, uint32_t flags);
 int rsk_rows_place(rsk_rounds *r, const int32_t *assign, int32_t S, const int32_t *cap_cpu, const int32_t *use_cpu,

@@ -563,7 +563,8 @@ __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restr
                                                               const int *__restrict__ keys, int runs,
                                                               int *__restrict__ cnt,
                                                               unsigned long long *__restrict__ cpu,
-                                                              unsigned long long *__restrict__ mem, int ablate) {
+                                                              unsigned long long *__restrict__ mem, int ablate,
+                                                              int run_len) {
 #ifndef RSK_ABLATIONS
     ablate = 0;  // profiling switches exist only in ablation builds
 #endif
@@ -572,7 +573,7 @@ __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restr
     const int s = chunk * 64 + (int)(threadIdx.x & 63);
     if (chunk * 64 >= S) return;
     const bool live = s < S;
-    const int j0 = run * kNrRun, j1 = min(P, j0 + kNrRun);
+    const int j0 = run * run_len, j1 = min(P, j0 + run_len);
     const cint_ptr cperm = const_ptr(perm), ckeys = const_ptr(keys), ccpu = const_ptr(pod_cpu);
     int rk = -1, rc = 0;
     long long rcpu = 0, rmem = 0;
@@ -992,7 +993,7 @@ int launch_detect(hipStream_t stream, const int *pct, int N, int S, int threshol
 // arrive zeroed (the move kernel clears its scenario's words after use).
 int launch_detect_use_keys(hipStream_t stream, const int *use, const int *cap, int N, int S, int threshold,
                            uint8_t *hazard, unsigned long long *key, int *zc_cnt, unsigned long long *zc_key) {
-    // ~512 workgroups of 64 scenarios x 16 waves (rsk_rows_detect's geometry):
+    // ~512 workgroups of 64 scenarios x 16 waves (the persistent loops' workgroup shape):
     // one atomic per scenario word per workgroup
     static const int w16 = RSK_KNOB(RSK_DET_W16, 1);
     static const int target = std::max(1, RSK_KNOB(RSK_DET_BLOCKS, 512));
@@ -1278,7 +1279,8 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
     if (d_ms) RSK_HIP(hipMemsetAsync(d_ms, 0, NS * 8, ctx->stream));
     const int nbk = (N >> kNrSubBits) + 1;  // key >> kNrSubBits buckets (keys 0..N)
     if (PS && S >= 32 && nbk <= kNrMaxBuckets) {  // segmented: group the pods by key node, per-key register sums
-        const int runs = (int)ceil_div(P, kNrRun);
+        static const int run_len = std::max(8, RSK_KNOB(RSK_NR_RUN, kNrRun));  // pods per wave
+        const int runs = (int)ceil_div(P, run_len);
         const int64_t waves = (int64_t)runs * ceil_div(S, 64);
         RSK_CHECK(waves < (int64_t)INT32_MAX - 4, "node_reduce grid too large");
         const int nblk1 = (int)ceil_div(P, kNrChunk);
@@ -1299,7 +1301,7 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
         nr_sub_kernel<<<nbk, 256, 0, ctx->stream>>>(perm1, keys1, bh, nblk1, nbk, P, perm, keys);
         node_reduce_seg_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, ctx->stream>>>(
             d_assign, P, S, d_cpu, reinterpret_cast<const long long *>(d_mem), N, perm, keys, runs, d_cnt,
-            reinterpret_cast<unsigned long long *>(d_cs), reinterpret_cast<unsigned long long *>(d_ms), nr_ablate);
+            reinterpret_cast<unsigned long long *>(d_cs), reinterpret_cast<unsigned long long *>(d_ms), nr_ablate, run_len);
         RSK_HIP(hipGetLastError());
     } else if (PS) {
         ScopedTimer tm(ctx, "node_reduce");

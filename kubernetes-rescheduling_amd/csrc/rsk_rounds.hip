@@ -960,81 +960,7 @@ __global__ __launch_bounds__(256) void rows_cut_delta_kernel(const int *__restri
     if (lane == 0 && d) cut[s] += d;
 }
 
-// ---- the row-sharded loop, fused (rsk_rows_detect / _pick / _place / _move) ----
-// The monitor's usage (base + the ranks' summed CPU partials, truncated to int32
-// as the torch path does) and detect_use_kernel's pass in one: hazard flags,
-// the packed (pct, ~node) maxima, the zero case; the usage is written out for
-// the placement's exact ties.
-template <int kW>
-__global__ __launch_bounds__(64 * kW) void rows_detect_kernel(const long long *__restrict__ base,
-                                                              const long long *__restrict__ cpu,
-                                                              const int *__restrict__ cap, int N, int S, int thr,
-                                                              int npw, int *__restrict__ use_out,
-                                                              uint8_t *__restrict__ haz,
-                                                              unsigned long long *__restrict__ most,
-                                                              int *__restrict__ zc_cnt,
-                                                              unsigned long long *__restrict__ zc_key) {
-    __shared__ unsigned long long lb[kW][64], lz[kW][64];
-    __shared__ int ln[kW][64];
-    constexpr int kU = 8;  // nodes per batch: their loads in flight together
-    const int lane = (int)threadIdx.x & 63, wv = (int)threadIdx.x >> 6;
-    const int nsc = (S + 63) >> 6;
-    const int sc = (int)blockIdx.x % nsc, nb = (int)blockIdx.x / nsc;
-    const int s = min(sc * 64 + lane, S - 1);
-    const int n0 = (nb * kW + wv) * npw, n1 = min(N, n0 + npw);
-    unsigned long long b = 0, bz = 0;
-    int nz = 0;
-    for (int n = n0; n < n1; n += kU) {
-        long long x[kU], y[kU];
-        int c[kU];
-#pragma unroll
-        for (int k = 0; k < kU; ++k) {  // clamped, always-valid addresses
-            const int m = min(n + k, n1 - 1);
-            const size_t idx = (size_t)m * S + s;
-            x[k] = base[idx];
-            y[k] = cpu[idx];
-            c[k] = cap[m];
-        }
-#pragma unroll
-        for (int k = 0; k < kU; ++k) {
-            if (n + k >= n1) break;
-            const int m = n + k;
-            const size_t idx = (size_t)m * S + s;
-            const int u = (int)(x[k] + y[k]);
-            const int v = c[k] == 0 ? -1 : (int)rint((double)u / (double)c[k] * 100.0);
-            const bool h = v >= thr;
-            if (sc * 64 + lane < S) {
-                use_out[idx] = u;
-                haz[idx] = h;
-            }
-            if (h) {
-                const unsigned long long kk = ((unsigned long long)((unsigned)v ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)m);
-                b = kk > b ? kk : b;
-            } else {
-                ++nz;
-                const unsigned long long kk = ((unsigned long long)((unsigned)(c[k] - u) ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)m);
-                bz = kk > bz ? kk : bz;
-            }
-        }
-    }
-    lb[wv][lane] = b;
-    lz[wv][lane] = bz;
-    ln[wv][lane] = nz;
-    __syncthreads();
-    if (wv != 0 || sc * 64 + lane >= S) return;
-#pragma unroll
-    for (int w = 1; w < kW; ++w) {
-        b = max(b, lb[w][lane]);
-        bz = max(bz, lz[w][lane]);
-        nz += ln[w][lane];
-    }
-    if (b) atomicMax(&most[s], b);
-    if (nz) {
-        atomicAdd(&zc_cnt[s], nz);
-        atomicMax(&zc_key[s], bz);
-    }
-}
-
+// ---- the row-sharded loop, fused (rsk_rows_detect_setup / _pick / _place / _move) ----
 // delete_replaced_pod.py:41-61 over this rank's rows (T = u16 shadow or int32
 // rows): the first max-CPU pod on most[s] (decoded from the detect key), as the
 // all-reduce MAX key pod_cpu << 32 | (2^32 - 1 - global pod); 0 = none.
@@ -1583,33 +1509,6 @@ int rsk_pick_max_pod16(rsk_ctx *ctx, const uint16_t *assign16, const int32_t *po
 }
 
 // ---- the row-sharded loop, fused (device pointers; keys zeroed on entry) ----
-int rsk_rows_detect(rsk_ctx *ctx, const int64_t *base, const int64_t *cpu, const int32_t *cap_cpu, int32_t N, int32_t S,
-                    int32_t threshold, int32_t *out_use, uint8_t *out_hazard, int64_t *key_most, int32_t *zc_cnt,
-                    int64_t *zc_key, uint32_t flags) {
-    RSK_TRY(activate(ctx));
-    RSK_CHECK((flags & RSK_F_DEVICE) && base && cpu && cap_cpu && out_use && out_hazard && key_most && zc_cnt && zc_key &&
-                  N > 0 && S > 0 && (int64_t)N * S < INT32_MAX,
-              "rsk_rows_detect: device pointers and N, S > 0 required");
-    // A workgroup = 64 scenarios x kW waves over consecutive node ranges; its
-    // waves meet in LDS, so a scenario's three words take one atomic each per
-    // workgroup: ~512 workgroups in all (RSK_DET_BLOCKS), 16 waves each.
-    static const int w16 = RSK_KNOB(RSK_DET_W16, 1);
-    static const int target = std::max(1, RSK_KNOB(RSK_DET_BLOCKS, 512));
-    const int kW = w16 ? 16 : 4;
-    const int64_t nsc = ceil_div(S, 64);
-    const int64_t nbk = std::max<int64_t>(1, std::min<int64_t>(ceil_div(N, kW * 4), ceil_div(target, nsc)));
-    const int npw = (int)ceil_div(N, nbk * kW);
-    const int64_t blocks = nsc * ceil_div(N, (int64_t)kW * npw);
-    ScopedTimer tm(ctx, "rows_detect");
-    auto *kern = w16 ? &rows_detect_kernel<16> : &rows_detect_kernel<4>;
-    kern<<<(unsigned)blocks, 64 * kW, 0, ctx->stream>>>(
-        reinterpret_cast<const long long *>(base), reinterpret_cast<const long long *>(cpu), cap_cpu, N, S, threshold,
-        npw, out_use, out_hazard, reinterpret_cast<unsigned long long *>(key_most), zc_cnt,
-        reinterpret_cast<unsigned long long *>(zc_key));
-    RSK_HIP(hipGetLastError());
-    return RSK_OK;
-}
-
 int rsk_rows_pick(rsk_ctx *ctx, const void *rows, int32_t elem_bytes, int32_t q, int32_t S, int32_t r0,
                   const int32_t *pod_cpu, const int64_t *key_most, int64_t *key_evict, uint32_t flags) {
     RSK_TRY(activate(ctx));

@@ -76,8 +76,6 @@ SIGNATURES = {
     "rsk_rows_cut_delta": (C.c_int, [_vp, _vp, _vp, _vp, _vp, C.c_int32, C.c_int32, C.c_int32, _vp, C.c_int32, _vp,
                                      _vp, C.c_int32, _vp, C.c_uint32]),
     "rsk_pick_max_pod16": (C.c_int, [_vp, _vp, _vp, C.c_int32, C.c_int32, _vp, _vp, C.c_uint32]),
-    "rsk_rows_detect": (C.c_int, [_vp, _vp, _vp, _vp, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, _vp, _vp, _vp,
-                                  C.c_uint32]),
     "rsk_rows_pick": (C.c_int, [_vp, _vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, _vp, C.c_uint32]),
     "rsk_rows_place": (C.c_int, [_vp, _vp, C.c_int32, _vp, _vp, _vp, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, _vp,
                                  _vp, _vp, _vp, C.c_uint32]),

@@ -236,7 +236,7 @@ class LibrskRoundsBackend:
         self.rev_ptr = torch.from_numpy(rvp).to(self.dev)
         self.rev_idx = torch.from_numpy(np.ascontiguousarray(src[order] if nnz else np.zeros(1, np.int32))).to(self.dev)
         self._F, self._check = RSK_F_DEVICE, check
-        # fused: the round as rsk_rows_detect / _pick / _place / _move (four
+        # fused: the round as rsk_rows_detect_setup once, then rsk_rows_pick / _place / _move (four
         # launches around the collectives); else the per-phase calls below
         self.fused = fused
 

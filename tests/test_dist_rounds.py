@@ -274,7 +274,7 @@ def test_row_sharded_rounds_stream_ordered_gloo_world2():
 def test_row_sharded_rounds_unfused_world2(ordered):
     """The per-phase librsk calls (fused=False: detect, pick, evict key / decode,
     place, cut delta, apply as separate launches) against oracle_rounds; the
-    tests above run the fused round (rsk_rows_detect / _pick / _place / _move)."""
+    tests above run the fused round (rsk_rows_detect_setup, rsk_rows_pick / _place / _move)."""
     R = 4
     c, pod_cpu, _ = _case()
     ev, tg, cut, a, u = _expected(c, pod_cpu, R)

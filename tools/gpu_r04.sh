@@ -32,6 +32,7 @@ for s in "${@:-test smoke bench}"; do
       hp:*) step "hostprobe_${w#hp:}" 300 python -u tools/hostprobe.py "${w#hp:}" ;;
       bnoev) step bench_noevents 600 python -u bench.py --no-cpu-baseline --no-kernel-events ;;
       nr:*) kv=${w#nr:}; step "nr_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_abl.so ${kv//,/ } python -u tools/nrbench.py ;;
+      nrk:*) kv=${w#nrk:}; step "nrk_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u tools/nrbench.py ;;
       dropin) step dropin 400 python -u tools/dropin_latency.py --calls 40 --out "$out/dropin.json" ;;
       prof) for c in headline 1m50k; do
               ./tools/gpu_prof.sh $c "$out/prof_$c" > "$out/prof_$c.log" 2>&1 || { tail -5 "$out/prof_$c.log"; exit 1; }
