@@ -257,8 +257,9 @@ int rsk_rows_cut_delta(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_
 int rsk_pick_max_pod16(rsk_ctx *ctx, const uint16_t *assign16, const int32_t *pod_cpu, int32_t P, int32_t S,
                        const int32_t *most, int32_t *out_pod, uint32_t flags);
 /* The row-sharded round fused into four launches (device pointers, RSK_F_DEVICE
- * required).  key_most / key_evict / zc_cnt / zc_key [S] are zero before the
- * first round; rsk_rows_place leaves them zero for the next one.
+ * required).  key_evict [S] is zero before the first round and rsk_rows_place
+ * leaves it zero for the next one; key_most / zc_cnt / zc_key [S] come from
+ * rsk_rows_detect_setup, and rsk_rows_move rewrites them every round.
  * rsk_rows_pick: delete_replaced_pod.py:41-61 over this rank's q rows (int32
  *   assign rows or the u16 shadow, elem_bytes 4 / 2; pod r0 + p): key_evict[s]
  *   = atomic max of pod_cpu[g] << 32 | (2^32 - 1 - g) over its pods on the
