@@ -555,7 +555,7 @@ __global__ __launch_bounds__(kNrScanB) void nr_blockscan_kernel(int *__restrict_
     if (i < n) off[i] = base + incl - v;
 }
 
-constexpr int kNrRun = 64;  // bucketed pods per wave
+constexpr int kNrRun = 256;  // bucketed pods per wave (64: 0.219 ms, 256: 0.212 at 1M x 50k x 64)
 __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restrict__ assign, int P, int S,
                                                               const int *__restrict__ pod_cpu,
                                                               const long long *__restrict__ pod_mem, int N,
