@@ -277,11 +277,35 @@ struct Prep16Args {
     int N, S;
     unsigned short *code;        // [N*S] or null
     int *nodekey;                // [N*S] (hazard ? KEY_HAZ : cap - use) or null
-    int *zc_cnt;                 // [S]
+    int *zc_cnt;                 // [S] (zero on entry: the previous execute's prep cleared this half)
     unsigned long long *zc_key;  // [S]
-    int *capmax;                 // [1] scratch: max(cap), written by launch_prep before the prep kernel
-                                 // (zc_key, zc_cnt: contiguous, zeroed there too)
+    unsigned *zc_clear;          // the other half of the double-buffered zero-case words, cleared
+    int clear_words;             // by the prep kernel for the next execute
 };
+
+// max(cap[0..N)) by the whole workgroup of kT threads, returned to every
+// thread (every workgroup reads the same caps: the same exact code window B
+// everywhere, without a launch of its own).  red: kT / 64 ints of LDS.
+template <int kT>
+__device__ __forceinline__ int block_capmax(const int *__restrict__ cap, int N, int *red) {
+    const int t = (int)threadIdx.x;
+    int mc = 0;
+    const int N4 = ((uintptr_t)cap % 16) == 0 ? N / 4 : 0;
+    const int4 *cap4 = reinterpret_cast<const int4 *>(cap);
+    for (int i = t; i < N4; i += kT) {
+        const int4 v = cap4[i];
+        mc = max(mc, max(max(v.x, v.y), max(v.z, v.w)));
+    }
+    for (int n = 4 * N4 + t; n < N; n += kT) mc = max(mc, cap[n]);
+    mc = dpp_max(mc);
+    if ((t & 63) == 0) red[t >> 6] = mc;
+    __syncthreads();
+    mc = red[0];
+#pragma unroll
+    for (int w = 1; w < kT / 64; ++w) mc = max(mc, red[w]);
+    __syncthreads();  // red free again
+    return mc;
+}
 
 struct Tile16Args {
     const int *img_pods;   // concatenated per-tile image pod lists
@@ -326,10 +350,10 @@ struct SideArgs {
     int ablate;               // profiling only (results wrong): 1 no exact recounts, 2 pass 1 only, 4 no (1), 8 no (2)
     unsigned *gscratch;       // teams whose table exceeds the LDS: lds_team bytes per block in global memory
     // on-the-fly node state (kOTF launches, code == null): codes from cap / use /
-    // haz with B from *capmax, the zero case scanned per scenario when needed, so
-    // the launch depends on car_prep0 only and runs beside car_prep
+    // haz with B from the workgroup's own max(cap), the zero case scanned per
+    // scenario when needed, so the launch depends on no prep kernel and runs
+    // beside car_prep
     const uint8_t *haz;
-    const int *capmax;
 };
 struct SideGeom {
     int dmax, Dc, H, hshift, K, T, W, kB;
@@ -353,9 +377,6 @@ int launch_side16(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool
 int launch_side16_otf(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch);
 
 int launch_prep(hipStream_t stream, const Prep16Args &a);
-// launch_prep in two halves: car_prep0 (zero-case reset, max(cap)), then car_prep
-int launch_prep0(hipStream_t stream, const Prep16Args &a);
-int launch_prep_main(hipStream_t stream, const Prep16Args &a);
 int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off32, bool heavy, unsigned blocks,
                   size_t lds);
 size_t tile16_lds_bytes(int rmax, int lsl, int rec_cap);

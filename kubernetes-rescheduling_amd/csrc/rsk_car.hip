@@ -875,6 +875,7 @@ struct rsk_car_plan {
     int side_dmax[kNumSide] = {};
     // per-execute workspace
     DevBuf nodekey, code, zc;
+    int zc_S = 0, zc_half = 0;  // the zero-case words' double buffer (S it is sized for, the half in use)
     // the deduplicated CSR and the row map on the device (the one-launch path of small batches)
     DevBuf drp, dci, drows;
     int ddmax = 0;
@@ -1352,7 +1353,6 @@ struct SideBufs {
     const unsigned long long *zkey;
     int *target, *score;
     const uint8_t *haz;   // on-the-fly launches (launch_side16_otf)
-    const int *capmax;
 };
 
 // car_side16 launches of classes [c0, c1) on `stream`, the longest rows first.
@@ -1400,7 +1400,6 @@ int launch_side16_classes(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, 
         if (otf) {
             a.code = nullptr;
             a.haz = b.haz;
-            a.capmax = b.capmax;
             RSK_TRY(launch_side16_otf(stream, a, g, off32, &plan->side_scratch));
         } else {
             RSK_TRY(launch_side16(stream, a, g, off32, &plan->side_scratch));
@@ -1634,10 +1633,21 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         RSK_TRY(plan->code.reserve((NS + (size_t)S) * 2));  // + row N, zeroed by the prep kernel
         d_code = plan->code.as<unsigned short>();
     }
-    RSK_TRY(plan->zc.reserve((size_t)S * 12 + 16));
-    unsigned long long *d_zkey = plan->zc.as<unsigned long long>();
+    // the zero-case words, double-buffered: half h = zc_key[S] u64, zc_cnt[S],
+    // zero on entry (cleared by the previous execute's prep kernel, or here
+    // when the buffer is new or S changed); this execute's prep clears the
+    // other half for the next one — no launch ahead of the prep kernel
+    const size_t zc_half_bytes = (size_t)S * 12 + 4;  // (+4: 8-B alignment of the second half)
+    if (plan->zc_S != S) {
+        RSK_TRY(plan->zc.reserve(2 * zc_half_bytes));
+        RSK_HIP(hipMemsetAsync(plan->zc.ptr, 0, 2 * zc_half_bytes, ctx->stream));
+        plan->zc_S = S;
+        plan->zc_half = 0;
+    }
+    unsigned char *zc_base = plan->zc.as<unsigned char>();
+    unsigned long long *d_zkey = reinterpret_cast<unsigned long long *>(zc_base + plan->zc_half * zc_half_bytes);
     int *d_zcnt = reinterpret_cast<int *>(d_zkey + S);
-    // zc_key[S] u64, zc_cnt[S], the capmax word: zeroed / written by launch_prep
+    unsigned *zc_other = reinterpret_cast<unsigned *>(zc_base + (plan->zc_half ^ 1) * zc_half_bytes);
 
     // K0: node state (codes and / or exact keys) + the zero case, launched below
     Prep16Args pa;
@@ -1650,7 +1660,8 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     pa.nodekey = d_key;
     pa.zc_cnt = d_zcnt;
     pa.zc_key = d_zkey;
-    pa.capmax = d_zcnt + S;  // the zc buffer's spare words
+    pa.zc_clear = zc_other;
+    pa.clear_words = (int)(zc_half_bytes / 4);
     SideBufs sb;
     sb.assign = d_assign;
     sb.key = d_key;
@@ -1662,7 +1673,6 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     sb.target = d_target;
     sb.score = d_score;
     sb.haz = d_haz;
-    sb.capmax = pa.capmax;
     static const int ablate = RSK_ABLATION(RSK_ABLATE_TILE);
     static const int order = RSK_KNOB(RSK_TILE_ORDER, 2);
     static const int sl_max = [] { int v = RSK_KNOB(RSK_TILE_SL, 64); return v >= 1 && v <= 64 ? v : 64; }();
@@ -1723,17 +1733,13 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     const int nfork = big_fork ? 1 : 0;
     if (big_fork) {
         // The rows too big for the fused grid run on a side stream from the
-        // start: their node codes computed on the fly (they need car_prep0's
-        // max(cap) only), so their workgroups take CUs beside car_prep, before
-        // the fused grid fills every slot and starves them.
-        {
-            ScopedTimer tm(ctx, "car_prep");
-            RSK_TRY(launch_prep0(ctx->stream, pa));
-        }
+        // start: their node codes computed on the fly (max(cap) by each of their
+        // workgroups), so they depend on no prep kernel and take CUs beside
+        // car_prep, before the fused grid fills every slot and starves them.
         RSK_TRY(aux_fork(ctx, nfork));
         RSK_TRY(launch_side16_classes(plan, ctx, ctx->aux[0], sb, S, N, big_hi, kNumSide, -1, true));
         ScopedTimer tm(ctx, "car_prep");
-        RSK_TRY(launch_prep_main(ctx->stream, pa));
+        RSK_TRY(launch_prep(ctx->stream, pa));
     } else {
         {
             ScopedTimer tm(ctx, "car_prep");
@@ -1742,6 +1748,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         if (compact && big_left)
             RSK_TRY(launch_side16_classes(plan, ctx, ctx->stream, sb, S, N, big_hi, kNumSide));
     }
+    plan->zc_half ^= 1;  // the prep kernel is queued: it clears the other half for the next execute
     RSK_TRY(launch_side(plan, ctx, ctx->stream, sb, S, N, compact, fuse_c));
     const bool off32 = (int64_t)std::max(plan->P, plan->Q) * S * 4 < ((int64_t)1 << 32);
     if (plan->T > 0 && compact) {   // K1 tiles, 32-bit {code, node} cells

@@ -57,46 +57,9 @@ __device__ __forceinline__ ushort4 cvec_make(const unsigned (&k)[4]) {
     return make_ushort4((unsigned short)k[0], (unsigned short)k[1], (unsigned short)k[2], (unsigned short)k[3]);
 }
 
-// Thread t -> (V consecutive scenarios, node chunk): V-wide loads of use /
-// hazard per node.  The zero case (non-hazard count, packed max of (rem,
-// ~node)) is reduced in LDS per workgroup first — threads of one workgroup
-// that share a scenario meet in one LDS slot — so a scenario receives one
-// global atomic per workgroup, not one per thread.
-// Ahead of the prep kernel, one workgroup: zero the zero-case words
-// (zc_key[S] u64, zc_cnt[S]) and, for the codes, max(cap) once per execute —
-// the exact code window B = max(0, max(cap) - 32766) — into *capmax (a
-// negative max reads as 0, which gives the same B).
-constexpr int kPrep0Threads = 1024;
-__global__ __launch_bounds__(kPrep0Threads) void car_prep0_kernel(const int *__restrict__ cap, int N,
-                                                                 unsigned *__restrict__ zc, int zc_words,
-                                                                 int *__restrict__ capmax) {
-    __shared__ int red[kPrep0Threads / 64];
-    for (int i = (int)threadIdx.x; i < zc_words; i += kPrep0Threads) zc[i] = 0u;
-    if (!capmax) return;
-    int mc = 0;
-    // 16-B loads, 8 in flight per thread (one workgroup: the latency of the
-    // chain of loads is the kernel's time; N = 50k in 2 rounds instead of 49)
-    const int N4 = ((uintptr_t)cap % 16) == 0 ? N / 4 : 0;
-    const int4 *cap4 = reinterpret_cast<const int4 *>(cap);
-    for (int i0 = (int)threadIdx.x; i0 < N4; i0 += 8 * kPrep0Threads) {
-        int4 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = cap4[min(i0 + u * kPrep0Threads, N4 - 1)];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) mc = max(mc, max(max(v[u].x, v[u].y), max(v[u].z, v[u].w)));
-    }
-    for (int n = 4 * N4 + (int)threadIdx.x; n < N; n += kPrep0Threads) mc = max(mc, cap[n]);
-    mc = dpp_max(mc);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < kPrep0Threads / 64; ++w) mc = max(mc, red[w]);
-        *capmax = mc;
-    }
-}
-
 // Small batches (N * S <= kPrepSmallCells, S <= kPrepSmallS; config 2 is
-// 64 cells): prep0 and prep in one workgroup, one launch instead of two.
+// 64 cells): max(cap) and the prep pass in one workgroup.
+constexpr int kPrep0Threads = 1024;
 constexpr int kPrepSmallCells = 32768, kPrepSmallS = 256;
 __global__ __launch_bounds__(kPrep0Threads) void car_prep_small_kernel(const int *__restrict__ cap,
                                                                       const int *__restrict__ use,
@@ -105,7 +68,8 @@ __global__ __launch_bounds__(kPrep0Threads) void car_prep_small_kernel(const int
                                                                       int *__restrict__ nodekey,
                                                                       int *__restrict__ zc_cnt,
                                                                       unsigned long long *__restrict__ zc_key,
-                                                                      int *__restrict__ capmax) {
+                                                                      unsigned *__restrict__ zc_clear,
+                                                                      int clear_words) {
     __shared__ int red[kPrep0Threads / 64];
     __shared__ int lcnt[kPrepSmallS];
     __shared__ unsigned long long lkey[kPrepSmallS];
@@ -122,7 +86,7 @@ __global__ __launch_bounds__(kPrep0Threads) void car_prep_small_kernel(const int
     mc = red[0];
     for (int w = 1; w < kPrep0Threads / 64; ++w) mc = max(mc, red[w]);
     const int B = max(0, mc - 32766);  // the exact code window (rsk_car.h)
-    if (t == 0 && capmax) *capmax = mc;
+    for (int i = t; i < clear_words; i += kPrep0Threads) zc_clear[i] = 0u;  // the next execute's half
     if (code)
         for (int i = t; i < S; i += kPrep0Threads) code[(size_t)N * S + i] = 0;  // row N: no candidate
     for (int i = t; i < N * S; i += kPrep0Threads) {
@@ -143,13 +107,21 @@ __global__ __launch_bounds__(kPrep0Threads) void car_prep_small_kernel(const int
     }
 }
 
+// Thread t -> (V consecutive scenarios, node chunk): V-wide loads of use /
+// hazard per node.  Every workgroup first reduces max(cap) itself (the exact
+// code window B = max(0, max(cap) - 32766), the same in every workgroup), so
+// no launch precedes this one; workgroup 0 clears the other half of the
+// double-buffered zero-case words for the next execute.  The zero case
+// (non-hazard count, packed max of (rem, ~node)) is reduced in LDS per
+// workgroup first — threads of one workgroup that share a scenario meet in one
+// LDS slot — so a scenario receives one global atomic per workgroup.
 template <int V, bool kCode, bool kKey, int kBlock = 256>
 __global__ __launch_bounds__(kBlock) void car_prep_kernel(const int *__restrict__ cap, const typename VecT<V>::I *__restrict__ use,
                                                        const typename VecT<V>::H *__restrict__ haz, int N, int SV,
                                                        int npb, unsigned total, typename VecT<V>::C *__restrict__ code,
                                                        typename VecT<V>::I *__restrict__ nodekey,
                                                        int *__restrict__ zc_cnt, unsigned long long *__restrict__ zc_key,
-                                                       const int *__restrict__ capmax) {
+                                                       unsigned *__restrict__ zc_clear, int clear_words) {
     // kBlock 1024 only with SV <= 256: the slots never exceed 256
     __shared__ int lcnt[256 * V];
     __shared__ unsigned long long lkey[256 * V];
@@ -158,7 +130,10 @@ __global__ __launch_bounds__(kBlock) void car_prep_kernel(const int *__restrict_
     const int nslot = min(256, SV);
     for (int i = threadIdx.x; i < nslot * V; i += kBlock) { lcnt[i] = 0; lkey[i] = 0ull; }
     __syncthreads();
-    const int B = kCode ? max(0, *capmax - 32766) : 0;  // the exact code window (rsk_car.h)
+    __shared__ int red[kBlock / 64];
+    const int B = kCode ? max(0, block_capmax<kBlock>(cap, N, red) - 32766) : 0;  // the exact code window
+    if (blockIdx.x == 0)  // the other half of the zero-case words, for the next execute
+        for (int i = (int)threadIdx.x; i < clear_words; i += kBlock) zc_clear[i] = 0u;
     if (kCode && t < (unsigned)SV) {  // code row N: code 0 for every scenario (clamped invalid assignments)
         const unsigned z[V] = {};
         code[(size_t)N * SV + t] = cvec_make(z);
@@ -220,39 +195,31 @@ static int prep_launch(hipStream_t stream, const Prep16Args &a, int SV, int npb,
     I *key = reinterpret_cast<I *>(a.nodekey);
     if (a.code && a.nodekey)
         car_prep_kernel<V, true, true, kBlock><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
-                                                                 a.capmax);
+                                                                 a.zc_clear, a.clear_words);
     else if (a.code)
         car_prep_kernel<V, true, false, kBlock><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
-                                                                 a.capmax);
+                                                                 a.zc_clear, a.clear_words);
     else
         car_prep_kernel<V, false, true, kBlock><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
-                                                                 a.capmax);
+                                                                 a.zc_clear, a.clear_words);
     RSK_HIP(hipGetLastError());
     return RSK_OK;
 }
 
+static int launch_prep_main(hipStream_t stream, const Prep16Args &a);
+
 int launch_prep(hipStream_t stream, const Prep16Args &a) {
+    RSK_CHECK(a.code || a.nodekey, "prep: nothing to write");
     if ((int64_t)a.N * a.S <= kPrepSmallCells && a.S <= kPrepSmallS) {
-        RSK_CHECK(a.code || a.nodekey, "prep: nothing to write");
         car_prep_small_kernel<<<1, kPrep0Threads, 0, stream>>>(a.cap, a.use, a.haz, a.N, a.S, a.code, a.nodekey,
-                                                               a.zc_cnt, a.zc_key, a.code ? a.capmax : nullptr);
+                                                               a.zc_cnt, a.zc_key, a.zc_clear, a.clear_words);
         RSK_HIP(hipGetLastError());
         return RSK_OK;
     }
-    RSK_TRY(launch_prep0(stream, a));
     return launch_prep_main(stream, a);
 }
 
-int launch_prep0(hipStream_t stream, const Prep16Args &a) {
-    RSK_CHECK(a.code || a.nodekey, "prep: nothing to write");
-    RSK_CHECK(!a.code || a.capmax, "prep: codes need the capmax scratch");
-    car_prep0_kernel<<<1, kPrep0Threads, 0, stream>>>(a.cap, a.N, reinterpret_cast<unsigned *>(a.zc_key), 3 * a.S,
-                                                      a.code ? a.capmax : nullptr);
-    RSK_HIP(hipGetLastError());
-    return RSK_OK;
-}
-
-int launch_prep_main(hipStream_t stream, const Prep16Args &a) {
+static int launch_prep_main(hipStream_t stream, const Prep16Args &a) {
     // 4 scenarios per thread when S % 4 == 0 (16-B use / key words, 8-B codes)
     const bool v4 = a.S % 4 == 0 && ((uintptr_t)a.use % 16) == 0 && ((uintptr_t)a.haz % 4) == 0;
     const int SV = v4 ? a.S / 4 : a.S;

@@ -214,7 +214,7 @@ __device__ __forceinline__ int side_pivot3(int x) {  // majority of lanes 0, 21,
 // candidates are: the table's entries with C >= 2 (a handful), and the lane's
 // deviation nodes — both small sets.
 template <int kW, int kT, int kB, bool kOff32, bool kPipe, bool kGlobal = false, bool kOTF = false>
-__device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slot = -1) {
+__device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slot = -1, int Bw = 0) {
     static_assert(kT == 1 || kT == kW, "a team is one wave or the whole workgroup");
     extern __shared__ __attribute__((aligned(16))) unsigned slds[];
     const int lane = (int)threadIdx.x & 63;
@@ -231,7 +231,7 @@ __device__ __forceinline__ void side16_block(const SideArgs &a, int blk, int slo
     const int s0 = chunk * 64;
     const int s = min(s0 + lane, a.S - 1);
     const int H = a.H, K = a.K;
-    const int B = kOTF ? max(0, *const_ptr(a.capmax) - 32766) : 0;  // the exact code window (rsk_car.h)
+    const int B = kOTF ? Bw : 0;  // the exact code window (rsk_car.h), from the kernel's max(cap)
 
     // kGlobal (one team per workgroup): the team's table, lists and merge area in
     // global scratch (a table beyond the LDS); the same code with global atomics

@@ -39,11 +39,16 @@ namespace rsk {
 // (a.xcd_per: workgroups per XCD run).
 template <int kW, int kT, int kB, bool kOff32, bool kPipe, bool kGlobal = false, bool kOTF = false>
 __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : (kOTF ? 4 : 8))) void car_side16_kernel(SideArgs a) {
+    int B = 0;
+    if (kOTF) {  // the exact code window from max(cap), by this workgroup (no prep kernel before it)
+        __shared__ int red[kW];
+        B = max(0, block_capmax<64 * kW>(a.cap, a.N, red) - 32766);
+    }
     if (kGlobal) {  // a capped grid strides over the items; work area = the resident block's slot
         static_assert(!kGlobal || kT == kW, "global work areas are per workgroup team");
         const int items = a.n_rows * a.nchunk;
         for (int blk = (int)blockIdx.x; blk < items; blk += (int)gridDim.x) {
-            side16_block<kW, kT, kB, kOff32, kPipe, kGlobal, kOTF>(a, blk, (int)blockIdx.x);
+            side16_block<kW, kT, kB, kOff32, kPipe, kGlobal, kOTF>(a, blk, (int)blockIdx.x, B);
             glob_fence(true);
             __syncthreads();  // every wave is done with the area before the next item clears it
         }
@@ -51,7 +56,7 @@ __global__ __launch_bounds__(64 * kW, (kT > 1 ? 1 : (kOTF ? 4 : 8))) void car_si
     }
     int blk = (int)blockIdx.x;
     if (a.xcd_per) blk = (int)(blockIdx.x & 7u) * a.xcd_per + (int)(blockIdx.x >> 3);
-    side16_block<kW, kT, kB, kOff32, kPipe, kGlobal, kOTF>(a, blk);
+    side16_block<kW, kT, kB, kOff32, kPipe, kGlobal, kOTF>(a, blk, -1, B);
 }
 
 constexpr int kSideH2Cap = 2048;  // listed nodes counted >= 2 (e.g. degree 5000 over 6000 nodes: ~1200)
@@ -166,7 +171,7 @@ int launch_side16(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool
 }
 
 int launch_side16_otf(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch) {
-    RSK_CHECK(a.haz && a.capmax && a.cap && a.use, "on-the-fly side rows need cap, use, hazard and capmax");
+    RSK_CHECK(a.haz && a.cap && a.use, "on-the-fly side rows need cap, use and hazard");
     return launch_side16_t<true>(stream, a, g, off32, scratch);
 }
 
