@@ -1637,7 +1637,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     // zero on entry (cleared by the previous execute's prep kernel, or here
     // when the buffer is new or S changed); this execute's prep clears the
     // other half for the next one — no launch ahead of the prep kernel
-    const size_t zc_half_bytes = (size_t)S * 12 + 4;  // (+4: 8-B alignment of the second half)
+    const size_t zc_half_bytes = ((size_t)S * 12 + 15) & ~(size_t)15;  // 16-B aligned halves (u64 atomics)
     if (plan->zc_S != S) {
         RSK_TRY(plan->zc.reserve(2 * zc_half_bytes));
         RSK_HIP(hipMemsetAsync(plan->zc.ptr, 0, 2 * zc_half_bytes, ctx->stream));
