@@ -151,7 +151,7 @@ using namespace rsk;
 
 extern "C" {
 
-int rsk_version(void) { return 100; }
+int rsk_version(void) { return 104; }  // 1.04: the fused row-sharded round, RSK_F_TILED
 
 const char *rsk_last_error(void) { return rsk::last_error(); }
 
