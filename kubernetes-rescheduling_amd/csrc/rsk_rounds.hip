@@ -97,7 +97,8 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
                                              unsigned *tab, unsigned long long *__restrict__ kpick,
                                              unsigned long long *__restrict__ kdet, int *__restrict__ ev_out,
                                              int *__restrict__ zc_cnt, unsigned long long *__restrict__ zc_key,
-                                             int own0, int own1, DevLists dl, int p_direct = -1) {
+                                             int own0, int own1, DevLists dl, int p_direct = -1,
+                                             int old_known = INT_MIN, int cpu_known = INT_MIN) {
     unsigned *keys = tab, *cnts = tab + H;
     unsigned long long *red64 = reinterpret_cast<unsigned long long *>(tab + 2 * H);  // best
     unsigned *red = tab + 2 * H + 2;                                                   // M, n_at_M, n_free
@@ -193,7 +194,9 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
         if (zc_cnt) zc_cnt[s] = 0, zc_key[s] = 0ull;
         if (update && t >= 0) {  // build-defined update: the pod's CPU moves with it
             const size_t pc = (size_t)p * S + s;
-            const int old = assign[pc], c = pod_cpu[p];
+            // (the persistent loop knows both: the hazard node and the pick key's CPU)
+            const int old = old_known != INT_MIN ? old_known : assign[pc];
+            const int c = cpu_known != INT_MIN ? cpu_known : pod_cpu[p];
             if ((unsigned)old < (unsigned)N) use[(size_t)old * S + s] -= c;
             use[(size_t)t * S + s] += c;
             assign[pc] = t;
@@ -701,7 +704,7 @@ template <typename T>
 __device__ __forceinline__ int scn_pick(const T *__restrict__ asg, const int *__restrict__ pod_cpu, int P, int S,
                                         int s, unsigned long long kd, const int *__restrict__ off,
                                         const int *__restrict__ pod, const DevLists &dl, unsigned long long *r64,
-                                        int *lsrc) {
+                                        int *lsrc, int *pcpu) {
     constexpr int kU = 4;
     const int t = (int)threadIdx.x;
     if (!kd) return -1;  // uniform
@@ -760,6 +763,7 @@ __device__ __forceinline__ int scn_pick(const T *__restrict__ asg, const int *__
     for (int w = 1; w < 4; ++w) best = r64[w] > best ? r64[w] : best;
     if (best && mine == best && bsrc >= 0) *lsrc = bsrc;  // the winner's entry (at most one per pod)
     __syncthreads();
+    *pcpu = (int)((unsigned)(best >> 32) ^ 0x80000000u);  // the winner's CPU (the key's high word)
     return best ? (int)~(unsigned)(best & 0xffffffffull) : -1;
 }
 
@@ -814,7 +818,8 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
         }
         for (int r = 0; r < a.R; ++r) {
             const unsigned long long kd = st.most;
-            const int p = scn_pick<int>(a.assign, a.pod_cpu, a.P, a.S, s, kd, a.off, a.pod, a.dl, r64, &lsrc);
+            int pcpu;
+            const int p = scn_pick<int>(a.assign, a.pod_cpu, a.P, a.S, s, kd, a.off, a.pod, a.dl, r64, &lsrc, &pcpu);
             int *tg_row = a.out_target + (size_t)r * a.S;
             if (t == 0) {
                 a.out_evict[(size_t)r * a.S + s] = p;
@@ -827,7 +832,7 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
             const int o = (int)~(unsigned)(kd & 0xffffffffull);  // the picked pod sits on the hazard node
             car_move_one<kGlobal>(a.row_ptr, a.col, a.pod_cpu, a.assign, a.use, a.cap, a.haz, nullptr, s, a.S, a.N,
                                   a.H, 1, tg_row, nullptr, tab, nullptr, nullptr, nullptr, a.zc_cnt, a.zc_key, 0,
-                                  INT_MAX, a.dl, p);
+                                  INT_MAX, a.dl, p, o, pcpu);
             move_sync<kGlobal>();  // the move's state update (thread 0) before it is read
             const int tt = (int)tab[2 * a.H + 7];  // car_move_one's target (red[5])
             if (tt >= 0) {  // two nodes' CPU changed: their blocks, then the scenario's maxima
