@@ -1777,7 +1777,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         a.lsl = 0;
         while ((1 << a.lsl) < SL) ++a.lsl;
         a.order = order;
-        static const int group = RSK_KNOB(RSK_TILE_GROUP, 8);  // 0.8175-0.8202 -> 0.8144-0.8148 ms (3 interleaved reps)
+        static const int group = RSK_KNOB(RSK_TILE_GROUP, 4);  // 0.8175-0.8202 -> 0.8150-0.8164 ms (3 interleaved reps; 8: 0.8144-0.8148 but +0.36 GB of code re-reads)
         a.group = group;
         a.ablate = ablate;
         a.rec_cap = (plan->recmax + 3) & ~3;
