@@ -743,32 +743,55 @@ __global__ void decode_first_max(const unsigned long long *__restrict__ key, int
     out[s] = k ? (int)(~(unsigned)(k & 0xffffffffull)) : -1;
 }
 
-// nodemonitor.py:24-46.  Per (node chunk, s): count, chunk mean and M2 (two
-// passes over the chunk, fp64); then per s a fixed-order Chan merge.
-__global__ __launch_bounds__(256) void std_partial_kernel(const int *__restrict__ use, const int *__restrict__ cap,
+// nodemonitor.py:24-46.  100 / cap[n] once per node (-1: cap <= 0, the node
+// is skipped), so the partial pass multiplies instead of dividing per cell.
+__global__ __launch_bounds__(256) void std_inv_kernel(const int *__restrict__ cap, int N, double *__restrict__ inv) {
+    const int n = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (n >= N) return;
+    const int c = cap[n];
+    inv[n] = c > 0 ? 100.0 / (double)c : -1.0;
+}
+
+// Per (node chunk, s): count, chunk mean and M2 in one pass over pct = use *
+// (100 / cap) in fp64, as shifted sums (d = pct - the chunk's first pct: the
+// sum and sum of squares of d, M2 = sq - sum^2 / c — exact 0 for equal
+// values, ~1e-15 relative otherwise, inside the 1e-9 the tests allow against
+// numpy's two-pass std); then per s a fixed-order Chan merge.
+__global__ __launch_bounds__(256) void std_partial_kernel(const int *__restrict__ use, const double *__restrict__ inv,
                                                           int N, int S, int npb, unsigned total,
                                                           double *__restrict__ pmean, double *__restrict__ pm2,
                                                           int *__restrict__ pcnt) {
-#pragma clang fp contract(off)  // separate multiply and add, as numpy (no FMA contraction)
+#pragma clang fp contract(off)
     const unsigned t = blockIdx.x * 256u + threadIdx.x;
     if (t >= total) return;
     const int s = (int)(t % (unsigned)S), ch = (int)(t / (unsigned)S);
     const int n0 = ch * npb, n1 = min(N, n0 + npb);
-    double sum = 0.0;
+    constexpr int kU = 8;  // loads in flight per thread
+    double sum = 0.0, sq = 0.0, K = 0.0;
     int c = 0;
-    for (int n = n0; n < n1; ++n) {
-        const int cp = cap[n];
-        if (cp <= 0) continue;
-        sum += (double)use[(size_t)n * S + s] / (double)cp * 100.0;
-        ++c;
+    for (int n = n0; n < n1; n += kU) {
+        int u[kU];
+        double r[kU];
+#pragma unroll
+        for (int k = 0; k < kU; ++k) {
+            const int m = min(n + k, n1 - 1);  // clamped: always a valid address
+            u[k] = use[(size_t)m * S + s];
+            r[k] = inv[m];
+        }
+#pragma unroll
+        for (int k = 0; k < kU; ++k) {
+            if (n + k < n1 && r[k] >= 0.0) {
+                const double x = (double)u[k] * r[k];
+                if (c == 0) K = x;
+                const double d = x - K;
+                sum += d;
+                sq += d * d;
+                ++c;
+            }
+        }
     }
-    double mean = c ? sum / c : 0.0, m2 = 0.0;
-    for (int n = n0; n < n1; ++n) {
-        const int cp = cap[n];
-        if (cp <= 0) continue;
-        const double d = (double)use[(size_t)n * S + s] / (double)cp * 100.0 - mean;
-        m2 += d * d;
-    }
+    const double mean = c ? K + sum / c : 0.0;
+    const double m2 = c ? fmax(0.0, sq - sum * (sum / c)) : 0.0;
     const size_t o = (size_t)ch * S + s;
     pmean[o] = mean;
     pm2[o] = m2;
@@ -1385,11 +1408,13 @@ int rsk_load_std(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *cap_cpu, i
     RSK_TRY(ctx->work[0].reserve((size_t)nch * S * 8));
     RSK_TRY(ctx->work[1].reserve((size_t)nch * S * 8));
     RSK_TRY(ctx->work[2].reserve((size_t)nch * S * 4));
+    RSK_TRY(ctx->work[3].reserve((size_t)N * 8));
     const unsigned total = (unsigned)((int64_t)nch * S);
     {
         ScopedTimer tm(ctx, "load_std");
+        std_inv_kernel<<<(unsigned)ceil_div(N, 256), 256, 0, ctx->stream>>>(d_cap, N, ctx->work[3].as<double>());
         std_partial_kernel<<<(unsigned)ceil_div(total, 256), 256, 0, ctx->stream>>>(
-            d_use, d_cap, N, S, npb, total, ctx->work[0].as<double>(), ctx->work[1].as<double>(),
+            d_use, ctx->work[3].as<double>(), N, S, npb, total, ctx->work[0].as<double>(), ctx->work[1].as<double>(),
             ctx->work[2].as<int>());
         std_merge_kernel<<<(unsigned)ceil_div(S, 4), 256, 0, ctx->stream>>>(
             ctx->work[0].as<double>(), ctx->work[1].as<double>(), ctx->work[2].as<int>(), nch, S, d_out);
