@@ -1403,7 +1403,8 @@ int rsk_load_std(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *cap_cpu, i
     RSK_TRY(stage_out(ctx, 2, out_std, (size_t)S * 8, dev, reinterpret_cast<void **>(&d_out)));
     // nodes per thread: at least 16, and at most 1,024 chunks for the merge
     // waves to walk (50k nodes x 64 scenarios: 49 nodes, 1,021 chunks)
-    const int npb = std::max({chunk_for(N, S), 16, (int)ceil_div(N, 1024)});
+    static const int max_chunks = std::max(16, RSK_KNOB(RSK_STD_CHUNKS, 1024));
+    const int npb = std::max({chunk_for(N, S), 16, (int)ceil_div(N, max_chunks)});
     const int nch = (int)ceil_div(N, npb);
     RSK_TRY(ctx->work[0].reserve((size_t)nch * S * 8));
     RSK_TRY(ctx->work[1].reserve((size_t)nch * S * 8));

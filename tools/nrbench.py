@@ -45,5 +45,17 @@ for _ in range(n):
 torch.cuda.synchronize(dev)
 ctx.set_profiling(False)
 ms, k = ctx.kernel_time("node_reduce")
+ucap = T(c.cap_cpu)
+use = T(c.use_cpu)
+std = torch.empty(S, dtype=torch.float64, device=dev)
+ctx.reset_profiling()
+ctx.set_profiling(True)
+for _ in range(n):
+    _lib.check(ctx.lib.rsk_load_std(ctx.handle, use.data_ptr(), ucap.data_ptr(), N, S, std.data_ptr(),
+                                    _lib.RSK_F_DEVICE))
+torch.cuda.synchronize(dev)
+ctx.set_profiling(False)
+ms2, k2 = ctx.kernel_time("load_std")
 print(json.dumps({"wall_ms": round(wall, 4), "node_reduce_ms": round(ms / max(k, 1), 4),
+                  "load_std_ms": round(ms2 / max(k2, 1), 4),
                   "env": {x: y for x, y in os.environ.items() if x.startswith("RSK_")}}), flush=True)
