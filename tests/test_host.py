@@ -25,7 +25,17 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), f"librsk.so does not export {s}"
     assert set(syms) == set(_lib.SIGNATURES), "ctypes signature table out of sync with include/rsk.h"
-    assert lib.rsk_version() >= 100
+    assert lib.rsk_version() >= 104
+
+
+def test_rows_blk_bytes_host_only():
+    """rsk_rows_blk_bytes (host arithmetic, no device): the row-sharded loop's
+    detect scratch = S x ceil(N / 64) blocks x 20 B (two u64 maxima and a count)."""
+    from rsk import _lib
+    lib = _lib.load_library()
+    for N, S in ((1, 1), (64, 1), (65, 3), (50_000, 64), (5_000, 1024)):
+        assert lib.rsk_rows_blk_bytes(N, S) == S * -(-N // 64) * 20
+    assert lib.rsk_rows_blk_bytes(0, 8) == 0 and lib.rsk_rows_blk_bytes(8, 0) == 0
 
 
 def test_library_is_gfx950_code_object():
