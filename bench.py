@@ -242,8 +242,8 @@ def bench_rounds(args, cfg, world, rank, local, dev):
     tg = torch.empty(R * S, dtype=torch.int32, device=dev)
     if args.warmup:
         rounds.run(T["assign"], S, T["cap_cpu"], T["use_cpu"], N, args.warmup, 30, ev, tg, device=True)
-    # the timed call's own starting state for its first k scenarios (parity below)
-    k = min(S, 16)
+    # the timed call's own starting state (parity of every scenario below)
+    k = S
     a_start = T["assign"].view(P, S)[:, :k].cpu().numpy().copy().reshape(-1)
     u_start = T["use_cpu"].view(N, S)[:, :k].cpu().numpy().copy().reshape(-1)
     # the timed call runs without kernel events (an event pair around every
@@ -264,12 +264,15 @@ def bench_rounds(args, cfg, world, rank, local, dev):
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     tgt = tg.cpu().numpy()[args.warmup * S:]
-    # parity of the timed call itself: its first k scenarios, all R rounds from
-    # the state it started from, against oracle_rounds (final assign / use,
-    # evictions and targets of every round)
+    # parity of the timed call itself: every scenario, all R rounds from the
+    # state it started from, against oracle_rounds (final assign / use,
+    # evictions and targets of every round; the scenarios split over threads)
     from oracle import oracle as orc
     R = args.steps
-    ea, eu, eev, etg = orc.rounds(c.row_ptr, c.col_idx, c.pod_cpu, a_start, k, c.cap_cpu, u_start, N, R)
+    t_par = time.perf_counter()
+    ea, eu, eev, etg = orc.rounds(c.row_ptr, c.col_idx, c.pod_cpu, a_start, k, c.cap_cpu, u_start, N, R,
+                                  threads=cpu_threads()[0])
+    parity_s = time.perf_counter() - t_par
     got_ev = ev.cpu().numpy()[w:].reshape(R, S)[:, :k].reshape(-1)
     got_a = T["assign"].view(P, S)[:, :k].cpu().numpy().reshape(-1)
     got_u = T["use_cpu"].view(N, S)[:, :k].cpu().numpy().reshape(-1)
@@ -305,7 +308,8 @@ def bench_rounds(args, cfg, world, rank, local, dev):
             "moves": int((tgt >= 0).sum()), "none": int((tgt == -1).sum()),
             "no_candidate": int((tgt == -2).sum()), "no_evict": int((tgt == -3).sum()),
             "parity_sample_ok": bool(parity_ok),
-            "parity_sample": f"the timed {R}-round call, scenarios 0..{k - 1}, vs oracle_rounds from its start state",
+            "parity_sample": f"the timed {R}-round call, all {k} scenarios (0..{k - 1}), vs oracle_rounds from its "
+                             f"start state ({parity_s:.1f} s on {cpu_threads()[0]} threads)",
             "rccl_world": args.rccl_world, "env": rsk_env(),
         }
         print(json.dumps(line), flush=True)
@@ -498,6 +502,7 @@ def main():
         thr = 40   # the synthetic nodes run at 2-43 % CPU: only the hottest are hazards, so pods move
         rr.run(a2, T["use_cpu"], T["cap_cpu"], pc, pm, N, S, 1, threshold=thr)   # warm-up round
         a2.copy_(T["assign"])   # the timed rounds start from the generated state (use0 matches assign)
+        a_start, u_start = T["assign"].cpu().numpy(), T["use_cpu"].cpu().numpy()
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -510,6 +515,24 @@ def main():
             dist.all_reduce(e, op=dist.ReduceOp.MAX)
             el = float(e.item())
         R = args.row_rounds
+        # parity of the whole loop (every scenario, every round) against
+        # oracle_rounds from the same start: evictions, targets, the final
+        # assign replica and usage, and the final cut count
+        rows_parity = None
+        if rank == 0:
+            from oracle import oracle as orc
+            t_par = time.perf_counter()
+            ea, eu, eev, etg = orc.rounds(c.row_ptr, c.col_idx, c.pod_cpu, a_start, S, c.cap_cpu, u_start, N, R,
+                                          threshold=thr, threads=cpu_threads()[0])
+            ecut = orc.cut_cost(c.row_ptr, c.col_idx, ea, P, S)
+            rows_parity = {
+                "ok": bool(np.array_equal(res["evict"].cpu().numpy().reshape(-1), eev)
+                           and np.array_equal(res["target"].cpu().numpy().reshape(-1), etg)
+                           and np.array_equal(a2.cpu().numpy(), ea) and np.array_equal(res["use"].cpu().numpy(), eu)
+                           and (R == 0 or np.array_equal(res["cut"][-1].cpu().numpy(), ecut))),
+                "scope": f"all {S} scenarios x {R} rounds vs oracle_rounds (evictions, targets, final assign / use, "
+                         f"final cut count)",
+                "seconds": round(time.perf_counter() - t_par, 2)}
         # the same rounds with every librsk call, torch op and collective on the
         # current torch stream (no host sync between phases): the loop's rate
         a3 = T["assign"].clone()
@@ -547,6 +570,7 @@ def main():
                       "setup_ms": round(el0 * 1e3, 4),
                       "steady_ms_per_round": round((el2 - el0) * 1e3 / R, 4),
                       "stream_ordered_matches_synced": same,
+                      "parity": rows_parity,
                       "ms_per_round_phase_synced": round(el * 1e3 / R, 4),
                       "phase_ms_per_round": {k: round(v / R, 4) for k, v in res["ms"].items()},
                       "scoring_only_ms_per_round": round(res["ms"]["place"] / R, 4),
@@ -589,7 +613,7 @@ def main():
         torch.cuda.synchronize(dev)
         ctx.set_profiling(False)
         k3_leg = {}
-        alg3 = {"node_reduce": 4 * P * S + 12 * P + 20 * N * S, "load_std": 8 * N * S + 4 * N,
+        alg3 = {"node_reduce": 4 * P * S + 12 * P + 20 * N * S, "load_std": 4 * N * S + 4 * N,
                 "cut_cost": 4 * (P + 1) + 4 * c.nnz + 4 * P * S + 4 * c.nnz * S}
         for name in ("node_reduce", "load_std", "cut_cost"):
             tms, n = ctx.kernel_time(name)
@@ -597,16 +621,23 @@ def main():
                 k3_leg[name] = {"avg_ms": round(tms / n, 4), "launches_per_call": n // reps,
                                 "algorithmic_bytes": alg3[name],
                                 "algorithmic_GBps": round(alg3[name] / (tms / n / 1e3) / 1e9, 1)}
-        # parity of kernel 3 on a few scenarios' worth of rows: the oracle's sums
+        # parity of kernel 3 over the whole batch (every scenario): the oracle's
+        # node sums and cut count exactly, its std within 1e-9 relative
         from oracle import oracle as orc
-        k = 4
-        sub = np.ascontiguousarray(c.assign.reshape(P, S)[:, :k]).reshape(-1)
-        ecnt, ecpu, emem = orc.node_reduce(sub, P, k, c.pod_cpu, c.pod_mem.astype(np.int64), N)
-        gsl = lambda t: t.view(N, S)[:, :k].cpu().numpy().reshape(-1)  # noqa: E731
-        k3_leg["parity_sample_ok"] = bool(np.array_equal(gsl(cnt), ecnt) and np.array_equal(gsl(cs), ecpu)
-                                          and np.array_equal(gsl(ms_), emem))
+        a_h, u_h = T["assign"].cpu().numpy(), T["use_cpu"].cpu().numpy()   # the inputs k3() read
+        ecnt, ecpu, emem = orc.node_reduce(a_h, P, S, c.pod_cpu, c.pod_mem.astype(np.int64), N)
+        estd = orc.load_std(u_h, c.cap_cpu, N, S)
+        ecut = orc.cut_cost(c.row_ptr, c.col_idx, a_h, P, S)
+        k3_leg["parity_node_reduce_ok"] = bool(np.array_equal(cnt.cpu().numpy(), ecnt)
+                                               and np.array_equal(cs.cpu().numpy(), ecpu)
+                                               and np.array_equal(ms_.cpu().numpy(), emem))
+        k3_leg["parity_load_std_max_rel"] = float(np.max(np.abs(std.cpu().numpy() / estd - 1.0)))
+        k3_leg["parity_cut_cost_ok"] = bool(np.array_equal(cut.cpu().numpy(), ecut))
+        k3_leg["parity_sample_ok"] = bool(k3_leg["parity_node_reduce_ok"] and k3_leg["parity_cut_cost_ok"]
+                                          and k3_leg["parity_load_std_max_rel"] <= 1e-9)
+        k3_leg["parity_sample"] = f"all {S} scenarios of the batch: node_reduce / cut_cost exact, load_std 1e-9 rel"
         k3_leg["note"] = ("algorithmic bytes: node_reduce reads assign + pod cpu/mem and writes the N*S count/cpu/mem"
-                          " words; load_std reads use (+ pct temp); cut_cost reads CSR + assign + one gather per edge")
+                          " words; load_std reads use and cap (its 20 B per (node chunk, scenario) partials not counted); cut_cost reads CSR + assign + one gather per edge")
 
     alg = {k: alg_bytes(k, P, N, S, info) for k in kernels}
     B = algorithmic_bytes(P, N, S, c.nnz)

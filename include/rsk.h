@@ -53,6 +53,13 @@ typedef struct rsk_rounds rsk_rounds;
 
 /* ---- library / context ---------------------------------------------------- */
 int rsk_version(void);                                /* 100*major + minor */
+/* Self-check of the library's u64 workspace layouts for N nodes, S scenarios
+ * and a move table of H slots (host arithmetic only, no device): RSK_OK, or
+ * RSK_EINVAL with rsk_last_error() naming the first u64 slice whose byte
+ * offset is not a multiple of 8.  Every entry point that uses such a layout
+ * runs the same check before launching (a misaligned 64-bit atomic faults the
+ * GPU, DESIGN.md §6 "r04p2"). */
+int rsk_check_ws_layout(int32_t N, int32_t S, int32_t H);
 const char *rsk_last_error(void);                     /* thread-local, never NULL */
 int rsk_ctx_create(int device, rsk_ctx **out);
 int rsk_ctx_destroy(rsk_ctx *ctx);

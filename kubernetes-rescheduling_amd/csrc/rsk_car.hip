@@ -1637,17 +1637,18 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     // zero on entry (cleared by the previous execute's prep kernel, or here
     // when the buffer is new or S changed); this execute's prep clears the
     // other half for the next one — no launch ahead of the prep kernel
-    const size_t zc_half_bytes = ((size_t)S * 12 + 15) & ~(size_t)15;  // 16-B aligned halves (u64 atomics)
+    const size_t zc_half = zc_half_bytes(S);  // 16-B aligned halves (u64 atomics)
+    RSK_TRY(ws_check_u64(N, S, 0));
     if (plan->zc_S != S) {
-        RSK_TRY(plan->zc.reserve(2 * zc_half_bytes));
-        RSK_HIP(hipMemsetAsync(plan->zc.ptr, 0, 2 * zc_half_bytes, ctx->stream));
+        RSK_TRY(plan->zc.reserve(2 * zc_half));
+        RSK_HIP(hipMemsetAsync(plan->zc.ptr, 0, 2 * zc_half, ctx->stream));
         plan->zc_S = S;
         plan->zc_half = 0;
     }
     unsigned char *zc_base = plan->zc.as<unsigned char>();
-    unsigned long long *d_zkey = reinterpret_cast<unsigned long long *>(zc_base + plan->zc_half * zc_half_bytes);
+    unsigned long long *d_zkey = reinterpret_cast<unsigned long long *>(zc_base + plan->zc_half * zc_half);
     int *d_zcnt = reinterpret_cast<int *>(d_zkey + S);
-    unsigned *zc_other = reinterpret_cast<unsigned *>(zc_base + (plan->zc_half ^ 1) * zc_half_bytes);
+    unsigned *zc_other = reinterpret_cast<unsigned *>(zc_base + (plan->zc_half ^ 1) * zc_half);
 
     // K0: node state (codes and / or exact keys) + the zero case, launched below
     Prep16Args pa;
@@ -1661,7 +1662,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     pa.zc_cnt = d_zcnt;
     pa.zc_key = d_zkey;
     pa.zc_clear = zc_other;
-    pa.clear_words = (int)(zc_half_bytes / 4);
+    pa.clear_words = (int)(zc_half / 4);
     SideBufs sb;
     sb.assign = d_assign;
     sb.key = d_key;

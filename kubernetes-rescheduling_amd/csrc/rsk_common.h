@@ -150,6 +150,29 @@ int launch_pick_keys(hipStream_t stream, const int *assign, const int *pod_cpu, 
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// ---- u64 workspace slices (the r04p2 fault class) ----
+// A 64-bit atomic on a word that is not 8-B aligned faults the GPU (r04p2: the
+// plan's second zero-case half at S*12 + 4).  Every workspace layout that holds
+// u64 words takes its slice offsets from the functions below, and the entry
+// points run ws_check_u64() on the layout (and ws_check_ptr() on caller-owned
+// u64 buffers) before any launch: a misaligned slice is RSK_EINVAL naming it.
+constexpr int kBlkNodes = 64;  // nodes per detect block (the rounds loops' block maxima)
+// the plan's zero-case words: two halves of zc_key[S] u64 + zc_cnt[S] int
+inline size_t zc_half_bytes(int64_t S) { return ((size_t)S * 12 + 15) & ~(size_t)15; }
+// a move workgroup's count table: 2H words of hash, then 8 words of which the
+// first two hold the u64 best (car_move_one's red64); one area per workgroup
+inline size_t move_tab_bytes(int64_t H) { return ((size_t)2 * H + 8) * 4; }
+// block maxima [S][NB] u64 bm, [S][NB] u64 bz, [S][NB] int bc (blk / rows blk)
+inline size_t blk_nb(int64_t N) { return (size_t)ceil_div(N, kBlkNodes); }
+struct U64Slice {
+    const char *name;
+    uint64_t off;  // byte offset of the slice's first u64 within its buffer
+};
+constexpr int kMaxU64Slices = 12;
+int ws_u64_layout(int64_t N, int64_t S, int64_t H, U64Slice *out);  // returns the count
+int ws_check_u64(int64_t N, int64_t S, int64_t H);
+int ws_check_ptr(const void *p, const char *name);
+
 // One-launch CAR of a small batch (rsk_rounds.hip): rows [0, Q) of the
 // deduplicated CSR rp / ci (pods rows[i], or i), S scenarios; targets only.
 int launch_car_direct(hipStream_t st, const int *rp, const int *ci, const int *rows, int Q, const int *assign,

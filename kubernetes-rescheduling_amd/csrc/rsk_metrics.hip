@@ -743,21 +743,16 @@ __global__ void decode_first_max(const unsigned long long *__restrict__ key, int
     out[s] = k ? (int)(~(unsigned)(k & 0xffffffffull)) : -1;
 }
 
-// nodemonitor.py:24-46.  100 / cap[n] once per node (-1: cap <= 0, the node
-// is skipped), so the partial pass multiplies instead of dividing per cell.
-__global__ __launch_bounds__(256) void std_inv_kernel(const int *__restrict__ cap, int N, double *__restrict__ inv) {
-    const int n = (int)(blockIdx.x * 256 + threadIdx.x);
-    if (n >= N) return;
-    const int c = cap[n];
-    inv[n] = c > 0 ? 100.0 / (double)c : -1.0;
-}
-
-// Per (node chunk, s): count, chunk mean and M2 in one pass over pct = use *
-// (100 / cap) in fp64, as shifted sums (d = pct - the chunk's first pct: the
-// sum and sum of squares of d, M2 = sq - sum^2 / c — exact 0 for equal
-// values, ~1e-15 relative otherwise, inside the 1e-9 the tests allow against
-// numpy's two-pass std); then per s a fixed-order Chan merge.
-__global__ __launch_bounds__(256) void std_partial_kernel(const int *__restrict__ use, const double *__restrict__ inv,
+// nodemonitor.py:24-46.  Per (node chunk, s): count, chunk mean and M2 in one
+// pass over pct = use / cap * 100 in fp64 — the reference's own operation
+// order (nodemonitor.py:39), so every node's pct is bit-identical to it; nodes
+// with cap <= 0 are skipped (:38-43).  Shifted sums (d = pct - the chunk's
+// first pct: the sum and sum of squares of d, M2 = sq - sum^2 / c — exact 0
+// for equal values, ~1e-15 relative otherwise); then per s a fixed-order Chan
+// merge.  The summation order differs from numpy's pairwise mean and two-pass
+// variance, so the std agrees within tolerance (the tests: 1e-9 relative; the
+// north star: 1e-5), not bit for bit.
+__global__ __launch_bounds__(256) void std_partial_kernel(const int *__restrict__ use, const int *__restrict__ cap,
                                                           int N, int S, int npb, unsigned total,
                                                           double *__restrict__ pmean, double *__restrict__ pm2,
                                                           int *__restrict__ pcnt) {
@@ -770,18 +765,17 @@ __global__ __launch_bounds__(256) void std_partial_kernel(const int *__restrict_
     double sum = 0.0, sq = 0.0, K = 0.0;
     int c = 0;
     for (int n = n0; n < n1; n += kU) {
-        int u[kU];
-        double r[kU];
+        int u[kU], cp[kU];
 #pragma unroll
         for (int k = 0; k < kU; ++k) {
             const int m = min(n + k, n1 - 1);  // clamped: always a valid address
             u[k] = use[(size_t)m * S + s];
-            r[k] = inv[m];
+            cp[k] = cap[m];
         }
 #pragma unroll
         for (int k = 0; k < kU; ++k) {
-            if (n + k < n1 && r[k] >= 0.0) {
-                const double x = (double)u[k] * r[k];
+            if (n + k < n1 && cp[k] > 0) {
+                const double x = (double)u[k] / (double)cp[k] * 100.0;
                 if (c == 0) K = x;
                 const double d = x - K;
                 sum += d;
@@ -1409,13 +1403,11 @@ int rsk_load_std(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *cap_cpu, i
     RSK_TRY(ctx->work[0].reserve((size_t)nch * S * 8));
     RSK_TRY(ctx->work[1].reserve((size_t)nch * S * 8));
     RSK_TRY(ctx->work[2].reserve((size_t)nch * S * 4));
-    RSK_TRY(ctx->work[3].reserve((size_t)N * 8));
     const unsigned total = (unsigned)((int64_t)nch * S);
     {
         ScopedTimer tm(ctx, "load_std");
-        std_inv_kernel<<<(unsigned)ceil_div(N, 256), 256, 0, ctx->stream>>>(d_cap, N, ctx->work[3].as<double>());
         std_partial_kernel<<<(unsigned)ceil_div(total, 256), 256, 0, ctx->stream>>>(
-            d_use, ctx->work[3].as<double>(), N, S, npb, total, ctx->work[0].as<double>(), ctx->work[1].as<double>(),
+            d_use, d_cap, N, S, npb, total, ctx->work[0].as<double>(), ctx->work[1].as<double>(),
             ctx->work[2].as<int>());
         std_merge_kernel<<<(unsigned)ceil_div(S, 4), 256, 0, ctx->stream>>>(
             ctx->work[0].as<double>(), ctx->work[1].as<double>(), ctx->work[2].as<int>(), nch, S, d_out);

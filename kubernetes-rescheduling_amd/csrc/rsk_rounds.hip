@@ -322,7 +322,7 @@ struct MoveGeom {
 MoveGeom move_geometry(rsk_rounds *r, int N, int S) {
     MoveGeom g;
     g.H = next_pow2(std::max(2, 2 * std::min(r->dmax, N)));
-    const size_t bytes = ((size_t)2 * g.H + 8) * 4;
+    const size_t bytes = move_tab_bytes(g.H);
     g.rc = RSK_OK;
     if (bytes <= 160 * 1024) {
         g.lds = bytes;
@@ -566,7 +566,6 @@ __global__ __launch_bounds__(256) void pick_list_kernel(const T *__restrict__ as
 // changes the CPU of two nodes; their 64-node blocks' maxima are recomputed and
 // the scenario's maxima re-reduced over the blocks), the pick over the pod
 // lists, CAR and the update by car_move_one.
-constexpr int kBlkNodes = 64;
 struct BlkArgs {
     unsigned long long *bm;  // [S][NB] packed (pct, ~node) max over the block's hazard nodes (0: none)
     unsigned long long *bz;  // [S][NB] packed (cap - use, ~node) max over its non-hazard nodes
@@ -1068,6 +1067,7 @@ __global__ __launch_bounds__(256) void rows_move_detect_kernel(
     if (moved) {
         int *ae = assign + (size_t)e * S + s;
         o = *ae;
+        __syncthreads();  // every wave holds the old node before wave 0 stores the new one
         if (w == 0) {
             int d = 0;
             if (e >= r0 && e < r1)
@@ -1152,7 +1152,7 @@ int launch_car_direct(hipStream_t st, const int *rp, const int *ci, const int *r
     if (Q <= 0) return RSK_OK;
     int H = 1;
     while (H < std::max(2, 2 * std::min(dmax, N))) H <<= 1;
-    const size_t bytes = ((size_t)2 * H + 8) * 4;
+    const size_t bytes = move_tab_bytes(H);
     const int64_t units = (int64_t)Q * S;
     RSK_CHECK(units < INT32_MAX, "direct grid too large");
     if (bytes <= 160 * 1024) {
@@ -1251,6 +1251,7 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
     RSK_TRY(r->key_ws.reserve((size_t)S * 28));  // the detect and pick keys, the zero case
     const MoveGeom g = move_geometry(r, N, S);
     RSK_TRY(g.rc);
+    RSK_TRY(ws_check_u64(N, S, g.H));
     // the eviction scan reads a u16 shadow of assign when node ids fit (kept in
     // step by the move kernel); otherwise the int32 scan
     static const bool lists_on = RSK_KNOB(RSK_ROUNDS_LISTS, 1) != 0;
@@ -1311,7 +1312,7 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         // one launch for all R rounds: the hazard flags and the block maxima
         // once, then a workgroup per scenario walks its rounds
         PersistArgs pa;
-        pa.ba.NB = (int)ceil_div(N, kBlkNodes);
+        pa.ba.NB = (int)blk_nb(N);
         const size_t nbs = (size_t)S * pa.ba.NB;
         RSK_TRY(r->blk.reserve(nbs * 20));
         pa.ba.bm = r->blk.as<unsigned long long>();
@@ -1346,7 +1347,7 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         }
         // the scenario's block row in LDS while it fits beside the hash
         const size_t blk_bytes = (size_t)pa.ba.NB * 20;
-        pa.hash_bytes = (unsigned)g.lds;
+        pa.hash_bytes = (unsigned)g.lds;  // move_tab_bytes(H) or 0: the block row's u64 slices start 8-B aligned
         pa.blk_lds = blk_bytes <= 32 * 1024 && g.lds + blk_bytes <= 160 * 1024;
         const size_t lds = g.lds + (pa.blk_lds ? blk_bytes : 0);
         ScopedTimer tm(ctx, "rounds_persist");
@@ -1520,6 +1521,8 @@ int rsk_rows_pick(rsk_ctx *ctx, const void *rows, int32_t elem_bytes, int32_t q,
     RSK_CHECK((flags & RSK_F_DEVICE) && pod_cpu && key_most && key_evict && (elem_bytes == 2 || elem_bytes == 4) &&
                   q >= 0 && S > 0 && r0 >= 0 && (q == 0 || rows),
               "rsk_rows_pick: device pointers, 2- or 4-byte rows required");
+    RSK_TRY(ws_check_ptr(key_most, "key_most"));
+    RSK_TRY(ws_check_ptr(key_evict, "key_evict"));
     if (q == 0) return RSK_OK;
     const int ppt = (int)std::max<int64_t>(1, ceil_div((int64_t)q * S, (int64_t)256 * 2048));
     const int64_t tot = ceil_div(q, ppt) * S;
@@ -1547,8 +1550,12 @@ int rsk_rows_place(rsk_rounds *r, const int32_t *assign, int32_t S, const int32_
                   zc_key && out_evict && out_target && S > 0 && N > 0 && 0 <= r0 && r0 <= r1 && r1 <= r->P &&
                   (int64_t)N * S < INT32_MAX && (int64_t)r->P * S < INT32_MAX,
               "rsk_rows_place: device pointers and rows [%d, %d) of P=%d required", r0, r1, r->P);
+    RSK_TRY(ws_check_ptr(key_most, "key_most"));
+    RSK_TRY(ws_check_ptr(key_evict, "key_evict"));
+    RSK_TRY(ws_check_ptr(zc_key, "zc_key"));
     const MoveGeom g = move_geometry(r, N, S);
     RSK_TRY(g.rc);
+    RSK_TRY(ws_check_u64(N, S, g.H));
     ScopedTimer tm(ctx, "rows_place");
     return launch_move(r, ctx->stream, g, const_cast<int *>(assign), const_cast<int *>(use_cpu), cap_cpu, hazard,
                        nullptr, S, N, 0, out_target, nullptr, reinterpret_cast<unsigned long long *>(key_evict),
@@ -1558,12 +1565,12 @@ int rsk_rows_place(rsk_rounds *r, const int32_t *assign, int32_t S, const int32_
 
 int64_t rsk_rows_blk_bytes(int32_t N, int32_t S) {
     if (N <= 0 || S <= 0) return 0;
-    return (int64_t)S * ceil_div(N, kBlkNodes) * 20;
+    return (int64_t)S * (int64_t)blk_nb(N) * 20;
 }
 
 static BlkArgs blk_args(void *blk, int N, int S) {
     BlkArgs ba;
-    ba.NB = (int)ceil_div(N, kBlkNodes);
+    ba.NB = (int)blk_nb(N);
     const size_t nbs = (size_t)S * ba.NB;
     ba.bm = static_cast<unsigned long long *>(blk);
     ba.bz = ba.bm + nbs;
@@ -1578,6 +1585,10 @@ int rsk_rows_detect_setup(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *c
     RSK_CHECK((flags & RSK_F_DEVICE) && use_cpu && cap_cpu && out_hazard && blk && key_most && zc_cnt && zc_key &&
                   N > 0 && S > 0 && (int64_t)N * S < INT32_MAX,
               "rsk_rows_detect_setup: device pointers and N, S > 0 required");
+    RSK_TRY(ws_check_ptr(blk, "blk"));
+    RSK_TRY(ws_check_ptr(key_most, "key_most"));
+    RSK_TRY(ws_check_ptr(zc_key, "zc_key"));
+    RSK_TRY(ws_check_u64(N, S, 0));
     const BlkArgs ba = blk_args(blk, N, S);
     ScopedTimer tm(ctx, "rows_detect");
     const int64_t waves = (int64_t)ba.NB * ceil_div(S, 64);
@@ -1604,6 +1615,10 @@ int rsk_rows_move(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, 
     if (blk) {  // the usage replica and the detection kept in step
         RSK_CHECK(use_cpu && cap_cpu && hazard && key_most && zc_cnt && zc_key,
                   "rsk_rows_move: the detect state (use, cap, hazard, keys) is required with blk");
+        RSK_TRY(ws_check_ptr(blk, "blk"));
+        RSK_TRY(ws_check_ptr(key_most, "key_most"));
+        RSK_TRY(ws_check_ptr(zc_key, "zc_key"));
+        RSK_TRY(ws_check_u64(N, S, 0));
         rows_move_detect_kernel<<<(unsigned)S, 256, 0, ctx->stream>>>(
             row_ptr, col_idx, rev_ptr, rev_idx, P, r0, r1, assign, S, evict, target, N, pod_cpu,
             reinterpret_cast<const long long *>(pod_mem), reinterpret_cast<long long *>(cpu_part),

@@ -145,13 +145,50 @@ int copy_back(rsk_ctx *ctx, void *host_dst, const void *dev_src, size_t bytes, b
     return RSK_OK;
 }
 
+int ws_u64_layout(int64_t N, int64_t S, int64_t H, U64Slice *out) {
+    int n = 0;
+    auto add = [&](const char *name, uint64_t off) { out[n++] = U64Slice{name, off}; };
+    const uint64_t nbs = (uint64_t)S * blk_nb(N);
+    add("plan.zc zc_key half 0", 0);
+    add("plan.zc zc_key half 1", zc_half_bytes(S));
+    add("rounds.key_ws kdet", 0);
+    add("rounds.key_ws kpick", (uint64_t)S * 8);
+    add("rounds.key_ws zc_key", (uint64_t)S * 16);
+    add("blk bm", 0);
+    add("blk bz", nbs * 8);
+    add("move table red64", (uint64_t)H * 8);
+    add("move global area 1", move_tab_bytes(H));
+    add("persist LDS bm", move_tab_bytes(H));
+    add("persist LDS bz", move_tab_bytes(H) + (uint64_t)blk_nb(N) * 8);
+    return n;
+}
+
+int ws_check_u64(int64_t N, int64_t S, int64_t H) {
+    U64Slice sl[kMaxU64Slices];
+    const int n = ws_u64_layout(N, S, H, sl);
+    for (int i = 0; i < n; ++i)
+        RSK_CHECK(sl[i].off % 8 == 0, "workspace slice '%s' at byte %llu is not 8-B aligned (N=%lld S=%lld H=%lld)",
+                  sl[i].name, (unsigned long long)sl[i].off, (long long)N, (long long)S, (long long)H);
+    return RSK_OK;
+}
+
+int ws_check_ptr(const void *p, const char *name) {
+    RSK_CHECK(((uintptr_t)p & 7) == 0, "u64 buffer '%s' at %p is not 8-B aligned", name, p);
+    return RSK_OK;
+}
+
 }  // namespace rsk
 
 using namespace rsk;
 
 extern "C" {
 
-int rsk_version(void) { return 104; }  // 1.04: the fused row-sharded round, RSK_F_TILED
+int rsk_version(void) { return 105; }  // 1.05: rsk_check_ws_layout
+
+int rsk_check_ws_layout(int32_t N, int32_t S, int32_t H) {
+    RSK_CHECK(N > 0 && S > 0 && H >= 0, "bad sizes N=%d S=%d H=%d", N, S, H);
+    return ws_check_u64(N, S, H);
+}
 
 const char *rsk_last_error(void) { return rsk::last_error(); }
 

@@ -33,6 +33,7 @@ _vp = C.c_void_p
 # same signature carries host (numpy) and device (HBM) pointers.
 SIGNATURES = {
     "rsk_version": (C.c_int, []),
+    "rsk_check_ws_layout": (C.c_int, [C.c_int32, C.c_int32, C.c_int32]),
     "rsk_last_error": (C.c_char_p, []),
     "rsk_ctx_create": (C.c_int, [C.c_int, C.POINTER(_vp)]),
     "rsk_ctx_destroy": (C.c_int, [_vp]),

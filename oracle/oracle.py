@@ -55,6 +55,8 @@ def lib():
         L.oracle_cut_cost.restype = None
         L.oracle_rounds.argtypes = [vp, vp, i32, vp, vp, i32, vp, vp, i32, i32, i32, vp, vp]
         L.oracle_rounds.restype = None
+        L.oracle_rounds_par.argtypes = L.oracle_rounds.argtypes + [C.c_int]
+        L.oracle_rounds_par.restype = None
         _lib = L
     return _lib
 
@@ -179,12 +181,33 @@ def dedup_csr(row_ptr, col_idx):
     return np.array(rp, np.int32), np.array(ci if ci else [0], np.int32)
 
 
-def rounds(row_ptr, col_idx, pod_cpu, assign, S, cap, use, N, R, threshold=30):
-    """The multi-round loop (oracle_rounds); returns (assign', use', evict[R*S], target[R*S])."""
-    rp, ci = dedup_csr(row_ptr, col_idx)
+def dedup_csr_fast(row_ptr, col_idx):
+    """dedup_csr in numpy (same rows: sorted, unique, no self edge), for graphs
+    of 10^5-10^6 rows."""
+    rp = np.asarray(row_ptr, np.int64)
+    ci = np.asarray(col_idx[:rp[-1]], np.int64)
+    P = len(rp) - 1
+    row = np.repeat(np.arange(P, dtype=np.int64), np.diff(rp))
+    key = np.unique(row * (P + 1) + ci)
+    r, q = key // (P + 1), key % (P + 1)
+    keep = r != q
+    r, q = r[keep], q[keep]
+    out_rp = np.zeros(P + 1, np.int32)
+    np.cumsum(np.bincount(r, minlength=P), out=out_rp[1:])
+    return out_rp, (q.astype(np.int32) if q.size else np.zeros(1, np.int32))
+
+
+def rounds(row_ptr, col_idx, pod_cpu, assign, S, cap, use, N, R, threshold=30, threads=0):
+    """The multi-round loop (oracle_rounds); returns (assign', use', evict[R*S], target[R*S]).
+    threads > 0: oracle_rounds_par, the scenarios split over that many threads."""
+    rp, ci = dedup_csr_fast(row_ptr, col_idx) if threads else dedup_csr(row_ptr, col_idx)
     P = len(rp) - 1
     a, u = np.array(assign, np.int32).copy(), np.array(use, np.int32).copy()
     pc, c = _c(pod_cpu, np.int32), _c(cap, np.int32)
     ev, tg = np.empty(max(R * S, 1), np.int32), np.empty(max(R * S, 1), np.int32)
-    lib().oracle_rounds(_p(rp), _p(ci), P, _p(pc), _p(a), S, _p(c), _p(u), N, threshold, R, _p(ev), _p(tg))
+    if threads:
+        lib().oracle_rounds_par(_p(rp), _p(ci), P, _p(pc), _p(a), S, _p(c), _p(u), N, threshold, R, _p(ev), _p(tg),
+                                threads)
+    else:
+        lib().oracle_rounds(_p(rp), _p(ci), P, _p(pc), _p(a), S, _p(c), _p(u), N, threshold, R, _p(ev), _p(tg))
     return a, u, ev[:R * S], tg[:R * S]

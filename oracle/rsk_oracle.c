@@ -448,17 +448,17 @@ void oracle_load_std(const int32_t *use, const int32_t *cap, int32_t N, int32_t 
 void oracle_cut_cost(const int32_t *row_ptr, const int32_t *col_idx, int32_t P,
                      const int32_t *assign, int32_t S, const int32_t *missing, int64_t *out_directed)
 {
-    for (int32_t s = 0; s < S; ++s) {
-        int64_t c = 0;
-        for (int32_t p = 0; p < P; ++p) {
-            int32_t a = assign[(int64_t)p * S + s];
-            for (int32_t k = row_ptr[p]; k < row_ptr[p + 1]; ++k) {
-                int32_t b = assign[(int64_t)col_idx[k] * S + s];
-                c += (a != b);
-            }
-            if (missing && a != -1) c += missing[p];
+    /* the same integer count per scenario, walked row-major so the scenario
+     * words of a row are contiguous (an exact sum: the order does not matter) */
+    memset(out_directed, 0, sizeof(int64_t) * (size_t)S);
+    for (int32_t p = 0; p < P; ++p) {
+        const int32_t *ap = assign + (int64_t)p * S;
+        for (int32_t k = row_ptr[p]; k < row_ptr[p + 1]; ++k) {
+            const int32_t *bq = assign + (int64_t)col_idx[k] * S;
+            for (int32_t s = 0; s < S; ++s) out_directed[s] += (ap[s] != bq[s]);
         }
-        out_directed[s] = c;
+        if (missing && missing[p])
+            for (int32_t s = 0; s < S; ++s) out_directed[s] += (ap[s] != -1) ? missing[p] : 0;
     }
 }
 
@@ -505,4 +505,45 @@ void oracle_rounds(const int32_t *row_ptr, const int32_t *col_idx, int32_t P, co
     free(haz);
     free(most);
     free(score);
+}
+
+/* oracle_rounds over the S scenarios in parallel.  Scenarios never share
+ * state in main.py's loop as restated above (each one's assign / use column,
+ * hazard flags and most-hazardous node are its own), so scenario s is the
+ * S = 1 run of oracle_rounds on its own contiguous columns: gathered, run,
+ * scattered back.  Same results as oracle_rounds (tests/test_rounds.py pins
+ * the two to each other); a thread per scenario at a time. */
+void oracle_rounds_par(const int32_t *row_ptr, const int32_t *col_idx, int32_t P, const int32_t *pod_cpu,
+                       int32_t *assign, int32_t S, const int32_t *cap, int32_t *use, int32_t N,
+                       int32_t threshold, int32_t R, int32_t *out_evict, int32_t *out_target, int nthreads)
+{
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel
+#endif
+    {
+        int32_t *a = (int32_t *)malloc(sizeof(int32_t) * (size_t)(P > 0 ? P : 1));
+        int32_t *u = (int32_t *)malloc(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
+        int32_t *ev = (int32_t *)malloc(sizeof(int32_t) * (size_t)(R > 0 ? R : 1));
+        int32_t *tg = (int32_t *)malloc(sizeof(int32_t) * (size_t)(R > 0 ? R : 1));
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+        for (int32_t s = 0; s < S; ++s) {
+            for (int64_t p = 0; p < P; ++p) a[p] = assign[p * S + s];
+            for (int64_t n = 0; n < N; ++n) u[n] = use[n * S + s];
+            oracle_rounds(row_ptr, col_idx, P, pod_cpu, a, 1, cap, u, N, threshold, R, ev, tg);
+            for (int64_t p = 0; p < P; ++p) assign[p * S + s] = a[p];
+            for (int64_t n = 0; n < N; ++n) use[n * S + s] = u[n];
+            for (int64_t r = 0; r < R; ++r) {
+                out_evict[r * S + s] = ev[r];
+                out_target[r * S + s] = tg[r];
+            }
+        }
+        free(a);
+        free(u);
+        free(ev);
+        free(tg);
+    }
+    (void)nthreads;
 }

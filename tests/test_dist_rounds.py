@@ -124,7 +124,7 @@ def _expected(c, pod_cpu, R):
     return np.array(ev), np.array(tg), np.array(cut), a, u
 
 
-def _worker(rank, world, port, R, out_q, use_gpu, pg="gloo", ordered=False, fused=True):
+def _worker(rank, world, port, R, out_q, use_gpu, pg="gloo", ordered=False, fused=True, case=None):
     import sys
     sys.path[:0] = [PKG, REPO]
     import torch
@@ -143,7 +143,7 @@ def _worker(rank, world, port, R, out_q, use_gpu, pg="gloo", ordered=False, fuse
     dist.init_process_group(pg, rank=rank, world_size=world)
     try:
         import contextlib
-        c, pod_cpu, pod_mem = _case()
+        c, pod_cpu, pod_mem = _case(**(case or {}))
         dev = torch.device("cuda:0" if use_gpu else "cpu")
         sh = rdist.row_shard_for(rank, world, c.row_ptr)
         T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
@@ -171,11 +171,12 @@ def _worker(rank, world, port, R, out_q, use_gpu, pg="gloo", ordered=False, fuse
         dist.destroy_process_group()
 
 
-def _run(world, R, use_gpu=False, pg="gloo", ordered=False, fused=True):
+def _run(world, R, use_gpu=False, pg="gloo", ordered=False, fused=True, case=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, R, q, use_gpu, pg, ordered, fused)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, R, q, use_gpu, pg, ordered, fused, case))
+             for r in range(world)]
     for p in procs:
         p.start()
     outs = []
@@ -279,5 +280,71 @@ def test_row_sharded_rounds_unfused_world2(ordered):
     c, pod_cpu, _ = _case()
     ev, tg, cut, a, u = _expected(c, pod_cpu, R)
     for rank, e, t, k, a_r, u_r in _run(2, R, use_gpu=True, ordered=ordered, fused=False):
+        assert np.array_equal(e, ev) and np.array_equal(t, tg), f"rank {rank}"
+        assert np.array_equal(k, cut) and np.array_equal(a_r, a) and np.array_equal(u_r, u), f"rank {rank}"
+
+
+# N = 300 nodes (five 64-node blocks): moves between blocks, so the fused move
+# launch re-reduces the old node's block beside the new one's (wave 1's
+# blk_update) and the scenario's maxima over several blocks (scn_reduce)
+BIG = dict(seed=7, P=6000, N=300, S=64)
+
+
+def _cross_block_moves(c, ev, tg):
+    """Moves whose pod leaves one 64-node block for another, replayed in order."""
+    a = c.assign.copy().reshape(c.P, c.S)
+    n = 0
+    for e_r, t_r in zip(ev, tg):
+        for s in range(c.S):
+            e, t = int(e_r[s]), int(t_r[s])
+            if e >= 0 and t >= 0:
+                n += int(a[e, s] // 64 != t // 64)
+                a[e, s] = t
+    return n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,pg", [(1, "nccl"), (2, "gloo")])
+def test_row_sharded_rounds_fused_cross_block(world, pg):
+    """the fused row-sharded round (rsk_rows_detect_setup / _pick /
+    _place / _move with the block maxima) at N = 300 over 12 rounds, world 1
+    over RCCL and world 2 over gloo, against oracle_rounds round by round;
+    most moves cross 64-node blocks."""
+    R = 12
+    c, pod_cpu, _ = _case(**BIG)
+    ev, tg, cut, a, u = _expected(c, pod_cpu, R)
+    assert (tg >= 0).sum() > R * c.S // 2
+    assert _cross_block_moves(c, ev, tg) > R * c.S // 4
+    for rank, e, t, k, a_r, u_r in _run(world, R, use_gpu=True, pg=pg, case=BIG):
+        assert np.array_equal(e, ev) and np.array_equal(t, tg), f"rank {rank}"
+        assert np.array_equal(k, cut) and np.array_equal(a_r, a) and np.array_equal(u_r, u), f"rank {rank}"
+
+
+@pytest.mark.gpu
+def test_row_sharded_rounds_fused_equals_unfused_world2():
+    """The fused round and the per-phase calls give the same rounds at N = 300."""
+    R = 12
+    f = _run(2, R, use_gpu=True, case=BIG)
+    g = _run(2, R, use_gpu=True, fused=False, case=BIG)
+    for x, y in zip(f, g):
+        for a_, b_ in zip(x[1:], y[1:]):
+            assert np.array_equal(a_, b_)
+
+
+def test_cross_block_case_moves_between_blocks():
+    """CPU: the BIG case really moves pods between 64-node blocks (oracle)."""
+    R = 12
+    c, pod_cpu, _ = _case(**BIG)
+    ev, tg, cut, a, u = _expected(c, pod_cpu, R)
+    assert (tg >= 0).sum() > R * c.S // 2
+    assert _cross_block_moves(c, ev, tg) > R * c.S // 4
+
+
+def test_row_sharded_rounds_cross_block_gloo_world2_cpu():
+    """The BIG case through the row-sharded loop on CPU (gloo, oracle backend)."""
+    R = 6
+    c, pod_cpu, _ = _case(**BIG)
+    ev, tg, cut, a, u = _expected(c, pod_cpu, R)
+    for rank, e, t, k, a_r, u_r in _run(2, R, case=BIG):
         assert np.array_equal(e, ev) and np.array_equal(t, tg), f"rank {rank}"
         assert np.array_equal(k, cut) and np.array_equal(a_r, a) and np.array_equal(u_r, u), f"rank {rank}"

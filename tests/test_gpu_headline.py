@@ -122,7 +122,8 @@ def test_config4_1m50k_s64(ctx):
 
 def _rounds_vs_oracle(ctx, c, S, R, k, threshold=30):
     """rsk_rounds_run over all S scenarios for R rounds; its first k scenarios
-    against oracle_rounds (final state, evictions and targets of every round)."""
+    (k = S: all of them) against oracle_rounds (final state, evictions and
+    targets of every round), the scenarios split over THREADS oracle threads."""
     from oracle import oracle as orc
     from rsk import api
     P, N = c.P, c.N
@@ -132,7 +133,8 @@ def _rounds_vs_oracle(ctx, c, S, R, k, threshold=30):
     a, u = c.assign.copy(), c.use_cpu.copy()
     ev, tg = rounds.run(a, S, c.cap_cpu, u, N, R, threshold=threshold)
     rounds.close()
-    ea, eu, eev, etg = orc.rounds(c.row_ptr, c.col_idx, c.pod_cpu, a0, k, c.cap_cpu, u0, N, R, threshold=threshold)
+    ea, eu, eev, etg = orc.rounds(c.row_ptr, c.col_idx, c.pod_cpu, a0, k, c.cap_cpu, u0, N, R, threshold=threshold,
+                                  threads=THREADS)
     got_t = tg.reshape(R, S)[:, :k]
     bad = np.argwhere(got_t != etg.reshape(R, k))
     assert bad.size == 0, f"targets differ first at round {bad[0][0]} scenario {bad[0][1]}"
@@ -146,11 +148,12 @@ def _rounds_vs_oracle(ctx, c, S, R, k, threshold=30):
 def test_config5_rounds_100k_s1024(ctx, R):
     """100k/5k x 1024 scenarios, R rounds of detect -> evict -> CAR -> update on
     the device: R = 10 is the reference's MAX_ROUNDS (main.py:28), R = 256
-    config 5's loop length; the first 16 scenarios against oracle_rounds."""
+    config 5's loop length; ALL 1,024 scenarios against oracle_rounds (every
+    round's eviction and target, the final assign and use)."""
     from rsk import synth
     c = synth.make_cluster(100_000, 5_000, S=1024, seed=0)
-    etg = _rounds_vs_oracle(ctx, c, 1024, R, 16)
-    assert (etg >= 0).sum() > R * 16 // 2  # real moves happened
+    etg = _rounds_vs_oracle(ctx, c, 1024, R, 1024)
+    assert (etg >= 0).sum() > R * 1024 // 2  # real moves happened
 
 
 def test_rounds_none_and_no_candidate_mid_run(ctx):
@@ -210,3 +213,47 @@ def test_rounds_hub_above_4096_neighbours(ctx, P, N, deg):
     assert (eev == 5).sum() > R * S // 2      # the hub is the evicted pod in most rounds
     etg = _rounds_vs_oracle(ctx, c, S, R, S)
     assert (etg >= 0).sum() > R * S // 2
+
+
+def test_kernel3_config4_1m50k_s64(ctx):
+    """North-star kernel 3 at config 4's shape (1M pods x 50k nodes x 64
+    scenarios): rsk_load_std (1,021 node chunks per scenario, so every merge
+    lane folds 16 chunks before the butterfly) with 700 nodes of cap <= 0
+    mixed in, and a near-constant-pct batch that stresses the shifted sums;
+    rsk_cut_cost over all 1M rows (with and without `missing`) and
+    rsk_node_reduce over all 64 M cells, against the oracle
+    (nodemonitor.py:24-46, communicationcost.py:37-45, podmonitor.py:104-121).
+    The std within 1e-9 relative (north star: 1e-5), the rest exact."""
+    from oracle import oracle as orc
+    from rsk import api, synth
+    P, N, S = 1_000_000, 50_000, 64
+    c = synth.make_cluster(P, N, S=S, seed=0)
+    rng = np.random.default_rng(11)
+    cap = c.cap_cpu.copy()
+    cap[rng.choice(N, 500, replace=False)] = 0
+    cap[rng.choice(N, 200, replace=False)] = -7
+    std = api.load_std(c.use_cpu, cap, N, S, ctx=ctx)
+    ostd = orc.load_std(c.use_cpu, cap, N, S)
+    assert np.allclose(std, ostd, rtol=1e-9, atol=0), f"max rel {np.max(np.abs(std / ostd - 1))}"
+    # near-constant pct: every node at ~37 % with a +-1-millicore jitter
+    base = (cap.astype(np.int64) * 37 // 100).clip(0)
+    use2 = (base[:, None] + rng.integers(-1, 2, (N, S))).clip(0).astype(np.int32).reshape(-1)
+    std2 = api.load_std(use2, cap, N, S, ctx=ctx)
+    ostd2 = orc.load_std(use2, cap, N, S)
+    assert (ostd2 < 0.05).all() and (ostd2 > 0).all()
+    assert np.allclose(std2, ostd2, rtol=1e-9, atol=1e-12), f"max rel {np.max(np.abs(std2 / ostd2 - 1))}"
+    # every pct equal (use = cap / 2 on even caps): std 0 on both sides, to rounding
+    cap3 = (cap // 2) * 2
+    use3 = np.repeat((cap3 // 2).clip(0)[:, None], S, axis=1).astype(np.int32).reshape(-1)
+    assert np.allclose(api.load_std(use3, cap3, N, S, ctx=ctx), orc.load_std(use3, cap3, N, S), rtol=0, atol=1e-12)
+    cut = api.cut_cost(c.row_ptr, c.col_idx, c.assign, P, S, ctx=ctx)
+    assert np.array_equal(cut, orc.cut_cost(c.row_ptr, c.col_idx, c.assign, P, S))
+    miss = rng.integers(0, 3, P).astype(np.int32)
+    a2 = c.assign.copy()
+    a2[rng.choice(P * S, 100_000, replace=False)] = -1
+    assert np.array_equal(api.cut_cost(c.row_ptr, c.col_idx, a2, P, S, miss, ctx=ctx),
+                          orc.cut_cost(c.row_ptr, c.col_idx, a2, P, S, miss))
+    got = api.node_reduce(c.assign, P, S, c.pod_cpu, c.pod_mem, N, ctx=ctx)
+    exp = orc.node_reduce(c.assign, P, S, c.pod_cpu, c.pod_mem.astype(np.int64), N)
+    for g, e, name in zip(got, exp, ("count", "cpu", "mem")):
+        assert np.array_equal(g, e), name

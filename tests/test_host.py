@@ -38,6 +38,22 @@ def test_rows_blk_bytes_host_only():
     assert lib.rsk_rows_blk_bytes(0, 8) == 0 and lib.rsk_rows_blk_bytes(8, 0) == 0
 
 
+def test_u64_workspace_slices_aligned_for_every_s():
+    """The r04p2 fault class (a 64-bit atomic on a misaligned workspace word):
+    rsk_check_ws_layout runs the layout arithmetic every entry point checks
+    before it launches (the plan's zero-case halves, the rounds keys, the block
+    maxima, the move tables and the persistent loop's LDS block row) for
+    S = 1..4,100 at several node counts and move-table sizes: every u64 slice
+    starts on an 8-B boundary.  Host arithmetic only (no device)."""
+    from rsk import _lib
+    lib = _lib.load_library()
+    for N in (1, 63, 64, 65, 5_000, 50_000):
+        for H in (0, 2, 4, 1024, 1 << 16):
+            bad = [S for S in range(1, 4101) if lib.rsk_check_ws_layout(N, S, H) != 0]
+            assert not bad, f"N={N} H={H}: misaligned at S={bad[:5]}: {lib.rsk_last_error().decode()}"
+    assert lib.rsk_check_ws_layout(0, 1, 2) != 0 and lib.rsk_check_ws_layout(5, 0, 2) != 0
+
+
 def test_library_is_gfx950_code_object():
     """The embedded device code object targets gfx950 (and nothing else)."""
     so = os.path.join(REPO, "kubernetes-rescheduling_amd", "rsk", "librsk.so")

@@ -71,6 +71,35 @@ def test_oracle_rounds_equals_composition(seed, thr, moves):
         assert (got[3][got[2] >= 0] == -2).all()
 
 
+@pytest.mark.parametrize("seed,thr,S,threads", [(1, 30, 6, 3), (2, 34, 37, 8), (3, 10, 5, 2), (4, 45, 64, 1)])
+def test_oracle_rounds_par_equals_serial(seed, thr, S, threads):
+    """oracle_rounds_par (each scenario an S = 1 run on its own columns, the
+    scenarios split over threads) gives oracle_rounds' results; its numpy
+    CSR dedup gives dedup_csr's rows (duplicates and self edges included)."""
+    from oracle import oracle as orc
+    c, pod_cpu, cap, use = _case(seed, P=600, N=20, S=S)
+    rng = np.random.default_rng(seed)
+    extra = rng.integers(0, c.P, 200).astype(np.int32)           # duplicate edges and self edges
+    rows = rng.integers(0, c.P, 200)
+    rp, ci = c.row_ptr.astype(np.int64), c.col_idx[:c.row_ptr[-1]].astype(np.int64)
+    lists = [list(ci[rp[p]:rp[p + 1]]) for p in range(c.P)]
+    for r, q in zip(rows, extra):
+        lists[r] += [q, q, r]
+    rp2 = np.zeros(c.P + 1, np.int32)
+    rp2[1:] = np.cumsum([len(x) for x in lists])
+    ci2 = np.array([q for x in lists for q in x], np.int32)
+    a1, b1 = orc.dedup_csr(rp2, ci2)
+    a2, b2 = orc.dedup_csr_fast(rp2, ci2)
+    assert np.array_equal(a1, a2) and np.array_equal(b1[:a1[-1]], b2[:a2[-1]])
+    R = 20
+    ser = orc.rounds(rp2, ci2, pod_cpu, c.assign, S, cap, use, c.N, R, thr)
+    par = orc.rounds(rp2, ci2, pod_cpu, c.assign, S, cap, use, c.N, R, thr, threads=threads)
+    for g, e, name in zip(par, ser, ("assign", "use", "evict", "target")):
+        assert np.array_equal(g, e), name
+    if thr != 10:
+        assert (ser[3] >= 0).any()  # real moves
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed,thr,S", [(1, 30, 6), (2, 45, 64), (3, 10, 65), (4, 30, 1)])
 def test_gpu_rounds_match_oracle(seed, thr, S):

@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-4 GPU session on one box.  usage: tools/gpu_r04.sh OUTDIR [steps...]
+# Round-5 GPU session on one box.  usage: tools/gpu_r05.sh OUTDIR [steps...]
 # steps: test (pytest -m gpu), smoke, bench (headline), b2k (config 2),
 #        b1m (config 4), brounds (config 5), prof (rocprof trace + PMC of headline
 #        and 1m50k), profh / prof1m (one config), dropin
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
-out=gpurun_out/${1:-r04}; shift
+out=gpurun_out/${1:-r05}; shift
 mkdir -p "$out"
 export TMPDIR=/tmp
 step() {  # step <name> <seconds> <cmd...>
