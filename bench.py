@@ -4,8 +4,10 @@
 Workload (BASELINE.json configs[2]): 100k pods, 5k
 nodes, preferential-attachment relation tree, S = 4096 what-if scenarios per
 GPU.  One step = one pass of the hot path over one batch: librsk's CAR pipeline
-(car_prep, the lean tiles fused with the side rows, the heavy tiles) scores every pod in every scenario against
-every node — P·N·S evaluations — with all inputs resident in HBM.
+(car_prep, then the tiles fused with the side rows in one launch — car_tile —
+and, at config 4, the largest side rows beside them on a second stream —
+car_side) scores every pod in every scenario against every node — P·N·S
+evaluations — with all inputs resident in HBM.
 
 Multi-GPU: ``python bench.py --gpus N`` with no ``WORLD_SIZE`` in the
 environment starts ``torch.distributed.run --nproc-per-node N`` on itself as a
@@ -201,11 +203,12 @@ def algorithmic_bytes(P, N, S, nnz, Q_light=None, light_rec_bytes=0):
 
 def alg_bytes(kernel, P, N, S, info):
     """Algorithmic bytes per step of one kernel timer (DESIGN.md "Roofline accounting"):
-      car_tile : the lean launch (tiles + the side rows fused into it) and the heavy tile launch:
-                 the assign slice of every distinct neighbour pod of those rows once (4·S per pod)
-                 + every row's target (4·S) + the tile plan and side items
+      car_tile : the tile launch (tiles + the side rows fused into it): the assign slice of every
+                 distinct neighbour pod of those rows once (4·S per pod) + every row's target (4·S)
+                 + the tile plan and side items
       car_side : target of each side row launched on its own (4·S) + side items / neighbour lists
                  (its neighbours' slices: re-reads of pods the tiles stage, not counted)
+      car_mid / car_heavy : the wide path's (N > 65535) side rows
       car_prep : use + hazard (5·N·S) + cap (4·N) read, the 16-bit code (2·N·S) written
     """
     fused = info.get("fused_side_rows", 0)
@@ -289,7 +292,7 @@ def bench_rounds(args, cfg, world, rank, local, dev):
         ctx.set_profiling(False)
         T["assign"].copy_(a_keep)
         T["use_cpu"].copy_(u_keep)
-        for name in ("rounds_lists", "rounds_shadow", "rounds_detect", "rounds_pick", "rounds_move", "rounds_persist"):
+        for name in ("rounds_lists", "rounds_detect", "rounds_persist"):
             ms, n = ctx.kernel_time(name)
             if n:
                 kernels[name] = {"avg_ms": ms / n, "launches": n, "per_step_ms": ms / args.steps}
@@ -407,9 +410,7 @@ def main():
     def step():
         plan.execute(T["assign"], S, T["cap_cpu"], T["use_cpu"], T["hazard"], N, out_t, None, device=True)
 
-    names = ("car_prep", "car_tile", "car_tile_heavy", "car_side", "car_side32", "car_side128", "car_side512",
-             "car_side2048", "car_side8192", "car_side65535", "car_slot", "car_mid", "car_heavy", "car_hub128",
-             "car_hub256", "car_hub512", "car_hub1024", "car_hub2048", "car_hub4096")
+    names = ("car_direct", "car_prep", "car_tile", "car_side", "car_mid", "car_heavy")   # librsk's CAR timers
 
     def collect():
         out = {}

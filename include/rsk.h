@@ -67,8 +67,8 @@ int rsk_ctx_destroy(rsk_ctx *ctx);
 int rsk_ctx_set_stream(rsk_ctx *ctx, void *hip_stream);
 int rsk_ctx_synchronize(rsk_ctx *ctx);
 /* Kernel timing with HIP events recorded on the stream of every launch of the
- * named kernel group: "car_prep" (the node-code pass), "car_tile" (the fused
- * lean tile + side launch; the heavy tile launch in RSK_LEAN32=0 builds),
+ * named kernel group: "car_prep" (the node-code pass), "car_tile" (the tile
+ * launch, with the side rows fused into it),
  * "car_direct" (a small batch's one launch), "car_side" (side rows launched
  * on their own, e.g. config 4's rows beyond the fused grid on the side stream),
  * "car_mid" / "car_heavy" (the wide path's 33..64 and hub rows, N > 65535),

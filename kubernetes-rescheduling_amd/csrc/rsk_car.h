@@ -307,6 +307,11 @@ __device__ __forceinline__ int block_capmax(const int *__restrict__ cap, int N, 
     return mc;
 }
 
+// chunks per group in the tile grid order (each group walked tile-major inside
+// its XCD's run: 0.8175-0.8202 -> 0.8150-0.8164 ms at config 3; groups of 8
+// are as fast but re-fetch 0.36 GB more code lines)
+constexpr int kTileGroup = 4;
+
 struct Tile16Args {
     const int *img_pods;   // concatenated per-tile image pod lists
     const int *meta;       // [T][kMetaW]
@@ -322,8 +327,7 @@ struct Tile16Args {
     int tile0;
     int img_cells;         // LDS cells of the largest image (rmax * SL); the records follow
     int rec_cap;           // record ints reserved in LDS; the unit counter follows
-    int order, xcd_per;    // grid order (RSK_TILE_ORDER) as in the wide kernel
-    int group;             // order 2: > 1 = groups of this many chunks walked tile-major (RSK_TILE_GROUP)
+    int xcd_per;           // tile units per XCD (the XCD-contiguous grid order)
     int ablate;            // profiling only (RSK_ABLATE_TILE): 1 skip image load, 2 skip scoring
     unsigned n_assign, n_out, n_pods, n_recs, n_key;  // element counts (debug bounds build)
 };
@@ -377,8 +381,7 @@ int launch_side16(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool
 int launch_side16_otf(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch);
 
 int launch_prep(hipStream_t stream, const Prep16Args &a);
-int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off32, bool heavy, unsigned blocks,
-                  size_t lds);
+int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off32, unsigned blocks, size_t lds);
 size_t tile16_lds_bytes(int rmax, int lsl, int rec_cap);
 unsigned tile16_debug_take();
 int tile16_rows_built();       // image rows per tile the compact kernels are compiled for (RSK_TILE16_ROWS)

@@ -91,8 +91,7 @@ struct TileArgs {
     int S, N, T, lsl, rmax;  // SL = 1 << lsl scenarios per workgroup
     int rec_cap;             // record ints reserved in LDS (largest tile, x4); the unit counter follows
     int ablate;              // profiling only (RSK_ABLATE_TILE): 1 skip image load, 2 skip scoring
-    int order;               // grid order (RSK_TILE_ORDER): 0 chunk-major, 1 tile-major, 2 XCD-contiguous
-    int xcd_per;             // order 2: (tile, chunk) units per XCD
+    int xcd_per;             // (tile, chunk) units per XCD (XCD-contiguous order)
     unsigned n_assign, n_out, n_pods, n_recs, n_key;  // element counts (debug bounds build)
 };
 
@@ -349,19 +348,14 @@ __device__ __forceinline__ void tile_load_image(const TileArgs &a, const Img &im
 template <bool kScore, bool kOff32>
 __global__ __launch_bounds__(kTileThreads, 4) void car_tile_kernel(TileArgs a) {
     extern __shared__ __attribute__((aligned(16))) int lds[];  // img {node,key} [rmax][SL], then records
-    // chunk-major (default: concurrent workgroups share a chunk's nodekey
-    // slice in L2) or tile-major (a tile's chunks back to back)
-    // or XCD-contiguous (blocks b and b + 8 share an XCD: each XCD walks its own
-    // run of chunk-major units, so a chunk's nodekey slice is fetched into one
-    // L2 instead of all eight)
+    // XCD-contiguous order: blocks b and b + 8 share an XCD, and each XCD walks
+    // its own run of chunk-major units, so a chunk's nodekey slice is fetched
+    // into one L2 instead of all eight
     const int nchunk = (a.S + (1 << a.lsl) - 1) >> a.lsl;
-    int unit = blockIdx.x;
-    if (a.order == 2) {
-        unit = (int)(blockIdx.x & 7u) * a.xcd_per + (int)(blockIdx.x >> 3);
-        if (unit >= nchunk * a.T) return;  // whole workgroup, before any barrier
-    }
-    const int tile = a.order == 1 ? unit / nchunk : unit % a.T;
-    const int chunk = a.order == 1 ? unit % nchunk : unit / a.T;
+    const int unit = (int)(blockIdx.x & 7u) * a.xcd_per + (int)(blockIdx.x >> 3);
+    if (unit >= nchunk * a.T) return;  // whole workgroup, before any barrier
+    const int tile = unit % a.T;
+    const int chunk = unit / a.T;
     const int lane = threadIdx.x & 63;
     const int SL = 1 << a.lsl;
     const int s0 = chunk * SL;
@@ -845,9 +839,9 @@ struct rsk_car_plan {
     int P = 0, Q = 0, max_deg = 0;
     int light_max = kLightMax;  // rows with deg <= light_max go to the tiles
     // tiles
-    int T = 0, T_lean = 0, rmax = 0, recmax = 0, n_tile_rows = 0, n_sorted_rows = 0;  // tiles [T_lean, T): heavy
-    int n_lean_rows = 0;  // tile rows in the lean tiles
-    int owners_cap = kTileOwners, rows_cap = kTileRows;  // tile limits (RSK_TILE_OWNERS / RSK_TILE_ROWS)
+    int T = 0, T_lean = 0, rmax = 0, recmax = 0, n_tile_rows = 0, n_sorted_rows = 0;  // T_lean == T (info field)
+    int n_lean_rows = 0;  // == n_tile_rows (info field)
+    int owners_cap = kTileOwners, rows_cap = kTileRows;  // tile limits
     int64_t img_rows_total = 0, img_pods_distinct = 0, n_img_pods = 0, n_recs = 0;
     DevBuf img_pods, meta, recs;
     // mid rows (17..64), only in a plan with light_max = kPairMax
@@ -1207,45 +1201,21 @@ int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_id
     std::stable_sort(light.begin(), light.end(), [&](int x, int y) {
         return pos[rows ? rows[x] : x] < pos[rows ? rows[y] : y];
     });
-    // Two tile lists: "heavy" tiles hold every row of degree 17..32 (the
-    // register-hungry class the compact kernel scores in its own, lower-occupancy
-    // instantiation) together with the rows that follow it in DFS order — its
-    // children, whose pods its record reads — and "lean" tiles everything else.
-    TileBuilder tl, th;
-    tl.owners_cap = th.owners_cap = plan->owners_cap;
-    tl.rows_cap = th.rows_cap = plan->rows_cap;
-    // RSK_LEAN32 (default): the 17..32 rows stay in the lean tiles (w64_ds_lean);
-    // 0: they and the d + 1 rows after each go to heavy tiles (w64_ds)
-    static const bool lean32 = RSK_KNOB(RSK_LEAN32, 1) != 0;
-    int heavy_left = 0;
+    // one tile list: every row of degree <= light_max in DFS order (the 17..32
+    // rows included: the tile kernel's register-light counting walk scores them)
+    TileBuilder tb;
+    tb.owners_cap = plan->owners_cap;
+    tb.rows_cap = plan->rows_cap;
     for (int i : light) {
         const int p = rows ? rows[i] : i;
         const int d = rp[p + 1] - rp[p];
         const int *nbp = ci.data() + rp[p];
-        if (!lean32 && light_class(d) == 5) heavy_left = std::max(heavy_left, d + 1);
-        TileBuilder &tb = heavy_left > 0 ? th : tl;
-        if (heavy_left > 0) --heavy_left;
         if (!tb.fits(nbp, d)) tb.close();
         tb.add(i, nbp, d);
     }
-    tl.close();
-    th.close();
-    plan->T_lean = tl.T;
-    plan->n_lean_rows = tl.n_rows;
-    TileBuilder &tb = tl;  // lean tiles first, then the heavy ones (offsets shifted)
-    for (int t = 0; t < th.T; ++t) {
-        int *m = th.meta.data() + (size_t)t * kMetaW;
-        m[0] += (int)tl.img_pods.size();
-        m[2] += (int)tl.recs.size();
-    }
-    tb.img_pods.insert(tb.img_pods.end(), th.img_pods.begin(), th.img_pods.end());
-    tb.meta.insert(tb.meta.end(), th.meta.begin(), th.meta.end());
-    tb.recs.insert(tb.recs.end(), th.recs.begin(), th.recs.end());
-    tb.T += th.T;
-    tb.rmax = std::max(tb.rmax, th.rmax);
-    tb.recmax = std::max(tb.recmax, th.recmax);
-    tb.n_sorted += th.n_sorted;
-    tb.img_total += th.img_total;
+    tb.close();
+    plan->T_lean = tb.T;
+    plan->n_lean_rows = tb.n_rows;
     plan->T = tb.T;
     plan->rmax = std::max(1, tb.rmax);
     plan->recmax = tb.recmax;
@@ -1320,10 +1290,10 @@ int plan_create(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_idx, in
     plan->ctx = ctx;
     plan->light_max = light_max;
     // tile limits: the image rows the compact kernels are built for (RSK_TILE16_ROWS), owners
-    // in the 128 : 144 ratio; RSK_TILE_ROWS / RSK_TILE_OWNERS override (experiments)
+    // in the 128 : 144 ratio
     const int rows_built = tile16_rows_built();
-    plan->owners_cap = std::min(kTileOwners, std::max(8, RSK_KNOB(RSK_TILE_OWNERS, rows_built * kTileOwners / kTileRows)));
-    plan->rows_cap = std::min(rows_built, std::max(kLightMax, RSK_KNOB(RSK_TILE_ROWS, rows_built)));  // a row fits alone
+    plan->owners_cap = std::min(kTileOwners, std::max(8, rows_built * kTileOwners / kTileRows));
+    plan->rows_cap = std::min(rows_built, std::max(kLightMax, rows_built));  // a row fits alone
     plan->P = P;
     plan->Q = Q;
     const int rc = build_plan(plan, row_ptr, col_idx, P, rows, Q);
@@ -1358,11 +1328,7 @@ struct SideBufs {
 // car_side16 launches of classes [c0, c1) on `stream`, the longest rows first.
 // Classes from kSideBig up (rows above 128 neighbours: few work items, each
 // latency-bound) run on a side stream beside the tiles (rsk_car_plan_execute).
-int side_big_class() {  // RSK_SIDE_AUX_FROM: the first class on the side stream (experiments)
-    static const int c = std::max(2, std::min(kNumSide, RSK_KNOB(RSK_SIDE_AUX_FROM, 2)));
-    return c;
-}
-#define kSideBig side_big_class()
+constexpr int kSideBig = 2;
 SideArgs side16_class_args(const rsk_car_plan *plan, int c, const SideBufs &b, int S, int N) {
     static const int sablate = RSK_ABLATION(RSK_ABLATE_SIDE);
     SideArgs a;
@@ -1389,14 +1355,11 @@ SideArgs side16_class_args(const rsk_car_plan *plan, int c, const SideBufs &b, i
 int launch_side16_classes(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, const SideBufs &b, int S, int N,
                           int c0, int c1, int skip = -1, bool otf = false) {
     const bool off32 = (int64_t)std::max(plan->P, plan->Q) * S * 4 < ((int64_t)1 << 32);
-    static const bool per_class = RSK_KNOB(RSK_SIDE_TIMERS, 0) != 0;
-    static const char *const kNames[kNumSide] = {"car_side32", "car_side128", "car_side512",
-                                                 "car_side2048", "car_side8192", "car_side65535"};
     for (int c = c1 - 1; c >= c0; --c) {
         if (c == skip || plan->side_end[c] == plan->side_beg[c]) continue;
         SideArgs a = side16_class_args(plan, c, b, S, N);
         const SideGeom g = side16_geometry(plan->side_dmax[c], N);
-        ScopedTimer tm(ctx, per_class ? kNames[c] : "car_side", stream);
+        ScopedTimer tm(ctx, "car_side", stream);
         if (otf) {
             a.code = nullptr;
             a.haz = b.haz;
@@ -1457,18 +1420,14 @@ int launch_side(rsk_car_plan *plan, rsk_ctx *ctx, hipStream_t stream, const Side
         RSK_CHECK(g.lds <= 160 * 1024, "hub class %d needs %zu B of LDS", c, g.lds);
         const int64_t groups = ceil_div(S, 1 << g.lg);
         // scenario groups per workgroup: enough workgroups to fill the GPU twice over
-        static const int gpw_env = RSK_KNOB(RSK_HUB_GPW, 0);
-        const int gpw = gpw_env > 0 ? gpw_env : (int)std::max<int64_t>(1, std::min<int64_t>(8, groups * n / 1024));
+        const int gpw = (int)std::max<int64_t>(1, std::min<int64_t>(8, groups * n / 1024));
         const int64_t gblocks = ceil_div(groups, gpw);
         RSK_CHECK(gblocks * n < INT32_MAX, "hub grid too large");
         const HubKern kern = g.waves == 8 ? hub_kern_mode<8>(g.mode, kHeavyNJ[c]) : hub_kern_mode<4>(g.mode, kHeavyNJ[c]);
         if (g.lds > 64 * 1024)
             RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds));
-        static const char *const kHubNames[kNumHeavy] = {"car_hub128", "car_hub256", "car_hub512",
-                                                         "car_hub1024", "car_hub2048", "car_hub4096"};
-        static const bool per_class = RSK_KNOB(RSK_HUB_TIMERS, 0) != 0;
-        ScopedTimer tm(ctx, per_class ? kHubNames[c] : "car_heavy", stream);
+        ScopedTimer tm(ctx, "car_heavy", stream);
         kern<<<dim3((unsigned)(gblocks * n)), dim3(64 * g.waves), g.lds, stream>>>(
             plan->heavy_items[c].as<HeavyItem>(), n, plan->hcol.as<int>(), d_assign, d_key, S, N, g.lg, g.dpad,
             g.H, gpw, d_zcnt, d_zkey, d_target, d_score);
@@ -1525,10 +1484,9 @@ int rsk_car_plan_create(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col
         RSK_CHECK(col_idx[k] >= 0 && col_idx[k] < P, "col_idx[%lld]=%d out of range", (long long)k, col_idx[k]);
     if (rows)
         for (int32_t i = 0; i < Q; ++i) RSK_CHECK(rows[i] >= 0 && rows[i] < P, "rows[%d]=%d out of range", i, rows[i]);
-    // rows up to light_max go to the LDS tiles, the rest to the side kernels;
-    // RSK_LIGHT_MAX = 16 sends the 17..32 rows to car_side16 (no heavy tiles)
-    static const int light_max = RSK_KNOB(RSK_LIGHT_MAX, kLightMax) == kPairMax ? kPairMax : kLightMax;
-    return plan_create(ctx, row_ptr, col_idx, P, rows, Q, light_max, out);
+    // rows up to kLightMax neighbours go to the LDS tiles, the rest to the side
+    // kernels (the wide path's kPairMax variant is built on first use, below)
+    return plan_create(ctx, row_ptr, col_idx, P, rows, Q, kLightMax, out);
 }
 
 int rsk_car_plan_info(const rsk_car_plan *plan, int64_t *out, int n) {
@@ -1579,11 +1537,10 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
               "N*S too large (N=%d S=%d; need N*S < 2^30, N < 2^25)", N, S);
     RSK_CHECK(out_target, "null out_target");
     // compact path (rsk_car16.hip) whenever node ids fit 16 bits
-    static const bool compact_ok = RSK_KNOB(RSK_COMPACT, 1) != 0;
     // (S < 2^23: the tile kernel's 24-bit code offsets, rsk_car16.hip t16_rows64)
     // (rows above kMaxDegree neighbours: the side tables count in 16 bits, so
     // such a plan runs the wide path, whose car_bigrow counts in 32)
-    const bool compact = N <= kMaxNodes16 && S < (1 << 23) && plan->max_deg <= kMaxDegree && compact_ok;
+    const bool compact = N <= kMaxNodes16 && S < (1 << 23) && plan->max_deg <= kMaxDegree;
     if (!compact && N >= kPackMaxN && plan->n_sorted_rows > 0) {
         // the wide sorted tile classes pack node << 8 | row into 32 bits: route
         // 17..64 rows through the mid kernel instead (variant built once)
@@ -1607,8 +1564,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
 
     // small batches: one launch (a workgroup per (row, scenario), exact rem from
     // cap / use, no node codes); the latency-bound case, config 2
-    static const bool direct_on = RSK_KNOB(RSK_CAR_DIRECT, 1) != 0;
-    if (direct_on && !(flags & RSK_F_TILED) && S <= 4 && QS <= 65536 && !d_score) {
+    if (!(flags & RSK_F_TILED) && S <= 4 && QS <= 65536 && !d_score) {
         {
             ScopedTimer tm(ctx, "car_direct");
             RSK_TRY(launch_car_direct(ctx->stream, plan->drp.as<int>(), plan->dci.as<int>(),
@@ -1675,23 +1631,19 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     sb.score = d_score;
     sb.haz = d_haz;
     static const int ablate = RSK_ABLATION(RSK_ABLATE_TILE);
-    static const int order = RSK_KNOB(RSK_TILE_ORDER, 2);
-    static const int sl_max = [] { int v = RSK_KNOB(RSK_TILE_SL, 64); return v >= 1 && v <= 64 ? v : 64; }();
     // The compact side rows run inside the lean tile launch (car_fused16_kernel)
     // where they fit its footprint: their latency-bound workgroups share the
-    // CUs with the memory-bound tiles instead of running alone (RSK_FUSE=0:
-    // launches of their own).
+    // CUs with the memory-bound tiles instead of running alone.
     //   class 1 (33..128 neighbours): single-wave items interleaved with the tiles;
     //   classes >= kSideBig (above 128): 4-wave teams at the front of the grid,
     //     while the largest row's table fits the tile's LDS; otherwise on a side
-    //     stream beside the tiles (RSK_SIDE_BIG_AUX=0: on the main stream).
-    static const bool fuse_env = RSK_KNOB(RSK_FUSE, 1) != 0;
+    //     stream beside the tiles.
     const size_t lean_lds = tile16_lds_bytes(plan->rmax, 6, 0);
     int fuse_c = -1, fside_blocks = 0;
     SideArgs fsa, fba;
     std::memset(&fsa, 0, sizeof(fsa));
     std::memset(&fba, 0, sizeof(fba));
-    const bool fuse_ok = compact && fuse_env && plan->T_lean > 0 && S >= 64 && sl_max == 64 && order == 2;
+    const bool fuse_ok = compact && plan->T > 0 && S >= 64;
     if (fuse_ok && plan->side_end[1] > plan->side_beg[1]) {
         const SideGeom g = side16_geometry(plan->side_dmax[1], N);
         if (g.T == 1 && g.W == 4 && g.kB == 16 && 4 * g.lds_team <= lean_lds) {
@@ -1721,8 +1673,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         side16_apply_geometry(fba, side16_geometry(dmax, N, 4));
         fba.xcd_per = 0;
     }
-    static const bool big_aux = RSK_KNOB(RSK_SIDE_BIG_AUX, 1) != 0;
-    // fused classes [lo, hi): class 0 (17..32, RSK_LIGHT_MAX=16 plans only) runs on its own
+    // fused classes [lo, hi): class 0 (17..32, the wide path's kPairMax plans only) runs on its own
     const bool c0 = plan->side_end[0] > plan->side_beg[0];
     plan->fused_lo = c0 ? kNumSide : (fuse_c >= 0 || plan->side_end[1] == plan->side_beg[1] ? 0 : kSideBig);
     plan->fused_hi = std::max(big_hi, fuse_c >= 0 ? 2 : 1);
@@ -1730,7 +1681,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     bool big_left = false;  // classes above the fused ones
     for (int c = big_hi; c < kNumSide; ++c) big_left = big_left || plan->side_end[c] > plan->side_beg[c];
     // (S < 64: the tiles are short, the fork's events would cost more than the overlap)
-    const bool big_fork = compact && big_left && big_aux && plan->T > 0 && S >= 64;
+    const bool big_fork = compact && big_left && plan->T > 0 && S >= 64;
     const int nfork = big_fork ? 1 : 0;
     if (big_fork) {
         // The rows too big for the fused grid run on a side stream from the
@@ -1774,40 +1725,27 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         a.n_pods = (unsigned)plan->n_img_pods;
         a.n_recs = (unsigned)plan->n_recs;
         a.n_key = (unsigned)NS;
-        const int SL = std::min(next_pow2(S), next_pow2(sl_max));
+        const int SL = std::min(next_pow2(S), 64);
         a.lsl = 0;
         while ((1 << a.lsl) < SL) ++a.lsl;
-        a.order = order;
-        static const int group = RSK_KNOB(RSK_TILE_GROUP, 4);  // 0.8175-0.8202 -> 0.8150-0.8164 ms (3 interleaved reps; 8: 0.8144-0.8148 but +0.36 GB of code re-reads)
-        a.group = group;
         a.ablate = ablate;
         a.rec_cap = (plan->recmax + 3) & ~3;
         a.img_cells = (plan->rmax * SL + 3) & ~3;
         const size_t lds = tile16_lds_bytes(plan->rmax, a.lsl, a.rec_cap);
         RSK_CHECK(plan->recmax <= kTileRecInts, "tile records exceed %d ints", kTileRecInts);
-        // one timer over both launches; RSK_TILE_TIMERS=1: car_tile (lean) and car_tile_heavy apart
-        static const bool split = RSK_KNOB(RSK_TILE_TIMERS, 0) != 0;
-        std::unique_ptr<ScopedTimer> tm(split ? nullptr : new ScopedTimer(ctx, "car_tile"));
-        // lean tiles [0, T_lean) at full occupancy, then the heavy tiles (17..32 rows)
-        // S < 64: one generic kernel scores every tile (no lean / heavy split)
-        const int t_split = a.lsl == 6 ? plan->T_lean : plan->T;
-        for (int part = 0; part < 2; ++part) {
-            const int t0 = part ? t_split : 0, nt = part ? plan->T - t_split : t_split;
-            if (nt <= 0) continue;
-            const hipStream_t ts = ctx->stream;
-            std::unique_ptr<ScopedTimer> tp(split ? new ScopedTimer(ctx, part ? "car_tile_heavy" : "car_tile", ts)
-                                                  : nullptr);
-            a.tile0 = t0;
-            a.T = nt;
-            const int64_t units = ceil_div(S, SL) * nt;
-            a.xcd_per = (int)ceil_div(units, 8);
-            const int64_t blocks = order == 2 ? 8 * (int64_t)a.xcd_per : units;
-            RSK_CHECK(blocks < INT32_MAX, "tile grid too large");
-            if (part == 0 && (fuse_c >= 0 || fuse_big))
-                RSK_TRY(launch_fused16(ts, a, fsa, fside_blocks, fba, d_score != nullptr, off32, (unsigned)blocks, lds));
-            else
-                RSK_TRY(launch_tile16(ts, a, d_score != nullptr, off32, part == 1, (unsigned)blocks, lds));
-        }
+        // S >= 64: 64-scenario tiles (fused with the side rows that fit);
+        // S < 64: one generic kernel scores every tile
+        ScopedTimer tm(ctx, "car_tile");
+        a.tile0 = 0;
+        const int64_t units = ceil_div(S, SL) * plan->T;
+        a.xcd_per = (int)ceil_div(units, 8);
+        const int64_t blocks = 8 * (int64_t)a.xcd_per;
+        RSK_CHECK(blocks < INT32_MAX, "tile grid too large");
+        if (fuse_c >= 0 || fuse_big)
+            RSK_TRY(launch_fused16(ctx->stream, a, fsa, fside_blocks, fba, d_score != nullptr, off32, (unsigned)blocks,
+                                   lds));
+        else
+            RSK_TRY(launch_tile16(ctx->stream, a, d_score != nullptr, off32, (unsigned)blocks, lds));
     } else if (plan->T > 0) {   // K1 tiles, wide {node, key} pairs
         TileArgs a;
         std::memset(&a, 0, sizeof(a));
@@ -1832,7 +1770,6 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         const int SL = std::min(next_pow2(S), 32);
         a.lsl = 0;
         while ((1 << a.lsl) < SL) ++a.lsl;
-        a.order = order;
         a.ablate = ablate;
         a.rec_cap = (plan->recmax + 3) & ~3;
         const int cells = plan->rmax * SL;
@@ -1840,7 +1777,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         RSK_CHECK(lds <= 160 * 1024 && plan->recmax <= kTileRecInts, "tile image needs %zu B of LDS", lds);
         const int64_t units = ceil_div(S, SL) * plan->T;
         a.xcd_per = (int)ceil_div(units, 8);
-        const int64_t blocks = order == 2 ? 8 * (int64_t)a.xcd_per : units;
+        const int64_t blocks = 8 * (int64_t)a.xcd_per;
         RSK_CHECK(blocks < INT32_MAX, "tile grid too large");
         using TileKern = void (*)(TileArgs);
         static const TileKern kerns[4] = {&car_tile_kernel<false, false>, &car_tile_kernel<false, true>,

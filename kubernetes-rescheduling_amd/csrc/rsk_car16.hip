@@ -227,21 +227,17 @@ static int launch_prep_main(hipStream_t stream, const Prep16Args &a) {
     // slot receives one atomic per workgroup over its node chunks — threads /
     // SV of them when SV >= 256, threads / 256 below — so aim at ~256 per slot:
     // 256 * max(SV, 256) threads within [2^16, 2^18] (config 3, SV = 1024:
-    // 2^18; config 4, SV = 16: 2^16, prep 0.029 -> 0.024 ms).  RSK_PREP_THREADS
-    // overrides (experiments).
+    // 2^18; config 4, SV = 16: 2^16, prep 0.029 -> 0.024 ms).
     // Few scenarios (SV <= 64, e.g. config 4: SV = 16): workgroups of 1024
     // threads, 4 nodes per thread — a scenario's slot still takes one atomic per
     // workgroup (N * SV / 4096 of them), with 4x the loads in flight of 256-thread
     // workgroups at 13 nodes per thread (prep 17 us at 50k nodes x 64).
-    static const bool big = RSK_KNOB(RSK_PREP_BIG, 1) != 0;
-    if (big && v4 && SV <= 64) {
+    if (v4 && SV <= 64) {
         const int npb = 4;
         const unsigned total = (unsigned)(ceil_div(a.N, npb) * SV);
         return prep_launch<4, 1024>(stream, a, SV, npb, total);
     }
-    static const int env_threads = RSK_KNOB(RSK_PREP_THREADS, 0);
-    const int target_threads = env_threads >= 1024 ? env_threads
-                                                   : (int)std::min<int64_t>(256 * 1024, std::max<int64_t>(65536, 256LL * std::max(SV, 256)));
+    const int target_threads = (int)std::min<int64_t>(256 * 1024, std::max<int64_t>(65536, 256LL * std::max(SV, 256)));
     const int npb = (int)std::max<int64_t>(1, ceil_div((int64_t)a.N * SV, target_threads));
     const int64_t chunks = ceil_div(a.N, npb);
     const unsigned total = (unsigned)(chunks * SV);
@@ -264,8 +260,8 @@ static int launch_prep_main(hipStream_t stream, const Prep16Args &a) {
 // element), except the exact tie resolution, which is rare.
 // ---------------------------------------------------------------------------
 
-// Image rows per tile the compact kernel is compiled for (the plan's
-// RSK_TILE_ROWS must not exceed it) and workgroups per CU it is register-sized for.
+// Image rows per tile the compact kernel is compiled for (the plan's rows_cap)
+// and workgroups per CU it is register-sized for.
 // 80 rows x 64 scenarios x 4 B = 20 KiB of LDS and <= 64 VGPRs: eight
 // workgroups (32 waves) per CU, the occupancy that hides the load phase of one
 // workgroup behind the store phase of others (measured: 144 rows / 4 per CU
@@ -276,8 +272,8 @@ static int launch_prep_main(hipStream_t stream, const Prep16Args &a) {
 #ifndef RSK_TILE16_WGS
 #define RSK_TILE16_WGS 8
 #endif
-#ifndef RSK_TILE16_WGS_HEAVY
-#define RSK_TILE16_WGS_HEAVY 6  // heavy tiles (17..32 rows): 32 cells in registers (<= 80 VGPRs)
+#ifndef RSK_TILE16_WGS_GENERIC
+#define RSK_TILE16_WGS_GENERIC 6  // the generic (S < 64) tiles: records and a work counter in LDS too
 #endif
 constexpr int kT16Rows = RSK_TILE16_ROWS;
 static_assert(kT16Rows % 4 == 0 && kT16Rows <= kTileRows, "bad RSK_TILE16_ROWS");
@@ -837,76 +833,14 @@ __device__ __forceinline__ void w64_dm(const Tile16Args &a, const W64 &w, cint_p
     emit64<kScore, kOff32>(a, r[0], s0, w, M < 0 ? w.zt : t, M < 0 ? w.zs : M + 1);
 }
 
-// 17 <= d <= 32, record j at R[20 * j]: [oi, d, -, -, rows from int 4].  The
-// 32 cells sorted in registers by a bitonic network (equal nodes form runs),
-// then two walks over the runs (sorted_runs_decide); the rare exact tie
-// rescans the LDS image (t16_exact_scan).
-template <bool kScore, bool kOff32>
-__device__ __forceinline__ void w64_ds(const Tile16Args &a, const W64 &w, cint_ptr R, int j, int s0) {
-    constexpr int D = 32;
-    const cint_ptr r = R + 20 * j;
-    const int d = r[1];
-    int M, t;
-    unsigned bk;
-    bool need;
-    {
-        unsigned x[D];
-#pragma unroll
-        for (int i = 0; i < D; ++i) {
-            if (i % 8 == 0) __builtin_amdgcn_sched_barrier(0);
-            const unsigned pr = (unsigned)r[4 + i / 2];
-            const int row = (i & 1) ? (int)(pr >> 16) : (int)(pr & 0xffffu);
-            x[i] = i < d ? w.cell(row) : kCellPad - (unsigned)i;  // distinct pads (code 0)
-        }
-        sort_cells<D, unsigned>(x);
-#if RSK_RUNS_TOP2
-        t = sorted_runs<D>(x, M, bk, need);
-#else
-        unsigned dup = 0u;  // equal cells sit next to each other now
-#pragma unroll
-        for (int i = 1; i < D; ++i) dup |= (unsigned)(x[i] == x[i - 1]);
-        if (!__builtin_amdgcn_ballot_w64(dup != 0u)) {
-            // no lane holds a node twice: every candidate counts 1 (as w64_dm's fast path)
-            unsigned bw = 0u;
-#pragma unroll
-            for (int i = 0; i < D; ++i) bw = max(bw, cell_cand(x[i]));
-            bk = cell_code(bw);
-            M = bk != kCodeHaz ? 1 : 0;
-            t = M == 0 ? INT_MIN : cand_node(bw);
-            need = false;
-            if (__builtin_amdgcn_ballot_w64(bk == kCodeNeg || code_inexact(bk))) {  // rare: count the ties
-                int rn = 0, nb = 0;
-#pragma unroll
-                for (int i = 0; i < D; ++i) {
-                    rn += cell_code(x[i]) != kCodeHaz;
-                    nb += cell_code(x[i]) == bk;
-                }
-                if (bk == kCodeNeg && rn > 1) t = RSK_TARGET_NONE;
-                need = code_inexact(bk) && nb > 1;
-            }
-        } else {
-            t = sorted_runs_decide<D>(x, M, bk, need);
-        }
-#endif
-    }
-    if (__builtin_amdgcn_ballot_w64(need)) {  // rare: wave-uniform branch
-        Img16 im;
-        im.w = reinterpret_cast<const unsigned *>(w.img);
-        im.lsl = 6;
-        const int te = t16_exact_scan(a, im, (const int *)(uintptr_t)(r + 4), d, (int)(w.col4 >> 2), M, bk, w.s);
-        t = need ? te : t;
-    }
-    emit64<kScore, kOff32>(a, r[0], s0, w, M == 0 ? w.zt : t, M == 0 ? w.zs : M);
-}
-
-// 17 <= d <= 32 in the lean tiles, record j at R[20 * j] (as w64_ds): the
+// 17 <= d <= 32, record j at R[20 * j] ([oi, d, -, -, rows from int 4]): the
 // counting walk of w64_dm with only the first 16 cells in registers.  Entry
 // e's count c = #{earlier entries equal to it}: for e < 16 against the
 // registers; for e >= 16 (cell read from the LDS image) against the 16
 // registers plus the earlier entries >= 16, re-read from the LDS one at a time
-// (<= 120 extra ds_read_b32 per record).  About 30 VGPRs instead of the sort
-// network's 32 cells + state, so the class fits the lean kernel's 64 and runs
-// at 8 workgroups per CU instead of in heavy tiles at 6.
+// (<= 120 extra ds_read_b32 per record).  About 30 VGPRs, so the class fits
+// the tile kernel's 64 and runs at 8 workgroups per CU (round 3's separate
+// heavy-tile launch sorted all 32 cells in registers at 6 per CU: slower).
 template <bool kScore, bool kOff32>
 __device__ __forceinline__ void w64_ds_lean(const Tile16Args &a, const W64 &w, cint_ptr R, int j, int s0) {
     const cint_ptr r = R + 20 * j;
@@ -965,18 +899,13 @@ __device__ __forceinline__ void w64_ds_lean(const Tile16Args &a, const W64 &w, c
 // first.  Record j of a class goes to wave (rot + j) % 4, rot carried from
 // class to class (and into part 2), so a tile's few records of each class do
 // not all start on wave 0.
-template <bool kScore, bool kOff32, bool kHeavy>
-__device__ __forceinline__ int w64_score_heavy(const Tile16Args &a, const W64 &w, cint_ptr m, cint_ptr R, int wave,
+template <bool kScore, bool kOff32>
+__device__ __forceinline__ int w64_score_multi(const Tile16Args &a, const W64 &w, cint_ptr m, cint_ptr R, int wave,
                                                int s0) {
     int rot = 0;
-    {   // d = 17..32: the sort network in heavy tiles (own instantiation, registers
-        // for 32 cells); the register-light walk in lean tiles (plans built with
-        // RSK_LEAN32, the default)
+    {   // d = 17..32: the register-light counting walk
         const cint_ptr Rc = R + m[15];
-        for (int j = (wave - rot) & 3; j < m[9]; j += 4) {
-            if (kHeavy) w64_ds<kScore, kOff32>(a, w, Rc, j, s0);
-            else w64_ds_lean<kScore, kOff32>(a, w, Rc, j, s0);
-        }
+        for (int j = (wave - rot) & 3; j < m[9]; j += 4) w64_ds_lean<kScore, kOff32>(a, w, Rc, j, s0);
         rot = (rot + m[9]) & 3;
     }
     {
@@ -1017,7 +946,7 @@ __device__ __forceinline__ void w64_score_light(const Tile16Args &a, const W64 &
 }
 
 // kL64 phase 2: the records of each class, spread over the 4 waves.
-template <bool kScore, bool kOff32, bool kHeavy>
+template <bool kScore, bool kOff32>
 __device__ __forceinline__ void w64_score(const Tile16Args &a, const W64 &w, cint_ptr m, cint_ptr R, int wave, int s0) {
     if (RSK_ABL(a) & 4) {  // profiling: the target stores alone (every record, zero-case value, no LDS reads)
         for (int c = 0; c < kNumCls; ++c) {
@@ -1026,28 +955,28 @@ __device__ __forceinline__ void w64_score(const Tile16Args &a, const W64 &w, cin
         }
         return;
     }
-    const int rot = w64_score_heavy<kScore, kOff32, kHeavy>(a, w, m, R, wave, s0);
+    const int rot = w64_score_multi<kScore, kOff32>(a, w, m, R, wave, s0);
     w64_score_light<kScore, kOff32>(a, w, m, R, wave, s0, rot);
 }
 
 // One tile workgroup; bid plays blockIdx.x (the fused kernel below maps its
 // own blocks onto tile blocks and side blocks).
-template <bool kScore, bool kOff32, bool kL64, bool kHeavy>
+template <bool kScore, bool kOff32, bool kL64>
 __device__ __forceinline__ void tile16_block(const Tile16Args &a, unsigned bid) {
     extern __shared__ __attribute__((aligned(16))) int lds[];  // img cells [rmax][SL] (+ records, unit counter: !kL64)
     const int lsl = kL64 ? 6 : a.lsl;
     const int SL = 1 << lsl;
     const int nchunk = (a.S + SL - 1) >> lsl;
-    int unit = (int)bid;
-    if (a.order == 2) {  // XCD-contiguous: blocks b and b + 8 share an XCD
-        unit = (int)(bid & 7u) * a.xcd_per + (int)(bid >> 3);
-        if (unit >= nchunk * a.T) return;  // whole workgroup, before any barrier
-    }
+    // XCD-contiguous units: blocks b and b + 8 share an XCD, so XCD x walks
+    // units [x * xcd_per, (x + 1) * xcd_per)
+    const int unit = (int)(bid & 7u) * a.xcd_per + (int)(bid >> 3);
+    if (unit >= nchunk * a.T) return;  // whole workgroup, before any barrier
+    // ... in groups of kTileGroup chunks, each group walked tile-major: the
+    // workgroups an XCD runs together read adjacent 256-B segments of the same
+    // pod rows while a group's code slices stay in its L2
     int tile, chunk;
-    if (a.order == 2 && a.group > 1) {
-        // groups of `group` chunks, each walked tile-major: the workgroups an XCD
-        // runs together read adjacent 256-B segments of the same pod rows
-        const int G = a.group, full = nchunk / G;
+    {
+        const int G = kTileGroup, full = nchunk / G;
         if (unit < full * a.T * G) {
             const int cg = unit / (a.T * G), r = unit - cg * a.T * G;
             tile = r / G;
@@ -1057,10 +986,6 @@ __device__ __forceinline__ void tile16_block(const Tile16Args &a, unsigned bid) 
             tile = r / g;
             chunk = full * G + (r - tile * g);
         }
-        tile += a.tile0;
-    } else {
-        tile = a.tile0 + (a.order == 1 ? unit / nchunk : unit % a.T);
-        chunk = a.order == 1 ? unit % nchunk : unit / a.T;
     }
     const int lane = threadIdx.x & 63;
     const int s0 = chunk * SL;
@@ -1082,7 +1007,7 @@ __device__ __forceinline__ void tile16_block(const Tile16Args &a, unsigned bid) 
         __syncthreads();
         if (RSK_ABL(a) & 2) return;  // profiling ablation: no scoring (results are wrong)
         const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-        w64_score<kScore, kOff32, kHeavy>(a, w, m, const_ptr(a.recs) + RSK_B16(rec_off, a.n_recs, 16u), wave, s0);
+        w64_score<kScore, kOff32>(a, w, m, const_ptr(a.recs) + RSK_B16(rec_off, a.n_recs, 16u), wave, s0);
         return;
     }
     int *rec = lds + a.img_cells;  // 16-B aligned (img_cells % 4 == 0) for the int4 record reads
@@ -1140,10 +1065,10 @@ __device__ __forceinline__ void tile16_block(const Tile16Args &a, unsigned bid) 
     }
 }
 
-template <bool kScore, bool kOff32, bool kL64, bool kHeavy>
-__global__ __launch_bounds__(kTileThreads, (kHeavy || !kL64) ? RSK_TILE16_WGS_HEAVY : RSK_TILE16_WGS) void car_tile16_kernel(
+template <bool kScore, bool kOff32, bool kL64>
+__global__ __launch_bounds__(kTileThreads, kL64 ? RSK_TILE16_WGS : RSK_TILE16_WGS_GENERIC) void car_tile16_kernel(
     Tile16Args a) {
-    tile16_block<kScore, kOff32, kL64, kHeavy>(a, blockIdx.x);
+    tile16_block<kScore, kOff32, kL64>(a, blockIdx.x);
 }
 
 // Lean tiles and side rows (rsk_side16.h) in one grid, so the latency- and
@@ -1159,12 +1084,12 @@ __global__ __launch_bounds__(kTileThreads, (kHeavy || !kL64) ? RSK_TILE16_WGS_HE
 //   rows the periods can hold).
 // Every side workgroup fits the tile's footprint (4 waves, <= 64 VGPRs, its
 // LDS within the tile's).
-// kPipe: the side items' next assign rows in flight while a batch is scored
-template <bool kScore, bool kOff32, bool kPipe>
+// (the side items keep their next assign rows in flight while a batch is scored)
+template <bool kScore, bool kOff32>
 __global__ __launch_bounds__(kTileThreads, RSK_TILE16_WGS) void car_fused16_kernel(Tile16Args ta, SideArgs sa,
                                                                                   SideArgs ba, FuseMap f) {
     if (blockIdx.x < (unsigned)f.big_blocks) {
-        side16_block<4, 4, 16, kOff32, kPipe>(ba, (int)blockIdx.x);
+        side16_block<4, 4, 16, kOff32, true>(ba, (int)blockIdx.x);
         return;
     }
     const unsigned v = blockIdx.x - (unsigned)f.big_blocks, row = v >> 3, x = v & 7u;
@@ -1180,29 +1105,24 @@ __global__ __launch_bounds__(kTileThreads, RSK_TILE16_WGS) void car_fused16_kern
         if (row - P1 >= t_rem) side = K1 + (row - P1 - t_rem);
     }
     if (side != 0xffffffffu) {
-        side16_block<4, 1, 16, kOff32, kPipe>(sa, (int)(side * 8u + x));
+        side16_block<4, 1, 16, kOff32, true>(sa, (int)(side * 8u + x));
         return;
     }
-    tile16_block<kScore, kOff32, true, false>(ta, (tile << 3) | x);
+    tile16_block<kScore, kOff32, true>(ta, (tile << 3) | x);
 }
 
-int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off32, bool heavy, unsigned blocks,
-                  size_t lds) {
+int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off32, unsigned blocks, size_t lds) {
     using K = void (*)(Tile16Args);
-    // [l64][heavy][score][off32]; the generic (S < 64) kernel scores every class
-    static const K kerns[16] = {
-        &car_tile16_kernel<false, false, false, false>, &car_tile16_kernel<false, true, false, false>,
-        &car_tile16_kernel<true, false, false, false>,  &car_tile16_kernel<true, true, false, false>,
-        &car_tile16_kernel<false, false, false, false>, &car_tile16_kernel<false, true, false, false>,
-        &car_tile16_kernel<true, false, false, false>,  &car_tile16_kernel<true, true, false, false>,
-        &car_tile16_kernel<false, false, true, false>,  &car_tile16_kernel<false, true, true, false>,
-        &car_tile16_kernel<true, false, true, false>,   &car_tile16_kernel<true, true, true, false>,
-        &car_tile16_kernel<false, false, true, true>,   &car_tile16_kernel<false, true, true, true>,
-        &car_tile16_kernel<true, false, true, true>,    &car_tile16_kernel<true, true, true, true>};
+    // [l64][score][off32]; the generic (S < 64) kernel scores every class
+    static const K kerns[8] = {
+        &car_tile16_kernel<false, false, false>, &car_tile16_kernel<false, true, false>,
+        &car_tile16_kernel<true, false, false>,  &car_tile16_kernel<true, true, false>,
+        &car_tile16_kernel<false, false, true>,  &car_tile16_kernel<false, true, true>,
+        &car_tile16_kernel<true, false, true>,   &car_tile16_kernel<true, true, true>};
     const bool l64 = a.lsl == 6;
     RSK_CHECK(!l64 || (size_t)a.img_cells * 4 <= (size_t)kT16Rows * 256,
               "tile image exceeds the %d rows the kernel was built for", kT16Rows);
-    const K kern = kerns[(l64 ? 8 : 0) + (heavy ? 4 : 0) + (score ? 2 : 0) + (off32 ? 1 : 0)];
+    const K kern = kerns[(l64 ? 4 : 0) + (score ? 2 : 0) + (off32 ? 1 : 0)];
     RSK_CHECK(lds <= 160 * 1024, "tile image needs %zu B of LDS", lds);
     if (lds > 64 * 1024)
         RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1216,7 +1136,7 @@ int launch_fused16(hipStream_t stream, const Tile16Args &a, const SideArgs &sa, 
                    bool score, bool off32, unsigned tile_blocks, size_t lds) {
     RSK_CHECK(a.lsl == 6 && (size_t)a.img_cells * 4 <= (size_t)kT16Rows * 256 && tile_blocks % 8 == 0,
               "fused launch needs 64-scenario tiles");
-    static const int spread = std::max(1, RSK_KNOB(RSK_FUSE_SPREAD, 2));
+    constexpr int spread = 2;  // side rows over the first half of the tile rows (1 / 4 of them: slower)
     FuseMap f;
     f.big_blocks = (int)(8 * ceil_div((int64_t)ba.n_rows * ba.nchunk, 8));
     f.side_rows = (int)ceil_div(side_blocks, 8);
@@ -1228,12 +1148,9 @@ int launch_fused16(hipStream_t stream, const Tile16Args &a, const SideArgs &sa, 
     const int64_t blocks = (int64_t)f.big_blocks + tile_blocks + 8LL * f.side_rows;
     RSK_CHECK(blocks < INT32_MAX, "fused grid too large");
     using K = void (*)(Tile16Args, SideArgs, SideArgs, FuseMap);
-    static const K kerns[8] = {&car_fused16_kernel<false, false, false>, &car_fused16_kernel<false, true, false>,
-                               &car_fused16_kernel<true, false, false>,  &car_fused16_kernel<true, true, false>,
-                               &car_fused16_kernel<false, false, true>,  &car_fused16_kernel<false, true, true>,
-                               &car_fused16_kernel<true, false, true>,   &car_fused16_kernel<true, true, true>};
-    static const bool pipe = RSK_KNOB(RSK_FUSE_PIPE, 1) != 0;
-    const K kern = kerns[(pipe ? 4 : 0) + (score ? 2 : 0) + (off32 ? 1 : 0)];
+    static const K kerns[4] = {&car_fused16_kernel<false, false>, &car_fused16_kernel<false, true>,
+                               &car_fused16_kernel<true, false>, &car_fused16_kernel<true, true>};
+    const K kern = kerns[(score ? 2 : 0) + (off32 ? 1 : 0)];
     RSK_CHECK(lds <= 160 * 1024, "fused tile needs %zu B of LDS", lds);
     if (lds > 64 * 1024)
         RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -140,13 +140,6 @@ int launch_pick_max_pod(hipStream_t stream, const int *assign, const int *pod_cp
                         unsigned long long *key_ws, int *out_pod);
 // key_ws[S] packed (cpu, ~pod) maxima -> pod index or -1 (the pick kernels' tail)
 int launch_decode_first_max(hipStream_t stream, const unsigned long long *key, int S, int *out_pod);
-// the rounds loop's forms: keys zeroed by the caller (no memset), no decode
-// launch (the next kernel decodes); launch_pick_keys decodes kdet into most_ws
-// for the int32 scan
-int launch_detect_use_keys(hipStream_t stream, const int *use, const int *cap, int N, int S, int threshold,
-                           uint8_t *hazard, unsigned long long *key, int *zc_cnt, unsigned long long *zc_key);
-int launch_pick_keys(hipStream_t stream, const int *assign, const int *pod_cpu, int P, int S,
-                     const unsigned long long *kdet, int *most_ws, unsigned long long *kpick);
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

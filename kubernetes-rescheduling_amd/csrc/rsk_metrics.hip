@@ -666,76 +666,6 @@ __global__ __launch_bounds__(256) void detect_kernel(const int *__restrict__ pct
     if (b) atomicMax(&most[s], b);
 }
 
-// detect_kernel with cpu_pct computed in place (get_resource_usage.py:37, the
-// same fp64 divide, multiply and rint as cpu_pct_kernel): the multi-round loop
-// needs only the hazard flags and the most hazardous node, not the pct array.
-// zc_cnt / zc_key (may be null): the round's zero case per scenario as
-// car_prep reduces it (non-hazard nodes, max packed (cap - use, ~node)), for
-// the move kernel's rows that reach no candidate node.  A workgroup = 64
-// scenarios (lane) x 4 waves over consecutive node ranges of npw nodes; the
-// waves' results meet in LDS, so a scenario's words take one atomic per
-// workgroup (125 per round at 5k nodes x 1024 scenarios, not 512).
-template <int kW>
-__global__ __launch_bounds__(64 * kW) void detect_use_kernel(const int *__restrict__ use, const int *__restrict__ cap,
-                                                             int N, int S, int thr, int npw,
-                                                             uint8_t *__restrict__ haz,
-                                                             unsigned long long *__restrict__ most,
-                                                             int *__restrict__ zc_cnt,
-                                                             unsigned long long *__restrict__ zc_key) {
-    __shared__ unsigned long long lb[kW][64], lz[kW][64];
-    __shared__ int ln[kW][64];
-    constexpr int kU = 8;  // nodes per batch: their loads in flight together
-    const int lane = (int)threadIdx.x & 63, wv = (int)threadIdx.x >> 6;
-    const int nsc = (S + 63) >> 6;
-    const int sc = (int)blockIdx.x % nsc, nb = (int)blockIdx.x / nsc;
-    const bool live = sc * 64 + lane < S;
-    const int s = min(sc * 64 + lane, S - 1);
-    const int n0 = (nb * kW + wv) * npw, n1 = min(N, n0 + npw);
-    unsigned long long b = 0, bz = 0;
-    int nz = 0;
-    for (int n = n0; n < n1; n += kU) {
-        int u[kU], c[kU];
-#pragma unroll
-        for (int k = 0; k < kU; ++k) {  // clamped, always-valid addresses
-            const int m = min(n + k, n1 - 1);
-            u[k] = use[(size_t)m * S + s];
-            c[k] = cap[m];
-        }
-#pragma unroll
-        for (int k = 0; k < kU; ++k) {
-            if (n + k >= n1) break;
-            const int m = n + k;
-            const int v = c[k] == 0 ? -1 : (int)rint((double)u[k] / (double)c[k] * 100.0);
-            const bool h = v >= thr;
-            if (live) haz[(size_t)m * S + s] = h;
-            if (h) {
-                const unsigned long long kk = pack_hi_lo(v, ~(unsigned)m);
-                b = kk > b ? kk : b;
-            } else {
-                ++nz;
-                const unsigned long long kk = zc_pack(c[k] - u[k], m);
-                bz = kk > bz ? kk : bz;
-            }
-        }
-    }
-    lb[wv][lane] = b;
-    lz[wv][lane] = bz;
-    ln[wv][lane] = nz;
-    __syncthreads();
-    if (wv != 0 || !live) return;
-#pragma unroll
-    for (int w = 1; w < kW; ++w) {
-        b = max(b, lb[w][lane]);
-        bz = max(bz, lz[w][lane]);
-        nz += ln[w][lane];
-    }
-    if (b) atomicMax(&most[s], b);
-    if (zc_cnt && nz) {
-        atomicAdd(&zc_cnt[s], nz);
-        atomicMax(&zc_key[s], bz);
-    }
-}
-
 __global__ void decode_first_max(const unsigned long long *__restrict__ key, int S, int *__restrict__ out) {
     const int s = blockIdx.x * 256 + threadIdx.x;
     if (s >= S) return;
@@ -1006,40 +936,6 @@ int launch_detect(hipStream_t stream, const int *pct, int N, int S, int threshol
     return RSK_OK;
 }
 
-// The multi-round loop's halves without memsets or decode launches: the keys
-// arrive zeroed (the move kernel clears its scenario's words after use).
-int launch_detect_use_keys(hipStream_t stream, const int *use, const int *cap, int N, int S, int threshold,
-                           uint8_t *hazard, unsigned long long *key, int *zc_cnt, unsigned long long *zc_key) {
-    // ~512 workgroups of 64 scenarios x 16 waves (the persistent loops' workgroup shape):
-    // one atomic per scenario word per workgroup
-    static const int w16 = RSK_KNOB(RSK_DET_W16, 1);
-    static const int target = std::max(1, RSK_KNOB(RSK_DET_BLOCKS, 512));
-    const int kW = w16 ? 16 : 4;
-    const int64_t nsc = ceil_div(S, 64);
-    const int64_t nbk = std::max<int64_t>(1, std::min<int64_t>(ceil_div(N, kW * 4), ceil_div(target, nsc)));
-    const int npw = (int)ceil_div(N, nbk * kW);
-    const int64_t blocks = nsc * ceil_div(N, (int64_t)kW * npw);
-    RSK_CHECK(blocks < INT32_MAX, "grid too large");
-    auto *kern = w16 ? &detect_use_kernel<16> : &detect_use_kernel<4>;
-    kern<<<(unsigned)blocks, 64 * kW, 0, stream>>>(use, cap, N, S, threshold, npw, hazard, key, zc_cnt, zc_key);
-    RSK_HIP(hipGetLastError());
-    return RSK_OK;
-}
-
-int launch_pick_keys(hipStream_t stream, const int *assign, const int *pod_cpu, int P, int S,
-                     const unsigned long long *kdet, int *most_ws, unsigned long long *kpick) {
-    decode_first_max<<<(unsigned)ceil_div(S, 256), 256, 0, stream>>>(kdet, S, most_ws);
-    if (P > 0) {
-        const int ppt = chunk_for(P, S);
-        const int64_t tot = ceil_div(P, ppt) * S;
-        RSK_CHECK(tot < INT32_MAX, "grid too large");
-        pick_pod_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, stream>>>(assign, pod_cpu, P, S, most_ws, ppt,
-                                                                          (unsigned)tot, kpick);
-    }
-    RSK_HIP(hipGetLastError());
-    return RSK_OK;
-}
-
 int launch_decode_first_max(hipStream_t stream, const unsigned long long *key, int S, int *out_pod) {
     decode_first_max<<<(unsigned)ceil_div(S, 256), 256, 0, stream>>>(key, S, out_pod);
     RSK_HIP(hipGetLastError());
@@ -1296,7 +1192,7 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
     if (d_ms) RSK_HIP(hipMemsetAsync(d_ms, 0, NS * 8, ctx->stream));
     const int nbk = (N >> kNrSubBits) + 1;  // key >> kNrSubBits buckets (keys 0..N)
     if (PS && S >= 32 && nbk <= kNrMaxBuckets) {  // segmented: group the pods by key node, per-key register sums
-        static const int run_len = std::max(8, RSK_KNOB(RSK_NR_RUN, kNrRun));  // pods per wave
+        constexpr int run_len = kNrRun;  // pods per wave
         const int runs = (int)ceil_div(P, run_len);
         const int64_t waves = (int64_t)runs * ceil_div(S, 64);
         RSK_CHECK(waves < (int64_t)INT32_MAX - 4, "node_reduce grid too large");
@@ -1397,7 +1293,7 @@ int rsk_load_std(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *cap_cpu, i
     RSK_TRY(stage_out(ctx, 2, out_std, (size_t)S * 8, dev, reinterpret_cast<void **>(&d_out)));
     // nodes per thread: at least 16, and at most 1,024 chunks for the merge
     // waves to walk (50k nodes x 64 scenarios: 49 nodes, 1,021 chunks)
-    static const int max_chunks = std::max(16, RSK_KNOB(RSK_STD_CHUNKS, 1024));
+    constexpr int max_chunks = 1024;
     const int npb = std::max({chunk_for(N, S), 16, (int)ceil_div(N, max_chunks)});
     const int nch = (int)ceil_div(N, npb);
     RSK_TRY(ctx->work[0].reserve((size_t)nch * S * 8));
@@ -1451,8 +1347,7 @@ int rsk_cut_cost_rows(rsk_ctx *ctx, const int32_t *row_ptr, const int32_t *col_i
         auto *bins = ctx->work[4].as<unsigned long long>();
         RSK_HIP(hipMemsetAsync(bins, 0, (size_t)kCutBins * S * 8, ctx->stream));
         ScopedTimer tm(ctx, "cut_cost");
-        static const bool wave_kernel = RSK_KNOB(RSK_CUT_THREAD, 0) == 0;
-        if (S >= 32 && wave_kernel) {  // lane = scenario, edge-balanced (nnz may be device-resident: grid-stride)
+        if (S >= 32) {  // lane = scenario, edge-balanced (nnz may be device-resident: grid-stride)
             const int nw = 4096;  // waves per 64-scenario chunk
             const int64_t waves = ceil_div(S, 64) * nw;
             RSK_CHECK(ceil_div(waves, 4) < INT32_MAX, "grid too large");

@@ -27,8 +27,7 @@ struct rsk_rounds {
     rsk_ctx *ctx = nullptr;
     int P = 0, dmax = 0;
     rsk::DevBuf row_ptr, col, pod_cpu;
-    rsk::DevBuf haz, most, evict, key_ws;
-    rsk::DevBuf asg16;  // u16 shadow of assign for the eviction scan (N <= 65535, S % 8 == 0)
+    rsk::DevBuf haz, key_ws;
     rsk::DevBuf gtab;   // global hash work areas (rows whose distinct nodes overflow the LDS)
     // the eviction pick's pod lists (rsk_rounds_run): base node per pod, the
     // pods of each base node (CSR), per scenario the pods off their base node
@@ -42,13 +41,10 @@ struct rsk_rounds {
         lcnt.release();
         llist.release();
         gtab.release();
-        asg16.release();
         row_ptr.release();
         col.release();
         pod_cpu.release();
         haz.release();
-        most.release();
-        evict.release();
         key_ws.release();
     }
 };
@@ -58,6 +54,11 @@ namespace {
 
 constexpr int kMoveThreads = 256;
 constexpr int kNoEvict = -3;
+
+__global__ __launch_bounds__(256) void fill_i32_kernel(int *__restrict__ out, size_t n, int v) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = v;
+}
 
 // Per-scenario lists of the pods off their base node (base = scenario 0's
 // node), as (pod, its current node) entries: every pod that has left its base
@@ -250,27 +251,12 @@ int next_pow2(int x) {
     return p;
 }
 
-// u16 shadow of assign: node ids < N <= 65535, anything outside [0, N) -> 0xffff
-// (never a hazard node)
-// (8 values per thread: two 16-B loads, one 16-B store; n % 8 == 0 since S % 8 == 0)
-__global__ __launch_bounds__(256) void asg16_kernel(const int4 *__restrict__ assign, size_t n8, int N,
-                                                     uint4 *__restrict__ out) {
-    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n8) return;
-    const int4 a = assign[2 * i], b = assign[2 * i + 1];
-    auto c = [N](int v) { return (unsigned)v < (unsigned)N ? (unsigned)v : 0xffffu; };
-    out[i] = make_uint4(c(a.x) | c(a.y) << 16, c(a.z) | c(a.w) << 16, c(b.x) | c(b.y) << 16, c(b.z) | c(b.w) << 16);
-}
-
 // delete_replaced_pod.py:41-61 over the u16 shadow: thread = (chunk of ppt pods,
 // 8 consecutive scenarios), one 16-B load per pod; the first max (cpu, -pod)
 // among pods on most[s] with cpu > -1, packed as pick_pod_kernel packs it.  Half
 // the bytes of the int32 scan (rsk_metrics.hip pick_pod_kernel).
-// kKeys (the loop): most[s] decoded from the detect kernel's packed key.
-template <bool kKeys>
 __global__ __launch_bounds__(256) void pick16_kernel(const uint4 *__restrict__ asg, const int *__restrict__ pod_cpu,
-                                                      int P, int S8, const int *__restrict__ most,
-                                                      const unsigned long long *__restrict__ kdet, int ppt,
+                                                      int P, int S8, const int *__restrict__ most, int ppt,
                                                       unsigned total, unsigned long long *__restrict__ best) {
     const unsigned t = blockIdx.x * 256u + threadIdx.x;
     if (t >= total) return;
@@ -280,13 +266,7 @@ __global__ __launch_bounds__(256) void pick16_kernel(const uint4 *__restrict__ a
     bool any = false;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        int v;
-        if (kKeys) {
-            const unsigned long long k = kdet[s8 * 8 + j];
-            v = k ? (int)(~(unsigned)(k & 0xffffffffull)) : -1;
-        } else {
-            v = most[s8 * 8 + j];
-        }
+        const int v = most[s8 * 8 + j];
         m[j] = v < 0 ? 0x10000u : (unsigned)v;  // no hazard node: matches nothing
         any |= v >= 0;
     }
@@ -470,93 +450,6 @@ __global__ __launch_bounds__(256) void list_fill_kernel(const int *__restrict__ 
                 ++q;
             }
         }
-    }
-}
-
-// delete_replaced_pod.py:41-61 per scenario by one workgroup: the pods on the
-// most hazardous node m (kdet) are the base pods of m still on m (their
-// assign word checked: ~P/N gathers) and the list entries whose node is m
-// (read in order, no gather); an overflowed list scans every pod's assign
-// word (T: the u16 shadow or int32).  Same packed key as pick16; src[s] = the
-// winning list entry (-1: a base pod), for the move kernel's entry update.
-template <typename T>
-__global__ __launch_bounds__(256) void pick_list_kernel(const T *__restrict__ asg, const int *__restrict__ pod_cpu,
-                                                        int P, int S, const unsigned long long *__restrict__ kdet,
-                                                        const int *__restrict__ off, const int *__restrict__ pod,
-                                                        const int *__restrict__ dcnt, const int2 *__restrict__ dlist,
-                                                        int cap, unsigned long long *__restrict__ kpick,
-                                                        int *__restrict__ src) {
-    constexpr int kU = 8;
-    __shared__ unsigned long long red[4];
-    __shared__ int lsrc;
-    const int s = (int)blockIdx.x, t = (int)threadIdx.x;
-    const unsigned long long kd = kdet[s];
-    if (!kd) return;  // no hazard node: kpick stays 0 (the whole workgroup)
-    const int m = (int)~(unsigned)(kd & 0xffffffffull);
-    const int b0 = off[m], nb = off[m + 1] - b0;
-    const int nd = dcnt[s];
-    const bool full = nd > cap;
-    const int2 *l = dlist + (size_t)s * cap;
-    auto key = [](int p, int c) {
-        return c >= 0 ? ((unsigned long long)((unsigned)c ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)p)
-                      : 0ull;
-    };
-    unsigned long long best = 0ull;
-    // the base pods of m (or, overflowed, every pod): assign word checked
-    const int ng = full ? P : nb;
-    for (int i0 = 0; i0 < ng; i0 += 256 * kU) {
-        int p[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const int i = min(i0 + u * 256 + t, ng - 1);  // clamped: always a valid entry
-            p[u] = full ? i : pod[b0 + i];
-        }
-        int a[kU], c[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            a[u] = (int)asg[(size_t)p[u] * S + s];
-            c[u] = pod_cpu[p[u]];
-        }
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const unsigned long long k = a[u] == m ? key(p[u], c[u]) : 0ull;
-            best = k > best ? k : best;
-        }
-    }
-    // the list entries on m
-    const int nl = full ? 0 : nd;
-    for (int i0 = 0; i0 < nl; i0 += 256 * kU) {
-        int2 e[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) e[u] = l[min(i0 + u * 256 + t, nl - 1)];
-        int c[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) c[u] = pod_cpu[e[u].x];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const unsigned long long k = e[u].y == m ? key(e[u].x, c[u]) : 0ull;
-            best = k > best ? k : best;
-        }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long x = __shfl_xor(best, o, 64);
-        best = x > best ? x : best;
-    }
-    if ((t & 63) == 0) red[t >> 6] = best;
-    if (t == 0) lsrc = -1;
-    __syncthreads();
-    best = red[0];
-    for (int w = 1; w < 4; ++w) best = red[w] > best ? red[w] : best;
-    if (!best) return;  // no pod on m with CPU >= 0 (the whole workgroup)
-    // the winner's list entry, if it has one (it then has exactly one, on m)
-    const int pw = (int)~(unsigned)(best & 0xffffffffull);
-    for (int i = t; i < nl; i += 256)
-        if (l[i].x == pw) lsrc = i;
-    __syncthreads();
-    if (t == 0) {
-        kpick[s] = best;
-        src[s] = lsrc;
     }
 }
 
@@ -1247,68 +1140,51 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         RSK_HIP(hipMemcpyAsync(d_use, use_cpu, NS * 4, hipMemcpyHostToDevice, st));
     }
     RSK_TRY(r->haz.reserve(NS));
-    RSK_TRY(r->most.reserve((size_t)S * 4));
     RSK_TRY(r->key_ws.reserve((size_t)S * 28));  // the detect and pick keys, the zero case
     const MoveGeom g = move_geometry(r, N, S);
     RSK_TRY(g.rc);
     RSK_TRY(ws_check_u64(N, S, g.H));
-    // the eviction scan reads a u16 shadow of assign when node ids fit (kept in
-    // step by the move kernel); otherwise the int32 scan
-    static const bool lists_on = RSK_KNOB(RSK_ROUNDS_LISTS, 1) != 0;
-    static const bool persist_on = RSK_KNOB(RSK_ROUNDS_PERSIST, 1) != 0;
-    const bool persist = lists_on && persist_on && r->P > 0 && R > 0;  // one launch, no shadow
-    const bool s16 = !persist && N <= 65535 && S % 8 == 0 && PS > 0 && ((uintptr_t)d_assign % 16) == 0;
-    unsigned short *a16 = nullptr;
-    if (s16) {
-        RSK_TRY(r->asg16.reserve(PS * 2));
-        a16 = r->asg16.as<unsigned short>();
-        ScopedTimer tm(ctx, "rounds_shadow");
-        asg16_kernel<<<(unsigned)ceil_div((int64_t)(PS / 8), 256), 256, 0, st>>>(
-            reinterpret_cast<const int4 *>(d_assign), PS / 8, N, reinterpret_cast<uint4 *>(a16));
-        RSK_HIP(hipGetLastError());
-    }
-    // Three launches per round: detect -> (packed key) -> pick -> (packed key) ->
-    // move, which decodes the eviction, writes it out and zeroes both keys for
-    // the next round (no memsets, no decode launches; zeroed once here).
-    unsigned long long *kdet = r->key_ws.as<unsigned long long>(), *kpick = kdet + S, *zkey = kpick + S;
+    unsigned long long *zkey = r->key_ws.as<unsigned long long>() + 2 * S;
     int *zcnt = reinterpret_cast<int *>(zkey + S);
-    RSK_HIP(hipMemsetAsync(kdet, 0, (size_t)S * 28, st));
-    // The eviction pick over pod lists: the pods on a node in scenario s are the
-    // node's base pods (scenario 0's node) plus those of s's list of pods off
-    // their base node; the move kernel appends a pod that leaves its base node.
-    // Per round one wave per scenario reads ~(P/N + list) pods instead of the
-    // P x S scan (rsk_rounds.hip pick16: 205 MB at config 5).  Built per call
-    // from one read of assign.
-    DevLists dl;
-    if (lists_on && r->P > 0 && R > 0) {
-        const int P = r->P;
-        int cap = (int)std::max<int64_t>(256, P / 16);
-        cap = (int)std::max<int64_t>(64, std::min<int64_t>(cap, ((int64_t)128 << 20) / ((int64_t)S * 8)));
-        RSK_TRY(r->lbase.reserve((size_t)P * 4));
-        RSK_TRY(r->loff.reserve((size_t)(N + 2) * 4 * 2));
-        RSK_TRY(r->lpod.reserve((size_t)P * 4));
-        RSK_TRY(r->lcnt.reserve((size_t)S * 8));  // counts, then the picks' source entries
-        RSK_TRY(r->llist.reserve((size_t)S * cap * 8));
-        int *cntb = r->loff.as<int>() + (N + 2);  // N + 1 counts, then the fill cursors
-        ScopedTimer tm(ctx, "rounds_lists");
-        RSK_HIP(hipMemsetAsync(cntb, 0, (size_t)(N + 1) * 4, st));
-        RSK_HIP(hipMemsetAsync(r->lcnt.ptr, 0, (size_t)S * 4, st));
-        list_base_kernel<<<(unsigned)ceil_div(P, 256), 256, 0, st>>>(d_assign, P, S, N, r->lbase.as<int>(), cntb);
-        list_scan_kernel<<<1, 1024, 0, st>>>(cntb, N + 1, r->loff.as<int>());
-        RSK_HIP(hipMemcpyAsync(cntb, r->loff.ptr, (size_t)(N + 1) * 4, hipMemcpyDeviceToDevice, st));
-        const int64_t blocks = ceil_div(P, kLF) * ceil_div(S, 64);
-        RSK_CHECK(blocks < INT32_MAX, "list grid too large");
-        list_fill_kernel<<<(unsigned)blocks, 256, 0, st>>>(d_assign, P, S, N, r->lbase.as<int>(), cntb,
-                                                                        r->lpod.as<int>(), r->lcnt.as<int>(),
-                                                                        r->llist.as<int2>(), cap);
+    if (R > 0 && r->P == 0) {  // no pod to evict: every round is RSK_TARGET_NO_EVICT
+        fill_i32_kernel<<<(unsigned)ceil_div((int64_t)RS, 256), 256, 0, st>>>(d_evict, RS, -1);
+        fill_i32_kernel<<<(unsigned)ceil_div((int64_t)RS, 256), 256, 0, st>>>(d_target, RS, kNoEvict);
         RSK_HIP(hipGetLastError());
-        dl.base = r->lbase.as<int>();
-        dl.cnt = r->lcnt.as<int>();
-        dl.src = dl.cnt + S;
-        dl.list = r->llist.as<int2>();
-        dl.cap = cap;
-    }
-    if (persist) {
+    } else if (R > 0) {
+        // The eviction pick over pod lists: the pods on a node in scenario s are
+        // the node's base pods (scenario 0's node) plus those of s's list of pods
+        // off their base node; the move appends a pod that leaves its base node.
+        // Per round a scenario reads ~(P/N + list) pods instead of its P-pod
+        // column.  Built per call from one read of assign.
+        DevLists dl;
+        const int P = r->P;
+        {
+            int cap = (int)std::max<int64_t>(256, P / 16);
+            cap = (int)std::max<int64_t>(64, std::min<int64_t>(cap, ((int64_t)128 << 20) / ((int64_t)S * 8)));
+            RSK_TRY(r->lbase.reserve((size_t)P * 4));
+            RSK_TRY(r->loff.reserve((size_t)(N + 2) * 4 * 2));
+            RSK_TRY(r->lpod.reserve((size_t)P * 4));
+            RSK_TRY(r->lcnt.reserve((size_t)S * 8));  // counts, then the picks' source entries
+            RSK_TRY(r->llist.reserve((size_t)S * cap * 8));
+            int *cntb = r->loff.as<int>() + (N + 2);  // N + 1 counts, then the fill cursors
+            ScopedTimer tm(ctx, "rounds_lists");
+            RSK_HIP(hipMemsetAsync(cntb, 0, (size_t)(N + 1) * 4, st));
+            RSK_HIP(hipMemsetAsync(r->lcnt.ptr, 0, (size_t)S * 4, st));
+            list_base_kernel<<<(unsigned)ceil_div(P, 256), 256, 0, st>>>(d_assign, P, S, N, r->lbase.as<int>(), cntb);
+            list_scan_kernel<<<1, 1024, 0, st>>>(cntb, N + 1, r->loff.as<int>());
+            RSK_HIP(hipMemcpyAsync(cntb, r->loff.ptr, (size_t)(N + 1) * 4, hipMemcpyDeviceToDevice, st));
+            const int64_t blocks = ceil_div(P, kLF) * ceil_div(S, 64);
+            RSK_CHECK(blocks < INT32_MAX, "list grid too large");
+            list_fill_kernel<<<(unsigned)blocks, 256, 0, st>>>(d_assign, P, S, N, r->lbase.as<int>(), cntb,
+                                                                 r->lpod.as<int>(), r->lcnt.as<int>(),
+                                                                 r->llist.as<int2>(), cap);
+            RSK_HIP(hipGetLastError());
+            dl.base = r->lbase.as<int>();
+            dl.cnt = r->lcnt.as<int>();
+            dl.src = dl.cnt + S;
+            dl.list = r->llist.as<int2>();
+            dl.cap = cap;
+        }
         // one launch for all R rounds: the hazard flags and the block maxima
         // once, then a workgroup per scenario walks its rounds
         PersistArgs pa;
@@ -1357,45 +1233,6 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
                                         (int)lds));
         kern<<<dim3((unsigned)g.grid), dim3(kMoveThreads), lds, st>>>(pa, g.lds ? nullptr : r->gtab.as<unsigned>());
         RSK_HIP(hipGetLastError());
-        R = 0;  // every round done
-    }
-    for (int round = 0; round < R; ++round) {
-        int *ev = d_evict + (size_t)round * S;
-        {
-            ScopedTimer tm(ctx, "rounds_detect");
-            RSK_TRY(launch_detect_use_keys(st, d_use, d_cap, N, S, threshold, r->haz.as<uint8_t>(), kdet, zcnt, zkey));
-        }
-        {
-            ScopedTimer tm(ctx, "rounds_pick");
-            if (dl.base) {
-                const unsigned blocks = (unsigned)S;
-                if (s16)
-                    pick_list_kernel<unsigned short><<<blocks, 256, 0, st>>>(
-                        a16, r->pod_cpu.as<int>(), r->P, S, kdet, r->loff.as<int>(), r->lpod.as<int>(), dl.cnt, dl.list,
-                        dl.cap, kpick, dl.src);
-                else
-                    pick_list_kernel<int><<<blocks, 256, 0, st>>>(d_assign, r->pod_cpu.as<int>(), r->P, S, kdet,
-                                                                  r->loff.as<int>(), r->lpod.as<int>(), dl.cnt,
-                                                                  dl.list, dl.cap, kpick, dl.src);
-                RSK_HIP(hipGetLastError());
-            } else if (s16) {
-                const int S8 = S / 8;
-                const int ppt = (int)std::max<int64_t>(1, ceil_div((int64_t)r->P * S8, (int64_t)256 * 4096));
-                const int64_t tot = ceil_div(r->P, ppt) * S8;
-                RSK_CHECK(tot < INT32_MAX, "grid too large");
-                pick16_kernel<true><<<(unsigned)ceil_div(tot, 256), 256, 0, st>>>(
-                    reinterpret_cast<const uint4 *>(a16), r->pod_cpu.as<int>(), r->P, S8, nullptr, kdet, ppt,
-                    (unsigned)tot, kpick);
-                RSK_HIP(hipGetLastError());
-            } else {
-                RSK_TRY(launch_pick_keys(st, d_assign, r->pod_cpu.as<int>(), r->P, S, kdet, r->most.as<int>(), kpick));
-            }
-        }
-        {
-            ScopedTimer tm(ctx, "rounds_move");
-            RSK_TRY(launch_move(r, st, g, d_assign, d_use, d_cap, r->haz.as<uint8_t>(), nullptr, S, N, 1,
-                                d_target + (size_t)round * S, a16, kpick, kdet, ev, zcnt, zkey, 0, INT_MAX, dl));
-        }
     }
     if (!dev) {
         if (PS) RSK_TRY(copy_back(ctx, assign, d_assign, PS * 4, false));
@@ -1507,8 +1344,8 @@ int rsk_pick_max_pod16(rsk_ctx *ctx, const uint16_t *assign16, const int32_t *po
         const int ppt = (int)std::max<int64_t>(1, ceil_div((int64_t)P * S8, (int64_t)256 * 4096));
         const int64_t tot = ceil_div(P, ppt) * S8;
         RSK_CHECK(tot < INT32_MAX, "grid too large");
-        pick16_kernel<false><<<(unsigned)ceil_div(tot, 256), 256, 0, ctx->stream>>>(
-            reinterpret_cast<const uint4 *>(assign16), pod_cpu, P, S8, most, nullptr, ppt, (unsigned)tot, key);
+        pick16_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, ctx->stream>>>(
+            reinterpret_cast<const uint4 *>(assign16), pod_cpu, P, S8, most, ppt, (unsigned)tot, key);
         RSK_HIP(hipGetLastError());
     }
     return launch_decode_first_max(ctx->stream, key, S, out_pod);

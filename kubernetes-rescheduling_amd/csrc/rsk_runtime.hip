@@ -80,12 +80,8 @@ int aux_fork(rsk_ctx *ctx, int k) {
     RSK_HIP(hipEventRecord(ctx->fork, ctx->stream));
     for (int i = 0; i < k; ++i) {
         if (!ctx->aux[i]) {
-            // side work is short and latency-bound: with RSK_SIDE_PRIO=1 its
-            // workgroups are dispatched ahead of the tile kernel's as CUs free up
-            static const bool prio = RSK_KNOB(RSK_SIDE_PRIO, 0) != 0;
-            int lo = 0, hi = 0;
-            if (prio) RSK_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-            RSK_HIP(hipStreamCreateWithPriority(&ctx->aux[i], hipStreamNonBlocking, prio ? hi : lo));
+            // (a high-priority side stream measured no change)
+            RSK_HIP(hipStreamCreateWithFlags(&ctx->aux[i], hipStreamNonBlocking));
             RSK_HIP(hipEventCreateWithFlags(&ctx->join[i], hipEventDisableTiming));
         }
         RSK_HIP(hipStreamWaitEvent(ctx->aux[i], ctx->fork, 0));

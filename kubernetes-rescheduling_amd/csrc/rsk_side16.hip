@@ -82,8 +82,7 @@ SideGeom side16_geometry(int dmax, int N, int T) {
     // neighbour loads in flight per wave (with their code gathers: 2 kB VGPRs;
     // 4-wave teams live in the fused tile launch: <= 64 VGPRs; 16-wave teams:
     // <= 128)
-    static const bool kb16 = RSK_KNOB(RSK_SIDE_KB16, 0) != 0;  // debug
-    g.kB = dmax <= 32 && !kb16 ? 8 : (g.T == 8 ? 32 : 16);
+    g.kB = dmax <= 32 ? 8 : (g.T == 8 ? 32 : 16);
     // words: tab H | dl 64 K (also the recount's cells) | ndl 64 | dummy 64 |
     // h2 1 + h2cap (the entries counted >= 2: at most min(Dc, dmax / 2); a
     // longer list sends the item to the exact recount; teams: bx 192 T after
@@ -146,9 +145,7 @@ static int launch_side16_t(hipStream_t stream, const SideArgs &a0, const SideGeo
         return RSK_OK;
     }
     using K = void (*)(SideArgs);
-    static const bool pipe = RSK_KNOB(RSK_SIDE_PIPE, 1) != 0;
-#define RSK_SIDE_P(W, T, B, O) \
-    (pipe ? &car_side16_kernel<W, T, B, O, true, false, kOTF> : &car_side16_kernel<W, T, B, O, false, false, kOTF>)
+#define RSK_SIDE_P(W, T, B, O) (&car_side16_kernel<W, T, B, O, true, false, kOTF>)
 #define RSK_SIDE_O(W, T, B) (off32 ? RSK_SIDE_P(W, T, B, true) : RSK_SIDE_P(W, T, B, false))
 #define RSK_SIDE_W(W) (g.kB == 8 ? RSK_SIDE_O(W, 1, 8) : RSK_SIDE_O(W, 1, 16))
     RSK_CHECK(g.T == 1 || g.T == 8 || g.T == 16, "side teams of %d waves are not built", g.T);

@@ -82,8 +82,7 @@ def test_config3_headline_s4096(ctx, synth_golden):
     assert _all_cells(c, S, t, "config 3") == 409_600_000
     rows, hard = _rows_to_check(c, 200, 7)
     assert hard.size == 640 and info["mid_rows"] + info["heavy_rows"] == 201
-    assert info["side_rows"] == (640 if info["light_max"] == 16 else 201)
-    assert info["sorted_rows"] == (0 if info["light_max"] == 16 else 439)
+    assert info["light_max"] == 32 and info["side_rows"] == 201 and info["sorted_rows"] == 439
     exp, _ = orc.car(c.row_ptr, c.col_idx, c.assign, S, c.cap_cpu, c.use_cpu, c.hazard, N, rows=rows,
                      threads=THREADS)
     got = t[rows].reshape(-1)

@@ -143,9 +143,8 @@ def test_car_degree_bucket_boundaries(ctx, S):
     _check_car(ctx, rp, ci, a, S, cap, use, haz, N, label=f"boundaries S={S}")
     from rsk import api
     info = api.CarPlan(rp, ci, ctx=ctx).info()
-    # 17..32 in heavy tiles (or, RSK_LIGHT_MAX=16, on the side kernel), 33..64 and > 64 side rows
-    l16 = os.environ.get("RSK_LIGHT_MAX") == "16" and "RSK_LIB" in os.environ   # knobs variant only
-    assert (info["sorted_rows"] == 0) if l16 else (info["sorted_rows"] >= 3), info
+    # 17..32 in the tiles (sorted class), 33..64 and > 64 side rows
+    assert info["sorted_rows"] >= 3, info
     assert info["mid_rows"] >= 3 and info["heavy_rows"] >= 5 and info["tile_rows"] > 0, info
 
 
