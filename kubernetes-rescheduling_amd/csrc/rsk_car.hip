@@ -1077,6 +1077,9 @@ struct SideBufs {
 // Classes from kSideBig up (rows above 128 neighbours: few work items, each
 // latency-bound) run on a side stream beside the tiles (rsk_car_plan_execute).
 constexpr int kSideBig = 2;
+// rows beyond the fused grid with at most this many (row, scenario) cells run
+// as one workgroup per cell (car_direct_kernel) instead of pivot teams
+constexpr int64_t kDirectBigCells = 8192;
 SideArgs side16_class_args(const rsk_car_plan *plan, int c, const SideBufs &b, int S, int N) {
     static const int sablate = RSK_ABLATION(RSK_ABLATE_SIDE);
     SideArgs a;
@@ -1433,11 +1436,26 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     const int nfork = big_fork ? 1 : 0;
     if (big_fork) {
         // The rows too big for the fused grid run on a side stream from the
-        // start: their node codes computed on the fly (max(cap) by each of their
-        // workgroups), so they depend on no prep kernel and take CUs beside
-        // car_prep, before the fused grid fills every slot and starves them.
+        // start, so they depend on no prep kernel and take CUs beside car_prep,
+        // before the fused grid fills every slot and starves them.  Few cells
+        // (config 4: 8 rows of 1,000-1,800 neighbours x 64 scenarios): a
+        // workgroup per (row, scenario) counting that cell's neighbour nodes in
+        // an LDS hash with exact cap - use (car_direct_kernel) — 512 workgroups
+        // in flight instead of 8 pivot teams; otherwise the pivot teams with
+        // node codes computed on the fly (max(cap) by each of their workgroups).
         RSK_TRY(aux_fork(ctx, nfork));
-        RSK_TRY(launch_side16_classes(plan, ctx, ctx->aux[0], sb, S, N, big_hi, kNumSide, -1, true));
+        const int b0 = plan->side_beg[kNumSide - 1], b1 = plan->side_end[big_hi];  // degree descending
+        if (!d_score && (int64_t)(b1 - b0) * S <= kDirectBigCells) {  // (targets only: no scores)
+            int dmax = 0;
+            for (int c = big_hi; c < kNumSide; ++c) dmax = std::max(dmax, plan->side_dmax[c]);
+            ScopedTimer tb(ctx, "car_side", ctx->aux[0]);
+            RSK_TRY(launch_car_direct(ctx->aux[0], plan->drp.as<int>(), plan->dci.as<int>(),
+                                      plan->drows.ptr ? plan->drows.as<int>() : nullptr, b1 - b0, d_assign, d_use,
+                                      d_cap, d_haz, S, N, dmax, d_target, &plan->side_scratch,
+                                      plan->side_items.as<int>() + (size_t)b0 * 4, 4));
+        } else {
+            RSK_TRY(launch_side16_classes(plan, ctx, ctx->aux[0], sb, S, N, big_hi, kNumSide, -1, true));
+        }
         ScopedTimer tm(ctx, "car_prep");
         RSK_TRY(launch_prep(ctx->stream, pa));
     } else {

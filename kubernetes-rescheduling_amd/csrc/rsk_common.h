@@ -129,10 +129,12 @@ int ws_u64_layout(int64_t N, int64_t S, int64_t H, U64Slice *out);  // returns t
 int ws_check_u64(int64_t N, int64_t S, int64_t H);
 int ws_check_ptr(const void *p, const char *name);
 
-// One-launch CAR of a small batch (rsk_rounds.hip): rows [0, Q) of the
-// deduplicated CSR rp / ci (pods rows[i], or i), S scenarios; targets only.
+// One-launch CAR, a workgroup per (row, scenario) (rsk_rounds.hip): plan rows
+// i = items[k * istride] for k < Q (items null: i = k) of the deduplicated CSR
+// rp / ci (pod rows[i], or i), S scenarios, into out_target[i * S + s]; targets
+// only, exact remaining CPU from cap / use (no node codes).
 int launch_car_direct(hipStream_t st, const int *rp, const int *ci, const int *rows, int Q, const int *assign,
                       const int *use, const int *cap, const uint8_t *haz, int S, int N, int dmax, int *out_target,
-                      DevBuf *scratch);
+                      DevBuf *scratch, const int *items = nullptr, int istride = 1);
 
 }  // namespace rsk
