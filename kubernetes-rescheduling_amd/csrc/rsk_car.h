@@ -11,36 +11,11 @@
 #include <cstdint>
 
 #include "rsk_common.h"
+#include "rsk_plan.h"
 
 namespace rsk {
 
 constexpr int kKeyHaz = INT_MIN;  // cap - use never reaches INT_MIN (both in [0, 2^31))
-constexpr int kMaxDegree = 65535;                  // 16-bit counts in the side kernel's tables (rsk_side16.hip)
-constexpr int kLightMax = 32;                      // LDS-tile rows: deg <= 32
-constexpr int kPairMax = 16;                       // pairwise-count classes: deg <= 16
-constexpr int kPackMaxN = (1 << 24) - 1;           // wide sorted classes pack node << 8 | image row: N < kPackMaxN
-constexpr int kMidMax = 64;                        // mid rows: 33..64 (17..64 when N >= kPackMaxN)
-constexpr int kNumMid = 2;                         // buckets D = 32, 64
-constexpr int kMidW[kNumMid] = {36, 68};           // record ints: oi, d, nb[D], pad to x4
-constexpr int kNumHeavy = 6;                       // hub classes: (64,128] (128,256] ... (2048,4096]
-constexpr int kHeavyMax[kNumHeavy] = {128, 255, 512, 1024, 2048, 4096};  // <= 255: u8 counters
-constexpr int kHeavyNJ[kNumHeavy] = {2, 4, 8, 16, 0, 0};  // register entries per lane (0: LDS re-reads)
-constexpr int kHubMax = 4096;                      // wide hub kernel: rows up to this degree
-
-// Light-row tiles.
-constexpr int kTileOwners = 128;                   // max rows scored per tile
-constexpr int kTileRows = 144;                     // max image rows (distinct neighbours) per tile (< 256)
-constexpr int kTileRecInts = 1020;                 // max record ints per tile (+4: unit counter)
-constexpr int kTileThreads = 256;
-constexpr int kNumCls = 6;                         // degree classes d = 1, 2, {0,3,4}, 5-8, 9-16, 17-32
-constexpr int kClsW[kNumCls] = {2, 2, 4, 8, 12, 20};  // record ints
-constexpr int kMetaW = 16;                         // tile meta ints: img_off, nrows, rec_off, rec_ints, n[6], off[6]
-static_assert(kTileRecInts <= kTileThreads * 4, "records are copied to LDS as one int4 per thread");
-
-struct HeavyItem {
-    int oi, rb, d, pad;
-};
-
 struct CarState {
     int bc;  // best count (max score); 0 = no non-hazard neighbour node
     int br;  // remaining CPU of the best node
@@ -334,8 +309,6 @@ struct Tile16Args {
 
 // Side rows of the compact path (rsk_side16.hip): every row above the tiles,
 // in launches by degree class; a work item is (row, chunk of 64 scenarios).
-constexpr int kNumSide = 6;
-constexpr int kSideMax[kNumSide] = {32, 128, 512, 2048, 8192, kMaxDegree};  // class upper degrees
 struct SideArgs {
     const int *items;         // [n_rows][4]: out row, offset into col, degree, 0 (degree descending)
     int n_rows, nchunk;       // work items = n_rows * nchunk, chunk-major

@@ -901,12 +901,6 @@ struct rsk_car_plan {
 namespace {
 
 
-int heavy_class(int d) {
-    for (int c = 0; c < kNumHeavy; ++c)
-        if (d <= kHeavyMax[c]) return c;
-    return -1;
-}
-
 int next_pow2(int x) {
     int p = 1;
     while (p < x) p <<= 1;
@@ -976,65 +970,6 @@ HubKern hub_kern_mode(int mode, int nj) {
     return hub_kern_nj<kHubHash, kW>(nj);
 }
 
-// Locality order of the pods: DFS over the (deduplicated) relation graph, each
-// node's DFS-tree children visited smallest subtree first, roots in pod order.
-// Consecutive runs of CP pods of this order become tiles.
-std::vector<int> locality_order(int P, const std::vector<int> &rp, const std::vector<int> &ci) {
-    std::vector<int> parent(P, -1), pre;
-    std::vector<char> seen(P, 0);
-    pre.reserve(P);
-    std::vector<std::pair<int, int>> st;  // (node, next edge)
-    for (int r = 0; r < P; ++r) {
-        if (seen[r]) continue;
-        seen[r] = 1;
-        pre.push_back(r);
-        st.push_back({r, rp[r]});
-        while (!st.empty()) {
-            auto &top = st.back();
-            const int u = top.first;
-            if (top.second >= rp[u + 1]) { st.pop_back(); continue; }
-            const int v = ci[top.second++];
-            if (seen[v]) continue;
-            seen[v] = 1;
-            parent[v] = u;
-            pre.push_back(v);
-            st.push_back({v, rp[v]});
-        }
-    }
-    std::vector<int> size(P, 1);
-    for (int k = P - 1; k >= 0; --k) {
-        const int v = pre[k];
-        if (parent[v] >= 0) size[parent[v]] += size[v];
-    }
-    std::vector<int> cptr(P + 1, 0), kids(P > 0 ? P : 1);
-    for (int v = 0; v < P; ++v) if (parent[v] >= 0) ++cptr[parent[v] + 1];
-    for (int v = 0; v < P; ++v) cptr[v + 1] += cptr[v];
-    {
-        std::vector<int> fill(cptr.begin(), cptr.end() - 1);
-        for (int k = 0; k < P; ++k) {
-            const int v = pre[k];
-            if (parent[v] >= 0) kids[fill[parent[v]]++] = v;
-        }
-    }
-    for (int u = 0; u < P; ++u)
-        std::stable_sort(kids.begin() + cptr[u], kids.begin() + cptr[u + 1],
-                         [&](int a, int b) { return size[a] < size[b]; });
-    std::vector<int> order;
-    order.reserve(P);
-    std::vector<int> stack;
-    for (int r = 0; r < P; ++r) {
-        if (parent[r] >= 0) continue;
-        stack.push_back(r);
-        while (!stack.empty()) {
-            const int u = stack.back();
-            stack.pop_back();
-            order.push_back(u);
-            for (int k = cptr[u + 1] - 1; k >= cptr[u]; --k) stack.push_back(kids[k]);
-        }
-    }
-    return order;
-}
-
 int upload(DevBuf &buf, const void *src, size_t bytes) {
     if (!bytes) return RSK_OK;
     RSK_TRY(buf.reserve(bytes));
@@ -1042,245 +977,58 @@ int upload(DevBuf &buf, const void *src, size_t bytes) {
     return RSK_OK;
 }
 
-int light_class(int d) {  // d = 0 rows go to the D = 4 class: all entries masked -> zero case
-    if (d == 1) return 0;
-    if (d == 2) return 1;
-    if (d <= 4) return 2;
-    if (d <= 8) return 3;
-    if (d <= 16) return 4;
-    return 5;
-}
-
-// Tiles: rows in DFS order are packed greedily into tiles of at most
-// owners_cap rows whose distinct neighbours (the image rows) number at most
-// rows_cap and whose records fit kTileRecInts.  On a relation tree in DFS order
-// a tile's image is essentially its own pods plus a few external neighbours.
-struct TileBuilder {
-    std::vector<int> img_pods, meta, recs;
-    std::vector<int> cur_pods;
-    std::unordered_map<int, int> cur_slot;
-    std::vector<int> cur_rec[kNumCls];
-    int cur_rows = 0, cur_rec_ints = 0, T = 0, rmax = 0, recmax = 0, n_sorted = 0, n_rows = 0;
-    int owners_cap = kTileOwners, rows_cap = kTileRows;
-    int64_t img_total = 0;
-
-    bool fits(const int *nb, int d) const {
-        if (cur_rows >= owners_cap) return false;
-        if (cur_rec_ints + kClsW[light_class(d)] + 2 > kTileRecInts) return false;  // + worst-case padding
-        int fresh = 0;
-        for (int j = 0; j < d; ++j) fresh += !cur_slot.count(nb[j]);  // nb is deduplicated
-        return (int)cur_pods.size() + fresh <= rows_cap;
-    }
-    void add(int oi, const int *nb, int d) {
-        int lr[kLightMax];
-        for (int j = 0; j < d; ++j) {
-            auto it = cur_slot.find(nb[j]);
-            if (it == cur_slot.end()) {
-                it = cur_slot.emplace(nb[j], (int)cur_pods.size()).first;
-                cur_pods.push_back(nb[j]);
-            }
-            lr[j] = it->second;
-        }
-        const int c = light_class(d);
-        auto &e = cur_rec[c];
-        const size_t o = e.size();
-        e.resize(o + kClsW[c], 0);
-        e[o] = oi;
-        if (c == 0) {
-            e[o + 1] = lr[0];
-        } else if (c == 1) {
-            e[o + 1] = lr[0] | (lr[1] << 16);
-        } else {
-            // [oi, d, rows...]; the sorted classes (c >= 5) start their rows at
-            // int 4 so the scorer reads them as aligned int4 words
-            const int r0 = c >= 5 ? 4 : 2;
-            e[o + 1] = d;
-            for (int j = 0; j < d; ++j) e[o + r0 + j / 2] |= lr[j] << ((j & 1) * 16);
-        }
-        n_sorted += c >= 5;
-        ++n_rows;
-        cur_rec_ints += kClsW[c];
-        ++cur_rows;
-    }
-    void close() {
-        if (!cur_rows) return;
-        // every tile stages >= 1 image row (a tile of deg-0 rows stages pod 0,
-        // which no record reads)
-        if (cur_pods.empty()) cur_pods.push_back(0);
-        const int rec_off = (int)recs.size();
-        int m[kMetaW] = {};
-        for (int c = 0; c < kNumCls; ++c) {
-            // every class starts 16-B aligned (int4 record reads, 16-B scalar block loads)
-            while ((recs.size() - rec_off) % 4) recs.push_back(0);
-            m[4 + kNumCls + c] = (int)recs.size() - rec_off;
-            m[4 + c] = (int)cur_rec[c].size() / kClsW[c];
-            recs.insert(recs.end(), cur_rec[c].begin(), cur_rec[c].end());
-            cur_rec[c].clear();
-        }
-        while ((recs.size() - rec_off) % 4) recs.push_back(0);
-        const int rec_ints = (int)recs.size() - rec_off;
-        m[0] = (int)img_pods.size();
-        m[1] = (int)cur_pods.size();
-        m[2] = rec_off;
-        m[3] = rec_ints;
-        meta.insert(meta.end(), m, m + kMetaW);
-        img_pods.insert(img_pods.end(), cur_pods.begin(), cur_pods.end());
-        img_total += (int64_t)cur_pods.size();
-        rmax = std::max(rmax, (int)cur_pods.size());
-        recmax = std::max(recmax, rec_ints);
-        ++T;
-        cur_pods.clear();
-        cur_slot.clear();
-        cur_rows = 0;
-        cur_rec_ints = 0;
-    }
-};
-
 int build_plan(rsk_car_plan *plan, const int32_t *row_ptr, const int32_t *col_idx, int32_t P, const int32_t *rows,
                int32_t Q) {
-    // deduplicated adjacency without self edges (the evicted pod is off the cluster)
-    std::vector<int> rp(P + 1, 0), ci;
-    ci.reserve(P ? row_ptr[P] : 0);
-    std::vector<int> nb;
-    for (int p = 0; p < P; ++p) {
-        nb.assign(col_idx + row_ptr[p], col_idx + row_ptr[p + 1]);
-        std::sort(nb.begin(), nb.end());
-        nb.erase(std::unique(nb.begin(), nb.end()), nb.end());
-        nb.erase(std::remove(nb.begin(), nb.end(), p), nb.end());
-        ci.insert(ci.end(), nb.begin(), nb.end());
-        rp[p + 1] = (int)ci.size();
-    }
-    {  // the deduplicated CSR for the one-launch path (rsk_rounds.hip car_direct_kernel)
-        RSK_TRY(plan->drp.reserve(rp.size() * 4));
-        RSK_TRY(plan->dci.reserve(std::max<size_t>(1, ci.size()) * 4));
-        RSK_HIP(hipMemcpy(plan->drp.ptr, rp.data(), rp.size() * 4, hipMemcpyHostToDevice));
-        if (!ci.empty()) RSK_HIP(hipMemcpy(plan->dci.ptr, ci.data(), ci.size() * 4, hipMemcpyHostToDevice));
+    PlanHost h;
+    RSK_TRY(plan_build_host(row_ptr, col_idx, P, rows, Q, plan->light_max, plan->owners_cap, plan->rows_cap, &h));
+    {   // the deduplicated CSR for the one-launch path (rsk_rounds.hip car_direct_kernel)
+        RSK_TRY(plan->drp.reserve(h.rp.size() * 4));
+        RSK_TRY(plan->dci.reserve(std::max<size_t>(1, h.ci.size()) * 4));
+        RSK_HIP(hipMemcpy(plan->drp.ptr, h.rp.data(), h.rp.size() * 4, hipMemcpyHostToDevice));
+        if (!h.ci.empty()) RSK_HIP(hipMemcpy(plan->dci.ptr, h.ci.data(), h.ci.size() * 4, hipMemcpyHostToDevice));
         if (rows && Q > 0) {
             RSK_TRY(plan->drows.reserve((size_t)Q * 4));
             RSK_HIP(hipMemcpy(plan->drows.ptr, rows, (size_t)Q * 4, hipMemcpyHostToDevice));
         }
-        for (int p = 0; p < P; ++p) plan->ddmax = std::max(plan->ddmax, rp[p + 1] - rp[p]);
+        plan->ddmax = h.ddmax;
     }
-    const std::vector<int> order = locality_order(P, rp, ci);
-    std::vector<int> pos(P);
-    for (int k = 0; k < P; ++k) pos[order[k]] = k;
-
-    std::vector<int> light;  // row indices i with deg <= light_max, to be tiled in DFS order
-    std::vector<std::vector<int>> midr(kNumMid);
-    std::vector<std::vector<HeavyItem>> hitems(kNumHeavy);
-    std::vector<int> hcol, pcol;
-    std::vector<HeavyItem> sitems;  // compact path: every side row
-    for (int i = 0; i < Q; ++i) {
-        const int p = rows ? rows[i] : i;
-        const int d = rp[p + 1] - rp[p];
-        plan->max_deg = std::max(plan->max_deg, d);
-        const int *nbp = ci.data() + rp[p];
-        if (d <= plan->light_max) {
-            light.push_back(i);
-        } else if (d <= kMidMax) {
-            const int b = d <= 32 ? 0 : 1;  // bucket 0 only in the N >= kPackMaxN variant
-            auto &e = midr[b];
-            const size_t o = e.size();
-            e.resize(o + kMidW[b], 0);
-            e[o] = i;
-            e[o + 1] = d;
-            for (int j = 0; j < d; ++j) e[o + 2 + j] = nbp[j];
-            plan->n_mid[b] += 1;
-        } else if (d <= kHubMax) {
-            const int c = heavy_class(d);
-            hitems[c].push_back({i, (int)hcol.size(), d, 0});
-            hcol.insert(hcol.end(), nbp, nbp + d);
-            plan->n_heavy[c] += 1;
-            plan->heavy_dmax[c] = std::max(plan->heavy_dmax[c], d);
-        }
-        if (d > plan->light_max) {  // compact path: every side row through car_side16
-            sitems.push_back({i, (int)pcol.size(), d, 0});
-            pcol.insert(pcol.end(), nbp, nbp + d);
-        }
+    plan->max_deg = h.max_deg;
+    plan->T = plan->T_lean = h.T;
+    plan->n_lean_rows = h.n_tile_rows;
+    plan->rmax = std::max(1, h.rmax);
+    plan->recmax = h.recmax;
+    plan->n_tile_rows = h.n_tile_rows;
+    plan->n_sorted_rows = h.n_sorted_rows;
+    plan->img_rows_total = h.img_rows_total;
+    plan->img_pods_distinct = h.img_pods_distinct;
+    plan->n_img_pods = (int64_t)h.img_pods.size();
+    plan->n_recs = h.n_recs;
+    if (h.T > 0) {
+        RSK_TRY(upload(plan->img_pods, h.img_pods.data(), h.img_pods.size() * 4));
+        RSK_TRY(upload(plan->meta, h.meta.data(), h.meta.size() * 4));
+        RSK_TRY(upload(plan->recs, h.recs.data(), h.recs.size() * 4));
     }
-    std::stable_sort(light.begin(), light.end(), [&](int x, int y) {
-        return pos[rows ? rows[x] : x] < pos[rows ? rows[y] : y];
-    });
-    // one tile list: every row of degree <= light_max in DFS order (the 17..32
-    // rows included: the tile kernel's register-light counting walk scores them)
-    TileBuilder tb;
-    tb.owners_cap = plan->owners_cap;
-    tb.rows_cap = plan->rows_cap;
-    for (int i : light) {
-        const int p = rows ? rows[i] : i;
-        const int d = rp[p + 1] - rp[p];
-        const int *nbp = ci.data() + rp[p];
-        if (!tb.fits(nbp, d)) tb.close();
-        tb.add(i, nbp, d);
+    for (int b = 0; b < kNumMid; ++b) {
+        plan->n_mid[b] = h.n_mid[b];
+        RSK_TRY(upload(plan->mid[b], h.mid[b].data(), h.mid[b].size() * 4));
     }
-    tb.close();
-    plan->T_lean = tb.T;
-    plan->n_lean_rows = tb.n_rows;
-    plan->T = tb.T;
-    plan->rmax = std::max(1, tb.rmax);
-    plan->recmax = tb.recmax;
-    plan->n_tile_rows = (int)light.size();
-    plan->n_sorted_rows = tb.n_sorted;
-    plan->img_rows_total = tb.img_total;
-    {
-        std::vector<char> seen(P, 0);
-        for (int q : tb.img_pods) seen[q] = 1;
-        plan->img_pods_distinct = std::count(seen.begin(), seen.end(), 1);
+    for (int c = 0; c < kNumHeavy; ++c) {
+        plan->n_heavy[c] = h.n_heavy[c];
+        plan->heavy_dmax[c] = h.heavy_dmax[c];
+        RSK_TRY(upload(plan->heavy_items[c], h.heavy_items[c].data(), h.heavy_items[c].size() * sizeof(HeavyItem)));
     }
-    plan->n_img_pods = (int64_t)tb.img_pods.size();
-    plan->n_recs = std::max<int64_t>(4, (int64_t)tb.recs.size());
-    if (tb.T > 0) {
-        RSK_TRY(upload(plan->img_pods, tb.img_pods.data(), tb.img_pods.size() * 4));
-        RSK_TRY(upload(plan->meta, tb.meta.data(), tb.meta.size() * 4));
-        // 64 zero ints past the last blob: the 64-scenario tile kernel reads
-        // record blocks through the scalar cache without clamping them
-        tb.recs.resize(tb.recs.size() + 64, 0);
-        RSK_TRY(upload(plan->recs, tb.recs.data(), tb.recs.size() * 4));
+    RSK_TRY(upload(plan->hcol, h.hcol.data(), h.hcol.size() * 4));
+    RSK_TRY(upload(plan->pcol, h.pcol.data(), h.pcol.size() * 4));
+    plan->n_big = h.n_big;
+    plan->big_dmax = h.big_dmax;
+    if (h.n_big) RSK_TRY(upload(plan->big_items, h.side_items.data(), (size_t)h.n_big * 4 * 4));
+    for (int c = 0; c < kNumSide; ++c) {
+        plan->side_beg[c] = h.side_beg[c];
+        plan->side_end[c] = h.side_end[c];
+        plan->side_dmax[c] = h.side_dmax[c];
     }
-    for (int b = 0; b < kNumMid; ++b) RSK_TRY(upload(plan->mid[b], midr[b].data(), midr[b].size() * 4));
-    for (int c = 0; c < kNumHeavy; ++c)
-        RSK_TRY(upload(plan->heavy_items[c], hitems[c].data(), hitems[c].size() * sizeof(HeavyItem)));
-    RSK_TRY(upload(plan->hcol, hcol.data(), hcol.size() * 4));
-    RSK_TRY(upload(plan->pcol, pcol.data(), pcol.size() * 4));
-    {   // car_side16 classes: all side rows, degree descending; class c holds
-        // the rows of degree (kSideMax[c - 1], kSideMax[c]] at [side_beg[c], side_end[c])
-        std::vector<HeavyItem> &all = sitems;
-        std::stable_sort(all.begin(), all.end(), [](const HeavyItem &x, const HeavyItem &y) { return x.d > y.d; });
-        {   // the wide path's rows above kHubMax (degree descending: a prefix)
-            int nb = 0;
-            while (nb < (int)all.size() && all[nb].d > kHubMax) ++nb;
-            plan->n_big = nb;
-            plan->big_dmax = nb ? all[0].d : 0;
-            if (nb) RSK_TRY(upload(plan->big_items, all.data(), (size_t)nb * sizeof(HeavyItem)));
-        }
-        int end = (int)all.size();
-        for (int c = 0; c < kNumSide; ++c) {
-            int b = end;
-            while (b > 0 && all[b - 1].d <= kSideMax[c]) --b;
-            plan->side_beg[c] = b;
-            plan->side_end[c] = end;
-            plan->side_dmax[c] = b < end ? all[b].d : 0;
-            end = b;
-        }
-        {   // cumulative distinct neighbour pods: the images, then side classes 0, 1, ...
-            std::vector<char> seen(P, 0);
-            int64_t n = 0;
-            for (int q : tb.img_pods) n += !seen[q], seen[q] = 1;
-            plan->nb_distinct[0] = n;
-            for (int c = 0; c < kNumSide; ++c) {
-                for (int k = plan->side_beg[c]; k < plan->side_end[c]; ++k)
-                    for (int j = 0; j < all[k].d; ++j) {
-                        const int q = pcol[all[k].rb + j];
-                        n += !seen[q], seen[q] = 1;
-                    }
-                plan->nb_distinct[c + 1] = n;
-            }
-        }
-        std::vector<int32_t> flat;
-        flat.reserve(all.size() * 4);
-        for (const HeavyItem &h : all) flat.insert(flat.end(), {h.oi, h.rb, h.d, 0});
-        RSK_TRY(upload(plan->side_items, flat.data(), flat.size() * 4));
-    }
+    for (int c = 0; c <= kNumSide; ++c) plan->nb_distinct[c] = h.nb_distinct[c];
+    RSK_TRY(upload(plan->side_items, h.side_items.data(), h.side_items.size() * 4));
     return RSK_OK;
 }
 
@@ -1329,6 +1077,9 @@ struct SideBufs {
 // Classes from kSideBig up (rows above 128 neighbours: few work items, each
 // latency-bound) run on a side stream beside the tiles (rsk_car_plan_execute).
 constexpr int kSideBig = 2;
+// rows beyond the fused grid with at most this many (row, scenario) cells run
+// as one workgroup per cell (car_direct_kernel) instead of pivot teams
+constexpr int64_t kDirectBigCells = 8192;
 SideArgs side16_class_args(const rsk_car_plan *plan, int c, const SideBufs &b, int S, int N) {
     static const int sablate = RSK_ABLATION(RSK_ABLATE_SIDE);
     SideArgs a;
@@ -1685,11 +1436,26 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     const int nfork = big_fork ? 1 : 0;
     if (big_fork) {
         // The rows too big for the fused grid run on a side stream from the
-        // start: their node codes computed on the fly (max(cap) by each of their
-        // workgroups), so they depend on no prep kernel and take CUs beside
-        // car_prep, before the fused grid fills every slot and starves them.
+        // start, so they depend on no prep kernel and take CUs beside car_prep,
+        // before the fused grid fills every slot and starves them.  Few cells
+        // (config 4: 8 rows of 1,000-1,800 neighbours x 64 scenarios): a
+        // workgroup per (row, scenario) counting that cell's neighbour nodes in
+        // an LDS hash with exact cap - use (car_direct_kernel) — 512 workgroups
+        // in flight instead of 8 pivot teams; otherwise the pivot teams with
+        // node codes computed on the fly (max(cap) by each of their workgroups).
         RSK_TRY(aux_fork(ctx, nfork));
-        RSK_TRY(launch_side16_classes(plan, ctx, ctx->aux[0], sb, S, N, big_hi, kNumSide, -1, true));
+        const int b0 = plan->side_beg[kNumSide - 1], b1 = plan->side_end[big_hi];  // degree descending
+        if (!d_score && (int64_t)(b1 - b0) * S <= kDirectBigCells) {  // (targets only: no scores)
+            int dmax = 0;
+            for (int c = big_hi; c < kNumSide; ++c) dmax = std::max(dmax, plan->side_dmax[c]);
+            ScopedTimer tb(ctx, "car_side", ctx->aux[0]);
+            RSK_TRY(launch_car_direct(ctx->aux[0], plan->drp.as<int>(), plan->dci.as<int>(),
+                                      plan->drows.ptr ? plan->drows.as<int>() : nullptr, b1 - b0, d_assign, d_use,
+                                      d_cap, d_haz, S, N, dmax, d_target, &plan->side_scratch,
+                                      plan->side_items.as<int>() + (size_t)b0 * 4, 4));
+        } else {
+            RSK_TRY(launch_side16_classes(plan, ctx, ctx->aux[0], sb, S, N, big_hi, kNumSide, -1, true));
+        }
         ScopedTimer tm(ctx, "car_prep");
         RSK_TRY(launch_prep(ctx->stream, pa));
     } else {

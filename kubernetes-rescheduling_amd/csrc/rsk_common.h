@@ -9,12 +9,9 @@
 #include <vector>
 
 #include "rsk.h"
+#include "rsk_host.h"
 
 namespace rsk {
-
-// Error reporting: thread-local last error, returned through rsk_last_error().
-void set_error(const char *fmt, ...);
-const char *last_error();
 
 #define RSK_HIP(expr)                                                                    \
     do {                                                                                 \
@@ -24,40 +21,6 @@ const char *last_error();
             return RSK_EHIP;                                                             \
         }                                                                                \
     } while (0)
-
-#define RSK_CHECK(cond, ...)                                                             \
-    do {                                                                                 \
-        if (!(cond)) {                                                                   \
-            ::rsk::set_error(__VA_ARGS__);                                               \
-            return RSK_EINVAL;                                                           \
-        }                                                                                \
-    } while (0)
-
-#define RSK_TRY(expr)                                                                    \
-    do {                                                                                 \
-        int _rc = (expr);                                                                \
-        if (_rc != RSK_OK) return _rc;                                                   \
-    } while (0)
-
-// Experiment switches.  The product librsk.so reads no environment variable:
-// RSK_KNOB(NAME, dflt) is the compiled default.  `make variant NAME=x
-// DEFS=-DRSK_ENV_KNOBS` builds librsk_x.so, whose knobs read getenv("NAME")
-// (A/B runs through RSK_LIB=.../librsk_x.so).  The profiling ablations, which
-// make results wrong on purpose, exist only with -DRSK_ABLATIONS: otherwise
-// RSK_ABL(args) is the constant 0 and the kernels compile without them.
-int env_int(const char *name, int dflt);
-#if defined(RSK_ENV_KNOBS) || defined(RSK_ABLATIONS)
-#define RSK_KNOB(name, dflt) ::rsk::env_int(#name, (dflt))
-#else
-#define RSK_KNOB(name, dflt) (dflt)
-#endif
-#ifdef RSK_ABLATIONS
-#define RSK_ABLATION(name) ::rsk::env_int(#name, 0)
-#define RSK_ABL(a) ((a).ablate)
-#else
-#define RSK_ABLATION(name) 0
-#define RSK_ABL(a) 0
-#endif
 
 // Grow-only device scratch buffer owned by a context or plan.
 struct DevBuf {
@@ -166,10 +129,12 @@ int ws_u64_layout(int64_t N, int64_t S, int64_t H, U64Slice *out);  // returns t
 int ws_check_u64(int64_t N, int64_t S, int64_t H);
 int ws_check_ptr(const void *p, const char *name);
 
-// One-launch CAR of a small batch (rsk_rounds.hip): rows [0, Q) of the
-// deduplicated CSR rp / ci (pods rows[i], or i), S scenarios; targets only.
+// One-launch CAR, a workgroup per (row, scenario) (rsk_rounds.hip): plan rows
+// i = items[k * istride] for k < Q (items null: i = k) of the deduplicated CSR
+// rp / ci (pod rows[i], or i), S scenarios, into out_target[i * S + s]; targets
+// only, exact remaining CPU from cap / use (no node codes).
 int launch_car_direct(hipStream_t st, const int *rp, const int *ci, const int *rows, int Q, const int *assign,
                       const int *use, const int *cap, const uint8_t *haz, int S, int N, int dmax, int *out_target,
-                      DevBuf *scratch);
+                      DevBuf *scratch, const int *items = nullptr, int istride = 1);
 
 }  // namespace rsk

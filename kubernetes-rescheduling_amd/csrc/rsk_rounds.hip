@@ -125,18 +125,31 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
     if (tid < 8) tab[2 * H + tid] = 0u;
     move_sync<kGlobal>();
     const unsigned mask = (unsigned)H - 1u;
-    // A: count every neighbour on a non-hazard node
-    for (int j = tid; j < d; j += kMoveThreads) {
-        const int x = assign[(size_t)col[b + j] * S + s];
-        if ((unsigned)x >= (unsigned)N || haz[(size_t)x * S + s]) continue;
-        const unsigned k = (unsigned)x + 1u;
-        unsigned h = (k * 2654435761u) & mask;
-        while (true) {
-            const unsigned prev = atomicCAS(&keys[h], 0u, k);
-            if (prev == 0u || prev == k) break;
-            h = (h + 1u) & mask;
+    // A: count every neighbour on a non-hazard node (kU neighbours per thread
+    // in flight: the col, assign and hazard loads of a batch issued together
+    // from clamped, always-valid addresses)
+    constexpr int kU = 4;
+    for (int j0 = tid; j0 < d; j0 += kMoveThreads * kU) {
+        int q[kU], x[kU];
+        uint8_t hz[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) q[u] = col[b + min(j0 + u * kMoveThreads, d - 1)];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) x[u] = assign[(size_t)q[u] * S + s];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) hz[u] = haz[(size_t)min((unsigned)x[u], (unsigned)N - 1u) * S + s];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            if (j0 + u * kMoveThreads >= d || (unsigned)x[u] >= (unsigned)N || hz[u]) continue;
+            const unsigned k = (unsigned)x[u] + 1u;
+            unsigned h = (k * 2654435761u) & mask;
+            while (true) {
+                const unsigned prev = atomicCAS(&keys[h], 0u, k);
+                if (prev == 0u || prev == k) break;
+                h = (h + 1u) & mask;
+            }
+            atomicAdd(&cnts[h], 1u);
         }
-        atomicAdd(&cnts[h], 1u);
     }
     move_sync<kGlobal>();
     // B: max count over the slots
@@ -753,7 +766,8 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
 // (rescheduling.py:183-214, the deduplicated rows without self edges).
 template <bool kGlobal>
 __global__ __launch_bounds__(kMoveThreads) void car_direct_kernel(const int *__restrict__ rp, const int *__restrict__ ci,
-                                                                  const int *__restrict__ rows, int Q,
+                                                                  const int *__restrict__ rows,
+                                                                  const int *__restrict__ items, int istride, int Q,
                                                                   const int *__restrict__ assign,
                                                                   const int *__restrict__ use,
                                                                   const int *__restrict__ cap,
@@ -764,7 +778,8 @@ __global__ __launch_bounds__(kMoveThreads) void car_direct_kernel(const int *__r
     unsigned *tab = kGlobal ? gtab + (size_t)blockIdx.x * (size_t)(2 * H + 8) : lds;
     const int units = Q * S;
     for (int u = (int)blockIdx.x; u < units; u += (int)gridDim.x) {
-        const int i = u / S, s = u - i * S;
+        const int k = u / S, s = u - k * S;
+        const int i = items ? items[(size_t)k * istride] : k;  // the plan row (its target row)
         const int p = rows ? rows[i] : i;
         car_move_one<kGlobal>(rp, ci, nullptr, const_cast<int *>(assign), const_cast<int *>(use), cap, haz, nullptr,
                               s, S, N, H, 0, out_target + (size_t)i * S, nullptr, tab, nullptr, nullptr, nullptr,
@@ -1041,7 +1056,7 @@ __global__ __launch_bounds__(256) void blk_scn_kernel(BlkArgs ba, unsigned long 
 
 int launch_car_direct(hipStream_t st, const int *rp, const int *ci, const int *rows, int Q, const int *assign,
                       const int *use, const int *cap, const uint8_t *haz, int S, int N, int dmax, int *out_target,
-                      DevBuf *scratch) {
+                      DevBuf *scratch, const int *items, int istride) {
     if (Q <= 0) return RSK_OK;
     int H = 1;
     while (H < std::max(2, 2 * std::min(dmax, N))) H <<= 1;
@@ -1054,13 +1069,13 @@ int launch_car_direct(hipStream_t st, const int *rp, const int *ci, const int *r
             RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&car_direct_kernel<false>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
         car_direct_kernel<false><<<dim3((unsigned)grid), dim3(kMoveThreads), bytes, st>>>(
-            rp, ci, rows, Q, assign, use, cap, haz, S, N, H, out_target, nullptr);
+            rp, ci, rows, items, istride, Q, assign, use, cap, haz, S, N, H, out_target, nullptr);
     } else {  // a table beyond the LDS: global work areas, one per resident workgroup
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>({units, 1024, (int64_t)((256u << 20) / bytes)}));
         RSK_CHECK(scratch, "direct CAR: no scratch for a %zu-B table", bytes);
         RSK_TRY(scratch->reserve((size_t)grid * bytes));
         car_direct_kernel<true><<<dim3((unsigned)grid), dim3(kMoveThreads), 0, st>>>(
-            rp, ci, rows, Q, assign, use, cap, haz, S, N, H, out_target, scratch->as<unsigned>());
+            rp, ci, rows, items, istride, Q, assign, use, cap, haz, S, N, H, out_target, scratch->as<unsigned>());
     }
     RSK_HIP(hipGetLastError());
     return RSK_OK;

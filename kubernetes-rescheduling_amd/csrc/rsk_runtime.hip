@@ -8,22 +8,6 @@
 
 namespace rsk {
 
-static thread_local char g_err[1024] = "";
-
-void set_error(const char *fmt, ...) {
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(g_err, sizeof(g_err), fmt, ap);
-    va_end(ap);
-}
-
-const char *last_error() { return g_err; }
-
-int env_int(const char *name, int dflt) {  // RSK_KNOB in -DRSK_ENV_KNOBS variant builds only
-    const char *e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
-
 int DevBuf::reserve(size_t need) {
     if (need <= bytes && ptr) return RSK_OK;
     release();
@@ -186,7 +170,6 @@ int rsk_check_ws_layout(int32_t N, int32_t S, int32_t H) {
     return ws_check_u64(N, S, H);
 }
 
-const char *rsk_last_error(void) { return rsk::last_error(); }
 
 int rsk_ctx_create(int device, rsk_ctx **out) {
     RSK_CHECK(out, "null output pointer");

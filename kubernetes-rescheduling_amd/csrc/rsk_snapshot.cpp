@@ -23,7 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 
-#include "rsk_common.h"
+#include "rsk_host.h"
 
 namespace {
 

@@ -23,7 +23,7 @@
 #include <unordered_map>
 #include <vector>
 
-#include "rsk_common.h"
+#include "rsk_host.h"
 
 struct rsk_workmodel {
     std::vector<std::string> names;
@@ -33,12 +33,12 @@ struct rsk_workmodel {
 namespace {
 
 struct Scanner {
-    const char *p, *end;
+    const char *p, *end, *begin;
     std::string err;
     std::string scratch;
 
     bool fail(const char *what) {
-        if (err.empty()) err = std::string(what) + " at byte offset " + std::to_string((long long)(end - p));
+        if (err.empty()) err = std::string(what) + " at byte offset " + std::to_string((long long)(p - begin));
         return false;
     }
     void ws() {
@@ -138,7 +138,7 @@ struct Scanner {
 };
 
 int build(const char *buf, size_t len, rsk_workmodel **out) {
-    Scanner sc{buf, buf + len, {}, {}};
+    Scanner sc{buf, buf + len, buf, {}, {}};
     // Every name gets a provisional id on first sight (as a service key or as
     // a callee); the final order is json.load's: defined services in order of
     // their first key, then callees that are never defined, in order of first

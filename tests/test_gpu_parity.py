@@ -913,3 +913,35 @@ def test_car_direct_small_batches(ctx, S):
         bad = np.nonzero(tgt != ot)[0]
         assert bad.size == 0, f"S={S}: {bad.size} differ, first {bad[0]}: gpu {tgt[bad[0]]} oracle {ot[bad[0]]}"
         assert (tgt.reshape(-1, S)[:, S - 1] == -2).all()     # no candidate anywhere in the last scenario
+
+
+@pytest.mark.parametrize("S,n_hubs", [(64, 6), (256, 40)])
+def test_car_big_rows_beyond_the_fused_grid(ctx, S, n_hubs):
+    """Rows whose tables exceed the fused grid's LDS (degree 1,200-1,900 over
+    5,000 nodes) run on the side stream beside car_prep: as one workgroup per
+    (row, scenario) when they make few cells (S = 64, 6 rows: 384 cells, targets
+    only) and as on-the-fly pivot teams otherwise (S = 256, 40 rows: 10,240
+    cells; and whenever scores are requested).  Both against the oracle, every
+    cell, with and without scores."""
+    from oracle import oracle as orc
+    from rsk import api
+    rng = np.random.default_rng(900 + S)
+    P, N = 4000, 5000
+    hubs = rng.integers(1200, 1900, n_hubs).tolist()
+    rp, ci, a, cap, use, haz = _random_case(rng, P, N, S, max_deg=6, hub_deg=hubs, p_haz=0.1)
+    A = a.reshape(P, S)   # what-if scenarios: mostly one base assignment
+    base = rng.integers(0, N, P)
+    keep = rng.random((P, S)) < 0.97
+    A[keep] = np.repeat(base[:, None], S, axis=1)[keep]
+    a = A.reshape(-1).astype(np.int32)
+    plan = api.CarPlan(rp, ci, ctx=ctx)
+    assert plan.info()["max_degree"] >= 1200
+    t0, _ = plan.execute(a, S, cap, use, haz, N)                    # targets only
+    t1, sc = plan.execute(a, S, cap, use, haz, N, want_score=True)  # pivot teams (scores)
+    plan.close()
+    rp2, ci2 = _dedup_csr(rp, ci)
+    ot, osc = orc.car_sparse(rp2, ci2, a, S, cap, use, haz, N, threads=min(16, os.cpu_count() or 1))
+    for t, label in ((t0, "targets only"), (t1, "with scores")):
+        bad = np.nonzero(t != ot)[0]
+        assert bad.size == 0, f"{label}: {bad.size} cells differ, first {bad[0]}: gpu {t[bad[0]]} oracle {ot[bad[0]]}"
+    assert np.array_equal(sc, osc)

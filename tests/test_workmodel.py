@@ -104,3 +104,12 @@ def test_missing_file_raises(tmp_path):
     from rsk._lib import RskError
     with pytest.raises(RskError):
         workmodel.read_workmodel(str(tmp_path / "nope.json"))
+
+
+def test_malformed_error_names_the_byte_offset():
+    _lib_or_skip()
+    from rsk import workmodel
+    from rsk._lib import RskError
+    text = '{"a": {"external_services": [{"services": ["b"'
+    with pytest.raises(RskError, match=f"byte offset {len(text)}"):
+        workmodel.read_workmodel(text.encode())
