@@ -267,9 +267,13 @@ __device__ __forceinline__ int block_capmax(const int *__restrict__ cap, int N, 
     int mc = 0;
     const int N4 = ((uintptr_t)cap % 16) == 0 ? N / 4 : 0;
     const int4 *cap4 = reinterpret_cast<const int4 *>(cap);
-    for (int i = t; i < N4; i += kT) {
-        const int4 v = cap4[i];
-        mc = max(mc, max(max(v.x, v.y), max(v.z, v.w)));
+    constexpr int kU = 8;  // 16-B loads in flight per thread (clamped: a repeated word does not change a max)
+    for (int i0 = t; i0 < N4; i0 += kT * kU) {
+        int4 v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) v[u] = cap4[min(i0 + u * kT, N4 - 1)];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) mc = max(mc, max(max(v[u].x, v[u].y), max(v[u].z, v[u].w)));
     }
     for (int n = 4 * N4 + t; n < N; n += kT) mc = max(mc, cap[n]);
     mc = dpp_max(mc);
