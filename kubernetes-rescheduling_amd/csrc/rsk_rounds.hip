@@ -54,6 +54,7 @@ namespace {
 
 constexpr int kMoveThreads = 256;
 constexpr int kNoEvict = -3;
+constexpr size_t kPersistLdsCols = 39 * 1024;  // LDS per persistent workgroup with the columns (4 per CU)
 
 __global__ __launch_bounds__(256) void fill_i32_kernel(int *__restrict__ out, size_t n, int v) {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -78,6 +79,29 @@ __device__ __forceinline__ unsigned long long move_pack(int rem, int n) {  // (r
     return ((unsigned long long)((unsigned)rem ^ 0x80000000u) << 32) | (unsigned long long)(0x7fffffffu - (unsigned)n);
 }
 
+// A scenario's node state as car_move_one and blk_update read and update it:
+// the global [N][S] usage and hazard arrays at scenario s, or (the persistent
+// loop) the scenario's own columns in LDS — usage as int[N], hazard as a
+// bitset — so the round's dependent reads of a node's state are LDS round trips.
+struct NodeGlobal {
+    int *use;
+    uint8_t *haz;
+    int S, s;
+    __device__ __forceinline__ int &u(int n) const { return use[(size_t)n * S + s]; }
+    __device__ __forceinline__ bool h(int n) const { return haz[(size_t)n * S + s] != 0; }
+    __device__ __forceinline__ void set_h(int n, bool v) const { haz[(size_t)n * S + s] = v; }
+};
+struct NodeCols {
+    int *use;       // [N] (LDS)
+    unsigned *hb;   // [ceil(N / 32)] hazard bits (LDS)
+    __device__ __forceinline__ int &u(int n) const { return use[n]; }
+    __device__ __forceinline__ bool h(int n) const { return (hb[n >> 5] >> (n & 31)) & 1u; }
+    __device__ __forceinline__ void set_h(int n, bool v) const {
+        if (v) atomicOr(&hb[n >> 5], 1u << (n & 31));
+        else atomicAnd(&hb[n >> 5], ~(1u << (n & 31)));
+    }
+};
+
 // One scenario s of car_move_kernel.  tab = the hash (keys[H] | cnts[H] | 8
 // reduction words): the workgroup's LDS, or (kGlobal: rows whose distinct
 // nodes overflow the LDS) its slot of a global work area, where every switch
@@ -89,10 +113,10 @@ __device__ __forceinline__ void move_sync() {
     __syncthreads();
 }
 
-template <bool kGlobal>
+template <bool kGlobal, class NS>
 __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, const int *__restrict__ col,
-                                             const int *__restrict__ pod_cpu, int *assign, int *use,
-                                             const int *__restrict__ cap, const uint8_t *__restrict__ haz,
+                                             const int *__restrict__ pod_cpu, int *assign, const NS &ns,
+                                             const int *__restrict__ cap,
                                              const int *__restrict__ evict, int s, int S, int N, int H, int update,
                                              int *__restrict__ out_target, unsigned short *__restrict__ asg16,
                                              unsigned *tab, unsigned long long *__restrict__ kpick,
@@ -137,7 +161,7 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
 #pragma unroll
         for (int u = 0; u < kU; ++u) x[u] = assign[(size_t)q[u] * S + s];
 #pragma unroll
-        for (int u = 0; u < kU; ++u) hz[u] = haz[(size_t)min((unsigned)x[u], (unsigned)N - 1u) * S + s];
+        for (int u = 0; u < kU; ++u) hz[u] = ns.h((int)min((unsigned)x[u], (unsigned)N - 1u));
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             if (j0 + u * kMoveThreads >= d || (unsigned)x[u] >= (unsigned)N || hz[u]) continue;
@@ -165,7 +189,7 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
             if (cnts[h] != M) continue;
             const int n = (int)keys[h] - 1;
             ++nb;
-            const unsigned long long k = move_pack(cap[n] - use[(size_t)n * S + s], n);
+            const unsigned long long k = move_pack(cap[n] - ns.u(n), n);
             best = k > best ? k : best;
         }
         if (nb) {
@@ -182,9 +206,9 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
         unsigned long long best = 0;
         unsigned nb = 0;
         for (int n = tid; n < N; n += kMoveThreads) {
-            if (haz[(size_t)n * S + s]) continue;
+            if (ns.h(n)) continue;
             ++nb;
-            const unsigned long long k = move_pack(cap[n] - use[(size_t)n * S + s], n);
+            const unsigned long long k = move_pack(cap[n] - ns.u(n), n);
             best = k > best ? k : best;
         }
         if (nb) {
@@ -211,8 +235,8 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
             // (the persistent loop knows both: the hazard node and the pick key's CPU)
             const int old = old_known != INT_MIN ? old_known : assign[pc];
             const int c = cpu_known != INT_MIN ? cpu_known : pod_cpu[p];
-            if ((unsigned)old < (unsigned)N) use[(size_t)old * S + s] -= c;
-            use[(size_t)t * S + s] += c;
+            if ((unsigned)old < (unsigned)N) ns.u(old) -= c;
+            ns.u(t) += c;
             assign[pc] = t;
             if (asg16) asg16[pc] = (unsigned short)t;
             if (dl.base) {  // the pod's entry follows it (one entry per pod off its base node)
@@ -252,7 +276,8 @@ __global__ __launch_bounds__(kMoveThreads) void car_move_kernel(const int *__res
     extern __shared__ __attribute__((aligned(16))) unsigned lds[];
     unsigned *tab = kGlobal ? gtab + (size_t)blockIdx.x * (size_t)(2 * H + 8) : lds;
     for (int s = (int)blockIdx.x; s < S; s += (int)gridDim.x) {
-        car_move_one<kGlobal>(row_ptr, col, pod_cpu, assign, use, cap, haz, evict, s, S, N, H, update, out_target,
+        car_move_one<kGlobal>(row_ptr, col, pod_cpu, assign, NodeGlobal{use, const_cast<uint8_t *>(haz), S, s}, cap,
+                              evict, s, S, N, H, update, out_target,
                               asg16, tab, kpick, kdet, ev_out, zc_cnt, zc_key, own0, own1, dl);
         if (kGlobal) move_sync<true>();  // the area is free before the next scenario clears it
     }
@@ -575,18 +600,17 @@ __device__ __forceinline__ void scn_reduce(const BlkArgs &sb, ScnState *st, unsi
 }
 
 // block b of scenario s re-reduced after a move, by one wave (lane = node)
-__device__ __forceinline__ void blk_update(const int *__restrict__ use, const int *__restrict__ cap, int N, int S,
-                                           int thr, uint8_t *__restrict__ haz, const BlkArgs &sb, int s, int b, int o,
-                                           int t) {
+template <class NS>
+__device__ __forceinline__ void blk_update(const NS &ns, const int *__restrict__ cap, int N, int thr,
+                                           const BlkArgs &sb, int b, int o, int t) {
     const int lane = (int)threadIdx.x & 63;
     const int n = b * kBlkNodes + lane;
     unsigned long long m = 0ull, z = 0ull;
     int cnt = 0;
     if (n < N) {
-        const size_t i = (size_t)n * S + s;
-        const int c = cap[n], u = use[i], v = pct_of(u, c);
+        const int c = cap[n], u = ns.u(n), v = pct_of(u, c);
         const bool h = v >= thr;
-        if (n == o || n == t) haz[i] = h;
+        if (n == o || n == t) ns.set_h(n, h);
         if (h) m = ((unsigned long long)((unsigned)v ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)n);
         else {
             cnt = 1;
@@ -685,9 +709,14 @@ struct PersistArgs {
     int P, N, S, H, R, thr;
     int blk_lds;                      // the scenario's block row kept in LDS (after the hash when it is there)
     unsigned hash_bytes;              // dynamic LDS of the hash (0: global work areas)
+    unsigned cols_off;                // kCols: byte offset of the usage column and hazard bits in the LDS
 };
 
-template <bool kGlobal>
+// kCols: the scenario's usage column and hazard bits live in LDS for its R
+// rounds (loaded at its start, the usage written back at its end): CAR's
+// hazard and cap - use reads, the update and the block re-reductions are LDS
+// round trips instead of L2 ones.
+template <bool kGlobal, bool kCols>
 __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArgs a, unsigned *__restrict__ gtab) {
     extern __shared__ __attribute__((aligned(16))) unsigned lds[];
     __shared__ unsigned long long r64[8];
@@ -696,6 +725,12 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
     __shared__ ScnState st;
     unsigned *tab = kGlobal ? gtab + (size_t)blockIdx.x * (size_t)(2 * a.H + 8) : lds;
     const int t = (int)threadIdx.x;
+    NodeCols nc;
+    if (kCols) {
+        char *cb = reinterpret_cast<char *>(lds) + a.cols_off;
+        nc.use = reinterpret_cast<int *>(cb);
+        nc.hb = reinterpret_cast<unsigned *>(cb + (size_t)a.N * 4);
+    }
     for (int s = (int)blockIdx.x; s < a.S; s += (int)gridDim.x) {
         BlkArgs sb;
         sb.NB = a.ba.NB;
@@ -710,50 +745,81 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
                 sb.bz[b] = a.ba.bz[row + b];
                 sb.bc[b] = a.ba.bc[row + b];
             }
-            __syncthreads();
         } else {
             sb.bm = a.ba.bm + row;
             sb.bz = a.ba.bz + row;
             sb.bc = a.ba.bc + row;
         }
+        if (kCols) {  // the usage column (8 loads in flight per thread) and its hazard bits (blk_detect's rule)
+            const int nw = (a.N + 31) >> 5;
+            for (int w = t; w < nw; w += kMoveThreads) nc.hb[w] = 0u;
+            __syncthreads();
+            constexpr int kU = 8;
+            for (int n0 = t; n0 < a.N; n0 += kMoveThreads * kU) {
+                int u[kU], c[kU];
+#pragma unroll
+                for (int k = 0; k < kU; ++k) {
+                    const int n = min(n0 + k * kMoveThreads, a.N - 1);
+                    u[k] = a.use[(size_t)n * a.S + s];
+                    c[k] = a.cap[n];
+                }
+#pragma unroll
+                for (int k = 0; k < kU; ++k) {
+                    const int n = n0 + k * kMoveThreads;
+                    if (n >= a.N) break;
+                    nc.use[n] = u[k];
+                    if (pct_of(u[k], c[k]) >= a.thr) atomicOr(&nc.hb[n >> 5], 1u << (n & 31));
+                }
+            }
+        }
+        __syncthreads();
         scn_reduce(sb, &st, r64, r32);
         if (t == 0) {
             a.zc_cnt[s] = st.zcnt;
             a.zc_key[s] = st.zkey;
         }
-        for (int r = 0; r < a.R; ++r) {
-            const unsigned long long kd = st.most;
-            int pcpu;
-            const int p = scn_pick<int>(a.assign, a.pod_cpu, a.P, a.S, s, kd, a.off, a.pod, a.dl, r64, &lsrc, &pcpu);
-            int *tg_row = a.out_target + (size_t)r * a.S;
-            if (t == 0) {
-                a.out_evict[(size_t)r * a.S + s] = p;
-                if (p >= 0) a.dl.src[s] = lsrc;  // read by car_move_one's thread 0
+        auto rounds = [&](const auto &ns) {
+            for (int r = 0; r < a.R; ++r) {
+                const unsigned long long kd = st.most;
+                int pcpu;
+                const int p = scn_pick<int>(a.assign, a.pod_cpu, a.P, a.S, s, kd, a.off, a.pod, a.dl, r64, &lsrc, &pcpu);
+                int *tg_row = a.out_target + (size_t)r * a.S;
+                if (t == 0) {
+                    a.out_evict[(size_t)r * a.S + s] = p;
+                    if (p >= 0) a.dl.src[s] = lsrc;  // read by car_move_one's thread 0
+                }
+                if (p < 0) {
+                    if (t == 0) tg_row[s] = kNoEvict;
+                    continue;  // uniform: the state is unchanged
+                }
+                const int o = (int)~(unsigned)(kd & 0xffffffffull);  // the picked pod sits on the hazard node
+                car_move_one<kGlobal>(a.row_ptr, a.col, a.pod_cpu, a.assign, ns, a.cap, nullptr, s, a.S, a.N, a.H, 1,
+                                      tg_row, nullptr, tab, nullptr, nullptr, nullptr, a.zc_cnt, a.zc_key, 0, INT_MAX,
+                                      a.dl, p, o, pcpu);
+                move_sync<kGlobal>();  // the move's state update (thread 0) before it is read
+                const int tt = (int)tab[2 * a.H + 7];  // car_move_one's target (red[5])
+                if (tt >= 0) {  // two nodes' CPU changed: their blocks, then the scenario's maxima
+                    const int bo = (unsigned)o < (unsigned)a.N ? o / kBlkNodes : -1, bt = tt / kBlkNodes;
+                    const int w = t >> 6;
+                    if (w == 0) blk_update(ns, a.cap, a.N, a.thr, sb, bt, o, tt);
+                    if (w == 1 && bo >= 0 && bo != bt) blk_update(ns, a.cap, a.N, a.thr, sb, bo, o, tt);
+                    __syncthreads();
+                    scn_reduce(sb, &st, r64, r32);
+                }
+                if (t == 0) {  // car_move_one zeroes the zero-case words (the launch loop's atomics)
+                    a.zc_cnt[s] = st.zcnt;
+                    a.zc_key[s] = st.zkey;
+                }
+                if (kGlobal) move_sync<true>();  // the area is free before the next round clears it
+                else __syncthreads();
             }
-            if (p < 0) {
-                if (t == 0) tg_row[s] = kNoEvict;
-                continue;  // uniform: the state is unchanged
-            }
-            const int o = (int)~(unsigned)(kd & 0xffffffffull);  // the picked pod sits on the hazard node
-            car_move_one<kGlobal>(a.row_ptr, a.col, a.pod_cpu, a.assign, a.use, a.cap, a.haz, nullptr, s, a.S, a.N,
-                                  a.H, 1, tg_row, nullptr, tab, nullptr, nullptr, nullptr, a.zc_cnt, a.zc_key, 0,
-                                  INT_MAX, a.dl, p, o, pcpu);
-            move_sync<kGlobal>();  // the move's state update (thread 0) before it is read
-            const int tt = (int)tab[2 * a.H + 7];  // car_move_one's target (red[5])
-            if (tt >= 0) {  // two nodes' CPU changed: their blocks, then the scenario's maxima
-                const int bo = (unsigned)o < (unsigned)a.N ? o / kBlkNodes : -1, bt = tt / kBlkNodes;
-                const int w = t >> 6;
-                if (w == 0) blk_update(a.use, a.cap, a.N, a.S, a.thr, a.haz, sb, s, bt, o, tt);
-                if (w == 1 && bo >= 0 && bo != bt) blk_update(a.use, a.cap, a.N, a.S, a.thr, a.haz, sb, s, bo, o, tt);
-                __syncthreads();
-                scn_reduce(sb, &st, r64, r32);
-            }
-            if (t == 0) {  // car_move_one zeroes the zero-case words (the launch loop's atomics)
-                a.zc_cnt[s] = st.zcnt;
-                a.zc_key[s] = st.zkey;
-            }
-            if (kGlobal) move_sync<true>();  // the area is free before the next round clears it
-            else __syncthreads();
+        };
+        if constexpr (kCols) {
+            rounds(nc);
+            for (int n = t; n < a.N; n += kMoveThreads) a.use[(size_t)n * a.S + s] = nc.use[n];  // the usage back
+            __syncthreads();  // the columns are free before the next scenario loads its own
+        } else {
+            rounds(NodeGlobal{a.use, a.haz, a.S, s});
         }
     }
 }
@@ -781,7 +847,8 @@ __global__ __launch_bounds__(kMoveThreads) void car_direct_kernel(const int *__r
         const int k = u / S, s = u - k * S;
         const int i = items ? items[(size_t)k * istride] : k;  // the plan row (its target row)
         const int p = rows ? rows[i] : i;
-        car_move_one<kGlobal>(rp, ci, nullptr, const_cast<int *>(assign), const_cast<int *>(use), cap, haz, nullptr,
+        car_move_one<kGlobal>(rp, ci, nullptr, const_cast<int *>(assign),
+                              NodeGlobal{const_cast<int *>(use), const_cast<uint8_t *>(haz), S, s}, cap, nullptr,
                               s, S, N, H, 0, out_target + (size_t)i * S, nullptr, tab, nullptr, nullptr, nullptr,
                               nullptr, nullptr, 0, INT_MAX, DevLists(), p);
         move_sync<kGlobal>();  // the hash is free before the next unit clears it
@@ -1017,8 +1084,9 @@ __global__ __launch_bounds__(256) void rows_move_detect_kernel(
         sb.bz = ba.bz + (size_t)s * ba.NB;
         sb.bc = ba.bc + (size_t)s * ba.NB;
         const int bo = (unsigned)o < (unsigned)N ? o / kBlkNodes : -1, bt = t / kBlkNodes;
-        if (w == 0) blk_update(use, cap, N, S, thr, haz, sb, s, bt, o, t);
-        if (w == 1 && bo >= 0 && bo != bt) blk_update(use, cap, N, S, thr, haz, sb, s, bo, o, t);
+        const NodeGlobal ng{use, haz, S, s};
+        if (w == 0) blk_update(ng, cap, N, thr, sb, bt, o, t);
+        if (w == 1 && bo >= 0 && bo != bt) blk_update(ng, cap, N, thr, sb, bo, o, t);
         __syncthreads();
     }
     BlkArgs sb = ba;
@@ -1240,9 +1308,16 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         const size_t blk_bytes = (size_t)pa.ba.NB * 20;
         pa.hash_bytes = (unsigned)g.lds;  // move_tab_bytes(H) or 0: the block row's u64 slices start 8-B aligned
         pa.blk_lds = blk_bytes <= 32 * 1024 && g.lds + blk_bytes <= 160 * 1024;
-        const size_t lds = g.lds + (pa.blk_lds ? blk_bytes : 0);
+        size_t lds = g.lds + (pa.blk_lds ? blk_bytes : 0);
+        // the scenario's usage column and hazard bits in LDS while four
+        // workgroups still fit a CU (config 5: 16.4 + 1.6 + 20 + 0.6 KB)
+        const size_t cols_bytes = (size_t)N * 4 + (size_t)((N + 31) / 32) * 4;
+        const bool cols = g.lds && pa.blk_lds && lds + cols_bytes <= kPersistLdsCols;
+        pa.cols_off = cols ? (unsigned)((lds + 15) & ~(size_t)15) : 0u;
+        if (cols) lds = pa.cols_off + cols_bytes;
         ScopedTimer tm(ctx, "rounds_persist");
-        auto *kern = g.lds ? &rounds_persist_kernel<false> : &rounds_persist_kernel<true>;
+        auto *kern = !g.lds ? &rounds_persist_kernel<true, false>
+                            : (cols ? &rounds_persist_kernel<false, true> : &rounds_persist_kernel<false, false>);
         if (lds > 64 * 1024)
             RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)lds));
