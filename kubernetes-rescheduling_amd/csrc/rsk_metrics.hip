@@ -419,6 +419,7 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(const int *__restrict_
 // on the N key counters, one per pod for the count and again for the scatter,
 // took 55 + 68 us at 1M pods over 50k nodes.)
 constexpr int kNrChunk = 4096;     // pods per level-1 workgroup
+constexpr int kNrThreads = 1024;   // its threads (4 pods each: 16 waves per CU at 1M pods, not 4)
 constexpr int kNrSubBits = 6, kNrSub = 1 << kNrSubBits;  // level-2 sub-buckets
 constexpr int kNrMaxBuckets = 16384;  // key >> kNrSubBits buckets held in LDS (N < 2^20)
 __device__ __forceinline__ int nr_key(const int *__restrict__ assign, int p, int S, int N) {
@@ -427,46 +428,46 @@ __device__ __forceinline__ int nr_key(const int *__restrict__ assign, int p, int
 }
 
 // level 1a: keys (kept in pkey) and this block's bucket counts -> bh[j * nblk + b]
-__global__ __launch_bounds__(256) void nr_hist_kernel(const int *__restrict__ assign, int P, int S, int N, int nbk,
+__global__ __launch_bounds__(kNrThreads) void nr_hist_kernel(const int *__restrict__ assign, int P, int S, int N, int nbk,
                                                       int *__restrict__ pkey, int *__restrict__ bh) {
     extern __shared__ int hist[];
-    for (int j = (int)threadIdx.x; j < nbk; j += 256) hist[j] = 0;
+    for (int j = (int)threadIdx.x; j < nbk; j += kNrThreads) hist[j] = 0;
     __syncthreads();
     const int p0 = (int)blockIdx.x * kNrChunk, p1 = min(P, p0 + kNrChunk);
-    constexpr int kU = kNrChunk / 256;  // the thread's pods: their (strided) key loads issued together
+    constexpr int kU = kNrChunk / kNrThreads;  // the thread's pods: their (strided) key loads issued together
     int k[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-        const int p = min(p0 + u * 256 + (int)threadIdx.x, P - 1);
+        const int p = min(p0 + u * kNrThreads + (int)threadIdx.x, P - 1);
         k[u] = nr_key(assign, p, S, N);
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-        const int p = p0 + u * 256 + (int)threadIdx.x;
+        const int p = p0 + u * kNrThreads + (int)threadIdx.x;
         if (p < p1) {
             pkey[p] = k[u];
             atomicAdd(&hist[k[u] >> kNrSubBits], 1);
         }
     }
     __syncthreads();
-    for (int j = (int)threadIdx.x; j < nbk; j += 256) bh[(size_t)j * gridDim.x + blockIdx.x] = hist[j];
+    for (int j = (int)threadIdx.x; j < nbk; j += kNrThreads) bh[(size_t)j * gridDim.x + blockIdx.x] = hist[j];
 }
 
 // level 1b: each block's pods to its slice of every bucket (bh scanned: offsets)
-__global__ __launch_bounds__(256) void nr_part_kernel(const int *__restrict__ pkey, int P, int nbk,
+__global__ __launch_bounds__(kNrThreads) void nr_part_kernel(const int *__restrict__ pkey, int P, int nbk,
                                                       const int *__restrict__ boff, int *__restrict__ perm1,
                                                       int *__restrict__ keys1) {
     extern __shared__ int cur[];
-    for (int j = (int)threadIdx.x; j < nbk; j += 256) cur[j] = boff[(size_t)j * gridDim.x + blockIdx.x];
+    for (int j = (int)threadIdx.x; j < nbk; j += kNrThreads) cur[j] = boff[(size_t)j * gridDim.x + blockIdx.x];
     __syncthreads();
     const int p0 = (int)blockIdx.x * kNrChunk, p1 = min(P, p0 + kNrChunk);
-    constexpr int kU = kNrChunk / 256;
+    constexpr int kU = kNrChunk / kNrThreads;
     int k[kU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) k[u] = pkey[min(p0 + u * 256 + (int)threadIdx.x, P - 1)];
+    for (int u = 0; u < kU; ++u) k[u] = pkey[min(p0 + u * kNrThreads + (int)threadIdx.x, P - 1)];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-        const int p = p0 + u * 256 + (int)threadIdx.x;
+        const int p = p0 + u * kNrThreads + (int)threadIdx.x;
         if (p < p1) {
             const int pos = atomicAdd(&cur[k[u] >> kNrSubBits], 1);
             perm1[pos] = p;
@@ -631,6 +632,165 @@ __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restr
     flush();
 }
 
+// ---- the owner form (round 5): no memsets, no flush atomics ----
+// key_off[n] = the first grouped position whose key is >= n (n = 0..N); the
+// pods unassigned in scenario 0 (key N) sit last.
+__global__ __launch_bounds__(256) void nr_keyoff_kernel(const int *__restrict__ keys, int P, int N,
+                                                        int *__restrict__ key_off) {
+    const int i = (int)(blockIdx.x * 256 + threadIdx.x);  // grouped position 0..P
+    if (i > P) return;
+    const int k = i < P ? keys[i] : N + 1;
+    const int kp = i > 0 ? keys[i - 1] : -1;
+    for (int n = kp + 1; n <= min(k, N); ++n) key_off[n] = i;
+}
+
+// A wave owns the cells (n, s) of kNrOwn consecutive key nodes n and one
+// 64-scenario chunk (lane = scenario).  It walks the pods grouped under those
+// keys: a lane whose pod sits on its key node adds it to register sums; when
+// the walk passes a node, the wave stores that node's cells (count, CPU,
+// memory) with plain coalesced stores — every cell of the output is stored
+// exactly once, by its owner, so no memset and no flush atomics.  A lane whose
+// pod sits on another node (an off-key cell, ~1 % at config 4) stages (cell,
+// pod) in LDS; the wave appends its staged entries to a global list with one
+// atomic per flush, and nr_offkey_kernel adds them after every owner store.
+constexpr int kNrOwn = 16;    // key nodes per wave
+constexpr int kNrStage = 512; // off-key entries staged per wave
+__global__ __launch_bounds__(256) void node_reduce_own_kernel(const int *__restrict__ assign, int P, int S,
+                                                              const int *__restrict__ pod_cpu,
+                                                              const long long *__restrict__ pod_mem, int N,
+                                                              const int *__restrict__ perm,
+                                                              const int *__restrict__ keys,
+                                                              const int *__restrict__ key_off, int nranges,
+                                                              int *__restrict__ cnt, long long *__restrict__ cpu,
+                                                              long long *__restrict__ mem, int2 *__restrict__ olist,
+                                                              unsigned *__restrict__ ocount, unsigned ocap) {
+    __shared__ int2 stage[4][kNrStage];
+    const int wv = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4) + wv);
+    const int chunk = w / nranges, r = w - chunk * nranges;
+    if (chunk * 64 >= S) return;  // whole wave (no barriers in this kernel)
+    const int s = chunk * 64 + lane;
+    const bool live = s < S;
+    const int n0 = r * kNrOwn, n1 = min(N, n0 + kNrOwn);
+    const int j0 = key_off[n0], j1 = n1 == N ? P : key_off[n1];  // the last range also walks the key-N pods
+    const cint_ptr cperm = const_ptr(perm), ckeys = const_ptr(keys), ccpu = const_ptr(pod_cpu);
+    int2 *st = stage[wv];
+    int nst = 0;  // staged entries (wave-uniform)
+    auto flush_stage = [&]() {
+        if (!nst) return;
+        unsigned base = 0;
+        if (lane == 0) base = atomicAdd(ocount, (unsigned)nst);
+        base = (unsigned)__builtin_amdgcn_readfirstlane((int)base);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the staged LDS writes before their reads
+        for (int i = lane; i < nst; i += 64)
+            if (base + (unsigned)i < ocap) olist[base + (unsigned)i] = st[i];
+        nst = 0;
+    };
+    int rk = n0, rc = 0;  // the next node to store, its sums
+    long long rcpu = 0, rmem = 0;
+    auto store_node = [&]() {  // node rk's cells, then the next node
+        if (live) {
+            const size_t o = (size_t)rk * S + s;
+            cnt[o] = rc;
+            cpu[o] = rcpu;
+            if (mem) mem[o] = rmem;
+        }
+        rc = 0;
+        rcpu = rmem = 0;
+        ++rk;
+    };
+    constexpr int kB = 8;
+    for (int j = j0; j < j1; j += kB) {
+        int a[kB], pp[kB], kk[kB], cc[kB];
+        long long mm[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            const int jj = min(j + u, j1 - 1);
+            pp[u] = cperm[jj];
+            kk[u] = ckeys[jj];
+        }
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            a[u] = live ? __builtin_nontemporal_load(&assign[(size_t)pp[u] * S + s]) : -1;
+            cc[u] = ccpu[pp[u]];
+            mm[u] = mem ? pod_mem[pp[u]] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            if (j + u >= j1) break;
+            const int k = kk[u];               // wave-uniform, ascending
+            while (rk < k && rk < n1) store_node();
+            const bool on = a[u] == k;         // k < N here whenever a[u] is a node
+            if (on) {
+                ++rc;
+                rcpu += cc[u];
+                rmem += mm[u];
+            }
+            const bool off = !on && (unsigned)a[u] < (unsigned)N;
+            const unsigned long long m = __builtin_amdgcn_ballot_w64(off);
+            if (m) {
+                if (nst + 64 > kNrStage) flush_stage();  // wave-uniform
+                const int pos = nst + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                if (off) st[pos] = make_int2((int)((unsigned)a[u] * (unsigned)S + (unsigned)s), pp[u]);
+                nst += __builtin_popcountll(m);
+            }
+        }
+    }
+    while (rk < n1) store_node();  // the rest of the range (nodes without pods: zeros)
+    flush_stage();
+}
+
+// The off-key cells, after every owner store (stream order): one thread per
+// entry, three atomics.  Entries past the list's capacity are not here: the
+// launch is then followed by the full recount below.
+__global__ __launch_bounds__(256) void nr_offkey_kernel(const int2 *__restrict__ olist,
+                                                        const unsigned *__restrict__ ocount, unsigned ocap,
+                                                        const int *__restrict__ pod_cpu,
+                                                        const long long *__restrict__ pod_mem, int *__restrict__ cnt,
+                                                        unsigned long long *__restrict__ cpu,
+                                                        unsigned long long *__restrict__ mem) {
+    const unsigned n = *ocount;
+    if (n > ocap) return;  // overflowed: nr_recount_kernel redoes every cell
+    for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        const int2 e = olist[i];
+        atomicAdd(&cnt[e.x], 1);
+        atomicAdd(&cpu[e.x], (unsigned long long)(long long)pod_cpu[e.y]);
+        if (mem) atomicAdd(&mem[e.x], (unsigned long long)pod_mem[e.y]);
+    }
+}
+
+// Only when the off-key list overflowed its capacity (far more moved cells
+// than what-if batches have): every cell again, zeroed then the atomic kernel's
+// rule, grid-striding (mode 0 zeroes, mode 1 adds).  Otherwise every thread
+// returns at once.
+__global__ __launch_bounds__(256) void nr_recount_kernel(int mode, const unsigned *__restrict__ ocount, unsigned ocap,
+                                                         const int *__restrict__ assign, int P, int S,
+                                                         const int *__restrict__ pod_cpu,
+                                                         const long long *__restrict__ pod_mem, int N,
+                                                         int *__restrict__ cnt, unsigned long long *__restrict__ cpu,
+                                                         unsigned long long *__restrict__ mem) {
+    if (*ocount <= ocap) return;
+    const size_t stride = (size_t)gridDim.x * 256;
+    if (mode == 0) {
+        for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < (size_t)N * S; i += stride) {
+            cnt[i] = 0;
+            cpu[i] = 0ull;
+            if (mem) mem[i] = 0ull;
+        }
+        return;
+    }
+    for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < (size_t)P * S; t += stride) {
+        const int a = assign[t];
+        if ((unsigned)a >= (unsigned)N) continue;
+        const int p = (int)(t / (size_t)S), s = (int)(t - (size_t)p * S);
+        const size_t o = (size_t)a * S + s;
+        atomicAdd(&cnt[o], 1);
+        atomicAdd(&cpu[o], (unsigned long long)(long long)pod_cpu[p]);
+        if (mem) atomicAdd(&mem[o], (unsigned long long)pod_mem[p]);
+    }
+}
+
 // get_resource_usage.py:37: int(round(u / c * 100)) — IEEE fp64 divide, then an
 // fp64 multiply (no FMA can form), then round-half-even (rint).
 __global__ __launch_bounds__(256) void cpu_pct_kernel(const int *__restrict__ use, const int *__restrict__ cap, int N,
@@ -745,9 +905,20 @@ __global__ __launch_bounds__(256) void std_merge_kernel(const double *__restrict
     if (s >= S) return;  // whole wave
     double mean = 0.0, m2 = 0.0;
     long long n = 0;
-    for (int ch = lane; ch < nchunks; ch += 64) {
-        const size_t o = (size_t)ch * S + s;
-        chan_merge(n, mean, m2, pcnt[o], pmean[o], pm2[o]);
+    constexpr int kU = 8;  // a batch of the lane's chunks loaded before it is merged (in order)
+    for (int ch0 = lane; ch0 < nchunks; ch0 += 64 * kU) {
+        int c[kU];
+        double mb[kU], qb[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int ch = ch0 + 64 * u;
+            const size_t o = (size_t)min(ch, nchunks - 1) * S + s;  // clamped; counted 0 past the end
+            c[u] = ch < nchunks ? pcnt[o] : 0;
+            mb[u] = pmean[o];
+            qb[u] = pm2[o];
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) chan_merge(n, mean, m2, c[u], mb[u], qb[u]);
     }
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -1187,10 +1358,8 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
     RSK_TRY(stage_out(ctx, 3, pod_count, NS * 4, dev, reinterpret_cast<void **>(&d_cnt)));
     RSK_TRY(stage_out(ctx, 4, cpu_sum, NS * 8, dev, reinterpret_cast<void **>(&d_cs)));
     if (mem_sum) RSK_TRY(stage_out(ctx, 5, mem_sum, NS * 8, dev, reinterpret_cast<void **>(&d_ms)));
-    RSK_HIP(hipMemsetAsync(d_cnt, 0, NS * 4, ctx->stream));
-    RSK_HIP(hipMemsetAsync(d_cs, 0, NS * 8, ctx->stream));
-    if (d_ms) RSK_HIP(hipMemsetAsync(d_ms, 0, NS * 8, ctx->stream));
     const int nbk = (N >> kNrSubBits) + 1;  // key >> kNrSubBits buckets (keys 0..N)
+    static const bool own = RSK_KNOB(RSK_NR_OWN, 1) != 0;
     if (PS && S >= 32 && nbk <= kNrMaxBuckets) {  // segmented: group the pods by key node, per-key register sums
         constexpr int run_len = kNrRun;  // pods per wave
         const int runs = (int)ceil_div(P, run_len);
@@ -1200,27 +1369,62 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
         const int64_t nbh = (int64_t)nbk * nblk1;
         RSK_CHECK(nbh < INT32_MAX / 2, "node_reduce grouping too large");
         const int nsb = (int)ceil_div(nbh, kNrScanB);
-        RSK_TRY(ctx->work[0].reserve((size_t)P * 20));
+        const int nranges = (int)ceil_div(N, kNrOwn);
+        const int64_t owaves = (int64_t)nranges * ceil_div(S, 64);
+        RSK_CHECK(owaves < (int64_t)INT32_MAX - 4, "node_reduce grid too large");
+        // off-key list: a quarter of the cells (what-if batches move ~1 %); beyond it the recount
+        const unsigned ocap = (unsigned)std::min<size_t>(PS, std::max<size_t>((size_t)1 << 20, PS / 4));
+        RSK_TRY(ctx->work[0].reserve((size_t)P * 20 + (size_t)(N + 1) * 4 + 16));
         RSK_TRY(ctx->work[1].reserve(((size_t)nbh + nsb) * 4));
+        if (own) RSK_TRY(ctx->work[2].reserve((size_t)ocap * 8));
         int *perm = ctx->work[0].as<int>(), *keys = perm + P, *pkey = keys + P, *perm1 = pkey + P, *keys1 = perm1 + P;
+        int *key_off = keys1 + P;
+        unsigned *ocount = reinterpret_cast<unsigned *>(key_off + N + 1);
         int *bh = ctx->work[1].as<int>(), *bsum = bh + nbh;
         ScopedTimer tm(ctx, "node_reduce");
+        if (!own) {
+            RSK_HIP(hipMemsetAsync(d_cnt, 0, NS * 4, ctx->stream));
+            RSK_HIP(hipMemsetAsync(d_cs, 0, NS * 8, ctx->stream));
+            if (d_ms) RSK_HIP(hipMemsetAsync(d_ms, 0, NS * 8, ctx->stream));
+        } else {
+            RSK_HIP(hipMemsetAsync(ocount, 0, 4, ctx->stream));
+        }
         const size_t hl = (size_t)nbk * 4;
         static const int nr_ablate = RSK_ABLATION(RSK_ABLATE_NR);
-        nr_hist_kernel<<<nblk1, 256, hl, ctx->stream>>>(d_assign, P, S, N, nbk, pkey, bh);
+        nr_hist_kernel<<<nblk1, kNrThreads, hl, ctx->stream>>>(d_assign, P, S, N, nbk, pkey, bh);
         nr_blocksum_kernel<<<nsb, kNrScanB, 0, ctx->stream>>>(bh, (int)nbh, bsum);
         nr_blockscan_kernel<<<nsb, kNrScanB, 0, ctx->stream>>>(bh, (int)nbh, bsum);
-        nr_part_kernel<<<nblk1, 256, hl, ctx->stream>>>(pkey, P, nbk, bh, perm1, keys1);
+        nr_part_kernel<<<nblk1, kNrThreads, hl, ctx->stream>>>(pkey, P, nbk, bh, perm1, keys1);
         nr_sub_kernel<<<nbk, 256, 0, ctx->stream>>>(perm1, keys1, bh, nblk1, nbk, P, perm, keys);
-        node_reduce_seg_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, ctx->stream>>>(
-            d_assign, P, S, d_cpu, reinterpret_cast<const long long *>(d_mem), N, perm, keys, runs, d_cnt,
-            reinterpret_cast<unsigned long long *>(d_cs), reinterpret_cast<unsigned long long *>(d_ms), nr_ablate, run_len);
+        if (own) {
+            const long long *dm = reinterpret_cast<const long long *>(d_mem);
+            auto *ucs = reinterpret_cast<unsigned long long *>(d_cs), *ums = reinterpret_cast<unsigned long long *>(d_ms);
+            nr_keyoff_kernel<<<(unsigned)ceil_div(P + 1, 256), 256, 0, ctx->stream>>>(keys, P, N, key_off);
+            node_reduce_own_kernel<<<(unsigned)ceil_div(owaves, 4), 256, 0, ctx->stream>>>(
+                d_assign, P, S, d_cpu, dm, N, perm, keys, key_off, nranges, d_cnt, reinterpret_cast<long long *>(d_cs),
+                reinterpret_cast<long long *>(d_ms), ctx->work[2].as<int2>(), ocount, ocap);
+            nr_offkey_kernel<<<1024, 256, 0, ctx->stream>>>(ctx->work[2].as<int2>(), ocount, ocap, d_cpu, dm, d_cnt, ucs,
+                                                           ums);
+            nr_recount_kernel<<<2048, 256, 0, ctx->stream>>>(0, ocount, ocap, d_assign, P, S, d_cpu, dm, N, d_cnt, ucs,
+                                                             ums);
+            nr_recount_kernel<<<2048, 256, 0, ctx->stream>>>(1, ocount, ocap, d_assign, P, S, d_cpu, dm, N, d_cnt, ucs,
+                                                             ums);
+        } else {
+            node_reduce_seg_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, ctx->stream>>>(
+                d_assign, P, S, d_cpu, reinterpret_cast<const long long *>(d_mem), N, perm, keys, runs, d_cnt,
+                reinterpret_cast<unsigned long long *>(d_cs), reinterpret_cast<unsigned long long *>(d_ms), nr_ablate,
+                run_len);
+        }
         RSK_HIP(hipGetLastError());
-    } else if (PS) {
+    } else {
         ScopedTimer tm(ctx, "node_reduce");
-        node_reduce_kernel<<<(unsigned)ceil_div(PS, 256), 256, 0, ctx->stream>>>(
-            d_assign, P, S, d_cpu, reinterpret_cast<const long long *>(d_mem), N, d_cnt,
-            reinterpret_cast<unsigned long long *>(d_cs), reinterpret_cast<unsigned long long *>(d_ms));
+        RSK_HIP(hipMemsetAsync(d_cnt, 0, NS * 4, ctx->stream));
+        RSK_HIP(hipMemsetAsync(d_cs, 0, NS * 8, ctx->stream));
+        if (d_ms) RSK_HIP(hipMemsetAsync(d_ms, 0, NS * 8, ctx->stream));
+        if (PS)
+            node_reduce_kernel<<<(unsigned)ceil_div(PS, 256), 256, 0, ctx->stream>>>(
+                d_assign, P, S, d_cpu, reinterpret_cast<const long long *>(d_mem), N, d_cnt,
+                reinterpret_cast<unsigned long long *>(d_cs), reinterpret_cast<unsigned long long *>(d_ms));
         RSK_HIP(hipGetLastError());
     }
     if (!dev) {

@@ -764,14 +764,17 @@ def test_dropin_random_matches_reference_choice(ctx, seed):
 
 
 @pytest.mark.parametrize("P,N,S,p_flip", [(3000, 97, 33, 0.01), (5000, 300, 64, 0.3), (20000, 2000, 130, 0.01),
-                                          (4000, 50, 1, 0.0), (1_000_000, 50_000, 64, 0.01)])
+                                          (4000, 50, 1, 0.0), (1_000_000, 50_000, 64, 0.01),
+                                          (100_000, 2_000, 64, 0.6), (3000, 70_000, 40, 0.05)])
 def test_node_reduce_segmented_vs_oracle(ctx, P, N, S, p_flip):
     """Kernel 3's per-node count / CPU / memory sums (podmonitor.py:104-121,
     nodemonitor.py:24-46) against the oracle: the segmented kernel (S >= 32:
     pods bucketed by key node, register sums per key) on perturbed batches,
     heavily perturbed ones (30 % of placements redrawn: most lanes off the key),
     a partial last chunk (S = 130), assignments outside [0, N) (skipped), and
-    the atomic kernel at S = 1; the last case is config 4's size."""
+    the atomic kernel at S = 1; config 4's size; 60 % redrawn over 6.4 M cells
+    (the off-key list overflows its quarter-of-the-cells capacity: the full
+    recount); more nodes than pods (most nodes' cells zeros)."""
     from oracle import oracle as orc
     from rsk import api
     rng = np.random.default_rng(P + S)
