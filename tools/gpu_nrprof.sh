@@ -1,0 +1,18 @@
+#!/bin/bash
+# Kernel trace of tools/nrbench.py (node_reduce at 1M x 50k x 64) for knob
+# variants of the knobs library.  usage: tools/gpu_nrprof.sh OUTDIR VAR=v ...
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+out=${1:-gpurun_out/nrprof}; shift
+mkdir -p "$out"
+export TMPDIR=/tmp
+export RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so
+k=0
+for v in "$@"; do
+  k=$((k+1))
+  export ${v//,/ }
+  timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d "$out/p$k" -o run -f csv -- python3 tools/nrbench.py > "$out/p$k.log" 2>&1
+  rc=$?
+  echo "== $v rc=$rc $(grep -o '"node_reduce_ms": [0-9.]*' "$out/p$k.log")"
+  [ $rc -ne 0 ] && { tail -5 "$out/p$k.log"; exit $rc; }
+done
+exit 0
