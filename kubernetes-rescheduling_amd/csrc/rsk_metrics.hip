@@ -588,24 +588,37 @@ __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restr
         rc = 0;
         rcpu = rmem = 0;
     };
-    constexpr int kB = 8;
+    // Batches of kB pods: the next batch's pod ids and keys (scalar loads) are
+    // fetched while this batch's rows are in flight, so each batch costs one
+    // vector round trip (the assign rows with the pods' CPU / memory) instead
+    // of two behind each other.
+    constexpr int kB = 16;
+    int pn[kB], kn[kB];
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+        const int jj = min(j0 + u, j1 - 1);
+        pn[u] = cperm[jj];
+        kn[u] = ckeys[jj];
+    }
     for (int j = j0; j < j1; j += kB) {
-        // every load of the batch issued before its first use: the assign rows,
-        // and the pods' CPU / memory (scattered pod ids: each a cache miss that,
-        // loaded per pod behind the previous pod's atomics, serialised the run)
         int a[kB], pp[kB], kk[kB], cc[kB];
         long long mm[kB];
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
-            const int jj = min(j + u, j1 - 1);
-            pp[u] = cperm[jj];
-            kk[u] = ckeys[jj];
+            pp[u] = pn[u];
+            kk[u] = kn[u];
         }
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
             a[u] = live ? __builtin_nontemporal_load(&assign[(size_t)pp[u] * S + s]) : -1;
             cc[u] = ccpu[pp[u]];
             mm[u] = mem ? pod_mem[pp[u]] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {  // the next batch's ids (clamped: always valid)
+            const int jj = min(j + kB + u, j1 - 1);
+            pn[u] = cperm[jj];
+            kn[u] = ckeys[jj];
         }
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
@@ -630,165 +643,6 @@ __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restr
         }
     }
     flush();
-}
-
-// ---- the owner form (round 5): no memsets, no flush atomics ----
-// key_off[n] = the first grouped position whose key is >= n (n = 0..N); the
-// pods unassigned in scenario 0 (key N) sit last.
-__global__ __launch_bounds__(256) void nr_keyoff_kernel(const int *__restrict__ keys, int P, int N,
-                                                        int *__restrict__ key_off) {
-    const int i = (int)(blockIdx.x * 256 + threadIdx.x);  // grouped position 0..P
-    if (i > P) return;
-    const int k = i < P ? keys[i] : N + 1;
-    const int kp = i > 0 ? keys[i - 1] : -1;
-    for (int n = kp + 1; n <= min(k, N); ++n) key_off[n] = i;
-}
-
-// A wave owns the cells (n, s) of kNrOwn consecutive key nodes n and one
-// 64-scenario chunk (lane = scenario).  It walks the pods grouped under those
-// keys: a lane whose pod sits on its key node adds it to register sums; when
-// the walk passes a node, the wave stores that node's cells (count, CPU,
-// memory) with plain coalesced stores — every cell of the output is stored
-// exactly once, by its owner, so no memset and no flush atomics.  A lane whose
-// pod sits on another node (an off-key cell, ~1 % at config 4) stages (cell,
-// pod) in LDS; the wave appends its staged entries to a global list with one
-// atomic per flush, and nr_offkey_kernel adds them after every owner store.
-constexpr int kNrOwn = 16;    // key nodes per wave
-constexpr int kNrStage = 512; // off-key entries staged per wave
-__global__ __launch_bounds__(256) void node_reduce_own_kernel(const int *__restrict__ assign, int P, int S,
-                                                              const int *__restrict__ pod_cpu,
-                                                              const long long *__restrict__ pod_mem, int N,
-                                                              const int *__restrict__ perm,
-                                                              const int *__restrict__ keys,
-                                                              const int *__restrict__ key_off, int nranges,
-                                                              int *__restrict__ cnt, long long *__restrict__ cpu,
-                                                              long long *__restrict__ mem, int2 *__restrict__ olist,
-                                                              unsigned *__restrict__ ocount, unsigned ocap) {
-    __shared__ int2 stage[4][kNrStage];
-    const int wv = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4) + wv);
-    const int chunk = w / nranges, r = w - chunk * nranges;
-    if (chunk * 64 >= S) return;  // whole wave (no barriers in this kernel)
-    const int s = chunk * 64 + lane;
-    const bool live = s < S;
-    const int n0 = r * kNrOwn, n1 = min(N, n0 + kNrOwn);
-    const int j0 = key_off[n0], j1 = n1 == N ? P : key_off[n1];  // the last range also walks the key-N pods
-    const cint_ptr cperm = const_ptr(perm), ckeys = const_ptr(keys), ccpu = const_ptr(pod_cpu);
-    int2 *st = stage[wv];
-    int nst = 0;  // staged entries (wave-uniform)
-    auto flush_stage = [&]() {
-        if (!nst) return;
-        unsigned base = 0;
-        if (lane == 0) base = atomicAdd(ocount, (unsigned)nst);
-        base = (unsigned)__builtin_amdgcn_readfirstlane((int)base);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the staged LDS writes before their reads
-        for (int i = lane; i < nst; i += 64)
-            if (base + (unsigned)i < ocap) olist[base + (unsigned)i] = st[i];
-        nst = 0;
-    };
-    int rk = n0, rc = 0;  // the next node to store, its sums
-    long long rcpu = 0, rmem = 0;
-    auto store_node = [&]() {  // node rk's cells, then the next node
-        if (live) {
-            const size_t o = (size_t)rk * S + s;
-            cnt[o] = rc;
-            cpu[o] = rcpu;
-            if (mem) mem[o] = rmem;
-        }
-        rc = 0;
-        rcpu = rmem = 0;
-        ++rk;
-    };
-    constexpr int kB = 8;
-    for (int j = j0; j < j1; j += kB) {
-        int a[kB], pp[kB], kk[kB], cc[kB];
-        long long mm[kB];
-#pragma unroll
-        for (int u = 0; u < kB; ++u) {
-            const int jj = min(j + u, j1 - 1);
-            pp[u] = cperm[jj];
-            kk[u] = ckeys[jj];
-        }
-#pragma unroll
-        for (int u = 0; u < kB; ++u) {
-            a[u] = live ? __builtin_nontemporal_load(&assign[(size_t)pp[u] * S + s]) : -1;
-            cc[u] = ccpu[pp[u]];
-            mm[u] = mem ? pod_mem[pp[u]] : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < kB; ++u) {
-            if (j + u >= j1) break;
-            const int k = kk[u];               // wave-uniform, ascending
-            while (rk < k && rk < n1) store_node();
-            const bool on = a[u] == k;         // k < N here whenever a[u] is a node
-            if (on) {
-                ++rc;
-                rcpu += cc[u];
-                rmem += mm[u];
-            }
-            const bool off = !on && (unsigned)a[u] < (unsigned)N;
-            const unsigned long long m = __builtin_amdgcn_ballot_w64(off);
-            if (m) {
-                if (nst + 64 > kNrStage) flush_stage();  // wave-uniform
-                const int pos = nst + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                                                     __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-                if (off) st[pos] = make_int2((int)((unsigned)a[u] * (unsigned)S + (unsigned)s), pp[u]);
-                nst += __builtin_popcountll(m);
-            }
-        }
-    }
-    while (rk < n1) store_node();  // the rest of the range (nodes without pods: zeros)
-    flush_stage();
-}
-
-// The off-key cells, after every owner store (stream order): one thread per
-// entry, three atomics.  Entries past the list's capacity are not here: the
-// launch is then followed by the full recount below.
-__global__ __launch_bounds__(256) void nr_offkey_kernel(const int2 *__restrict__ olist,
-                                                        const unsigned *__restrict__ ocount, unsigned ocap,
-                                                        const int *__restrict__ pod_cpu,
-                                                        const long long *__restrict__ pod_mem, int *__restrict__ cnt,
-                                                        unsigned long long *__restrict__ cpu,
-                                                        unsigned long long *__restrict__ mem) {
-    const unsigned n = *ocount;
-    if (n > ocap) return;  // overflowed: nr_recount_kernel redoes every cell
-    for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
-        const int2 e = olist[i];
-        atomicAdd(&cnt[e.x], 1);
-        atomicAdd(&cpu[e.x], (unsigned long long)(long long)pod_cpu[e.y]);
-        if (mem) atomicAdd(&mem[e.x], (unsigned long long)pod_mem[e.y]);
-    }
-}
-
-// Only when the off-key list overflowed its capacity (far more moved cells
-// than what-if batches have): every cell again, zeroed then the atomic kernel's
-// rule, grid-striding (mode 0 zeroes, mode 1 adds).  Otherwise every thread
-// returns at once.
-__global__ __launch_bounds__(256) void nr_recount_kernel(int mode, const unsigned *__restrict__ ocount, unsigned ocap,
-                                                         const int *__restrict__ assign, int P, int S,
-                                                         const int *__restrict__ pod_cpu,
-                                                         const long long *__restrict__ pod_mem, int N,
-                                                         int *__restrict__ cnt, unsigned long long *__restrict__ cpu,
-                                                         unsigned long long *__restrict__ mem) {
-    if (*ocount <= ocap) return;
-    const size_t stride = (size_t)gridDim.x * 256;
-    if (mode == 0) {
-        for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < (size_t)N * S; i += stride) {
-            cnt[i] = 0;
-            cpu[i] = 0ull;
-            if (mem) mem[i] = 0ull;
-        }
-        return;
-    }
-    for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < (size_t)P * S; t += stride) {
-        const int a = assign[t];
-        if ((unsigned)a >= (unsigned)N) continue;
-        const int p = (int)(t / (size_t)S), s = (int)(t - (size_t)p * S);
-        const size_t o = (size_t)a * S + s;
-        atomicAdd(&cnt[o], 1);
-        atomicAdd(&cpu[o], (unsigned long long)(long long)pod_cpu[p]);
-        if (mem) atomicAdd(&mem[o], (unsigned long long)pod_mem[p]);
-    }
 }
 
 // get_resource_usage.py:37: int(round(u / c * 100)) — IEEE fp64 divide, then an
@@ -894,24 +748,27 @@ __device__ __forceinline__ void chan_merge(long long &n, double &mean, double &m
     n = nt;
 }
 
-// One wave per scenario: lane l merges chunks l, l + 64, ... in order, then the
-// 64 lane states pairwise (xor butterfly, 6 levels); lane 0 writes the std.
-// (One thread per scenario walking every chunk in a chain of fp64 divides took
-// 1.6 ms at 50k nodes x 64 scenarios: 3,125 chunks.)
+// One workgroup per scenario: thread t merges chunks t, t + 256, ... in order
+// (a batch of loads in flight before it is merged), then each wave's 64
+// states pairwise (xor butterfly, 6 levels), then thread 0 the four waves in
+// order; the result is the same for every run (fixed order).  (One thread per
+// scenario walking every chunk in a chain of fp64 divides took 1.6 ms at 50k
+// nodes x 64 scenarios; one wave per scenario 15 us.)
 __global__ __launch_bounds__(256) void std_merge_kernel(const double *__restrict__ pmean, const double *__restrict__ pm2,
                                                         const int *__restrict__ pcnt, int nchunks, int S,
                                                         double *__restrict__ out) {
-    const int s = (int)blockIdx.x * 4 + ((int)threadIdx.x >> 6), lane = (int)threadIdx.x & 63;
-    if (s >= S) return;  // whole wave
+    __shared__ double wm[4], wq[4];
+    __shared__ long long wn[4];
+    const int s = (int)blockIdx.x, t = (int)threadIdx.x, lane = t & 63, w = t >> 6;
     double mean = 0.0, m2 = 0.0;
     long long n = 0;
-    constexpr int kU = 8;  // a batch of the lane's chunks loaded before it is merged (in order)
-    for (int ch0 = lane; ch0 < nchunks; ch0 += 64 * kU) {
+    constexpr int kU = 4;
+    for (int ch0 = t; ch0 < nchunks; ch0 += 256 * kU) {
         int c[kU];
         double mb[kU], qb[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-            const int ch = ch0 + 64 * u;
+            const int ch = ch0 + 256 * u;
             const size_t o = (size_t)min(ch, nchunks - 1) * S + s;  // clamped; counted 0 past the end
             c[u] = ch < nchunks ? pcnt[o] : 0;
             mb[u] = pmean[o];
@@ -934,7 +791,17 @@ __global__ __launch_bounds__(256) void std_merge_kernel(const double *__restrict
             chan_merge(n, mean, m2, nb, mb, m2b);
         }
     }
-    if (lane == 0) out[s] = n ? sqrt(m2 / (double)n) : 0.0;
+    if (lane == 0) {
+        wn[w] = n;
+        wm[w] = mean;
+        wq[w] = m2;
+    }
+    __syncthreads();
+    if (t == 0) {
+        n = wn[0], mean = wm[0], m2 = wq[0];
+        for (int k = 1; k < 4; ++k) chan_merge(n, mean, m2, wn[k], wm[k], wq[k]);
+        out[s] = n ? sqrt(m2 / (double)n) : 0.0;
+    }
 }
 
 constexpr int kCutBins = 64;
@@ -1359,7 +1226,6 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
     RSK_TRY(stage_out(ctx, 4, cpu_sum, NS * 8, dev, reinterpret_cast<void **>(&d_cs)));
     if (mem_sum) RSK_TRY(stage_out(ctx, 5, mem_sum, NS * 8, dev, reinterpret_cast<void **>(&d_ms)));
     const int nbk = (N >> kNrSubBits) + 1;  // key >> kNrSubBits buckets (keys 0..N)
-    static const bool own = RSK_KNOB(RSK_NR_OWN, 1) != 0;
     if (PS && S >= 32 && nbk <= kNrMaxBuckets) {  // segmented: group the pods by key node, per-key register sums
         constexpr int run_len = kNrRun;  // pods per wave
         const int runs = (int)ceil_div(P, run_len);
@@ -1369,26 +1235,14 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
         const int64_t nbh = (int64_t)nbk * nblk1;
         RSK_CHECK(nbh < INT32_MAX / 2, "node_reduce grouping too large");
         const int nsb = (int)ceil_div(nbh, kNrScanB);
-        const int nranges = (int)ceil_div(N, kNrOwn);
-        const int64_t owaves = (int64_t)nranges * ceil_div(S, 64);
-        RSK_CHECK(owaves < (int64_t)INT32_MAX - 4, "node_reduce grid too large");
-        // off-key list: a quarter of the cells (what-if batches move ~1 %); beyond it the recount
-        const unsigned ocap = (unsigned)std::min<size_t>(PS, std::max<size_t>((size_t)1 << 20, PS / 4));
-        RSK_TRY(ctx->work[0].reserve((size_t)P * 20 + (size_t)(N + 1) * 4 + 16));
+        RSK_TRY(ctx->work[0].reserve((size_t)P * 20));
         RSK_TRY(ctx->work[1].reserve(((size_t)nbh + nsb) * 4));
-        if (own) RSK_TRY(ctx->work[2].reserve((size_t)ocap * 8));
         int *perm = ctx->work[0].as<int>(), *keys = perm + P, *pkey = keys + P, *perm1 = pkey + P, *keys1 = perm1 + P;
-        int *key_off = keys1 + P;
-        unsigned *ocount = reinterpret_cast<unsigned *>(key_off + N + 1);
         int *bh = ctx->work[1].as<int>(), *bsum = bh + nbh;
         ScopedTimer tm(ctx, "node_reduce");
-        if (!own) {
-            RSK_HIP(hipMemsetAsync(d_cnt, 0, NS * 4, ctx->stream));
-            RSK_HIP(hipMemsetAsync(d_cs, 0, NS * 8, ctx->stream));
-            if (d_ms) RSK_HIP(hipMemsetAsync(d_ms, 0, NS * 8, ctx->stream));
-        } else {
-            RSK_HIP(hipMemsetAsync(ocount, 0, 4, ctx->stream));
-        }
+        RSK_HIP(hipMemsetAsync(d_cnt, 0, NS * 4, ctx->stream));
+        RSK_HIP(hipMemsetAsync(d_cs, 0, NS * 8, ctx->stream));
+        if (d_ms) RSK_HIP(hipMemsetAsync(d_ms, 0, NS * 8, ctx->stream));
         const size_t hl = (size_t)nbk * 4;
         static const int nr_ablate = RSK_ABLATION(RSK_ABLATE_NR);
         nr_hist_kernel<<<nblk1, kNrThreads, hl, ctx->stream>>>(d_assign, P, S, N, nbk, pkey, bh);
@@ -1396,25 +1250,10 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
         nr_blockscan_kernel<<<nsb, kNrScanB, 0, ctx->stream>>>(bh, (int)nbh, bsum);
         nr_part_kernel<<<nblk1, kNrThreads, hl, ctx->stream>>>(pkey, P, nbk, bh, perm1, keys1);
         nr_sub_kernel<<<nbk, 256, 0, ctx->stream>>>(perm1, keys1, bh, nblk1, nbk, P, perm, keys);
-        if (own) {
-            const long long *dm = reinterpret_cast<const long long *>(d_mem);
-            auto *ucs = reinterpret_cast<unsigned long long *>(d_cs), *ums = reinterpret_cast<unsigned long long *>(d_ms);
-            nr_keyoff_kernel<<<(unsigned)ceil_div(P + 1, 256), 256, 0, ctx->stream>>>(keys, P, N, key_off);
-            node_reduce_own_kernel<<<(unsigned)ceil_div(owaves, 4), 256, 0, ctx->stream>>>(
-                d_assign, P, S, d_cpu, dm, N, perm, keys, key_off, nranges, d_cnt, reinterpret_cast<long long *>(d_cs),
-                reinterpret_cast<long long *>(d_ms), ctx->work[2].as<int2>(), ocount, ocap);
-            nr_offkey_kernel<<<1024, 256, 0, ctx->stream>>>(ctx->work[2].as<int2>(), ocount, ocap, d_cpu, dm, d_cnt, ucs,
-                                                           ums);
-            nr_recount_kernel<<<2048, 256, 0, ctx->stream>>>(0, ocount, ocap, d_assign, P, S, d_cpu, dm, N, d_cnt, ucs,
-                                                             ums);
-            nr_recount_kernel<<<2048, 256, 0, ctx->stream>>>(1, ocount, ocap, d_assign, P, S, d_cpu, dm, N, d_cnt, ucs,
-                                                             ums);
-        } else {
-            node_reduce_seg_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, ctx->stream>>>(
-                d_assign, P, S, d_cpu, reinterpret_cast<const long long *>(d_mem), N, perm, keys, runs, d_cnt,
-                reinterpret_cast<unsigned long long *>(d_cs), reinterpret_cast<unsigned long long *>(d_ms), nr_ablate,
-                run_len);
-        }
+        node_reduce_seg_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, ctx->stream>>>(
+            d_assign, P, S, d_cpu, reinterpret_cast<const long long *>(d_mem), N, perm, keys, runs, d_cnt,
+            reinterpret_cast<unsigned long long *>(d_cs), reinterpret_cast<unsigned long long *>(d_ms), nr_ablate,
+            run_len);
         RSK_HIP(hipGetLastError());
     } else {
         ScopedTimer tm(ctx, "node_reduce");
@@ -1495,9 +1334,9 @@ int rsk_load_std(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *cap_cpu, i
     RSK_TRY(stage_in(ctx, 0, use_cpu, NS * 4, dev, reinterpret_cast<const void **>(&d_use)));
     RSK_TRY(stage_in(ctx, 1, cap_cpu, (size_t)N * 4, dev, reinterpret_cast<const void **>(&d_cap)));
     RSK_TRY(stage_out(ctx, 2, out_std, (size_t)S * 8, dev, reinterpret_cast<void **>(&d_out)));
-    // nodes per thread: at least 16, and at most 1,024 chunks for the merge
-    // waves to walk (50k nodes x 64 scenarios: 49 nodes, 1,021 chunks)
-    constexpr int max_chunks = 1024;
+    // nodes per thread: at least 16, and at most 2,048 chunks for the merge
+    // workgroups to walk (50k nodes x 64 scenarios: 25 nodes, 2,000 chunks)
+    constexpr int max_chunks = 2048;
     const int npb = std::max({chunk_for(N, S), 16, (int)ceil_div(N, max_chunks)});
     const int nch = (int)ceil_div(N, npb);
     RSK_TRY(ctx->work[0].reserve((size_t)nch * S * 8));
@@ -1509,7 +1348,7 @@ int rsk_load_std(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *cap_cpu, i
         std_partial_kernel<<<(unsigned)ceil_div(total, 256), 256, 0, ctx->stream>>>(
             d_use, d_cap, N, S, npb, total, ctx->work[0].as<double>(), ctx->work[1].as<double>(),
             ctx->work[2].as<int>());
-        std_merge_kernel<<<(unsigned)ceil_div(S, 4), 256, 0, ctx->stream>>>(
+        std_merge_kernel<<<(unsigned)S, 256, 0, ctx->stream>>>(
             ctx->work[0].as<double>(), ctx->work[1].as<double>(), ctx->work[2].as<int>(), nch, S, d_out);
         RSK_HIP(hipGetLastError());
     }

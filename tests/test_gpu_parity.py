@@ -773,8 +773,8 @@ def test_node_reduce_segmented_vs_oracle(ctx, P, N, S, p_flip):
     heavily perturbed ones (30 % of placements redrawn: most lanes off the key),
     a partial last chunk (S = 130), assignments outside [0, N) (skipped), and
     the atomic kernel at S = 1; config 4's size; 60 % redrawn over 6.4 M cells
-    (the off-key list overflows its quarter-of-the-cells capacity: the full
-    recount); more nodes than pods (most nodes' cells zeros)."""
+    (most cells off their key node); more nodes than pods (most nodes' cells
+    zeros)."""
     from oracle import oracle as orc
     from rsk import api
     rng = np.random.default_rng(P + S)
