@@ -62,16 +62,18 @@ __global__ __launch_bounds__(256) void fill_i32_kernel(int *__restrict__ out, si
 }
 
 // Per-scenario lists of the pods off their base node (base = scenario 0's
-// node), as (pod, its current node) entries: every pod that has left its base
-// node in scenario s has exactly one entry in list s, holding the node it is
-// on now (the move kernel updates it in place, or appends the pod when it
-// first leaves its base node).  src[s]: the entry the round's pick came from
-// (-1: the base list).  cnt[s] > cap: the list overflowed, scenario s is
-// scanned in full from then on.
+// node), as (pod, its current node, its CPU, 0) entries: every pod that has
+// left its base node in scenario s has exactly one entry in list s, holding
+// the node it is on now (the move kernel updates it in place, or appends the
+// pod when it first leaves its base node).  In the persistent loop a
+// workgroup's DevLists is its own scenario's: list = the scenario's entries,
+// cnt / src = the list length and the entry the round's pick came from (-1:
+// the base list), both in LDS.  cnt > cap: the list overflowed, the scenario
+// is scanned in full from then on.
 struct DevLists {
     const int *base = nullptr;
     int *cnt = nullptr, *src = nullptr;
-    int2 *list = nullptr;
+    int4 *list = nullptr;
     int cap = 0;
 };
 
@@ -240,15 +242,15 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
             assign[pc] = t;
             if (asg16) asg16[pc] = (unsigned short)t;
             if (dl.base) {  // the pod's entry follows it (one entry per pod off its base node)
-                const int j = dl.src[s], q = dl.cnt[s];
+                const int j = *dl.src, q = *dl.cnt;
                 if (q <= dl.cap) {
                     if (j >= 0) {
-                        dl.list[(size_t)s * dl.cap + j].y = t;
+                        dl.list[j].y = t;
                     } else if (q < dl.cap) {
-                        dl.list[(size_t)s * dl.cap + q] = make_int2(p, t);
-                        dl.cnt[s] = q + 1;
+                        dl.list[q] = make_int4(p, t, c, 0);
+                        *dl.cnt = q + 1;
                     } else {
-                        dl.cnt[s] = dl.cap + 1;  // overflow: full scans from now on
+                        *dl.cnt = dl.cap + 1;  // overflow: full scans from now on
                     }
                 }
             }
@@ -420,7 +422,8 @@ constexpr int kLF = 1024;
 __global__ __launch_bounds__(256) void list_fill_kernel(const int *__restrict__ assign, int P, int S, int N,
                                                         const int *__restrict__ base, int *__restrict__ cur,
                                                         int *__restrict__ pod, int *__restrict__ dcnt,
-                                                        int2 *__restrict__ dlist, int cap) {
+                                                        const int *__restrict__ pod_cpu, int4 *__restrict__ dlist,
+                                                        int cap) {
     constexpr int kK = 16;  // deviations kept per (wave, lane) in LDS; more: the rows are walked again
     __shared__ int wc[4][64];
     __shared__ int2 keep[4][kK][64];
@@ -469,7 +472,10 @@ __global__ __launch_bounds__(256) void list_fill_kernel(const int *__restrict__ 
     int q = wc[wv][lane];
     if (n <= kK) {  // the kept entries
         for (int k = 0; k < n; ++k, ++q)
-            if (q < cap) dlist[(size_t)s * cap + q] = keep[wv][k][lane];
+            if (q < cap) {
+                const int2 e = keep[wv][k][lane];
+                dlist[(size_t)s * cap + q] = make_int4(e.x, e.y, pod_cpu[e.x], 0);
+            }
         return;
     }
     for (int p0 = q0; p0 < q1; p0 += kB) {
@@ -484,7 +490,7 @@ __global__ __launch_bounds__(256) void list_fill_kernel(const int *__restrict__ 
         for (int u = 0; u < kB; ++u) {
             const int x = (unsigned)a[u] < (unsigned)N ? a[u] : N;
             if (p0 + u < q1 && x != b[u]) {
-                if (q < cap) dlist[(size_t)s * cap + q] = make_int2(p0 + u, x);
+                if (q < cap) dlist[(size_t)s * cap + q] = make_int4(p0 + u, x, pod_cpu[p0 + u], 0);
                 ++q;
             }
         }
@@ -627,8 +633,15 @@ __device__ __forceinline__ void blk_update(const NS &ns, const int *__restrict__
     }
 }
 
-// delete_replaced_pod.py:41-61 for scenario s by the workgroup (pick_list_kernel's
-// rule); returns the pod (-1 none) to every thread, the winning entry in *src
+// delete_replaced_pod.py:41-61 for scenario s by the workgroup: the pods on
+// the most hazardous node m are m's base pods still on m (their assign word
+// checked) and the list entries whose node is m (the entry carries the pod's
+// CPU); an overflowed list scans every pod's assign word.  Both lists' loads
+// are issued together, so the pick costs two dependent round trips after the
+// node's base range (ids / entries, then the base pods' assign words).  The
+// first max (CPU, -pod) wins, as the reference's strict '>' from -1 over pods
+// in order; returns the pod (-1 none) to every thread, the winning list entry
+// in *src (-1: a base pod) and its CPU in *pcpu.
 template <typename T>
 __device__ __forceinline__ int scn_pick(const T *__restrict__ asg, const int *__restrict__ pod_cpu, int P, int S,
                                         int s, unsigned long long kd, const int *__restrict__ off,
@@ -639,22 +652,28 @@ __device__ __forceinline__ int scn_pick(const T *__restrict__ asg, const int *__
     if (!kd) return -1;  // uniform
     const int m = (int)~(unsigned)(kd & 0xffffffffull);
     const int b0 = off[m], nb = off[m + 1] - b0;
-    const int nd = dl.cnt[s];
+    const int nd = *dl.cnt;
     const bool full = nd > dl.cap;
-    const int2 *l = dl.list + (size_t)s * dl.cap;
+    const int4 *l = dl.list;
     auto key = [](int p, int c) {
         return c >= 0 ? ((unsigned long long)((unsigned)c ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)p)
                       : 0ull;
     };
     unsigned long long best = 0ull;
     int bsrc = -1;  // the list entry of this thread's best (-1: a base pod)
-    const int ng = full ? P : nb;
-    for (int i0 = 0; i0 < ng; i0 += 256 * kU) {
+    const int ng = full ? P : nb, nl = full ? 0 : nd;
+    const int nmax = max(ng, nl);
+    for (int i0 = 0; i0 < nmax; i0 += 256 * kU) {
         int p[kU], a[kU], c[kU];
+        int4 e[kU];
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const int i = min(i0 + u * 256 + t, ng - 1);
-            p[u] = full ? i : pod[b0 + i];
+        for (int u = 0; u < kU; ++u) {  // clamped, always-valid ids (a pod of an empty range: pod 0, masked below)
+            const int i = min(i0 + u * 256 + t, max(ng, 1) - 1);
+            p[u] = full ? i : (ng > 0 ? pod[b0 + i] : 0);
+        }
+        if (nl > 0) {  // uniform
+#pragma unroll
+            for (int u = 0; u < kU; ++u) e[u] = l[min(i0 + u * 256 + t, nl - 1)];
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
@@ -663,24 +682,14 @@ __device__ __forceinline__ int scn_pick(const T *__restrict__ asg, const int *__
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-            const unsigned long long k = a[u] == m ? key(p[u], c[u]) : 0ull;
-            best = k > best ? k : best;
-        }
-    }
-    const int nl = full ? 0 : nd;
-    for (int i0 = 0; i0 < nl; i0 += 256 * kU) {
-        int2 e[kU];
-        int c[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) e[u] = l[min(i0 + u * 256 + t, nl - 1)];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) c[u] = pod_cpu[e[u].x];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const unsigned long long k = e[u].y == m ? key(e[u].x, c[u]) : 0ull;
-            // >=: an entry of the same pod as a base hit carries the pod's entry index
-            if (k && k >= best) bsrc = min(i0 + u * 256 + t, nl - 1);
-            best = k > best ? k : best;
+            const int i = i0 + u * 256 + t;
+            const unsigned long long kb = (i < ng && a[u] == m) ? key(p[u], c[u]) : 0ull;
+            if (kb > best) best = kb, bsrc = -1;
+            if (nl > 0) {
+                const unsigned long long ke = (i < nl && e[u].y == m) ? key(e[u].x, e[u].z) : 0ull;
+                // >=: an entry of the same pod as a base hit carries the pod's entry index
+                if (ke && ke >= best) best = ke, bsrc = i;
+            }
         }
     }
     const unsigned long long mine = best;
@@ -721,7 +730,7 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
     extern __shared__ __attribute__((aligned(16))) unsigned lds[];
     __shared__ unsigned long long r64[8];
     __shared__ int r32[4];
-    __shared__ int lsrc;
+    __shared__ int lsrc, lcnt;  // the scenario's pick source entry and list length
     __shared__ ScnState st;
     unsigned *tab = kGlobal ? gtab + (size_t)blockIdx.x * (size_t)(2 * a.H + 8) : lds;
     const int t = (int)threadIdx.x;
@@ -772,6 +781,11 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
                 }
             }
         }
+        if (t == 0) lcnt = a.dl.cnt[s];  // the list setup's count (the loop keeps it in LDS)
+        DevLists dl = a.dl;
+        dl.cnt = &lcnt;
+        dl.src = &lsrc;
+        dl.list = a.dl.list + (size_t)s * a.dl.cap;
         __syncthreads();
         scn_reduce(sb, &st, r64, r32);
         if (t == 0) {
@@ -782,12 +796,9 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
             for (int r = 0; r < a.R; ++r) {
                 const unsigned long long kd = st.most;
                 int pcpu;
-                const int p = scn_pick<int>(a.assign, a.pod_cpu, a.P, a.S, s, kd, a.off, a.pod, a.dl, r64, &lsrc, &pcpu);
+                const int p = scn_pick<int>(a.assign, a.pod_cpu, a.P, a.S, s, kd, a.off, a.pod, dl, r64, &lsrc, &pcpu);
                 int *tg_row = a.out_target + (size_t)r * a.S;
-                if (t == 0) {
-                    a.out_evict[(size_t)r * a.S + s] = p;
-                    if (p >= 0) a.dl.src[s] = lsrc;  // read by car_move_one's thread 0
-                }
+                if (t == 0) a.out_evict[(size_t)r * a.S + s] = p;  // (lsrc: read by car_move_one's thread 0)
                 if (p < 0) {
                     if (t == 0) tg_row[s] = kNoEvict;
                     continue;  // uniform: the state is unchanged
@@ -795,7 +806,7 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
                 const int o = (int)~(unsigned)(kd & 0xffffffffull);  // the picked pod sits on the hazard node
                 car_move_one<kGlobal>(a.row_ptr, a.col, a.pod_cpu, a.assign, ns, a.cap, nullptr, s, a.S, a.N, a.H, 1,
                                       tg_row, nullptr, tab, nullptr, nullptr, nullptr, a.zc_cnt, a.zc_key, 0, INT_MAX,
-                                      a.dl, p, o, pcpu);
+                                      dl, p, o, pcpu);
                 move_sync<kGlobal>();  // the move's state update (thread 0) before it is read
                 const int tt = (int)tab[2 * a.H + 7];  // car_move_one's target (red[5])
                 if (tt >= 0) {  // two nodes' CPU changed: their blocks, then the scenario's maxima
@@ -1243,12 +1254,12 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         const int P = r->P;
         {
             int cap = (int)std::max<int64_t>(256, P / 16);
-            cap = (int)std::max<int64_t>(64, std::min<int64_t>(cap, ((int64_t)128 << 20) / ((int64_t)S * 8)));
+            cap = (int)std::max<int64_t>(64, std::min<int64_t>(cap, ((int64_t)256 << 20) / ((int64_t)S * 16)));
             RSK_TRY(r->lbase.reserve((size_t)P * 4));
             RSK_TRY(r->loff.reserve((size_t)(N + 2) * 4 * 2));
             RSK_TRY(r->lpod.reserve((size_t)P * 4));
             RSK_TRY(r->lcnt.reserve((size_t)S * 8));  // counts, then the picks' source entries
-            RSK_TRY(r->llist.reserve((size_t)S * cap * 8));
+            RSK_TRY(r->llist.reserve((size_t)S * cap * 16));
             int *cntb = r->loff.as<int>() + (N + 2);  // N + 1 counts, then the fill cursors
             ScopedTimer tm(ctx, "rounds_lists");
             RSK_HIP(hipMemsetAsync(cntb, 0, (size_t)(N + 1) * 4, st));
@@ -1260,12 +1271,12 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
             RSK_CHECK(blocks < INT32_MAX, "list grid too large");
             list_fill_kernel<<<(unsigned)blocks, 256, 0, st>>>(d_assign, P, S, N, r->lbase.as<int>(), cntb,
                                                                  r->lpod.as<int>(), r->lcnt.as<int>(),
-                                                                 r->llist.as<int2>(), cap);
+                                                                 r->pod_cpu.as<int>(), r->llist.as<int4>(), cap);
             RSK_HIP(hipGetLastError());
             dl.base = r->lbase.as<int>();
             dl.cnt = r->lcnt.as<int>();
             dl.src = dl.cnt + S;
-            dl.list = r->llist.as<int2>();
+            dl.list = r->llist.as<int4>();
             dl.cap = cap;
         }
         // one launch for all R rounds: the hazard flags and the block maxima
