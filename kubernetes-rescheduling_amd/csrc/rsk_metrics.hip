@@ -557,7 +557,6 @@ __global__ __launch_bounds__(kNrScanB) void nr_blockscan_kernel(int *__restrict_
 }
 
 constexpr int kNrRun = 256;  // bucketed pods per wave (64: 0.219 ms, 256: 0.212 at 1M x 50k x 64)
-template <int kB, bool kPre>
 __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restrict__ assign, int P, int S,
                                                               const int *__restrict__ pod_cpu,
                                                               const long long *__restrict__ pod_mem, int N,
@@ -589,44 +588,26 @@ __global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restr
         rc = 0;
         rcpu = rmem = 0;
     };
-    // Batches of kB pods; kPre: the next batch's pod ids and keys (scalar
-    // loads) are fetched while this batch's rows are in flight.
-    int pn[kB], kn[kB];
-    if (kPre) {
-#pragma unroll
-        for (int u = 0; u < kB; ++u) {
-            const int jj = min(j0 + u, j1 - 1);
-            pn[u] = cperm[jj];
-            kn[u] = ckeys[jj];
-        }
-    }
+    // Batches of 8 pods, every load of a batch issued before its first use:
+    // the assign rows, and the pods' CPU / memory (scattered pod ids: each a
+    // cache miss that, loaded per pod behind the previous pod's atomics,
+    // serialised the run).  (Fetching the next batch's ids during a batch, or
+    // batches of 16: no gain, 0.238 / 0.239 / 0.269 ms against 0.238.)
+    constexpr int kB = 8;
     for (int j = j0; j < j1; j += kB) {
         int a[kB], pp[kB], kk[kB], cc[kB];
         long long mm[kB];
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
-            if (kPre) {
-                pp[u] = pn[u];
-                kk[u] = kn[u];
-            } else {
-                const int jj = min(j + u, j1 - 1);
-                pp[u] = cperm[jj];
-                kk[u] = ckeys[jj];
-            }
+            const int jj = min(j + u, j1 - 1);
+            pp[u] = cperm[jj];
+            kk[u] = ckeys[jj];
         }
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
             a[u] = live ? __builtin_nontemporal_load(&assign[(size_t)pp[u] * S + s]) : -1;
             cc[u] = ccpu[pp[u]];
             mm[u] = mem ? pod_mem[pp[u]] : 0;
-        }
-        if (kPre) {
-#pragma unroll
-            for (int u = 0; u < kB; ++u) {  // the next batch's ids (clamped: always valid)
-                const int jj = min(j + kB + u, j1 - 1);
-                pn[u] = cperm[jj];
-                kn[u] = ckeys[jj];
-            }
         }
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
@@ -1258,11 +1239,7 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
         nr_blockscan_kernel<<<nsb, kNrScanB, 0, ctx->stream>>>(bh, (int)nbh, bsum);
         nr_part_kernel<<<nblk1, kNrThreads, hl, ctx->stream>>>(pkey, P, nbk, bh, perm1, keys1);
         nr_sub_kernel<<<nbk, 256, 0, ctx->stream>>>(perm1, keys1, bh, nblk1, nbk, P, perm, keys);
-        static const int nrv = RSK_KNOB(RSK_NR_VAR, 0);
-        auto *nrk = nrv == 1 ? &node_reduce_seg_kernel<8, true>
-                  : nrv == 2 ? &node_reduce_seg_kernel<16, true>
-                  : nrv == 3 ? &node_reduce_seg_kernel<16, false> : &node_reduce_seg_kernel<8, false>;
-        nrk<<<(unsigned)ceil_div(waves, 4), 256, 0, ctx->stream>>>(
+        node_reduce_seg_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, ctx->stream>>>(
             d_assign, P, S, d_cpu, reinterpret_cast<const long long *>(d_mem), N, perm, keys, runs, d_cnt,
             reinterpret_cast<unsigned long long *>(d_cs), reinterpret_cast<unsigned long long *>(d_ms), nr_ablate,
             run_len);
