@@ -36,6 +36,10 @@ BENCH_NAME = {"car_tile16": "car_tile", "car_fused16": "car_tile", "car_hub": "c
 # the heavy tile launch, two grid sizes of car_tile16): their per-"launch"
 # traffic is the sum over the grids, not the mean
 SUM_GRIDS = {"car_tile"}
+# kernel 3 (bench.py's "kernel3" leg): the launches of one librsk call, summed per call
+KERNEL3 = ("node_reduce", "nr_", "cut_cost", "cut_bins", "std_")
+KERNEL3_CALL = {"node_reduce": ("node_reduce_seg", "nr_hist", "nr_blocksum", "nr_blockscan", "nr_part", "nr_sub"),
+                "load_std": ("std_partial", "std_merge"), "cut_cost": ("cut_cost_wave", "cut_bins_sum")}
 
 
 def short(name: str) -> str:
@@ -72,7 +76,7 @@ def main():
                         ("l2", "TCC_MISS_sum"))}
     summary = {}
     for (k, grid), durs in sorted(trace.items()):
-        if not k.startswith("car") and k not in ("pick_node", "node_reduce"):
+        if not k.startswith("car") and not k.startswith(KERNEL3) and k not in ("pick_node",):
             continue
         e = {"grid": int(grid), "launches": len(durs), "avg_us": round(sum(durs) / len(durs) / 1e3, 2)}
         for c, d in pmc.items():
@@ -111,6 +115,21 @@ def main():
     for k, (bytes_, n, us) in by_kernel.items():
         entry[k] = {"S": args.S, "hbm_bytes_per_launch": bytes_ // max(n, 1), "avg_us": round(us / max(n, 1), 2),
                     "source": f"profiles/{args.tag}_summary.json"}
+    # kernel 3: every launch of one call summed (durations and PMC bytes per call)
+    k3 = {}
+    for call, parts in KERNEL3_CALL.items():
+        tot_b, tot_us, seen = 0, 0.0, []
+        for key, e in summary.items():
+            k = key.split("@")[0]
+            if k in parts and "hbm_bytes_per_launch" in e:
+                tot_b += e["hbm_bytes_per_launch"]
+                tot_us += e["avg_us"]
+                seen.append(k)
+        if seen:
+            k3[call] = {"S": args.S, "hbm_bytes_per_call": tot_b, "kernels_us_per_call": round(tot_us, 2),
+                        "launches": sorted(seen), "source": f"profiles/{args.tag}_summary.json"}
+    if k3:
+        traffic.setdefault("kernel3", {})[args.config] = k3
     with open(path, "w") as f:
         json.dump(traffic, f, indent=1)
     print(json.dumps(summary, indent=1))
