@@ -616,12 +616,22 @@ def main():
         k3_leg = {}
         alg3 = {"node_reduce": 4 * P * S + 12 * P + 20 * N * S, "load_std": 4 * N * S + 4 * N,
                 "cut_cost": 4 * (P + 1) + 4 * c.nnz + 4 * P * S + 4 * c.nnz * S}
+        try:
+            with open(args.pmc_json) as f:
+                pmc3 = json.load(f).get("kernel3", {}).get(args.config, {})
+        except (OSError, ValueError):
+            pmc3 = {}
         for name in ("node_reduce", "load_std", "cut_cost"):
             tms, n = ctx.kernel_time(name)
             if n:
                 k3_leg[name] = {"avg_ms": round(tms / n, 4), "launches_per_call": n // reps,
                                 "algorithmic_bytes": alg3[name],
                                 "algorithmic_GBps": round(alg3[name] / (tms / n / 1e3) / 1e9, 1)}
+                e = pmc3.get(name)
+                if e and e.get("S") == S:   # rocprof PMC bytes of the call's launches (tools/pmc_summary.py)
+                    k3_leg[name]["traffic"] = e["hbm_bytes_per_call"]
+                    k3_leg[name]["traffic_over_algorithmic"] = round(e["hbm_bytes_per_call"] / alg3[name], 3)
+                    k3_leg[name]["traffic_source"] = e["source"]
         # parity of kernel 3 over the whole batch (every scenario): the oracle's
         # node sums and cut count exactly, its std within 1e-9 relative
         from oracle import oracle as orc
