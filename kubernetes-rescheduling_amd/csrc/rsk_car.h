@@ -287,8 +287,9 @@ __device__ __forceinline__ int block_capmax(const int *__restrict__ cap, int N, 
 }
 
 // chunks per group in the tile grid order (each group walked tile-major inside
-// its XCD's run: 0.8175-0.8202 -> 0.8150-0.8164 ms at config 3; groups of 8
-// are as fast but re-fetch 0.36 GB more code lines)
+// its XCD's run): round 5's interleaved A/B at config 3 gave 0.8167 / 0.8170 ms
+// for 4, 0.8196 / 0.8188 for 2, 0.8198 / 0.8196 for 1, with the same reads
+// (2.14-2.17 GB): the group does not move the code lines' L2 misses)
 constexpr int kTileGroup = 4;
 
 struct Tile16Args {
@@ -307,7 +308,6 @@ struct Tile16Args {
     int img_cells;         // LDS cells of the largest image (rmax * SL); the records follow
     int rec_cap;           // record ints reserved in LDS; the unit counter follows
     int xcd_per;           // tile units per XCD (the XCD-contiguous grid order)
-    int group;             // chunks per group (temporary A/B; kTileGroup)
     int ablate;            // profiling only (RSK_ABLATE_TILE): 1 skip image load, 2 skip scoring
     unsigned n_assign, n_out, n_pods, n_recs, n_key;  // element counts (debug bounds build)
 };

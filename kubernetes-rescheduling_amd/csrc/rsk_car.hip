@@ -1495,8 +1495,6 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         a.lsl = 0;
         while ((1 << a.lsl) < SL) ++a.lsl;
         a.ablate = ablate;
-        static const int tgroup = std::max(1, RSK_KNOB(RSK_TILE_GROUP, kTileGroup));
-        a.group = tgroup;
         a.rec_cap = (plan->recmax + 3) & ~3;
         a.img_cells = (plan->rmax * SL + 3) & ~3;
         const size_t lds = tile16_lds_bytes(plan->rmax, a.lsl, a.rec_cap);

@@ -976,7 +976,7 @@ __device__ __forceinline__ void tile16_block(const Tile16Args &a, unsigned bid) 
     // pod rows while a group's code slices stay in its L2
     int tile, chunk;
     {
-        const int G = a.group, full = nchunk / G;
+        const int G = kTileGroup, full = nchunk / G;
         if (unit < full * a.T * G) {
             const int cg = unit / (a.T * G), r = unit - cg * a.T * G;
             tile = r / G;
