@@ -201,8 +201,9 @@ def algorithmic_bytes(P, N, S, nnz, Q_light=None, light_rec_bytes=0):
     return 4 * (P + 1) + 4 * nnz + 4 * P * S + 4 * N + 5 * N * S + 4 * P * S
 
 
-def alg_bytes(kernel, P, N, S, info):
+def alg_bytes(kernel, P, N, S, info, step_bytes=0):
     """Algorithmic bytes per step of one kernel timer (DESIGN.md "Roofline accounting"):
+      car_direct : the one-launch small batch (config 2): the whole step's SURVEY §8d bytes
       car_tile : the tile launch (tiles + the side rows fused into it): the assign slice of every
                  distinct neighbour pod of those rows once (4·S per pod) + every row's target (4·S)
                  + the tile plan and side items
@@ -218,7 +219,8 @@ def alg_bytes(kernel, P, N, S, info):
             "car_side": 4 * S * (info.get("side_rows", 0) - fused) + info.get("side_bytes", 0),
             "car_mid": 4 * S * info["mid_rows"] + info["mid_bytes"],
             "car_heavy": 4 * S * info["heavy_rows"] + info["heavy_bytes"],
-            "car_prep": 7 * N * S + 4 * N}.get(kernel, 0)
+            "car_prep": 7 * N * S + 4 * N,
+            "car_direct": step_bytes}.get(kernel, 0)
 
 
 def bench_rounds(args, cfg, world, rank, local, dev):
@@ -433,11 +435,17 @@ def main():
     # dominant kernel: the one carrying the most algorithmic bytes (car_tile at the
     # headline config); summed durations of launches that overlap on side streams
     # would not rank by time
-    dom = max(kernels, key=lambda k: alg_bytes(k, P, N, S, plan.info())) if kernels else None
-    # the timed region: events only around the dominant kernel's launches
+    B = algorithmic_bytes(P, N, S, c.nnz)
+    dom = max(kernels, key=lambda k: alg_bytes(k, P, N, S, plan.info(), B)) if kernels else None
+    # the timed region: events only around the dominant kernel's launches —
+    # unless the step is latency-bound (its launches under 50 us: config 2),
+    # where an event pair costs as much as the kernel; then the steps are timed
+    # bare and the kernel's duration is the breakdown pass's
+    latency_bound = sum(v["per_step_ms"] for v in kernels.values()) < 0.05
+    live_events = dom is not None and not args.no_kernel_events and not latency_bound
     ctx.reset_profiling()
     ctx.set_profile_only(dom)
-    ctx.set_profiling(dom is not None and not args.no_kernel_events)
+    ctx.set_profiling(live_events)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -457,6 +465,8 @@ def main():
     timed = collect()
     if dom in timed:  # the dominant kernel's duration measured inside the timed region
         kernels[dom] = dict(timed[dom], breakdown_pass_avg_ms=kernels[dom]["avg_ms"])
+    elif dom is not None:
+        kernels[dom]["duration_source"] = "breakdown pass (latency-bound step timed without events)"
     ms_step = elapsed * 1e3 / args.steps
     evals = P * N * S
     # scenario sharding: every rank scores P x N x S of its own (weak scaling);
@@ -650,8 +660,7 @@ def main():
         k3_leg["note"] = ("algorithmic bytes: node_reduce reads assign + pod cpu/mem and writes the N*S count/cpu/mem"
                           " words; load_std reads use and cap (its 20 B per (node chunk, scenario) partials not counted); cut_cost reads CSR + assign + one gather per edge")
 
-    alg = {k: alg_bytes(k, P, N, S, info) for k in kernels}
-    B = algorithmic_bytes(P, N, S, c.nnz)
+    alg = {k: alg_bytes(k, P, N, S, info, B) for k in kernels}
     roof = None
     if dom in kernels and dom in alg:
         launches_per_step = kernels[dom]["launches"] / args.steps

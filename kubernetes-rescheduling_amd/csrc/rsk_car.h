@@ -344,15 +344,32 @@ struct SideGeom {
 };
 SideGeom side16_geometry(int dmax, int N, int T = 0);  // T: waves per item (0: 1 up to 256 neighbours, else 8)
 void side16_apply_geometry(SideArgs &a, const SideGeom &g);  // the geometry's LDS layout into the launch arguments
+// Rows above the side classes, scored in the fused grid one (row, scenario)
+// cell per workgroup (targets only): the cell's neighbour nodes counted in an
+// LDS hash of packed words ((node + 1) << 16 | count), H words + 4 reduction
+// words within the tile's LDS, exact cap - use of the nodes at the max count.
+struct DirectArgs {
+    const int *rp, *ci;       // the plan's deduplicated rows without self edges
+    const int *rows;          // plan row -> pod (null: the identity)
+    const int *items;         // item k's plan row at items[k * istride]
+    int istride, Q;           // Q rows: cells = Q * S
+    const int *assign, *use, *cap;
+    const uint8_t *haz;
+    int S, N, H;
+    int *out_target;
+};
+// H for a packed table of rows up to dmax neighbours within lds bytes (0: none fits)
+int direct16_table(int dmax, int N, size_t lds);
 struct FuseMap {
-    int big_blocks;    // the first big_blocks blocks: 4-wave side teams (ba), a multiple of 8
+    int direct_blocks; // the first direct_blocks blocks: one (row, scenario) cell each (da), a multiple of 8
+    int big_blocks;    // then big_blocks blocks: 4-wave side teams (ba), a multiple of 8
     int R, k1;         // then k1 periods of R rows of 8 blocks: R - 1 tile rows, one single-wave side row (sa)
     int side_rows, tile_rows;  // then the tile rows left, then the side rows left
 };
 // lean tiles + single-wave side items of one class (4 per workgroup, kB 16) +
 // optionally 4-wave side teams (kB 16) in one grid; ba.n_rows == 0: no teams
 int launch_fused16(hipStream_t stream, const Tile16Args &a, const SideArgs &sa, int side_blocks, const SideArgs &ba,
-                   bool score, bool off32, unsigned tile_blocks, size_t lds);
+                   const DirectArgs &da, bool score, bool off32, unsigned tile_blocks, size_t lds);
 // scratch: device memory for rows whose table exceeds the LDS (grown on demand)
 int launch_side16(hipStream_t stream, const SideArgs &a, const SideGeom &g, bool off32, DevBuf *scratch);
 // the same rows with node state computed on the fly (a.code null, a.haz / a.capmax set)

@@ -1431,6 +1431,37 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     if (!fuse_ok || (fuse_c < 0 && !fuse_big) || plan->fused_lo == kNumSide) plan->fused_lo = plan->fused_hi = 0;
     bool big_left = false;  // classes above the fused ones
     for (int c = big_hi; c < kNumSide; ++c) big_left = big_left || plan->side_end[c] > plan->side_beg[c];
+    // The rows too big for the fused grid's side classes: when few cells
+    // (config 4: 8 rows of 1,000-1,800 neighbours x 64 scenarios) and targets
+    // only, a workgroup per (row, scenario) at the front of the fused grid
+    // (direct16_block: packed LDS hash within the tile's LDS, exact cap - use) —
+    // no side stream, no fork / join packets between the launches.
+    DirectArgs fda;
+    std::memset(&fda, 0, sizeof(fda));
+    if (fuse_ok && big_left && !d_score) {
+        const int b0 = plan->side_beg[kNumSide - 1], b1 = plan->side_end[big_hi];  // degree descending
+        int dmax = 0;
+        for (int c = big_hi; c < kNumSide; ++c) dmax = std::max(dmax, plan->side_dmax[c]);
+        const int H = direct16_table(dmax, N, lean_lds);
+        if (H && (int64_t)(b1 - b0) * S <= kDirectBigCells) {
+            fda.rp = plan->drp.as<int>();
+            fda.ci = plan->dci.as<int>();
+            fda.rows = plan->drows.ptr ? plan->drows.as<int>() : nullptr;
+            fda.items = plan->side_items.as<int>() + (size_t)b0 * 4;
+            fda.istride = 4;
+            fda.Q = b1 - b0;
+            fda.assign = d_assign;
+            fda.use = d_use;
+            fda.cap = d_cap;
+            fda.haz = d_haz;
+            fda.S = S;
+            fda.N = N;
+            fda.H = H;
+            fda.out_target = d_target;
+            big_left = false;
+        }
+    }
+    const bool fuse_direct = fda.Q > 0;
     // (S < 64: the tiles are short, the fork's events would cost more than the overlap)
     const bool big_fork = compact && big_left && plan->T > 0 && S >= 64;
     const int nfork = big_fork ? 1 : 0;
@@ -1507,9 +1538,9 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         a.xcd_per = (int)ceil_div(units, 8);
         const int64_t blocks = 8 * (int64_t)a.xcd_per;
         RSK_CHECK(blocks < INT32_MAX, "tile grid too large");
-        if (fuse_c >= 0 || fuse_big)
-            RSK_TRY(launch_fused16(ctx->stream, a, fsa, fside_blocks, fba, d_score != nullptr, off32, (unsigned)blocks,
-                                   lds));
+        if (fuse_c >= 0 || fuse_big || fuse_direct)
+            RSK_TRY(launch_fused16(ctx->stream, a, fsa, fside_blocks, fba, fda, d_score != nullptr, off32,
+                                   (unsigned)blocks, lds));
         else
             RSK_TRY(launch_tile16(ctx->stream, a, d_score != nullptr, off32, (unsigned)blocks, lds));
     } else if (plan->T > 0) {   // K1 tiles, wide {node, key} pairs

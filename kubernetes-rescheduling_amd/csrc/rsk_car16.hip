@@ -1085,14 +1085,103 @@ __global__ __launch_bounds__(kTileThreads, kL64 ? RSK_TILE16_WGS : RSK_TILE16_WG
 // Every side workgroup fits the tile's footprint (4 waves, <= 64 VGPRs, its
 // LDS within the tile's).
 // (the side items keep their next assign rows in flight while a batch is scored)
-template <bool kScore, bool kOff32>
+//
+// direct16_block: one (row, scenario) cell of the rows above the side classes
+// (DirectArgs, targets only), in the front of the fused grid: the neighbours'
+// nodes (hazard nodes skipped) counted in an LDS hash of packed words
+// ((node + 1) << 16 | count: N <= 65535, degree < 65536), then the exact
+// (cap - use, -node) maximum over the nodes at the max count, or the
+// scenario's zero case from the prep kernel — rescheduling.py:183-214 on the
+// deduplicated row without its self edge, as car_direct_kernel.
+__device__ __forceinline__ void direct16_block(const DirectArgs &a, const Tile16Args &ta, int cell) {
+    extern __shared__ __attribute__((aligned(16))) unsigned dtab[];
+    const int H = a.H, S = a.S, N = a.N, t = (int)threadIdx.x;
+    unsigned *red = dtab + H;                                                   // M, nbest
+    unsigned long long *best64 = reinterpret_cast<unsigned long long *>(dtab + H + 2);  // (H even: 8-B aligned)
+    const int k = cell / S, s = cell - k * S;
+    const int i = a.items[(size_t)k * a.istride];
+    const int p = a.rows ? a.rows[i] : i;
+    const int b = a.rp[p], d = a.rp[p + 1] - b;
+    for (int h = t; h < H + 4; h += kTileThreads) dtab[h] = 0u;
+    __syncthreads();
+    const unsigned mask = (unsigned)H - 1u;
+    constexpr int kU = 4;  // neighbours in flight per thread (clamped, always-valid addresses)
+    for (int j0 = t; j0 < d; j0 += kTileThreads * kU) {
+        int q[kU], x[kU];
+        uint8_t hz[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) q[u] = a.ci[b + min(j0 + u * kTileThreads, d - 1)];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) x[u] = a.assign[(size_t)q[u] * S + s];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) hz[u] = a.haz[(size_t)min((unsigned)x[u], (unsigned)N - 1u) * S + s];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            if (j0 + u * kTileThreads >= d || (unsigned)x[u] >= (unsigned)N || hz[u]) continue;
+            const unsigned key = (unsigned)x[u] + 1u;
+            unsigned h = (key * 2654435761u) & mask;
+            while (true) {
+                const unsigned prev = atomicCAS(&dtab[h], 0u, (key << 16) | 1u);
+                if (prev == 0u) break;
+                if ((prev >> 16) == key) { atomicAdd(&dtab[h], 1u); break; }
+                h = (h + 1u) & mask;
+            }
+        }
+    }
+    __syncthreads();
+    int m = 0;
+    for (int h = t; h < H; h += kTileThreads) m = max(m, (int)(dtab[h] & 0xffffu));
+    m = dpp_max(m);
+    if ((t & 63) == 0 && m) atomicMax(&red[0], (unsigned)m);
+    __syncthreads();
+    const unsigned M = red[0];
+    if (M > 0) {
+        unsigned long long bk = 0;
+        unsigned nb = 0;
+        for (int h = t; h < H; h += kTileThreads) {
+            const unsigned w = dtab[h];
+            if ((w & 0xffffu) != M) continue;
+            const int n = (int)(w >> 16) - 1;
+            ++nb;
+            const unsigned long long kk = pack_rn(a.cap[n] - a.use[(size_t)n * S + s], n);
+            bk = kk > bk ? kk : bk;
+        }
+        if (nb) {
+            atomicAdd(&red[1], nb);
+            atomicMax(best64, bk);
+        }
+    }
+    __syncthreads();
+    if (t == 0) {
+        int score, tg;
+        if (M == 0) {
+            tg = zero_target(load_zc(ta.zc_cnt, ta.zc_key, s), score);
+        } else {
+            CarState st;
+            st.bc = (int)M;
+            st.nm = red[1] == 1u ? (int)M : 0;  // one node at the max count: it, even if overloaded
+            st.br = (int)((unsigned)(*best64 >> kNodeBits) ^ 0x80000000u);
+            st.bn = (int)(kNodeMask - (unsigned)(*best64 & kNodeMask));
+            tg = car_finalize(st, ZeroCase{}, score);
+        }
+        a.out_target[(size_t)i * S + s] = tg;
+    }
+}
+
+template <bool kScore, bool kOff32, bool kDirect>
 __global__ __launch_bounds__(kTileThreads, RSK_TILE16_WGS) void car_fused16_kernel(Tile16Args ta, SideArgs sa,
-                                                                                  SideArgs ba, FuseMap f) {
-    if (blockIdx.x < (unsigned)f.big_blocks) {
-        side16_block<4, 4, 16, kOff32, true>(ba, (int)blockIdx.x);
+                                                                                  SideArgs ba, DirectArgs da,
+                                                                                  FuseMap f) {
+    if (kDirect && blockIdx.x < (unsigned)f.direct_blocks) {
+        if ((int)blockIdx.x < da.Q * da.S) direct16_block(da, ta, (int)blockIdx.x);
         return;
     }
-    const unsigned v = blockIdx.x - (unsigned)f.big_blocks, row = v >> 3, x = v & 7u;
+    const unsigned v0 = blockIdx.x - (unsigned)f.direct_blocks;
+    if (v0 < (unsigned)f.big_blocks) {
+        side16_block<4, 4, 16, kOff32, true>(ba, (int)v0);
+        return;
+    }
+    const unsigned v = v0 - (unsigned)f.big_blocks, row = v >> 3, x = v & 7u;
     const unsigned R = (unsigned)f.R, K1 = (unsigned)f.k1, P1 = K1 * R;
     unsigned side = 0xffffffffu, tile;
     if (row < P1) {
@@ -1132,12 +1221,25 @@ int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off3
     return RSK_OK;
 }
 
+int direct16_table(int dmax, int N, size_t lds) {
+    const int distinct = std::min(dmax, N);
+    if (N > 65535 || dmax >= 65536) return 0;  // the packed (node + 1, count) words
+    int H = 2;
+    while (H < 2 * distinct) H <<= 1;          // load factor <= 1/2
+    while (H > 2 && (size_t)(H + 4) * 4 > lds) H >>= 1;
+    return H > distinct && (size_t)(H + 4) * 4 <= lds ? H : 0;
+}
+
 int launch_fused16(hipStream_t stream, const Tile16Args &a, const SideArgs &sa, int side_blocks, const SideArgs &ba,
-                   bool score, bool off32, unsigned tile_blocks, size_t lds) {
+                   const DirectArgs &da, bool score, bool off32, unsigned tile_blocks, size_t lds) {
     RSK_CHECK(a.lsl == 6 && (size_t)a.img_cells * 4 <= (size_t)kT16Rows * 256 && tile_blocks % 8 == 0,
               "fused launch needs 64-scenario tiles");
+    const int64_t cells = (int64_t)da.Q * da.S;
+    RSK_CHECK(cells == 0 || (!score && da.H > 0 && (size_t)(da.H + 4) * 4 <= lds && cells < INT32_MAX),
+              "direct cells in the fused grid: targets only, a table within the tile's LDS");
     constexpr int spread = 2;  // side rows over the first half of the tile rows (1 / 4 of them: slower)
     FuseMap f;
+    f.direct_blocks = (int)(8 * ceil_div(cells, 8));  // (XCD alignment of the blocks after them)
     f.big_blocks = (int)(8 * ceil_div((int64_t)ba.n_rows * ba.nchunk, 8));
     f.side_rows = (int)ceil_div(side_blocks, 8);
     f.tile_rows = (int)(tile_blocks / 8);
@@ -1145,17 +1247,19 @@ int launch_fused16(hipStream_t stream, const Tile16Args &a, const SideArgs &sa, 
     // side rows the periods cannot hold go after the tiles
     f.R = std::max(2, f.tile_rows / std::max(1, f.side_rows * spread));
     f.k1 = std::min(f.side_rows, f.tile_rows / (f.R - 1));
-    const int64_t blocks = (int64_t)f.big_blocks + tile_blocks + 8LL * f.side_rows;
+    const int64_t blocks = (int64_t)f.direct_blocks + f.big_blocks + tile_blocks + 8LL * f.side_rows;
     RSK_CHECK(blocks < INT32_MAX, "fused grid too large");
-    using K = void (*)(Tile16Args, SideArgs, SideArgs, FuseMap);
-    static const K kerns[4] = {&car_fused16_kernel<false, false>, &car_fused16_kernel<false, true>,
-                               &car_fused16_kernel<true, false>, &car_fused16_kernel<true, true>};
-    const K kern = kerns[(score ? 2 : 0) + (off32 ? 1 : 0)];
+    using K = void (*)(Tile16Args, SideArgs, SideArgs, DirectArgs, FuseMap);
+    // [direct][score][off32]; direct cells only without scores
+    static const K kerns[6] = {&car_fused16_kernel<false, false, false>, &car_fused16_kernel<false, true, false>,
+                               &car_fused16_kernel<true, false, false>,  &car_fused16_kernel<true, true, false>,
+                               &car_fused16_kernel<false, false, true>,  &car_fused16_kernel<false, true, true>};
+    const K kern = kerns[(cells ? 4 : 0) + (score ? 2 : 0) + (off32 ? 1 : 0)];
     RSK_CHECK(lds <= 160 * 1024, "fused tile needs %zu B of LDS", lds);
     if (lds > 64 * 1024)
         RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds));
-    kern<<<dim3((unsigned)blocks), dim3(kTileThreads), lds, stream>>>(a, sa, ba, f);
+    kern<<<dim3((unsigned)blocks), dim3(kTileThreads), lds, stream>>>(a, sa, ba, da, f);
     RSK_HIP(hipGetLastError());
     return RSK_OK;
 }

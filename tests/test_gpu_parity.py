@@ -921,11 +921,11 @@ def test_car_direct_small_batches(ctx, S):
 @pytest.mark.parametrize("S,n_hubs", [(64, 6), (256, 40)])
 def test_car_big_rows_beyond_the_fused_grid(ctx, S, n_hubs):
     """Rows whose tables exceed the fused grid's LDS (degree 1,200-1,900 over
-    5,000 nodes) run on the side stream beside car_prep: as one workgroup per
-    (row, scenario) when they make few cells (S = 64, 6 rows: 384 cells, targets
-    only) and as on-the-fly pivot teams otherwise (S = 256, 40 rows: 10,240
-    cells; and whenever scores are requested).  Both against the oracle, every
-    cell, with and without scores."""
+    5,000 nodes): as one workgroup per (row, scenario) at the front of the fused
+    grid when they make few cells (S = 64, 6 rows: 384 cells, targets only) and
+    as on-the-fly pivot teams on the side stream beside car_prep otherwise
+    (S = 256, 40 rows: 10,240 cells; and whenever scores are requested).  Both
+    against the oracle, every cell, with and without scores."""
     from oracle import oracle as orc
     from rsk import api
     rng = np.random.default_rng(900 + S)
@@ -948,3 +948,53 @@ def test_car_big_rows_beyond_the_fused_grid(ctx, S, n_hubs):
         bad = np.nonzero(t != ot)[0]
         assert bad.size == 0, f"{label}: {bad.size} cells differ, first {bad[0]}: gpu {t[bad[0]]} oracle {ot[bad[0]]}"
     assert np.array_equal(sc, osc)
+
+
+def test_car_big_rows_direct_cells_edge_cases(ctx):
+    """The big rows as direct cells at the front of the fused grid (S = 64, 6
+    rows of 1,200-1,900 neighbours, targets only: no side launch) through every
+    branch of the rule (rescheduling.py:183-214), each in its own scenario:
+    every neighbour node hazardous (max score 0: the prep kernel's zero case
+    over 5 free nodes with equal remaining CPU: the lowest index), every node
+    hazardous (no candidate), all neighbours on one overloaded node (the single
+    best), neighbours split over two nodes with equal remaining CPU, fitting and
+    overloaded, every neighbour unassigned.  Every cell against the oracle."""
+    from oracle import oracle as orc
+    from rsk import api
+    rng = np.random.default_rng(4242)
+    P, N, S = 4000, 5000, 64
+    hubs = rng.integers(1200, 1900, 6).tolist()
+    rp, ci, a, cap, use, haz = _random_case(rng, P, N, S, max_deg=6, hub_deg=hubs, p_haz=0.05)
+    A, U, Hz = a.reshape(P, S), use.reshape(N, S), haz.reshape(N, S)
+    A[:] = rng.integers(0, N, P)[:, None]
+    nb = np.unique(np.concatenate([ci[rp[k]:rp[k + 1]] for k in range(6)]))
+    nb = nb[nb >= 6]   # the hubs' neighbours (rows 0-5 keep their own nodes)
+    free = np.setdiff1d(np.arange(N), A[:, 1])[:5]
+    Hz[:, 1] = 1
+    Hz[free, 1] = 0                                   # s = 1: zero case over the free nodes, tied
+    U[free, 1] = cap[free] - 100
+    Hz[:, 2] = 1                                      # s = 2: no candidate
+    A[nb, 3] = 7
+    Hz[7, 3] = 0
+    U[7, 3] = cap[7] + 5                              # s = 3: one overloaded best
+    for s, over in ((4, False), (5, True)):           # s = 4 / 5: a two-node tie, fitting / overloaded
+        A[nb, s] = np.where(np.arange(nb.size) % 2 == 0, 10, 11)
+        Hz[[10, 11], s] = 0
+        U[10, s] = cap[10] + (3 if over else -100)
+        U[11, s] = cap[11] + (3 if over else -100)
+    A[nb, 6] = -1                                     # s = 6: every neighbour unassigned
+    a, use, haz = A.reshape(-1).copy(), U.reshape(-1).copy(), Hz.reshape(-1).copy()
+    plan = api.CarPlan(rp, ci, ctx=ctx)
+    ctx.reset_profiling()
+    ctx.set_profiling(True)
+    t0, _ = plan.execute(a, S, cap, use, haz, N)
+    ctx.set_profiling(False)
+    assert ctx.kernel_time("car_side")[1] == 0 and ctx.kernel_time("car_tile")[1] == 1   # one fused launch
+    plan.close()
+    rp2, ci2 = _dedup_csr(rp, ci)
+    ot, _ = orc.car_sparse(rp2, ci2, a, S, cap, use, haz, N, threads=min(16, os.cpu_count() or 1))
+    bad = np.nonzero(t0 != ot)[0]
+    assert bad.size == 0, f"{bad.size} cells differ, first {bad[0]}: gpu {t0[bad[0]]} oracle {ot[bad[0]]}"
+    T = t0.reshape(P, S)
+    assert (T[:6, 2] == -2).all() and (T[:6, 3] == 7).all() and np.isin(T[:6, 4:6], (10, 11)).all()
+    assert (T[:6, 1] == free.min()).all()
