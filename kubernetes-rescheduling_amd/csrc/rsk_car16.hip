@@ -1177,8 +1177,8 @@ __global__ __launch_bounds__(kTileThreads, RSK_TILE16_WGS) void car_fused16_kern
         return;
     }
     const unsigned v0 = blockIdx.x - (unsigned)f.direct_blocks;
-    if (v0 < (unsigned)f.big_blocks) {
-        side16_block<4, 4, 16, kOff32, true>(ba, (int)v0);
+    if (v0 < (unsigned)f.big_blocks) {  // (XCD x: the x-th eighth of the chunk-major team items)
+        side16_block<4, 4, 16, kOff32, true>(ba, (int)((v0 & 7u) * ((unsigned)f.big_blocks >> 3) + (v0 >> 3)));
         return;
     }
     const unsigned v = v0 - (unsigned)f.big_blocks, row = v >> 3, x = v & 7u;
@@ -1193,8 +1193,8 @@ __global__ __launch_bounds__(kTileThreads, RSK_TILE16_WGS) void car_fused16_kern
         tile = K1 * (R - 1u) + (row - P1);
         if (row - P1 >= t_rem) side = K1 + (row - P1 - t_rem);
     }
-    if (side != 0xffffffffu) {
-        side16_block<4, 1, 16, kOff32, true>(sa, (int)(side * 8u + x));
+    if (side != 0xffffffffu) {  // XCD x: the x-th eighth of the chunk-major items (its tiles' chunks)
+        side16_block<4, 1, 16, kOff32, true>(sa, (int)(x * (unsigned)f.side_rows + side));
         return;
     }
     tile16_block<kScore, kOff32, true>(ta, (tile << 3) | x);
@@ -1241,6 +1241,8 @@ int launch_fused16(hipStream_t stream, const Tile16Args &a, const SideArgs &sa, 
     FuseMap f;
     f.direct_blocks = (int)(8 * ceil_div(cells, 8));  // (XCD alignment of the blocks after them)
     f.big_blocks = (int)(8 * ceil_div((int64_t)ba.n_rows * ba.nchunk, 8));
+    // (side_blocks = ceil(items / 4): XCD x takes blocks [x * side_rows, (x + 1) * side_rows), chunk-major
+    // items, so its side items read the code and assign columns of its own tiles' chunks)
     f.side_rows = (int)ceil_div(side_blocks, 8);
     f.tile_rows = (int)(tile_blocks / 8);
     // one side row every R rows over the first 1 / spread of the tile rows; the

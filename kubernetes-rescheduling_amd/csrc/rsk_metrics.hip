@@ -402,34 +402,45 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(const int *__restrict_
     if (mem) atomicAdd(&mem[o], (unsigned long long)pod_mem[p]);
 }
 
-// The segmented form (S >= 32).  What-if scenarios perturb a common base, so a
-// pod sits on the same node in most scenarios.  The pods are bucketed by a key
-// node (its node in scenario 0; a counting sort: count, scan,
-// scatter), and a wave walks a run of consecutive bucketed pods with lane =
-// scenario: a lane whose pod sits on the key node adds it to a register
-// accumulator, flushed once per key (three coalesced atomics per 64 scenarios
-// per node instead of per pod); a lane whose pod sits elsewhere adds it
-// directly.  The sums are integers, so the result is the atomic kernel's,
-// whatever the order.  podmonitor.py:104-121 (pods grouped by node),
-// nodemonitor.py:24-46 (per-node sums).
-// Grouping the pods by key node (its node in scenario 0, N when it has none) is
-// a two-level counting sort that keeps every counter in LDS: level 1 buckets
-// by key >> 6 (per-block histograms, a scan over them, a block-local scatter),
-// level 2 sorts each bucket by key & 63 in one workgroup.  (Global atomics
-// on the N key counters, one per pod for the count and again for the scatter,
-// took 55 + 68 us at 1M pods over 50k nodes.)
+// The bucketed form (S >= 32).  What-if scenarios perturb a common base, so a
+// pod sits on the same node in most scenarios.  The pods are grouped by the
+// 32-node bucket of a key node (its node in scenario 0, N when it has none)
+// with a counting sort whose counters stay in LDS (per-block histograms, a
+// scan over them, a block-local scatter of (pod, cpu, mem) records), and a
+// workgroup per (bucket, 64 scenarios) walks the bucket's pods with lane =
+// scenario: a cell whose node lies in the bucket adds the pod to the
+// workgroup's LDS sums of those 32 nodes; a cell elsewhere (a perturbed pod,
+// ~1 % of cells) adds it to the output directly.  The LDS sums are then added
+// to the output (zeroed by the launches before) with coalesced atomics.  The sums
+// are integers, so the result is the atomic kernel's whatever the order.
+// podmonitor.py:104-121 (pods grouped by node), nodemonitor.py:24-46 (per-node
+// sums).  Each assign row is read once, the pods' CPU / memory travel with
+// the records (no per-pod gathers), and no key-level sort is needed.
 constexpr int kNrChunk = 4096;     // pods per level-1 workgroup
 constexpr int kNrThreads = 1024;   // its threads (4 pods each: 16 waves per CU at 1M pods, not 4)
-constexpr int kNrSubBits = 6, kNrSub = 1 << kNrSubBits;  // level-2 sub-buckets
-constexpr int kNrMaxBuckets = 16384;  // key >> kNrSubBits buckets held in LDS (N < 2^20)
+constexpr int kNrBucketBits = 5, kNrBucketNodes = 1 << kNrBucketBits;  // nodes per bucket
+constexpr int kNrMaxBuckets = 16384;  // buckets held in LDS by the level-1 kernels (N < 2^19)
+constexpr int kNrSlice = 2048;     // a bucket workgroup's pods; larger buckets continue in the overflow launch
+static_assert((long long)kNrSlice << 32 < (1ll << 44), "packed LDS count + cpu sums");
 __device__ __forceinline__ int nr_key(const int *__restrict__ assign, int p, int S, int N) {
     const int a = assign[(size_t)p * S];
     return (unsigned)a < (unsigned)N ? a : N;
 }
 
-// level 1a: keys (kept in pkey) and this block's bucket counts -> bh[j * nblk + b]
+// The outputs are zeroed by the launches ahead of the bucket kernel (which
+// adds into them), one array each, beside their own latency-bound work: this
+// block's slice of n int4 words at z.
+__device__ __forceinline__ void nr_zero_slice(int4 *__restrict__ z, size_t n) {
+    const size_t per = (n + gridDim.x - 1) / gridDim.x;
+    const size_t i0 = per * blockIdx.x, i1 = min(n, i0 + per);
+    for (size_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) z[i] = make_int4(0, 0, 0, 0);
+}
+
+// level 1a: keys (kept in pkey) and this block's bucket counts -> bh[j * nblk + b];
+// the overflow count reset
 __global__ __launch_bounds__(kNrThreads) void nr_hist_kernel(const int *__restrict__ assign, int P, int S, int N, int nbk,
-                                                      int *__restrict__ pkey, int *__restrict__ bh) {
+                                                      int *__restrict__ pkey, int *__restrict__ bh,
+                                                      int *__restrict__ ovf) {
     extern __shared__ int hist[];
     for (int j = (int)threadIdx.x; j < nbk; j += kNrThreads) hist[j] = 0;
     __syncthreads();
@@ -441,69 +452,47 @@ __global__ __launch_bounds__(kNrThreads) void nr_hist_kernel(const int *__restri
         const int p = min(p0 + u * kNrThreads + (int)threadIdx.x, P - 1);
         k[u] = nr_key(assign, p, S, N);
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0) ovf[0] = 0;
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
         const int p = p0 + u * kNrThreads + (int)threadIdx.x;
         if (p < p1) {
             pkey[p] = k[u];
-            atomicAdd(&hist[k[u] >> kNrSubBits], 1);
+            atomicAdd(&hist[k[u] >> kNrBucketBits], 1);
         }
     }
     __syncthreads();
     for (int j = (int)threadIdx.x; j < nbk; j += kNrThreads) bh[(size_t)j * gridDim.x + blockIdx.x] = hist[j];
 }
 
-// level 1b: each block's pods to its slice of every bucket (bh scanned: offsets)
+// level 1b: each block's pods to its slice of every bucket (bh scanned:
+// offsets), as (pod, cpu, mem lo, mem hi) records
 __global__ __launch_bounds__(kNrThreads) void nr_part_kernel(const int *__restrict__ pkey, int P, int nbk,
-                                                      const int *__restrict__ boff, int *__restrict__ perm1,
-                                                      int *__restrict__ keys1) {
+                                                      const int *__restrict__ boff, const int *__restrict__ pod_cpu,
+                                                      const long long *__restrict__ pod_mem, int4 *__restrict__ rec,
+                                                      int4 *__restrict__ z, size_t nz) {
     extern __shared__ int cur[];
+    nr_zero_slice(z, nz);
     for (int j = (int)threadIdx.x; j < nbk; j += kNrThreads) cur[j] = boff[(size_t)j * gridDim.x + blockIdx.x];
     __syncthreads();
     const int p0 = (int)blockIdx.x * kNrChunk, p1 = min(P, p0 + kNrChunk);
     constexpr int kU = kNrChunk / kNrThreads;
-    int k[kU];
+    int k[kU], c[kU];
+    long long m[kU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) k[u] = pkey[min(p0 + u * kNrThreads + (int)threadIdx.x, P - 1)];
+    for (int u = 0; u < kU; ++u) {
+        const int p = min(p0 + u * kNrThreads + (int)threadIdx.x, P - 1);
+        k[u] = pkey[p];
+        c[u] = pod_cpu[p];
+        m[u] = pod_mem ? pod_mem[p] : 0;
+    }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
         const int p = p0 + u * kNrThreads + (int)threadIdx.x;
         if (p < p1) {
-            const int pos = atomicAdd(&cur[k[u] >> kNrSubBits], 1);
-            perm1[pos] = p;
-            keys1[pos] = k[u];
+            const int pos = atomicAdd(&cur[k[u] >> kNrBucketBits], 1);
+            rec[pos] = make_int4(p, c[u], (int)(unsigned)(unsigned long long)m[u], (int)(m[u] >> 32));
         }
-    }
-}
-
-// level 2: bucket j (one workgroup, any size) sorted by key & (kNrSub - 1)
-__global__ __launch_bounds__(256) void nr_sub_kernel(const int *__restrict__ perm1, const int *__restrict__ keys1,
-                                                     const int *__restrict__ boff, int nblk1, int nbk, int P,
-                                                     int *__restrict__ perm, int *__restrict__ keys) {
-    __shared__ int cnt[kNrSub];
-    const int j = (int)blockIdx.x, t = (int)threadIdx.x;
-    const int lo = boff[(size_t)j * nblk1], hi = j + 1 < nbk ? boff[(size_t)(j + 1) * nblk1] : P;
-    if (t < kNrSub) cnt[t] = 0;
-    __syncthreads();
-    for (int i = lo + t; i < hi; i += 256) atomicAdd(&cnt[keys1[i] & (kNrSub - 1)], 1);
-    __syncthreads();
-    if (t < 64) {  // one wave scans the kNrSub (<= 64) counts
-        static_assert(kNrSub <= 64, "one wave scans the sub-buckets");
-        const int c = t < kNrSub ? cnt[t] : 0;
-        int x = c;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int y = __shfl_up(x, d, 64);
-            x += t >= d ? y : 0;
-        }
-        if (t < kNrSub) cnt[t] = lo + x - c;  // the sub-bucket's first slot, then its cursor
-    }
-    __syncthreads();
-    for (int i = lo + t; i < hi; i += 256) {
-        const int k = keys1[i];
-        const int pos = atomicAdd(&cnt[k & (kNrSub - 1)], 1);
-        perm[pos] = perm1[i];
-        keys[pos] = k;
     }
 }
 
@@ -524,7 +513,8 @@ __device__ __forceinline__ int nr_block_incl_scan(int v, int *lds) {
 }
 
 __global__ __launch_bounds__(kNrScanB) void nr_blocksum_kernel(const int *__restrict__ off, int n,
-                                                               int *__restrict__ bsum) {
+                                                               int *__restrict__ bsum, int4 *__restrict__ z, size_t nz) {
+    nr_zero_slice(z, nz);
     __shared__ int red[kNrScanB / 64];
     const int i = (int)blockIdx.x * kNrScanB + (int)threadIdx.x;
     int v = i < n ? off[i] : 0;
@@ -540,7 +530,9 @@ __global__ __launch_bounds__(kNrScanB) void nr_blocksum_kernel(const int *__rest
 }
 
 __global__ __launch_bounds__(kNrScanB) void nr_blockscan_kernel(int *__restrict__ off, int n,
-                                                                const int *__restrict__ bsum) {
+                                                                const int *__restrict__ bsum, int4 *__restrict__ z,
+                                                                size_t nz) {
+    nr_zero_slice(z, nz);
     __shared__ int lds[kNrScanB];
     __shared__ int base;
     if (threadIdx.x < 64) {  // the blocks before this one
@@ -556,82 +548,107 @@ __global__ __launch_bounds__(kNrScanB) void nr_blockscan_kernel(int *__restrict_
     if (i < n) off[i] = base + incl - v;
 }
 
-constexpr int kNrRun = 256;  // bucketed pods per wave (64: 0.219 ms, 256: 0.212 at 1M x 50k x 64)
-__global__ __launch_bounds__(256) void node_reduce_seg_kernel(const int *__restrict__ assign, int P, int S,
-                                                              const int *__restrict__ pod_cpu,
-                                                              const long long *__restrict__ pod_mem, int N,
-                                                              const int *__restrict__ perm,
-                                                              const int *__restrict__ keys, int runs,
-                                                              int *__restrict__ cnt,
-                                                              unsigned long long *__restrict__ cpu,
-                                                              unsigned long long *__restrict__ mem, int ablate,
-                                                              int run_len) {
+// A bucket's pods, one workgroup per (work item, 64-scenario chunk).  Work
+// item = bucket b's pods [b0 + k * kNrSlice, ...) up to kNrSlice of them: the
+// first launch takes k = 0 of every bucket and lists the k >= 1 items of the
+// buckets beyond kNrSlice pods (ovf: count, then (b, k) pairs), which the
+// overflow launch takes (none for uniform clusters: its workgroups exit).
+// LDS: the 32 nodes x 64 scenarios' count + cpu (/ mem) sums, 32 KB: 4
+// workgroups of 8 waves per CU.  Each wave walks its eighth of the item's pods
+// 64 records at a time (one coalesced 16-B load per lane, the next 64
+// prefetched), the pod's fields broadcast from the lane holding them, 16 assign
+// rows in flight: one memory trip per batch.
+constexpr int kNrBucketThreads = 512;
+template <bool kMem>
+__global__ __launch_bounds__(kNrBucketThreads, 4) void nr_bucket_kernel(
+    const int *__restrict__ assign, int P, int S, int N, const int4 *__restrict__ rec, const int *__restrict__ boff,
+    int nblk1, int nbk, int nchunk, int *__restrict__ cnt, unsigned long long *__restrict__ cpu,
+    unsigned long long *__restrict__ mem, int *__restrict__ ovf, int overflow, int ablate) {
 #ifndef RSK_ABLATIONS
-    ablate = 0;  // profiling switches exist only in ablation builds
+    ablate = 0;  // profiling switches (wrong results) exist only in ablation builds
 #endif
-    const int w = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
-    const int chunk = w / runs, run = w - chunk * runs;
-    const int s = chunk * 64 + (int)(threadIdx.x & 63);
-    if (chunk * 64 >= S) return;
+    constexpr int kE = kNrBucketNodes * 64, kW = kNrBucketThreads / 64;
+    // (count << 44) + the sum of (cpu + 2^31): one u64 atomic for both (a
+    // workgroup adds at most kNrSlice pods: the sum stays below 2^43)
+    __shared__ unsigned long long lcc[kE];
+    __shared__ unsigned long long lmem[kMem ? kE : 1];
+    const int t = (int)threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int item = (int)blockIdx.x / nchunk, chunk = (int)blockIdx.x - item * nchunk;
+    int b, k = 0;
+    if (!overflow) {
+        b = item;
+    } else {
+        if (item >= __builtin_nontemporal_load(&ovf[0])) return;
+        b = ovf[1 + 2 * item];
+        k = ovf[2 + 2 * item];
+    }
+    const int b0 = boff[(size_t)b * nblk1], b1 = b + 1 < nbk ? boff[(size_t)(b + 1) * nblk1] : P;
+    if (!overflow && chunk == 0 && t == 0 && b1 - b0 > kNrSlice) {  // the bucket's other slices
+        const int ns = (b1 - b0 + kNrSlice - 1) / kNrSlice - 1;
+        const int at = atomicAdd(&ovf[0], ns);
+        for (int j = 0; j < ns; ++j) {
+            ovf[1 + 2 * (at + j)] = b;
+            ovf[2 + 2 * (at + j)] = j + 1;
+        }
+    }
+    const int lo = b0 + k * kNrSlice, hi = min(b1, lo + kNrSlice);
+    if (lo >= hi) return;
+    for (int e = t; e < kE; e += kNrBucketThreads) {
+        lcc[e] = 0ull;
+        if (kMem) lmem[e] = 0ull;
+    }
+    __syncthreads();
+    const int s = chunk * 64 + lane, n0 = b * kNrBucketNodes;
     const bool live = s < S;
-    const int j0 = run * run_len, j1 = min(P, j0 + run_len);
-    const cint_ptr cperm = const_ptr(perm), ckeys = const_ptr(keys), ccpu = const_ptr(pod_cpu);
-    int rk = -1, rc = 0;
-    long long rcpu = 0, rmem = 0;
-    auto flush = [&]() {
-        if (live && rk >= 0 && rk < N && rc > 0 && !(ablate & 2)) {  // ablate 2: no run flushes
-            const size_t o = (size_t)rk * S + s;
-            atomicAdd(&cnt[o], rc);
-            atomicAdd(&cpu[o], (unsigned long long)rcpu);
-            if (mem) atomicAdd(&mem[o], (unsigned long long)rmem);
-        }
-        rc = 0;
-        rcpu = rmem = 0;
-    };
-    // Batches of 8 pods, every load of a batch issued before its first use:
-    // the assign rows, and the pods' CPU / memory (scattered pod ids: each a
-    // cache miss that, loaded per pod behind the previous pod's atomics,
-    // serialised the run).  (Fetching the next batch's ids during a batch, or
-    // batches of 16: no gain, 0.238 / 0.239 / 0.269 ms against 0.238.)
-    constexpr int kB = 8;
-    for (int j = j0; j < j1; j += kB) {
-        int a[kB], pp[kB], kk[kB], cc[kB];
-        long long mm[kB];
+    const int q = (hi - lo + kW - 1) / kW, j0 = lo + wv * q, j1 = min(hi, j0 + q);
+    int4 rn = j0 < j1 ? rec[min(j0 + lane, j1 - 1)] : make_int4(0, 0, 0, 0);
+    for (int c0 = j0; c0 < j1; c0 += 64) {
+        const int4 r = rn;
+        if (c0 + 64 < j1) rn = rec[min(c0 + 64 + lane, j1 - 1)];  // the next 64 records, in flight meanwhile
+        const int cn = min(64, j1 - c0);
+        constexpr int kB = 16;
+        for (int ub = 0; ub < cn; ub += kB) {
+            int a[kB];
 #pragma unroll
-        for (int u = 0; u < kB; ++u) {
-            const int jj = min(j + u, j1 - 1);
-            pp[u] = cperm[jj];
-            kk[u] = ckeys[jj];
-        }
-#pragma unroll
-        for (int u = 0; u < kB; ++u) {
-            a[u] = live ? __builtin_nontemporal_load(&assign[(size_t)pp[u] * S + s]) : -1;
-            cc[u] = ccpu[pp[u]];
-            mm[u] = mem ? pod_mem[pp[u]] : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < kB; ++u) {
-            if (j + u >= j1) break;
-            const int k = kk[u];
-            if (k != rk) {  // wave-uniform: a new key node
-                flush();
-                rk = k;
+            for (int u = 0; u < kB; ++u) {
+                const int p = __builtin_amdgcn_readlane(r.x, min(ub + u, cn - 1));
+                a[u] = live ? __builtin_nontemporal_load(&assign[(size_t)p * S + s]) : -1;
             }
-            const int c = cc[u];
-            const long long m = mm[u];
-            if (a[u] == k) {
-                ++rc;
-                rcpu += c;
-                rmem += m;
-            } else if ((unsigned)a[u] < (unsigned)N && !(ablate & 1)) {  // ablate 1: no off-key atomics
-                const size_t o = (size_t)a[u] * S + s;
-                atomicAdd(&cnt[o], 1);
-                atomicAdd(&cpu[o], (unsigned long long)(long long)c);
-                if (mem) atomicAdd(&mem[o], (unsigned long long)m);
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                if (ub + u >= cn) break;
+                const int c = __builtin_amdgcn_readlane(r.y, ub + u);
+                const long long m = kMem ? (long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane(r.w, ub + u)
+                                                        << 32) |
+                                                       (unsigned)__builtin_amdgcn_readlane(r.z, ub + u))
+                                         : 0;
+                const int rel = a[u] - n0;
+                if ((unsigned)rel < (unsigned)kNrBucketNodes) {
+                    if (a[u] < N && !(ablate & 2)) {  // (the key-N bucket's range may pass N; ablate 2: no LDS sums)
+                        const int e = rel * 64 + lane;
+                        atomicAdd(&lcc[e], (1ull << 44) + (unsigned long long)((long long)c + 0x80000000ll));
+                        if (kMem) atomicAdd(&lmem[e], (unsigned long long)m);
+                    }
+                } else if ((unsigned)a[u] < (unsigned)N && !(ablate & 1)) {  // off the bucket: to the output (ablate 1: not)
+                    const size_t o = (size_t)a[u] * S + s;
+                    atomicAdd(&cnt[o], 1);
+                    atomicAdd(&cpu[o], (unsigned long long)(long long)c);
+                    if (kMem) atomicAdd(&mem[o], (unsigned long long)m);
+                }
             }
         }
     }
-    flush();
+    __syncthreads();
+    for (int e = t; e < kE; e += kNrBucketThreads) {
+        const unsigned long long w = lcc[e];
+        const unsigned c = (unsigned)(w >> 44);
+        const int n = n0 + (e >> 6), ss = chunk * 64 + (e & 63);
+        if (c == 0u || n >= N || ss >= S || (ablate & 4)) continue;  // ablate 4: no flush
+        const size_t o = (size_t)n * S + ss;
+        atomicAdd(&cnt[o], (int)c);
+        atomicAdd(&cpu[o], (unsigned long long)((long long)(w & ((1ull << 44) - 1)) - ((long long)c << 31)));
+        if (kMem) atomicAdd(&mem[o], lmem[e]);
+    }
 }
 
 // get_resource_usage.py:37: int(round(u / c * 100)) — IEEE fp64 divide, then an
@@ -1214,35 +1231,39 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
     RSK_TRY(stage_out(ctx, 3, pod_count, NS * 4, dev, reinterpret_cast<void **>(&d_cnt)));
     RSK_TRY(stage_out(ctx, 4, cpu_sum, NS * 8, dev, reinterpret_cast<void **>(&d_cs)));
     if (mem_sum) RSK_TRY(stage_out(ctx, 5, mem_sum, NS * 8, dev, reinterpret_cast<void **>(&d_ms)));
-    const int nbk = (N >> kNrSubBits) + 1;  // key >> kNrSubBits buckets (keys 0..N)
-    if (PS && S >= 32 && nbk <= kNrMaxBuckets) {  // segmented: group the pods by key node, per-key register sums
-        constexpr int run_len = kNrRun;  // pods per wave
-        const int runs = (int)ceil_div(P, run_len);
-        const int64_t waves = (int64_t)runs * ceil_div(S, 64);
-        RSK_CHECK(waves < (int64_t)INT32_MAX - 4, "node_reduce grid too large");
+    const int nbk = (N >> kNrBucketBits) + 1;  // key >> kNrBucketBits buckets (keys 0..N)
+    const bool z16 = (uintptr_t)d_cnt % 16 == 0 && (uintptr_t)d_cs % 16 == 0 && (uintptr_t)d_ms % 16 == 0 &&
+                     NS % 4 == 0;  // the outputs zeroed in int4 words by the first launch
+    if (PS && S >= 32 && nbk <= kNrMaxBuckets && z16) {  // bucketed: LDS sums per (32 nodes, 64 scenarios)
+        const int nchunk = (int)ceil_div(S, 64);
         const int nblk1 = (int)ceil_div(P, kNrChunk);
         const int64_t nbh = (int64_t)nbk * nblk1;
-        RSK_CHECK(nbh < INT32_MAX / 2, "node_reduce grouping too large");
+        const int64_t ovf_cap = ceil_div(P, kNrSlice) + 1;
+        RSK_CHECK(nbh < INT32_MAX / 2 && (int64_t)nbk * nchunk < INT32_MAX && ovf_cap * nchunk < INT32_MAX,
+                  "node_reduce grouping too large");
         const int nsb = (int)ceil_div(nbh, kNrScanB);
-        RSK_TRY(ctx->work[0].reserve((size_t)P * 20));
-        RSK_TRY(ctx->work[1].reserve(((size_t)nbh + nsb) * 4));
-        int *perm = ctx->work[0].as<int>(), *keys = perm + P, *pkey = keys + P, *perm1 = pkey + P, *keys1 = perm1 + P;
-        int *bh = ctx->work[1].as<int>(), *bsum = bh + nbh;
+        RSK_TRY(ctx->work[0].reserve((size_t)P * 20 + 16));  // keys, then the records
+        RSK_TRY(ctx->work[1].reserve(((size_t)nbh + nsb + 1 + 2 * (size_t)ovf_cap) * 4));
+        int *pkey = ctx->work[0].as<int>();
+        int4 *rec = reinterpret_cast<int4 *>(ctx->work[0].as<char>() + (((size_t)P * 4 + 15) & ~(size_t)15));
+        int *bh = ctx->work[1].as<int>(), *bsum = bh + nbh, *ovf = bsum + nsb;
         ScopedTimer tm(ctx, "node_reduce");
-        RSK_HIP(hipMemsetAsync(d_cnt, 0, NS * 4, ctx->stream));
-        RSK_HIP(hipMemsetAsync(d_cs, 0, NS * 8, ctx->stream));
-        if (d_ms) RSK_HIP(hipMemsetAsync(d_ms, 0, NS * 8, ctx->stream));
         const size_t hl = (size_t)nbk * 4;
+        nr_hist_kernel<<<nblk1, kNrThreads, hl, ctx->stream>>>(d_assign, P, S, N, nbk, pkey, bh, ovf);
+        nr_blocksum_kernel<<<nsb, kNrScanB, 0, ctx->stream>>>(bh, (int)nbh, bsum, reinterpret_cast<int4 *>(d_cnt),
+                                                               NS / 4);
+        nr_blockscan_kernel<<<nsb, kNrScanB, 0, ctx->stream>>>(bh, (int)nbh, bsum, reinterpret_cast<int4 *>(d_cs),
+                                                                NS / 2);
+        nr_part_kernel<<<nblk1, kNrThreads, hl, ctx->stream>>>(pkey, P, nbk, bh, d_cpu,
+                                                                reinterpret_cast<const long long *>(d_mem), rec,
+                                                                reinterpret_cast<int4 *>(d_ms), d_ms ? NS / 2 : 0);
         static const int nr_ablate = RSK_ABLATION(RSK_ABLATE_NR);
-        nr_hist_kernel<<<nblk1, kNrThreads, hl, ctx->stream>>>(d_assign, P, S, N, nbk, pkey, bh);
-        nr_blocksum_kernel<<<nsb, kNrScanB, 0, ctx->stream>>>(bh, (int)nbh, bsum);
-        nr_blockscan_kernel<<<nsb, kNrScanB, 0, ctx->stream>>>(bh, (int)nbh, bsum);
-        nr_part_kernel<<<nblk1, kNrThreads, hl, ctx->stream>>>(pkey, P, nbk, bh, perm1, keys1);
-        nr_sub_kernel<<<nbk, 256, 0, ctx->stream>>>(perm1, keys1, bh, nblk1, nbk, P, perm, keys);
-        node_reduce_seg_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, ctx->stream>>>(
-            d_assign, P, S, d_cpu, reinterpret_cast<const long long *>(d_mem), N, perm, keys, runs, d_cnt,
-            reinterpret_cast<unsigned long long *>(d_cs), reinterpret_cast<unsigned long long *>(d_ms), nr_ablate,
-            run_len);
+        auto *bk = d_ms ? &nr_bucket_kernel<true> : &nr_bucket_kernel<false>;
+        auto *ucs = reinterpret_cast<unsigned long long *>(d_cs), *ums = reinterpret_cast<unsigned long long *>(d_ms);
+        bk<<<(unsigned)(nbk * nchunk), kNrBucketThreads, 0, ctx->stream>>>(d_assign, P, S, N, rec, bh, nblk1, nbk,
+                                                                          nchunk, d_cnt, ucs, ums, ovf, 0, nr_ablate);
+        bk<<<(unsigned)(ovf_cap * nchunk), kNrBucketThreads, 0, ctx->stream>>>(d_assign, P, S, N, rec, bh, nblk1, nbk,
+                                                                              nchunk, d_cnt, ucs, ums, ovf, 1, nr_ablate);
         RSK_HIP(hipGetLastError());
     } else {
         ScopedTimer tm(ctx, "node_reduce");

@@ -1,13 +1,14 @@
 #!/bin/bash
-# Kernel trace of tools/nrbench.py (node_reduce at 1M x 50k x 64) for knob
-# variants of the knobs library.  usage: tools/gpu_nrprof.sh OUTDIR VAR=v ...
+# Kernel trace of tools/nrbench.py (node_reduce at 1M x 50k x 64), once per
+# environment variant (none given: once).  RSK_LIB picks the library (default
+# the product librsk.so).  usage: tools/gpu_nrprof.sh OUTDIR [VAR=v,VAR2=w ...]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 out=${1:-gpurun_out/nrprof}; shift
 mkdir -p "$out"
 export TMPDIR=/tmp
-export RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so
+export RSK_LIB=${RSK_LIB:-kubernetes-rescheduling_amd/rsk/librsk.so}
 k=0
-for v in "$@"; do
+for v in "${@:-RSK_NRPROF=base}"; do
   k=$((k+1))
   export ${v//,/ }
   timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d "$out/p$k" -o run -f csv -- python3 tools/nrbench.py > "$out/p$k.log" 2>&1

@@ -1,6 +1,5 @@
 """rsk_node_reduce at 1M pods x 50k nodes x 64 scenarios (bench.py's kernel-3
-case) with librsk's timer: for A/B of library variants (RSK_LIB; an ablation
-build takes RSK_ABLATE_NR here — bench.py refuses those).  One JSON line."""
+case) with librsk's timer: for A/B of library variants (RSK_LIB).  One JSON line."""
 import json
 import os
 import sys
