@@ -402,252 +402,431 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(const int *__restrict_
     if (mem) atomicAdd(&mem[o], (unsigned long long)pod_mem[p]);
 }
 
-// The bucketed form (S >= 32).  What-if scenarios perturb a common base, so a
-// pod sits on the same node in most scenarios.  The pods are grouped by the
-// 32-node bucket of a key node (its node in scenario 0, N when it has none)
-// with a counting sort whose counters stay in LDS (per-block histograms, a
-// scan over them, a block-local scatter of (pod, cpu, mem) records), and a
-// workgroup per (bucket, 64 scenarios) walks the bucket's pods with lane =
-// scenario: a cell whose node lies in the bucket adds the pod to the
-// workgroup's LDS sums of those 32 nodes; a cell elsewhere (a perturbed pod,
-// ~1 % of cells) adds it to the output directly.  The LDS sums are then added
-// to the output (zeroed by the launches before) with coalesced atomics.  The sums
-// are integers, so the result is the atomic kernel's whatever the order.
+// The deviation form (S >= 32).  What-if scenarios perturb a common base, so a
+// pod sits on one node in most scenarios: its key node k(p), the majority of
+// its nodes in scenarios 0, 21 and 42 (scenario 0's when S < 43), or N when
+// that is not a node.  The integer sums split exactly into
+//   out[n, s] = base[n] + dev[n, s]
+//   base[n]   = the sum over the pods with k(p) = n of (1, cpu, mem), every s
+//   dev[n, s] = the sum over the cells a(p, s) = n != k(p) of (1, cpu, mem)
+//             - the sum over the cells k(p) = n != a(p, s) of (1, cpu, mem)
+// so only the deviation cells (~2 % of the bench batches' cells) carry a
+// per-scenario term.  Five launches, no zeroing pass and (unless a block's
+// deviations overflow) no global atomics:
+//  1 nr_scan: every assign row read once, coalesced (lane = scenario, the next
+//    16 rows in flight while a batch is examined): the keys (pkey), and per
+//    block of kNrPods pods the count of its keys per 32-node bucket and of its
+//    deviation records per (bucket, 64-scenario chunk) bin (a + at the cell's
+//    node, a - at the key node), one entry per deviation cell (int2: node or
+//    kNrNoNode | (p - p0) << 20, s) into its wave's eighth of the block's
+//    region of ecap = cells / 8 entries;
+//  2 nr_colscan: per counter (bucket or bin) the exclusive scan of its
+//    per-block counts, laid out [counter][block], and its total;
+//  3 nr_place: the counters' bases (a scan of the totals in the workgroup);
+//    the block's pods to their key bucket's slice as (node & 31, cpu, mem)
+//    records, each entry's + and - to their bins' slices as (node & 31 |
+//    minus << 5 | (s & 63) << 6, cpu, mem) records (key / cpu / mem from LDS);
+//  4 nr_sum: a workgroup per bin sums the bucket's pod records (base, 32
+//    nodes) and the bin's entries (dev, 32 nodes x 64 scenarios) in LDS and
+//    stores out = base + dev, 64 scenarios per coalesced store;
+//  5 nr_spill: a block whose entries overflowed its region listed none; its
+//    deviation cells are added here, after the stores, by global atomics.
 // podmonitor.py:104-121 (pods grouped by node), nodemonitor.py:24-46 (per-node
-// sums).  Each assign row is read once, the pods' CPU / memory travel with
-// the records (no per-pod gathers), and no key-level sort is needed.
-constexpr int kNrChunk = 4096;     // pods per level-1 workgroup
-constexpr int kNrThreads = 1024;   // its threads (4 pods each: 16 waves per CU at 1M pods, not 4)
+// sums).  Integer sums: the result does not depend on any order.
+constexpr int kNrPods = 2048;     // pods per block of the scan / place / spill launches
+constexpr int kNrThreads = 512;   // their threads: 8 waves of 256 pods
+constexpr int kNrBatch = 16;      // assign rows per batch (two batches in flight per wave)
 constexpr int kNrBucketBits = 5, kNrBucketNodes = 1 << kNrBucketBits;  // nodes per bucket
-constexpr int kNrMaxBuckets = 16384;  // buckets held in LDS by the level-1 kernels (N < 2^19)
-constexpr int kNrSlice = 2048;     // a bucket workgroup's pods; larger buckets continue in the overflow launch
-static_assert((long long)kNrSlice << 32 < (1ll << 44), "packed LDS count + cpu sums");
-__device__ __forceinline__ int nr_key(const int *__restrict__ assign, int p, int S, int N) {
-    const int a = assign[(size_t)p * S];
-    return (unsigned)a < (unsigned)N ? a : N;
+constexpr int kNrMaxCounters = 16384;  // buckets + bins: a block's counters in LDS (N < 2^19)
+constexpr int kNrEntDiv = 8;           // a block's entry region: its cells / 8 entries
+constexpr int kNrMaxS = 65536;         // (a block's entry count stays below 2^32)
+constexpr int kNrNoNode = 0x7ffff;     // an entry's node field when the cell is not on a node
+
+__device__ __forceinline__ int nr_rank(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
-// The outputs are zeroed by the launches ahead of the bucket kernel (which
-// adds into them), one array each, beside their own latency-bound work: this
-// block's slice of n int4 words at z.
-__device__ __forceinline__ void nr_zero_slice(int4 *__restrict__ z, size_t n) {
-    const size_t per = (n + gridDim.x - 1) / gridDim.x;
-    const size_t i0 = per * blockIdx.x, i1 = min(n, i0 + per);
-    for (size_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) z[i] = make_int4(0, 0, 0, 0);
+// byte offset of assign[i * S + s] (32-bit arithmetic when P * S * 4 < 2^32:
+// the saddr form of the load)
+template <bool kOff32>
+__device__ __forceinline__ size_t nr_off(unsigned i, unsigned S, unsigned s) {
+    if (kOff32) return (size_t)((i * S + s) << 2);
+    return ((size_t)i * S + s) << 2;
 }
 
-// level 1a: keys (kept in pkey) and this block's bucket counts -> bh[j * nblk + b];
-// the overflow count reset
-__global__ __launch_bounds__(kNrThreads) void nr_hist_kernel(const int *__restrict__ assign, int P, int S, int N, int nbk,
-                                                      int *__restrict__ pkey, int *__restrict__ bh,
-                                                      int *__restrict__ ovf) {
-    extern __shared__ int hist[];
-    for (int j = (int)threadIdx.x; j < nbk; j += kNrThreads) hist[j] = 0;
+// The scan / place / spill launches map workgroup i to block (i & 7) * per +
+// (i >> 3), per = ceil(nblk / 8): an XCD runs a run of consecutive blocks, so
+// the neighbouring slices they write (counters, records) meet in its L2.
+__device__ __forceinline__ int nr_block(int nblk) {
+    const int per = (nblk + 7) >> 3;
+    return (int)(blockIdx.x & 7u) * per + (int)(blockIdx.x >> 3);
+}
+
+// launch 1: a wave walks its pods' (batch of 16, chunk) units, the next unit's
+// 16 rows (and the 16 pods' scenario 0 / 21 / 42 words: their keys, one per
+// lane) loaded while one is examined.  A unit's test is one compare and a
+// ballot; only units with deviations (~half of the bench's rows) write
+// entries, into the wave's own eighth of the block's region.  Counters ->
+// bh[j * nblk + b] (the entry bins zeroed when a wave overflowed), the waves'
+// entry counts (-1: the block overflowed) -> ecount[b * 8 + w].
+template <bool kOff32, bool kMaj>
+__global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restrict__ assign, int P, int S, int N,
+                                                             int nbk, int nchunk, int nblk, size_t ecap,
+                                                             int *__restrict__ pkey, int *__restrict__ bh,
+                                                             int2 *__restrict__ ent, int *__restrict__ ecount) {
+    extern __shared__ int lh[];  // [nbk] key buckets, then [nbk * nchunk] entry bins
+    __shared__ int over;
+    const int b = nr_block(nblk);
+    if (b >= nblk) return;
+    const int t = (int)threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int nh = nbk * (1 + nchunk);
+    for (int j = t; j < nh; j += kNrThreads) lh[j] = 0;
+    if (t == 0) over = 0;
     __syncthreads();
-    const int p0 = (int)blockIdx.x * kNrChunk, p1 = min(P, p0 + kNrChunk);
-    constexpr int kU = kNrChunk / kNrThreads;  // the thread's pods: their (strided) key loads issued together
-    int k[kU];
+    constexpr int kPW = kNrPods / (kNrThreads / 64), kW = kNrThreads / 64;
+    const int p0 = b * kNrPods, q0 = p0 + wv * kPW, q1 = min(P, q0 + kPW);
+    const int nv = q1 > q0 ? (q1 - q0 + kNrBatch - 1) / kNrBatch * nchunk : 0;  // the wave's units
+    const char *__restrict__ asg = reinterpret_cast<const char *>(assign);
+    const size_t wcap = ecap / kW;
+    int2 *__restrict__ E = ent + (size_t)b * ecap + (size_t)wv * wcap;
+    unsigned wpos = 0u;
+    bool wover = false;
+    auto load = [&](int v, int (&r)[kNrBatch], int (&kr)[3]) {  // clamped: always valid addresses
+        v = min(v, nv - 1);
+        const int bt = v / nchunk, c = v - bt * nchunk, pb = q0 + bt * kNrBatch, last = min(q1, pb + kNrBatch) - 1;
+        const unsigned sc = (unsigned)min(c * 64 + lane, S - 1);
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-        const int p = min(p0 + u * kNrThreads + (int)threadIdx.x, P - 1);
-        k[u] = nr_key(assign, p, S, N);
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) ovf[0] = 0;
+        for (int u = 0; u < kNrBatch; ++u)
+            r[u] = __builtin_nontemporal_load(
+                reinterpret_cast<const int *>(asg + nr_off<kOff32>((unsigned)min(pb + u, last), (unsigned)S, sc)));
+        const unsigned pk = (unsigned)min(pb + (lane & (kNrBatch - 1)), last);
+        kr[0] = *reinterpret_cast<const int *>(asg + nr_off<kOff32>(pk, (unsigned)S, 0u));
+        if (kMaj) {
+            kr[1] = *reinterpret_cast<const int *>(asg + nr_off<kOff32>(pk, (unsigned)S, 21u));
+            kr[2] = *reinterpret_cast<const int *>(asg + nr_off<kOff32>(pk, (unsigned)S, 42u));
+        }
+    };
+    auto examine = [&](int v, const int (&r)[kNrBatch], const int (&kr)[3]) {
+        const int bt = v / nchunk, c = v - bt * nchunk, pb = q0 + bt * kNrBatch, nb = min(kNrBatch, q1 - pb);
+        int kv = kr[0];  // lane u < 16: pod pb + u's key
+        if (kMaj) kv = (kv == kr[1] || kv == kr[2]) ? kv : (kr[1] == kr[2] ? kr[1] : kv);
+        kv = (unsigned)kv < (unsigned)N ? kv : N;
+        if (c == 0 && lane < nb) {
+            pkey[pb + lane] = kv;
+            if (kv < N) atomicAdd(&lh[kv >> kNrBucketBits], 1);
+        }
+        const int s = c * 64 + lane;
+        const bool live = s < S;
+        // bit u of dev: the lane's cell of unit u is off the pod's key node; D:
+        // the units with any such lane (an OR over the wave)
+        unsigned dev = 0u;
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-        const int p = p0 + u * kNrThreads + (int)threadIdx.x;
-        if (p < p1) {
-            pkey[p] = k[u];
-            atomicAdd(&hist[k[u] >> kNrBucketBits], 1);
+        for (int u = 0; u < kNrBatch; ++u) dev |= (live && r[u] != __builtin_amdgcn_readlane(kv, u)) ? 1u << u : 0u;
+        unsigned D = dev;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) D |= (unsigned)__shfl_xor((int)D, o, 64);
+        D = (unsigned)__builtin_amdgcn_readfirstlane((int)D) & ((1u << nb) - 1u);
+#pragma unroll
+        for (int u = 0; u < kNrBatch; ++u) {
+            if (!((D >> u) & 1u)) continue;
+            const int k = __builtin_amdgcn_readlane(kv, u);
+            const bool d = (dev >> u) & 1u;
+            const unsigned long long dm = __builtin_amdgcn_ballot_w64(d);
+            const unsigned nd = (unsigned)__popcll(dm);
+            if (wpos + nd > wcap) {
+                wover = true;  // (the block lists none: nr_spill adds its cells)
+                continue;
+            }
+            if (d) {
+                const bool inN = (unsigned)r[u] < (unsigned)N;
+                E[wpos + nr_rank(dm)] = make_int2((inN ? r[u] : kNrNoNode) | ((pb + u - p0) << 20), s);
+                if (inN) atomicAdd(&lh[nbk + (r[u] >> kNrBucketBits) * nchunk + c], 1);
+            }
+            if (k < N && lane == 0) atomicAdd(&lh[nbk + (k >> kNrBucketBits) * nchunk + c], (int)nd);
+            wpos += nd;
+        }
+    };
+    if (nv > 0) {
+        int ra[kNrBatch], rb[kNrBatch], ka[3], kb[3];
+        load(0, ra, ka);
+        // (the empty asm after each prefetch: the compiler may not hoist the
+        // examined unit's first uses of its keys above the next unit's loads)
+        for (int v = 0; v < nv; v += 2) {
+            load(v + 1, rb, kb);
+            asm volatile("" : "+v"(ka[0]), "+v"(ka[1]), "+v"(ka[2])::"memory");
+            examine(v, ra, ka);
+            load(v + 2, ra, ka);
+            asm volatile("" : "+v"(kb[0]), "+v"(kb[1]), "+v"(kb[2])::"memory");
+            if (v + 1 < nv) examine(v + 1, rb, kb);
         }
     }
+    if (wover && lane == 0) over = 1;
     __syncthreads();
-    for (int j = (int)threadIdx.x; j < nbk; j += kNrThreads) bh[(size_t)j * gridDim.x + blockIdx.x] = hist[j];
+    const bool bo = over != 0;
+    for (int j = t; j < nh; j += kNrThreads) bh[(size_t)j * nblk + b] = (bo && j >= nbk) ? 0 : lh[j];
+    if (lane == 0) ecount[b * kW + wv] = bo ? -1 : (int)wpos;
 }
 
-// level 1b: each block's pods to its slice of every bucket (bh scanned:
-// offsets), as (pod, cpu, mem lo, mem hi) records
-__global__ __launch_bounds__(kNrThreads) void nr_part_kernel(const int *__restrict__ pkey, int P, int nbk,
-                                                      const int *__restrict__ boff, const int *__restrict__ pod_cpu,
-                                                      const long long *__restrict__ pod_mem, int4 *__restrict__ rec,
-                                                      int4 *__restrict__ z, size_t nz) {
-    extern __shared__ int cur[];
-    nr_zero_slice(z, nz);
-    for (int j = (int)threadIdx.x; j < nbk; j += kNrThreads) cur[j] = boff[(size_t)j * gridDim.x + blockIdx.x];
-    __syncthreads();
-    const int p0 = (int)blockIdx.x * kNrChunk, p1 = min(P, p0 + kNrChunk);
-    constexpr int kU = kNrChunk / kNrThreads;
+// inclusive scan over a wave
+__device__ __forceinline__ int nr_wave_scan(int v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int x = __shfl_up(v, d, 64);
+        v += lane >= d ? x : 0;
+    }
+    return v;
+}
+
+// launch 2: one wave per counter j: bh[j][0..nblk) -> its exclusive prefix,
+// tot[j] = the sum (kPer > 0: each lane's kPer blocks in registers, one
+// memory trip; 0: nblk > 64 * 8, loops)
+template <int kPer>
+__global__ __launch_bounds__(256) void nr_colscan_kernel(int *__restrict__ bh, int nh, int nblk,
+                                                         int *__restrict__ tot) {
+    const int lane = (int)threadIdx.x & 63, j = (int)blockIdx.x * 4 + ((int)threadIdx.x >> 6);
+    if (j >= nh) return;
+    int *__restrict__ row = bh + (size_t)j * nblk;
+    const int per = kPer ? kPer : (nblk + 63) >> 6, b0 = lane * per, b1 = min(nblk, b0 + per);
+    int sum = 0;
+    if (kPer) {
+        int x[kPer > 0 ? kPer : 1];
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) x[i] = row[min(b0 + i, nblk - 1)];
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) sum += b0 + i < b1 ? x[i] : 0;
+        const int incl = nr_wave_scan(sum, lane);
+        int run = incl - sum;
+#pragma unroll
+        for (int i = 0; i < kPer; ++i)
+            if (b0 + i < b1) {
+                row[b0 + i] = run;
+                run += x[i];
+            }
+        if (lane == 63) tot[j] = incl;
+        return;
+    }
+    for (int i = b0; i < b1; ++i) sum += row[i];
+    const int incl = nr_wave_scan(sum, lane);
+    int run = incl - sum;
+    for (int i = b0; i < b1; ++i) {
+        const int x = row[i];
+        row[i] = run;
+        run += x;
+    }
+    if (lane == 63) tot[j] = incl;
+}
+
+// launch 3: LDS = the block's cursors [nh], the pods' cpu [kNrPods], keys
+// [kNrPods] and (kMem) mem [kNrPods]; the counters' bases (exclusive scan of tot) are computed by
+// every block, and written out by block 0 (base[nh] = the total)
+template <bool kMem>
+__global__ __launch_bounds__(kNrThreads) void nr_place_kernel(const int *__restrict__ pkey, int P, int N, int nbk,
+                                                              int nchunk, int nblk, const int *__restrict__ bh,
+                                                              const int *__restrict__ tot, int *__restrict__ base,
+                                                              const int *__restrict__ pod_cpu,
+                                                              const long long *__restrict__ pod_mem,
+                                                              const int2 *__restrict__ ent, size_t ecap,
+                                                              const int *__restrict__ ecount, int4 *__restrict__ rec) {
+    extern __shared__ __align__(16) int cur[];
+    __shared__ int wsum[kNrThreads / 64];
+    const int b = nr_block(nblk);
+    if (b >= nblk) return;
+    const int t = (int)threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int nh = nbk * (1 + nchunk);
+    int *lc = cur + nh, *lk = lc + kNrPods;
+    long long *lm = reinterpret_cast<long long *>(lk + kNrPods + (nh & 1));  // 8-B aligned
+    const int p0 = b * kNrPods, p1 = min(P, p0 + kNrPods);
+    constexpr int kU = kNrPods / kNrThreads;
     int k[kU], c[kU];
     long long m[kU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-        const int p = min(p0 + u * kNrThreads + (int)threadIdx.x, P - 1);
+    for (int u = 0; u < kU; ++u) {  // the pods' fields in flight while the bases are scanned
+        const int p = min(p0 + u * kNrThreads + t, P - 1);
         k[u] = pkey[p];
         c[u] = pod_cpu[p];
-        m[u] = pod_mem ? pod_mem[p] : 0;
+        m[u] = kMem ? pod_mem[p] : 0;
     }
+    // bases: thread t scans tot[t * per, ...) after the block's exclusive scan of the threads' sums
+    const int per = (nh + kNrThreads - 1) / kNrThreads, j0 = min(nh, t * per), j1 = min(nh, j0 + per);
+    int s = 0;
+    for (int j = j0; j < j1; ++j) s += tot[j];
+    const int incl = nr_wave_scan(s, lane);
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    int run = incl - s;
+    for (int w = 0; w < wv; ++w) run += wsum[w];
+    for (int j = j0; j < j1; ++j) {
+        const int x = tot[j];
+        cur[j] = run + bh[(size_t)j * nblk + b];
+        if (b == 0) base[j] = run;
+        run += x;
+    }
+    if (b == 0 && t == kNrThreads - 1) base[nh] = run;
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-        const int p = p0 + u * kNrThreads + (int)threadIdx.x;
-        if (p < p1) {
+        lc[u * kNrThreads + t] = c[u];
+        lk[u * kNrThreads + t] = k[u];
+        if (kMem) lm[u * kNrThreads + t] = m[u];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        const int p = p0 + u * kNrThreads + t;
+        if (p < p1 && k[u] < N) {
             const int pos = atomicAdd(&cur[k[u] >> kNrBucketBits], 1);
-            rec[pos] = make_int4(p, c[u], (int)(unsigned)(unsigned long long)m[u], (int)(m[u] >> 32));
+            rec[pos] = make_int4(k[u] & (kNrBucketNodes - 1), c[u], (int)(unsigned)(unsigned long long)m[u],
+                                 (int)(m[u] >> 32));
         }
     }
-}
-
-// Exclusive scan of off[0..n) in two launches of 1024-element blocks: the block
-// sums, then each block's scan plus the sum of the blocks before it.
-constexpr int kNrScanB = 1024;
-__device__ __forceinline__ int nr_block_incl_scan(int v, int *lds) {
-    const int t = (int)threadIdx.x;
-    lds[t] = v;
-    __syncthreads();
-    for (int d = 1; d < kNrScanB; d <<= 1) {  // Hillis-Steele
-        const int x = t >= d ? lds[t - d] : 0;
-        __syncthreads();
-        lds[t] += x;
-        __syncthreads();
-    }
-    return lds[t];
-}
-
-__global__ __launch_bounds__(kNrScanB) void nr_blocksum_kernel(const int *__restrict__ off, int n,
-                                                               int *__restrict__ bsum, int4 *__restrict__ z, size_t nz) {
-    nr_zero_slice(z, nz);
-    __shared__ int red[kNrScanB / 64];
-    const int i = (int)blockIdx.x * kNrScanB + (int)threadIdx.x;
-    int v = i < n ? off[i] : 0;
+    // the entries of the block's 8 wave regions, concatenated (-1: overflowed,
+    // nr_spill adds the block's deviations)
+    constexpr int kW = kNrThreads / 64;
+    int wc[kW], ne = 0;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int t = 0;
-        for (int w = 0; w < kNrScanB / 64; ++w) t += red[w];
-        bsum[blockIdx.x] = t;
+    for (int w = 0; w < kW; ++w) {
+        wc[w] = max(0, ecount[b * kW + w]);
+        ne += wc[w];
     }
-}
-
-__global__ __launch_bounds__(kNrScanB) void nr_blockscan_kernel(int *__restrict__ off, int n,
-                                                                const int *__restrict__ bsum, int4 *__restrict__ z,
-                                                                size_t nz) {
-    nr_zero_slice(z, nz);
-    __shared__ int lds[kNrScanB];
-    __shared__ int base;
-    if (threadIdx.x < 64) {  // the blocks before this one
-        int b = 0;
-        for (int j = (int)threadIdx.x; j < (int)blockIdx.x; j += 64) b += bsum[j];
+    const size_t wcap = ecap / kW;
+    const int2 *__restrict__ E = ent + (size_t)b * ecap;
+    constexpr int kV = 4;
+    for (int i0 = 0; i0 < ne; i0 += kNrThreads * kV) {
+        int2 e[kV];
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) b += __shfl_xor(b, o, 64);
-        if (threadIdx.x == 0) base = b;
-    }
-    const int i = (int)blockIdx.x * kNrScanB + (int)threadIdx.x;
-    const int v = i < n ? off[i] : 0;
-    const int incl = nr_block_incl_scan(v, lds);  // (its barriers also publish `base`)
-    if (i < n) off[i] = base + incl - v;
-}
-
-// A bucket's pods, one workgroup per (work item, 64-scenario chunk).  Work
-// item = bucket b's pods [b0 + k * kNrSlice, ...) up to kNrSlice of them: the
-// first launch takes k = 0 of every bucket and lists the k >= 1 items of the
-// buckets beyond kNrSlice pods (ovf: count, then (b, k) pairs), which the
-// overflow launch takes (none for uniform clusters: its workgroups exit).
-// LDS: the 32 nodes x 64 scenarios' count + cpu (/ mem) sums, 32 KB: 4
-// workgroups of 8 waves per CU.  Each wave walks its eighth of the item's pods
-// 64 records at a time (one coalesced 16-B load per lane, the next 64
-// prefetched), the pod's fields broadcast from the lane holding them, 16 assign
-// rows in flight: one memory trip per batch.
-constexpr int kNrBucketThreads = 512;
-template <bool kMem>
-__global__ __launch_bounds__(kNrBucketThreads, 4) void nr_bucket_kernel(
-    const int *__restrict__ assign, int P, int S, int N, const int4 *__restrict__ rec, const int *__restrict__ boff,
-    int nblk1, int nbk, int nchunk, int *__restrict__ cnt, unsigned long long *__restrict__ cpu,
-    unsigned long long *__restrict__ mem, int *__restrict__ ovf, int overflow, int ablate) {
-#ifndef RSK_ABLATIONS
-    ablate = 0;  // profiling switches (wrong results) exist only in ablation builds
-#endif
-    constexpr int kE = kNrBucketNodes * 64, kW = kNrBucketThreads / 64;
-    // (count << 44) + the sum of (cpu + 2^31): one u64 atomic for both (a
-    // workgroup adds at most kNrSlice pods: the sum stays below 2^43)
-    __shared__ unsigned long long lcc[kE];
-    __shared__ unsigned long long lmem[kMem ? kE : 1];
-    const int t = (int)threadIdx.x, lane = t & 63, wv = t >> 6;
-    const int item = (int)blockIdx.x / nchunk, chunk = (int)blockIdx.x - item * nchunk;
-    int b, k = 0;
-    if (!overflow) {
-        b = item;
-    } else {
-        if (item >= __builtin_nontemporal_load(&ovf[0])) return;
-        b = ovf[1 + 2 * item];
-        k = ovf[2 + 2 * item];
-    }
-    const int b0 = boff[(size_t)b * nblk1], b1 = b + 1 < nbk ? boff[(size_t)(b + 1) * nblk1] : P;
-    if (!overflow && chunk == 0 && t == 0 && b1 - b0 > kNrSlice) {  // the bucket's other slices
-        const int ns = (b1 - b0 + kNrSlice - 1) / kNrSlice - 1;
-        const int at = atomicAdd(&ovf[0], ns);
-        for (int j = 0; j < ns; ++j) {
-            ovf[1 + 2 * (at + j)] = b;
-            ovf[2 + 2 * (at + j)] = j + 1;
+        for (int v = 0; v < kV; ++v) {
+            int i = min(i0 + v * kNrThreads + t, ne - 1), w = 0;
+#pragma unroll
+            for (int x = 0; x < kW - 1; ++x)
+                if (w == x && i >= wc[x]) {
+                    i -= wc[x];
+                    w = x + 1;
+                }
+            e[v] = E[(size_t)w * wcap + i];
         }
-    }
-    const int lo = b0 + k * kNrSlice, hi = min(b1, lo + kNrSlice);
-    if (lo >= hi) return;
-    for (int e = t; e < kE; e += kNrBucketThreads) {
-        lcc[e] = 0ull;
-        if (kMem) lmem[e] = 0ull;
-    }
-    __syncthreads();
-    const int s = chunk * 64 + lane, n0 = b * kNrBucketNodes;
-    const bool live = s < S;
-    const int q = (hi - lo + kW - 1) / kW, j0 = lo + wv * q, j1 = min(hi, j0 + q);
-    int4 rn = j0 < j1 ? rec[min(j0 + lane, j1 - 1)] : make_int4(0, 0, 0, 0);
-    for (int c0 = j0; c0 < j1; c0 += 64) {
-        const int4 r = rn;
-        if (c0 + 64 < j1) rn = rec[min(c0 + 64 + lane, j1 - 1)];  // the next 64 records, in flight meanwhile
-        const int cn = min(64, j1 - c0);
-        constexpr int kB = 16;
-        for (int ub = 0; ub < cn; ub += kB) {
-            int a[kB];
 #pragma unroll
-            for (int u = 0; u < kB; ++u) {
-                const int p = __builtin_amdgcn_readlane(r.x, min(ub + u, cn - 1));
-                a[u] = live ? __builtin_nontemporal_load(&assign[(size_t)p * S + s]) : -1;
+        for (int v = 0; v < kV; ++v) {
+            if (i0 + v * kNrThreads + t < ne) {
+                const int node = e[v].x & kNrNoNode, lp = (int)((unsigned)e[v].x >> 20), sc = e[v].y;
+                const int key = lk[lp], lane = (sc & 63) << 6;
+                const long long mm = kMem ? lm[lp] : 0;
+                const int mlo = (int)(unsigned)(unsigned long long)mm, mhi = (int)(mm >> 32);
+                if (node < N) {  // + the pod at its node
+                    const int pos = atomicAdd(&cur[nbk + (node >> kNrBucketBits) * nchunk + (sc >> 6)], 1);
+                    rec[pos] = make_int4((node & (kNrBucketNodes - 1)) | lane, lc[lp], mlo, mhi);
+                }
+                if (key < N) {  // - the pod at its key node
+                    const int pos = atomicAdd(&cur[nbk + (key >> kNrBucketBits) * nchunk + (sc >> 6)], 1);
+                    rec[pos] = make_int4((key & (kNrBucketNodes - 1)) | 32 | lane, lc[lp], mlo, mhi);
+                }
             }
+        }
+    }
+}
+
+// launch 4: a workgroup per bin (bucket b, chunk c)
+constexpr int kNrSumThreads = 256;
+template <bool kMem>
+__global__ __launch_bounds__(kNrSumThreads) void nr_sum_kernel(const int *__restrict__ base, int nbk, int nchunk,
+                                                               const int4 *__restrict__ rec, int N, int S,
+                                                               int *__restrict__ cnt,
+                                                               unsigned long long *__restrict__ cpu,
+                                                               unsigned long long *__restrict__ mem) {
+    constexpr int kE = kNrBucketNodes * 64;
+    __shared__ int bc[kNrBucketNodes];
+    __shared__ unsigned long long bcpu[kNrBucketNodes], bmem[kNrBucketNodes];
+    __shared__ int dc[kE];
+    __shared__ unsigned long long dcpu[kE], dmem[kMem ? kE : 1];
+    const int t = (int)threadIdx.x, g = (int)blockIdx.x, b = g / nchunk, c = g - b * nchunk;
+    const int lo = base[b], hi = base[b + 1];
+    const int j = nbk + b * nchunk + c, elo = base[j], ehi = base[j + 1];
+    if (t < kNrBucketNodes) {
+        bc[t] = 0;
+        bcpu[t] = 0ull;
+        bmem[t] = 0ull;
+    }
+    for (int e = t; e < kE; e += kNrSumThreads) {
+        dc[e] = 0;
+        dcpu[e] = 0ull;
+        if (kMem) dmem[e] = 0ull;
+    }
+    __syncthreads();
+    constexpr int kV = 4;
+    for (int i0 = lo; i0 < hi; i0 += kNrSumThreads * kV) {  // the bucket's pods: base
+        int4 r[kV];
 #pragma unroll
-            for (int u = 0; u < kB; ++u) {
-                if (ub + u >= cn) break;
-                const int c = __builtin_amdgcn_readlane(r.y, ub + u);
-                const long long m = kMem ? (long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane(r.w, ub + u)
-                                                        << 32) |
-                                                       (unsigned)__builtin_amdgcn_readlane(r.z, ub + u))
-                                         : 0;
-                const int rel = a[u] - n0;
-                if ((unsigned)rel < (unsigned)kNrBucketNodes) {
-                    if (a[u] < N && !(ablate & 2)) {  // (the key-N bucket's range may pass N; ablate 2: no LDS sums)
-                        const int e = rel * 64 + lane;
-                        atomicAdd(&lcc[e], (1ull << 44) + (unsigned long long)((long long)c + 0x80000000ll));
-                        if (kMem) atomicAdd(&lmem[e], (unsigned long long)m);
-                    }
-                } else if ((unsigned)a[u] < (unsigned)N && !(ablate & 1)) {  // off the bucket: to the output (ablate 1: not)
-                    const size_t o = (size_t)a[u] * S + s;
-                    atomicAdd(&cnt[o], 1);
-                    atomicAdd(&cpu[o], (unsigned long long)(long long)c);
-                    if (kMem) atomicAdd(&mem[o], (unsigned long long)m);
+        for (int v = 0; v < kV; ++v) r[v] = rec[min(i0 + v * kNrSumThreads + t, hi - 1)];
+#pragma unroll
+        for (int v = 0; v < kV; ++v) {
+            if (i0 + v * kNrSumThreads + t < hi) {
+                const int n = r[v].x;
+                atomicAdd(&bc[n], 1);
+                atomicAdd(&bcpu[n], (unsigned long long)(long long)r[v].y);
+                if (kMem) atomicAdd(&bmem[n], ((unsigned long long)(unsigned)r[v].w << 32) | (unsigned)r[v].z);
+            }
+        }
+    }
+    for (int i0 = elo; i0 < ehi; i0 += kNrSumThreads * kV) {  // the bin's deviation entries
+        int4 r[kV];
+#pragma unroll
+        for (int v = 0; v < kV; ++v) r[v] = rec[min(i0 + v * kNrSumThreads + t, ehi - 1)];
+#pragma unroll
+        for (int v = 0; v < kV; ++v) {
+            if (i0 + v * kNrSumThreads + t < ehi) {
+                const int x = r[v].x, e = (x & (kNrBucketNodes - 1)) * 64 + ((x >> 6) & 63);
+                const bool neg = (x >> 5) & 1;
+                const long long cv = r[v].y;
+                atomicAdd(&dc[e], neg ? -1 : 1);
+                atomicAdd(&dcpu[e], (unsigned long long)(neg ? -cv : cv));
+                if (kMem) {
+                    const unsigned long long mv = ((unsigned long long)(unsigned)r[v].w << 32) | (unsigned)r[v].z;
+                    atomicAdd(&dmem[e], neg ? 0ull - mv : mv);
                 }
             }
         }
     }
     __syncthreads();
-    for (int e = t; e < kE; e += kNrBucketThreads) {
-        const unsigned long long w = lcc[e];
-        const unsigned c = (unsigned)(w >> 44);
-        const int n = n0 + (e >> 6), ss = chunk * 64 + (e & 63);
-        if (c == 0u || n >= N || ss >= S || (ablate & 4)) continue;  // ablate 4: no flush
-        const size_t o = (size_t)n * S + ss;
-        atomicAdd(&cnt[o], (int)c);
-        atomicAdd(&cpu[o], (unsigned long long)((long long)(w & ((1ull << 44) - 1)) - ((long long)c << 31)));
-        if (kMem) atomicAdd(&mem[o], lmem[e]);
+    for (int e = t; e < kE; e += kNrSumThreads) {
+        const int l = e >> 6, n = b * kNrBucketNodes + l, s = c * 64 + (e & 63);
+        if (n >= N || s >= S) continue;
+        const size_t o = (size_t)n * S + s;
+        cnt[o] = bc[l] + dc[e];
+        cpu[o] = bcpu[l] + dcpu[e];
+        if (kMem) mem[o] = bmem[l] + dmem[e];
+    }
+}
+
+// launch 5: the deviation cells of the blocks that overflowed, by atomics on
+// the stored sums (none on the bench batches: every block exits at once)
+template <bool kMem>
+__global__ __launch_bounds__(kNrThreads) void nr_spill_kernel(const int *__restrict__ assign, int P, int S, int N,
+                                                              int nblk, const int *__restrict__ pkey,
+                                                              const int *__restrict__ ecount,
+                                                              const int *__restrict__ pod_cpu,
+                                                              const long long *__restrict__ pod_mem,
+                                                              int *__restrict__ cnt,
+                                                              unsigned long long *__restrict__ cpu,
+                                                              unsigned long long *__restrict__ mem) {
+    const int b = nr_block(nblk);
+    if (b >= nblk || ecount[b * (kNrThreads / 64)] >= 0) return;
+    const int p0 = b * kNrPods, p1 = min(P, p0 + kNrPods);
+    const size_t n = (size_t)(p1 - p0) * S;
+    for (size_t i = threadIdx.x; i < n; i += kNrThreads) {
+        const int p = p0 + (int)(i / (size_t)S), s = (int)(i % (size_t)S);
+        const int a = assign[(size_t)p * S + s], k = pkey[p];
+        if (a == k) continue;
+        const long long c = pod_cpu[p], m = kMem ? pod_mem[p] : 0;
+        if ((unsigned)a < (unsigned)N) {
+            const size_t o = (size_t)a * S + s;
+            atomicAdd(&cnt[o], 1);
+            atomicAdd(&cpu[o], (unsigned long long)c);
+            if (kMem) atomicAdd(&mem[o], (unsigned long long)m);
+        }
+        if (k < N) {
+            const size_t o = (size_t)k * S + s;
+            atomicAdd(&cnt[o], -1);
+            atomicAdd(&cpu[o], (unsigned long long)-c);
+            if (kMem) atomicAdd(&mem[o], (unsigned long long)-m);
+        }
     }
 }
 
@@ -1231,39 +1410,41 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
     RSK_TRY(stage_out(ctx, 3, pod_count, NS * 4, dev, reinterpret_cast<void **>(&d_cnt)));
     RSK_TRY(stage_out(ctx, 4, cpu_sum, NS * 8, dev, reinterpret_cast<void **>(&d_cs)));
     if (mem_sum) RSK_TRY(stage_out(ctx, 5, mem_sum, NS * 8, dev, reinterpret_cast<void **>(&d_ms)));
-    const int nbk = (N >> kNrBucketBits) + 1;  // key >> kNrBucketBits buckets (keys 0..N)
-    const bool z16 = (uintptr_t)d_cnt % 16 == 0 && (uintptr_t)d_cs % 16 == 0 && (uintptr_t)d_ms % 16 == 0 &&
-                     NS % 4 == 0;  // the outputs zeroed in int4 words by the first launch
-    if (PS && S >= 32 && nbk <= kNrMaxBuckets && z16) {  // bucketed: LDS sums per (32 nodes, 64 scenarios)
-        const int nchunk = (int)ceil_div(S, 64);
-        const int nblk1 = (int)ceil_div(P, kNrChunk);
-        const int64_t nbh = (int64_t)nbk * nblk1;
-        const int64_t ovf_cap = ceil_div(P, kNrSlice) + 1;
-        RSK_CHECK(nbh < INT32_MAX / 2 && (int64_t)nbk * nchunk < INT32_MAX && ovf_cap * nchunk < INT32_MAX,
-                  "node_reduce grouping too large");
-        const int nsb = (int)ceil_div(nbh, kNrScanB);
-        RSK_TRY(ctx->work[0].reserve((size_t)P * 20 + 16));  // keys, then the records
-        RSK_TRY(ctx->work[1].reserve(((size_t)nbh + nsb + 1 + 2 * (size_t)ovf_cap) * 4));
+    const int nbk = (int)ceil_div(N, kNrBucketNodes), nchunk = (int)ceil_div(S, 64);
+    const int64_t nh = (int64_t)nbk * (1 + nchunk);  // a block's counters: key buckets + entry bins
+    if (PS && S >= 32 && S <= kNrMaxS && nh <= kNrMaxCounters) {  // the deviation form
+        const int nblk = (int)ceil_div(P, kNrPods);
+        const int64_t ncnt = nh * nblk;
+        const size_t ecap = ((size_t)kNrPods * S / kNrEntDiv + 64) & ~(size_t)63;  // a block's entry region (8 waves')
+        const int64_t nrec = (int64_t)P + 2 * (int64_t)nblk * (int64_t)ecap;  // pod records + 2 per entry
+        RSK_CHECK(ncnt < INT32_MAX / 2 && nrec < INT32_MAX, "node_reduce grouping too large");
+        const size_t kb = ((size_t)P * 4 + 15) & ~(size_t)15;
+        RSK_TRY(ctx->work[0].reserve(kb + (size_t)nrec * 16));  // keys, then the records
+        RSK_TRY(ctx->work[1].reserve(((size_t)ncnt + 2 * (size_t)nh + 1 + (size_t)nblk * (kNrThreads / 64)) * 4));
+        RSK_TRY(ctx->work[2].reserve((size_t)nblk * ecap * 8));
         int *pkey = ctx->work[0].as<int>();
-        int4 *rec = reinterpret_cast<int4 *>(ctx->work[0].as<char>() + (((size_t)P * 4 + 15) & ~(size_t)15));
-        int *bh = ctx->work[1].as<int>(), *bsum = bh + nbh, *ovf = bsum + nsb;
-        ScopedTimer tm(ctx, "node_reduce");
-        const size_t hl = (size_t)nbk * 4;
-        nr_hist_kernel<<<nblk1, kNrThreads, hl, ctx->stream>>>(d_assign, P, S, N, nbk, pkey, bh, ovf);
-        nr_blocksum_kernel<<<nsb, kNrScanB, 0, ctx->stream>>>(bh, (int)nbh, bsum, reinterpret_cast<int4 *>(d_cnt),
-                                                               NS / 4);
-        nr_blockscan_kernel<<<nsb, kNrScanB, 0, ctx->stream>>>(bh, (int)nbh, bsum, reinterpret_cast<int4 *>(d_cs),
-                                                                NS / 2);
-        nr_part_kernel<<<nblk1, kNrThreads, hl, ctx->stream>>>(pkey, P, nbk, bh, d_cpu,
-                                                                reinterpret_cast<const long long *>(d_mem), rec,
-                                                                reinterpret_cast<int4 *>(d_ms), d_ms ? NS / 2 : 0);
-        static const int nr_ablate = RSK_ABLATION(RSK_ABLATE_NR);
-        auto *bk = d_ms ? &nr_bucket_kernel<true> : &nr_bucket_kernel<false>;
+        int4 *rec = reinterpret_cast<int4 *>(ctx->work[0].as<char>() + kb);
+        int *bh = ctx->work[1].as<int>(), *tot = bh + ncnt, *base = tot + nh, *ecount = base + nh + 1;
+        int2 *ent = ctx->work[2].as<int2>();
         auto *ucs = reinterpret_cast<unsigned long long *>(d_cs), *ums = reinterpret_cast<unsigned long long *>(d_ms);
-        bk<<<(unsigned)(nbk * nchunk), kNrBucketThreads, 0, ctx->stream>>>(d_assign, P, S, N, rec, bh, nblk1, nbk,
-                                                                          nchunk, d_cnt, ucs, ums, ovf, 0, nr_ablate);
-        bk<<<(unsigned)(ovf_cap * nchunk), kNrBucketThreads, 0, ctx->stream>>>(d_assign, P, S, N, rec, bh, nblk1, nbk,
-                                                                              nchunk, d_cnt, ucs, ums, ovf, 1, nr_ablate);
+        const auto *lmem = reinterpret_cast<const long long *>(d_mem);
+        ScopedTimer tm(ctx, "node_reduce");
+        const bool o32 = PS * 4 < ((size_t)1 << 32), maj = S >= 43;
+        auto *sc = o32 ? (maj ? &nr_scan_kernel<true, true> : &nr_scan_kernel<true, false>)
+                       : (maj ? &nr_scan_kernel<false, true> : &nr_scan_kernel<false, false>);
+        const unsigned g8 = (unsigned)(8 * ceil_div(nblk, 8));  // (nr_block: XCD runs of consecutive blocks)
+        sc<<<g8, kNrThreads, (size_t)nh * 4, ctx->stream>>>(d_assign, P, S, N, nbk, nchunk, nblk, ecap, pkey, bh, ent,
+                                                             ecount);
+        auto *cs = nblk <= 64 * 8 ? &nr_colscan_kernel<8> : &nr_colscan_kernel<0>;
+        cs<<<(unsigned)ceil_div(nh, 4), 256, 0, ctx->stream>>>(bh, (int)nh, nblk, tot);
+        const size_t pl = (size_t)nh * 4 + 8 + (size_t)kNrPods * (d_ms ? 16 : 8);
+        auto *pk = d_ms ? &nr_place_kernel<true> : &nr_place_kernel<false>;
+        pk<<<g8, kNrThreads, pl, ctx->stream>>>(pkey, P, N, nbk, nchunk, nblk, bh, tot, base, d_cpu, lmem, ent, ecap,
+                                                ecount, rec);
+        auto *sk = d_ms ? &nr_sum_kernel<true> : &nr_sum_kernel<false>;
+        sk<<<(unsigned)(nbk * nchunk), kNrSumThreads, 0, ctx->stream>>>(base, nbk, nchunk, rec, N, S, d_cnt, ucs, ums);
+        auto *xk = d_ms ? &nr_spill_kernel<true> : &nr_spill_kernel<false>;
+        xk<<<g8, kNrThreads, 0, ctx->stream>>>(d_assign, P, S, N, nblk, pkey, ecount, d_cpu, lmem, d_cnt, ucs, ums);
         RSK_HIP(hipGetLastError());
     } else {
         ScopedTimer tm(ctx, "node_reduce");

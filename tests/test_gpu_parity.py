@@ -791,6 +791,44 @@ def test_node_reduce_segmented_vs_oracle(ctx, P, N, S, p_flip):
         assert np.array_equal(g, e), name
 
 
+@pytest.mark.parametrize("P,N,S", [(20_000, 3_000, 64), (9_000, 500, 4096), (12_000, 1_000, 100)])
+def test_node_reduce_deviation_form_edges(ctx, P, N, S):
+    """The deviation form of kernel 3's node sums (out = base[key node] +
+    per-scenario deviations, podmonitor.py:104-121) against the oracle where
+    its bookkeeping branches: one 4096-pod block with 40 % of its cells
+    redrawn (its entry region overflows: its deviations go through the spill
+    launch) beside blocks that list theirs; pods whose scenario-0 node is
+    redrawn (the key is the majority of scenarios 0 / 21 / 42), pods with no
+    key (unscheduled in two of the three), pods unscheduled in scenario 0 only,
+    assignments equal to N; 64 chunks per pod (S = 4096) and a partial chunk
+    (S = 100)."""
+    from oracle import oracle as orc
+    from rsk import api
+    rng = np.random.default_rng(P * 7 + S)
+    base = rng.integers(0, N, P)
+    a = np.repeat(base[:, None], S, axis=1).astype(np.int32)
+    flip = rng.random((P, S)) < 0.01
+    flip[4096:8192] = rng.random((4096, S)) < 0.4         # the second block overflows
+    a[flip] = rng.integers(-2, N + 2, int(flip.sum()))
+    q = rng.integers(0, P, 300)
+    a[q, 0] = rng.integers(0, N, 300)                      # scenario 0 redrawn: key from 21 / 42
+    q = rng.integers(0, P, 100)
+    a[q, 0] = -1                                           # unscheduled in scenario 0 only
+    q = rng.integers(0, P, 100)
+    a[q, 0] = -1
+    a[q, 21] = N                                           # no key node
+    a[rng.integers(0, P, 50), :] = -1
+    pod_cpu = rng.integers(-500, 500, P).astype(np.int32)
+    pod_mem = rng.integers(-(1 << 40), 1 << 40, P).astype(np.int64)
+    for mem in (pod_mem, None):
+        got = api.node_reduce(a.reshape(-1), P, S, pod_cpu, mem, N, ctx=ctx)
+        exp = orc.node_reduce(a.reshape(-1), P, S, pod_cpu, pod_mem, N)
+        assert np.array_equal(got[0], exp[0]), "count"
+        assert np.array_equal(got[1], exp[1]), "cpu"
+        if mem is not None:
+            assert np.array_equal(got[2], exp[2]), "mem"
+
+
 @pytest.mark.parametrize("S", [64, 130])
 def test_car_early_side_rows_on_the_fly_codes(ctx, S):
     """Rows too big for the fused grid's 20 KB teams (degree 1,200-2,000 over

@@ -2,7 +2,8 @@
 # Round-5 GPU session on one box.  usage: tools/gpu_r05.sh OUTDIR [steps...]
 # steps: test (pytest -m gpu), smoke, bench (headline), b2k (config 2),
 #        b1m (config 4), brounds (config 5), prof (rocprof trace + PMC of headline
-#        and 1m50k), profh / prof1m (one config), dropin
+#        and 1m50k), profh / prof1m (one config), dropin, nrb (tools/nrbench.py),
+#        nrprof (its kernel trace)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 out=gpurun_out/${1:-r05}; shift
 mkdir -p "$out"
@@ -33,6 +34,8 @@ for s in "${@:-test smoke bench}"; do
       bnoev) step bench_noevents 600 python -u bench.py --no-cpu-baseline --no-kernel-events ;;
       nr:*) kv=${w#nr:}; step "nr_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_abl.so ${kv//,/ } python -u tools/nrbench.py ;;
       nrk:*) kv=${w#nrk:}; step "nrk_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u tools/nrbench.py ;;
+      nrb) step nrbench 300 python -u tools/nrbench.py ;;
+      nrprof) ./tools/gpu_nrprof.sh "$out/nrprof" > "$out/nrprof.log" 2>&1 || { tail -5 "$out/nrprof.log"; exit 1; }; cat "$out/nrprof.log" ;;
       dropin) step dropin 400 python -u tools/dropin_latency.py --calls 40 --out "$out/dropin.json" ;;
       prof) for c in headline 1m50k; do
               ./tools/gpu_prof.sh $c "$out/prof_$c" > "$out/prof_$c.log" 2>&1 || { tail -5 "$out/prof_$c.log"; exit 1; }
