@@ -38,7 +38,7 @@ BENCH_NAME = {"car_tile16": "car_tile", "car_fused16": "car_tile", "car_hub": "c
 SUM_GRIDS = {"car_tile"}
 # kernel 3 (bench.py's "kernel3" leg): the launches of one librsk call, summed per call
 KERNEL3 = ("node_reduce", "nr_", "cut_cost", "cut_bins", "std_")
-KERNEL3_CALL = {"node_reduce": ("node_reduce_seg", "nr_hist", "nr_blocksum", "nr_blockscan", "nr_part", "nr_sub"),
+KERNEL3_CALL = {"node_reduce": ("nr_scan", "nr_colscan", "nr_place", "nr_sum", "nr_spill"),
                 "load_std": ("std_partial", "std_merge"), "cut_cost": ("cut_cost_wave", "cut_bins_sum")}
 
 
