@@ -1271,15 +1271,20 @@ int launch_fused16(hipStream_t stream, const Tile16Args &a, const SideArgs &sa, 
     static int cus = 0;
     if (!cus) RSK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     static const int pw = RSK_KNOB(RSK_FUSE_PW, 0);  // persistent workgroups per CU (0: one per block)
-    const int64_t grid = pw > 0 && !cells && !score ? std::min<int64_t>(blocks, (int64_t)8 * ceil_div((int64_t)pw * cus, 8)) : blocks;
+    const int64_t grid = pw > 0 && !score ? std::min<int64_t>(blocks, (int64_t)8 * ceil_div((int64_t)pw * cus, 8)) : blocks;
     using K = void (*)(Tile16Args, SideArgs, SideArgs, DirectArgs, FuseMap);
     // [direct][score][off32]; direct cells only without scores
     static const K kerns[6] = {&car_fused16_kernel<false, false, false>, &car_fused16_kernel<false, true, false>,
                                &car_fused16_kernel<true, false, false>,  &car_fused16_kernel<true, true, false>,
                                &car_fused16_kernel<false, false, true>,  &car_fused16_kernel<false, true, true>};
     K kern = kerns[(cells ? 4 : 0) + (score ? 2 : 0) + (off32 ? 1 : 0)];
-    if (grid < blocks && !cells && !score)
-        kern = off32 ? &car_fused16_kernel<false, true, false, true> : &car_fused16_kernel<false, false, false, true>;
+    if (grid < blocks && !score) {
+        static const K loops[4] = {&car_fused16_kernel<false, false, false, true>,
+                                   &car_fused16_kernel<false, true, false, true>,
+                                   &car_fused16_kernel<false, false, true, true>,
+                                   &car_fused16_kernel<false, true, true, true>};
+        kern = loops[(cells ? 2 : 0) + (off32 ? 1 : 0)];
+    }
     RSK_CHECK(lds <= 160 * 1024, "fused tile needs %zu B of LDS", lds);
     if (lds > 64 * 1024)
         RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
