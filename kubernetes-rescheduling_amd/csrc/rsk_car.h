@@ -365,7 +365,6 @@ struct FuseMap {
     int big_blocks;    // then big_blocks blocks: 4-wave side teams (ba), a multiple of 8
     int R, k1;         // then k1 periods of R rows of 8 blocks: R - 1 tile rows, one single-wave side row (sa)
     int side_rows, tile_rows;  // then the tile rows left, then the side rows left
-    int blocks;        // all of them (a persistent grid loops over them)
 };
 // lean tiles + single-wave side items of one class (4 per workgroup, kB 16) +
 // optionally 4-wave side teams (kB 16) in one grid; ba.n_rows == 0: no teams

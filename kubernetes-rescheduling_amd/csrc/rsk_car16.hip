@@ -1169,13 +1169,14 @@ __device__ __forceinline__ void direct16_block(const DirectArgs &a, const Tile16
 }
 
 template <bool kScore, bool kOff32, bool kDirect>
-__device__ __forceinline__ void fused16_item(const Tile16Args &ta, const SideArgs &sa, const SideArgs &ba,
-                                             const DirectArgs &da, const FuseMap &f, unsigned vb) {
-    if (kDirect && vb < (unsigned)f.direct_blocks) {
-        if ((int)vb < da.Q * da.S) direct16_block(da, ta, (int)vb);
+__global__ __launch_bounds__(kTileThreads, RSK_TILE16_WGS) void car_fused16_kernel(Tile16Args ta, SideArgs sa,
+                                                                                  SideArgs ba, DirectArgs da,
+                                                                                  FuseMap f) {
+    if (kDirect && blockIdx.x < (unsigned)f.direct_blocks) {
+        if ((int)blockIdx.x < da.Q * da.S) direct16_block(da, ta, (int)blockIdx.x);
         return;
     }
-    const unsigned v0 = vb - (unsigned)f.direct_blocks;
+    const unsigned v0 = blockIdx.x - (unsigned)f.direct_blocks;
     if (v0 < (unsigned)f.big_blocks) {  // (XCD x: the x-th eighth of the chunk-major team items)
         side16_block<4, 4, 16, kOff32, true>(ba, (int)((v0 & 7u) * ((unsigned)f.big_blocks >> 3) + (v0 >> 3)));
         return;
@@ -1197,23 +1198,6 @@ __device__ __forceinline__ void fused16_item(const Tile16Args &ta, const SideArg
         return;
     }
     tile16_block<kScore, kOff32, true>(ta, (tile << 3) | x);
-}
-
-// The grid's blocks, or (f.blocks > gridDim.x) a persistent grid whose
-// workgroup i takes blocks i, i + G, ... (G a multiple of 8: the same XCD);
-// the barrier after each block: its LDS is the next one's
-template <bool kScore, bool kOff32, bool kDirect, bool kLoop = false>
-__global__ __launch_bounds__(kTileThreads, RSK_TILE16_WGS) void car_fused16_kernel(Tile16Args ta, SideArgs sa,
-                                                                                  SideArgs ba, DirectArgs da,
-                                                                                  FuseMap f) {
-    if (!kLoop) {
-        fused16_item<kScore, kOff32, kDirect>(ta, sa, ba, da, f, blockIdx.x);
-        return;
-    }
-    for (unsigned vb = blockIdx.x; vb < (unsigned)f.blocks; vb += gridDim.x) {
-        fused16_item<kScore, kOff32, kDirect>(ta, sa, ba, da, f, vb);
-        __syncthreads();
-    }
 }
 
 int launch_tile16(hipStream_t stream, const Tile16Args &a, bool score, bool off32, unsigned blocks, size_t lds) {
@@ -1267,29 +1251,17 @@ int launch_fused16(hipStream_t stream, const Tile16Args &a, const SideArgs &sa, 
     f.k1 = std::min(f.side_rows, f.tile_rows / (f.R - 1));
     const int64_t blocks = (int64_t)f.direct_blocks + f.big_blocks + tile_blocks + 8LL * f.side_rows;
     RSK_CHECK(blocks < INT32_MAX, "fused grid too large");
-    f.blocks = (int)blocks;
-    static int cus = 0;
-    if (!cus) RSK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-    static const int pw = RSK_KNOB(RSK_FUSE_PW, 0);  // persistent workgroups per CU (0: one per block)
-    const int64_t grid = pw > 0 && !score ? std::min<int64_t>(blocks, (int64_t)8 * ceil_div((int64_t)pw * cus, 8)) : blocks;
     using K = void (*)(Tile16Args, SideArgs, SideArgs, DirectArgs, FuseMap);
     // [direct][score][off32]; direct cells only without scores
     static const K kerns[6] = {&car_fused16_kernel<false, false, false>, &car_fused16_kernel<false, true, false>,
                                &car_fused16_kernel<true, false, false>,  &car_fused16_kernel<true, true, false>,
                                &car_fused16_kernel<false, false, true>,  &car_fused16_kernel<false, true, true>};
-    K kern = kerns[(cells ? 4 : 0) + (score ? 2 : 0) + (off32 ? 1 : 0)];
-    if (grid < blocks && !score) {
-        static const K loops[4] = {&car_fused16_kernel<false, false, false, true>,
-                                   &car_fused16_kernel<false, true, false, true>,
-                                   &car_fused16_kernel<false, false, true, true>,
-                                   &car_fused16_kernel<false, true, true, true>};
-        kern = loops[(cells ? 2 : 0) + (off32 ? 1 : 0)];
-    }
+    const K kern = kerns[(cells ? 4 : 0) + (score ? 2 : 0) + (off32 ? 1 : 0)];
     RSK_CHECK(lds <= 160 * 1024, "fused tile needs %zu B of LDS", lds);
     if (lds > 64 * 1024)
         RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds));
-    kern<<<dim3((unsigned)grid), dim3(kTileThreads), lds, stream>>>(a, sa, ba, da, f);
+    kern<<<dim3((unsigned)blocks), dim3(kTileThreads), lds, stream>>>(a, sa, ba, da, f);
     RSK_HIP(hipGetLastError());
     return RSK_OK;
 }

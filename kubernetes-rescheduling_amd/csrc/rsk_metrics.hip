@@ -469,7 +469,7 @@ __device__ __forceinline__ int nr_block(int nblk) {
 // entries, into the wave's own eighth of the block's region.  Counters ->
 // bh[j * nblk + b] (the entry bins zeroed when a wave overflowed), the waves'
 // entry counts (-1: the block overflowed) -> ecount[b * 8 + w].
-template <bool kOff32, bool kMaj>
+template <bool kOff32, bool kMaj, int kB>
 __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restrict__ assign, int P, int S, int N,
                                                              int nbk, int nchunk, int nblk, size_t ecap,
                                                              int *__restrict__ pkey, int *__restrict__ bh,
@@ -485,21 +485,21 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
     __syncthreads();
     constexpr int kPW = kNrPods / (kNrThreads / 64), kW = kNrThreads / 64;
     const int p0 = b * kNrPods, q0 = p0 + wv * kPW, q1 = min(P, q0 + kPW);
-    const int nv = q1 > q0 ? (q1 - q0 + kNrBatch - 1) / kNrBatch * nchunk : 0;  // the wave's units
+    const int nv = q1 > q0 ? (q1 - q0 + kB - 1) / kB * nchunk : 0;  // the wave's units
     const char *__restrict__ asg = reinterpret_cast<const char *>(assign);
     const size_t wcap = ecap / kW;
     int2 *__restrict__ E = ent + (size_t)b * ecap + (size_t)wv * wcap;
     unsigned wpos = 0u;
     bool wover = false;
-    auto load = [&](int v, int (&r)[kNrBatch], int (&kr)[3]) {  // clamped: always valid addresses
+    auto load = [&](int v, int (&r)[kB], int (&kr)[3]) {  // clamped: always valid addresses
         v = min(v, nv - 1);
-        const int bt = v / nchunk, c = v - bt * nchunk, pb = q0 + bt * kNrBatch, last = min(q1, pb + kNrBatch) - 1;
+        const int bt = v / nchunk, c = v - bt * nchunk, pb = q0 + bt * kB, last = min(q1, pb + kB) - 1;
         const unsigned sc = (unsigned)min(c * 64 + lane, S - 1);
 #pragma unroll
-        for (int u = 0; u < kNrBatch; ++u)
+        for (int u = 0; u < kB; ++u)
             r[u] = __builtin_nontemporal_load(
                 reinterpret_cast<const int *>(asg + nr_off<kOff32>((unsigned)min(pb + u, last), (unsigned)S, sc)));
-        const unsigned pk = (unsigned)min(pb + (lane & (kNrBatch - 1)), last);
+        const unsigned pk = (unsigned)min(pb + (lane & (kB - 1)), last);
         if (abl & 4) return;
         kr[0] = *reinterpret_cast<const int *>(asg + nr_off<kOff32>(pk, (unsigned)S, 0u));
         if (kMaj) {
@@ -507,13 +507,13 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
             kr[2] = *reinterpret_cast<const int *>(asg + nr_off<kOff32>(pk, (unsigned)S, 42u));
         }
     };
-    auto examine = [&](int v, const int (&r)[kNrBatch], const int (&kr)[3]) {
-        const int bt = v / nchunk, c = v - bt * nchunk, pb = q0 + bt * kNrBatch, nb = min(kNrBatch, q1 - pb);
+    auto examine = [&](int v, const int (&r)[kB], const int (&kr)[3]) {
+        const int bt = v / nchunk, c = v - bt * nchunk, pb = q0 + bt * kB, nb = min(kB, q1 - pb);
         int kv = kr[0];  // lane u < 16: pod pb + u's key
         if (kMaj) kv = (kv == kr[1] || kv == kr[2]) ? kv : (kr[1] == kr[2] ? kr[1] : kv);
         if (abl & 4) {  // (nchunk == 1) keys from the rows themselves
 #pragma unroll
-            for (int u = 0; u < kNrBatch; ++u) {
+            for (int u = 0; u < kB; ++u) {
                 int k = __builtin_amdgcn_readlane(r[u], 0);
                 if (kMaj) {
                     const int k1 = __builtin_amdgcn_readlane(r[u], 21), k2 = __builtin_amdgcn_readlane(r[u], 42);
@@ -532,16 +532,16 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
         // bit u of dev: the lane's cell of unit u is off the pod's key node; D:
         // the units with any such lane (an OR over the wave)
         unsigned dev = 0u;
-        if (abl & 2) { int x = 0; for (int u = 0; u < kNrBatch; ++u) x ^= r[u]; if (x == 0x7654321) pkey[0] = x; return; }
+        if (abl & 2) { int x = 0; for (int u = 0; u < kB; ++u) x ^= r[u]; if (x == 0x7654321) pkey[0] = x; return; }
 #pragma unroll
-        for (int u = 0; u < kNrBatch; ++u) dev |= (live && r[u] != __builtin_amdgcn_readlane(kv, u)) ? 1u << u : 0u;
+        for (int u = 0; u < kB; ++u) dev |= (live && r[u] != __builtin_amdgcn_readlane(kv, u)) ? 1u << u : 0u;
         unsigned D = dev;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) D |= (unsigned)__shfl_xor((int)D, o, 64);
-        D = (unsigned)__builtin_amdgcn_readfirstlane((int)D) & ((1u << nb) - 1u);
+        D = (unsigned)__builtin_amdgcn_readfirstlane((int)D) & (nb >= 32 ? 0xffffffffu : (1u << nb) - 1u);
         if (abl & 1) { if (D == 0x7654321) pkey[0] = D; return; }
 #pragma unroll
-        for (int u = 0; u < kNrBatch; ++u) {
+        for (int u = 0; u < kB; ++u) {
             if (!((D >> u) & 1u)) continue;
             const int k = __builtin_amdgcn_readlane(kv, u);
             const bool d = (dev >> u) & 1u;
@@ -561,7 +561,7 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
         }
     };
     if (nv > 0) {
-        int ra[kNrBatch], rb[kNrBatch], ka[3], kb[3];
+        int ra[kB], rb[kB], ka[3], kb[3];
         load(0, ra, ka);
         // (the empty asm after each prefetch: the compiler may not hoist the
         // examined unit's first uses of its keys above the next unit's loads)
@@ -1444,10 +1444,18 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
         const auto *lmem = reinterpret_cast<const long long *>(d_mem);
         ScopedTimer tm(ctx, "node_reduce");
         const bool o32 = PS * 4 < ((size_t)1 << 32), maj = S >= 43;
-        auto *sc = o32 ? (maj ? &nr_scan_kernel<true, true> : &nr_scan_kernel<true, false>)
-                       : (maj ? &nr_scan_kernel<false, true> : &nr_scan_kernel<false, false>);
-        const unsigned g8 = (unsigned)(8 * ceil_div(nblk, 8));  // (nr_block: XCD runs of consecutive blocks)
         const int nr_abl = RSK_KNOB(RSK_NR_ABL, 0) & (nchunk == 1 ? 7 : 3);
+        const int nr_b = RSK_KNOB(RSK_NR_B, 16);
+        using SK = void (*)(const int *, int, int, int, int, int, int, size_t, int *, int *, int2 *, int *, int);
+        static const SK sks[3][4] = {
+            {&nr_scan_kernel<false, false, 8>, &nr_scan_kernel<false, true, 8>, &nr_scan_kernel<true, false, 8>,
+             &nr_scan_kernel<true, true, 8>},
+            {&nr_scan_kernel<false, false, 16>, &nr_scan_kernel<false, true, 16>, &nr_scan_kernel<true, false, 16>,
+             &nr_scan_kernel<true, true, 16>},
+            {&nr_scan_kernel<false, false, 32>, &nr_scan_kernel<false, true, 32>, &nr_scan_kernel<true, false, 32>,
+             &nr_scan_kernel<true, true, 32>}};
+        const SK sc = sks[nr_b == 8 ? 0 : nr_b == 32 ? 2 : 1][(o32 ? 2 : 0) + (maj ? 1 : 0)];
+        const unsigned g8 = (unsigned)(8 * ceil_div(nblk, 8));  // (nr_block: XCD runs of consecutive blocks)
         sc<<<g8, kNrThreads, (size_t)nh * 4, ctx->stream>>>(d_assign, P, S, N, nbk, nchunk, nblk, ecap, pkey, bh, ent,
                                                              ecount, nr_abl);
         auto *cs = nblk <= 64 * 8 ? &nr_colscan_kernel<8> : &nr_colscan_kernel<0>;
