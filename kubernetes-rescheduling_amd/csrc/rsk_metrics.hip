@@ -469,11 +469,11 @@ __device__ __forceinline__ int nr_block(int nblk) {
 // entries, into the wave's own eighth of the block's region.  Counters ->
 // bh[j * nblk + b] (the entry bins zeroed when a wave overflowed), the waves'
 // entry counts (-1: the block overflowed) -> ecount[b * 8 + w].
-template <bool kOff32, bool kMaj, int kB>
+template <bool kOff32, bool kMaj, int kB = kNrBatch>
 __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restrict__ assign, int P, int S, int N,
                                                              int nbk, int nchunk, int nblk, size_t ecap,
                                                              int *__restrict__ pkey, int *__restrict__ bh,
-                                                             int2 *__restrict__ ent, int *__restrict__ ecount, int abl) {
+                                                             int2 *__restrict__ ent, int *__restrict__ ecount) {
     extern __shared__ int lh[];  // [nbk] key buckets, then [nbk * nchunk] entry bins
     __shared__ int over;
     const int b = nr_block(nblk);
@@ -500,7 +500,6 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
             r[u] = __builtin_nontemporal_load(
                 reinterpret_cast<const int *>(asg + nr_off<kOff32>((unsigned)min(pb + u, last), (unsigned)S, sc)));
         const unsigned pk = (unsigned)min(pb + (lane & (kB - 1)), last);
-        if (abl & 4) return;
         kr[0] = *reinterpret_cast<const int *>(asg + nr_off<kOff32>(pk, (unsigned)S, 0u));
         if (kMaj) {
             kr[1] = *reinterpret_cast<const int *>(asg + nr_off<kOff32>(pk, (unsigned)S, 21u));
@@ -511,17 +510,6 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
         const int bt = v / nchunk, c = v - bt * nchunk, pb = q0 + bt * kB, nb = min(kB, q1 - pb);
         int kv = kr[0];  // lane u < 16: pod pb + u's key
         if (kMaj) kv = (kv == kr[1] || kv == kr[2]) ? kv : (kr[1] == kr[2] ? kr[1] : kv);
-        if (abl & 4) {  // (nchunk == 1) keys from the rows themselves
-#pragma unroll
-            for (int u = 0; u < kB; ++u) {
-                int k = __builtin_amdgcn_readlane(r[u], 0);
-                if (kMaj) {
-                    const int k1 = __builtin_amdgcn_readlane(r[u], 21), k2 = __builtin_amdgcn_readlane(r[u], 42);
-                    k = (k == k1 || k == k2) ? k : (k1 == k2 ? k1 : k);
-                }
-                kv = lane == u ? k : kv;
-            }
-        }
         kv = (unsigned)kv < (unsigned)N ? kv : N;
         if (c == 0 && lane < nb) {
             pkey[pb + lane] = kv;
@@ -532,14 +520,12 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
         // bit u of dev: the lane's cell of unit u is off the pod's key node; D:
         // the units with any such lane (an OR over the wave)
         unsigned dev = 0u;
-        if (abl & 2) { int x = 0; for (int u = 0; u < kB; ++u) x ^= r[u]; if (x == 0x7654321) pkey[0] = x; return; }
 #pragma unroll
         for (int u = 0; u < kB; ++u) dev |= (live && r[u] != __builtin_amdgcn_readlane(kv, u)) ? 1u << u : 0u;
         unsigned D = dev;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) D |= (unsigned)__shfl_xor((int)D, o, 64);
         D = (unsigned)__builtin_amdgcn_readfirstlane((int)D) & (nb >= 32 ? 0xffffffffu : (1u << nb) - 1u);
-        if (abl & 1) { if (D == 0x7654321) pkey[0] = D; return; }
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
             if (!((D >> u) & 1u)) continue;
@@ -1444,20 +1430,11 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
         const auto *lmem = reinterpret_cast<const long long *>(d_mem);
         ScopedTimer tm(ctx, "node_reduce");
         const bool o32 = PS * 4 < ((size_t)1 << 32), maj = S >= 43;
-        const int nr_abl = RSK_KNOB(RSK_NR_ABL, 0) & (nchunk == 1 ? 7 : 3);
-        const int nr_b = RSK_KNOB(RSK_NR_B, 16);
-        using SK = void (*)(const int *, int, int, int, int, int, int, size_t, int *, int *, int2 *, int *, int);
-        static const SK sks[3][4] = {
-            {&nr_scan_kernel<false, false, 8>, &nr_scan_kernel<false, true, 8>, &nr_scan_kernel<true, false, 8>,
-             &nr_scan_kernel<true, true, 8>},
-            {&nr_scan_kernel<false, false, 16>, &nr_scan_kernel<false, true, 16>, &nr_scan_kernel<true, false, 16>,
-             &nr_scan_kernel<true, true, 16>},
-            {&nr_scan_kernel<false, false, 32>, &nr_scan_kernel<false, true, 32>, &nr_scan_kernel<true, false, 32>,
-             &nr_scan_kernel<true, true, 32>}};
-        const SK sc = sks[nr_b == 8 ? 0 : nr_b == 32 ? 2 : 1][(o32 ? 2 : 0) + (maj ? 1 : 0)];
+        auto *sc = o32 ? (maj ? &nr_scan_kernel<true, true> : &nr_scan_kernel<true, false>)
+                       : (maj ? &nr_scan_kernel<false, true> : &nr_scan_kernel<false, false>);
         const unsigned g8 = (unsigned)(8 * ceil_div(nblk, 8));  // (nr_block: XCD runs of consecutive blocks)
         sc<<<g8, kNrThreads, (size_t)nh * 4, ctx->stream>>>(d_assign, P, S, N, nbk, nchunk, nblk, ecap, pkey, bh, ent,
-                                                             ecount, nr_abl);
+                                                             ecount);
         auto *cs = nblk <= 64 * 8 ? &nr_colscan_kernel<8> : &nr_colscan_kernel<0>;
         cs<<<(unsigned)ceil_div(nh, 4), 256, 0, ctx->stream>>>(bh, (int)nh, nblk, tot);
         const size_t pl = (size_t)nh * 4 + 8 + (size_t)kNrPods * (d_ms ? 16 : 8);
