@@ -478,7 +478,7 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
     __shared__ int over;
     const int b = nr_block(nblk);
     if (b >= nblk) return;
-    const int t = (int)threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int t = (int)threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);  // (uniform)
     const int nh = nbk * (1 + nchunk);
     for (int j = t; j < nh; j += kNrThreads) lh[j] = 0;
     if (t == 0) over = 0;
@@ -487,7 +487,7 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
     const int p0 = b * kNrPods, q0 = p0 + wv * kPW, q1 = min(P, q0 + kPW);
     const int nv = q1 > q0 ? (q1 - q0 + kB - 1) / kB * nchunk : 0;  // the wave's units
     const char *__restrict__ asg = reinterpret_cast<const char *>(assign);
-    const size_t wcap = ecap / kW;
+    const unsigned wcap = (unsigned)(ecap / kW);  // (< 2^24: kNrPods * kNrMaxS / kNrEntDiv / 8)
     int2 *__restrict__ E = ent + (size_t)b * ecap + (size_t)wv * wcap;
     unsigned wpos = 0u;
     bool wover = false;
@@ -496,20 +496,21 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
         const int bt = v / nchunk, c = v - bt * nchunk, pb = q0 + bt * kB, last = min(q1, pb + kB) - 1;
         const unsigned sc = (unsigned)min(c * 64 + lane, S - 1);
 #pragma unroll
-        for (int u = 0; u < kB; ++u)
-            r[u] = __builtin_nontemporal_load(
-                reinterpret_cast<const int *>(asg + nr_off<kOff32>((unsigned)min(pb + u, last), (unsigned)S, sc)));
+        for (int u = 0; u < kB; ++u)  // a wave-uniform row base: the load's address is the lane's 32-bit offset
+            r[u] = __builtin_nontemporal_load(assign + (size_t)min(pb + u, last) * S + sc);
+        // the keys' words in one gather: lane l reads pod pb + l % 16's scenario 0
+        // (l < 16), 21 (l < 32) or 42 (kMaj; S < 43: scenario 0 only)
         const unsigned pk = (unsigned)min(pb + (lane & (kB - 1)), last);
-        kr[0] = *reinterpret_cast<const int *>(asg + nr_off<kOff32>(pk, (unsigned)S, 0u));
-        if (kMaj) {
-            kr[1] = *reinterpret_cast<const int *>(asg + nr_off<kOff32>(pk, (unsigned)S, 21u));
-            kr[2] = *reinterpret_cast<const int *>(asg + nr_off<kOff32>(pk, (unsigned)S, 42u));
-        }
+        const unsigned ks = kMaj ? (lane < kB ? 0u : lane < 2 * kB ? 21u : 42u) : 0u;
+        kr[0] = *reinterpret_cast<const int *>(asg + nr_off<kOff32>(pk, (unsigned)S, ks));
     };
     auto examine = [&](int v, const int (&r)[kB], const int (&kr)[3]) {
         const int bt = v / nchunk, c = v - bt * nchunk, pb = q0 + bt * kB, nb = min(kB, q1 - pb);
         int kv = kr[0];  // lane u < 16: pod pb + u's key
-        if (kMaj) kv = (kv == kr[1] || kv == kr[2]) ? kv : (kr[1] == kr[2] ? kr[1] : kv);
+        if (kMaj) {
+            const int k1 = __shfl(kr[0], lane + kB, 64), k2 = __shfl(kr[0], lane + 2 * kB, 64);
+            kv = (kv == k1 || kv == k2) ? kv : (k1 == k2 ? k1 : kv);
+        }
         kv = (unsigned)kv < (unsigned)N ? kv : N;
         if (c == 0 && lane < nb) {
             pkey[pb + lane] = kv;
@@ -521,7 +522,8 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
         // the units with any such lane (an OR over the wave)
         unsigned dev = 0u;
 #pragma unroll
-        for (int u = 0; u < kB; ++u) dev |= (live && r[u] != __builtin_amdgcn_readlane(kv, u)) ? 1u << u : 0u;
+        for (int u = 0; u < kB; ++u) dev |= (unsigned)(r[u] != __builtin_amdgcn_readlane(kv, u)) << u;
+        dev = live ? dev : 0u;  // (one select: a per-lane branch per row costs exec-mask juggling)
         unsigned D = dev;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) D |= (unsigned)__shfl_xor((int)D, o, 64);
@@ -553,10 +555,10 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
         // examined unit's first uses of its keys above the next unit's loads)
         for (int v = 0; v < nv; v += 2) {
             load(v + 1, rb, kb);
-            asm volatile("" : "+v"(ka[0]), "+v"(ka[1]), "+v"(ka[2])::"memory");
+            asm volatile("" : "+v"(ka[0])::"memory");
             examine(v, ra, ka);
             load(v + 2, ra, ka);
-            asm volatile("" : "+v"(kb[0]), "+v"(kb[1]), "+v"(kb[2])::"memory");
+            asm volatile("" : "+v"(kb[0])::"memory");
             if (v + 1 < nv) examine(v + 1, rb, kb);
         }
     }
@@ -631,7 +633,7 @@ __global__ __launch_bounds__(kNrThreads) void nr_place_kernel(const int *__restr
     __shared__ int wsum[kNrThreads / 64];
     const int b = nr_block(nblk);
     if (b >= nblk) return;
-    const int t = (int)threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int t = (int)threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);  // (uniform)
     const int nh = nbk * (1 + nchunk);
     int *lc = cur + nh, *lk = lc + kNrPods;
     long long *lm = reinterpret_cast<long long *>(lk + kNrPods + (nh & 1));  // 8-B aligned
@@ -1435,7 +1437,8 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
         const unsigned g8 = (unsigned)(8 * ceil_div(nblk, 8));  // (nr_block: XCD runs of consecutive blocks)
         sc<<<g8, kNrThreads, (size_t)nh * 4, ctx->stream>>>(d_assign, P, S, N, nbk, nchunk, nblk, ecap, pkey, bh, ent,
                                                              ecount);
-        auto *cs = nblk <= 64 * 8 ? &nr_colscan_kernel<8> : &nr_colscan_kernel<0>;
+        auto *cs = nblk <= 64 * 8 ? &nr_colscan_kernel<8>
+                   : nblk <= 64 * 16 ? &nr_colscan_kernel<16> : &nr_colscan_kernel<0>;
         cs<<<(unsigned)ceil_div(nh, 4), 256, 0, ctx->stream>>>(bh, (int)nh, nblk, tot);
         const size_t pl = (size_t)nh * 4 + 8 + (size_t)kNrPods * (d_ms ? 16 : 8);
         auto *pk = d_ms ? &nr_place_kernel<true> : &nr_place_kernel<false>;

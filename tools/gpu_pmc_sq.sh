@@ -1,10 +1,10 @@
 #!/bin/bash
-# SQ / TA counter passes on the headline bench (one rocprofv3 --pmc run per group).
+# SQ / TA counter passes on the headline bench, or on SQ_CMD (one rocprofv3 --pmc run per group).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out/sq gpurun_out/sq_abl "${SQ_OUT:-gpurun_out/sq}"
 export TMPDIR=/tmp RSK_OVERLAP=0
 OUT=${SQ_OUT:-gpurun_out/sq}
-B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline"
+B=${SQ_CMD:-"python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline"}
 pass() {  # pass <name> <counters...>
     local name=$1; shift
     timeout -s KILL 120 rocprofv3 --pmc "$@" -d $OUT -o "$name" -f csv -- $B > "$OUT/$name.log" 2>&1
