@@ -1412,6 +1412,9 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
     RSK_TRY(stage_out(ctx, 3, pod_count, NS * 4, dev, reinterpret_cast<void **>(&d_cnt)));
     RSK_TRY(stage_out(ctx, 4, cpu_sum, NS * 8, dev, reinterpret_cast<void **>(&d_cs)));
     if (mem_sum) RSK_TRY(stage_out(ctx, 5, mem_sum, NS * 8, dev, reinterpret_cast<void **>(&d_ms)));
+    RSK_TRY(ws_check_ptr(d_cs, "cpu_sum"));  // (u64 stores and atomics)
+    if (d_ms) RSK_TRY(ws_check_ptr(d_ms, "mem_sum"));
+    if (d_mem) RSK_TRY(ws_check_ptr(d_mem, "pod_mem"));
     const int nbk = (int)ceil_div(N, kNrBucketNodes), nchunk = (int)ceil_div(S, 64);
     const int64_t nh = (int64_t)nbk * (1 + nchunk);  // a block's counters: key buckets + entry bins
     if (PS && S >= 32 && S <= kNrMaxS && nh <= kNrMaxCounters) {  // the deviation form

@@ -1036,3 +1036,39 @@ def test_car_big_rows_direct_cells_edge_cases(ctx):
     T = t0.reshape(P, S)
     assert (T[:6, 2] == -2).all() and (T[:6, 3] == 7).all() and np.isin(T[:6, 4:6], (10, 11)).all()
     assert (T[:6, 1] == free.min()).all()
+
+
+def test_node_reduce_rejects_misaligned_u64_outputs(ctx):
+    """rsk_node_reduce stores (and, for an overflowing block, atomically adds)
+    64-bit sums: a cpu_sum / mem_sum / pod_mem device pointer that is not 8-B
+    aligned is an argument error naming the buffer, before any launch (the
+    r04p2 fault class); the aligned call still matches the oracle."""
+    import torch
+    from oracle import oracle as orc
+    from rsk import _lib
+    dev = torch.device("cuda:0")
+    P, N, S = 3000, 100, 64
+    rng = np.random.default_rng(11)
+    a = np.repeat(rng.integers(0, N, P)[:, None], S, axis=1).astype(np.int32)
+    pc = rng.integers(1, 500, P).astype(np.int32)
+    pm = rng.integers(1, 1 << 30, P).astype(np.int64)
+    T = lambda x: torch.from_numpy(x).to(dev)  # noqa: E731
+    ta, tpc, tpm = T(a.reshape(-1)), T(pc), T(pm)
+    cnt = torch.empty(N * S, dtype=torch.int32, device=dev)
+    big = torch.empty(N * S + 1, dtype=torch.int64, device=dev)   # + 4 B: misaligned views
+    mem = torch.empty(N * S, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)  # (the context's own stream reads what torch's stream wrote)
+    L, h = ctx.lib, ctx.handle
+    for bad, name in ((0, "cpu_sum"), (1, "mem_sum")):
+        cs = big.data_ptr() + 4 if bad == 0 else big.data_ptr()
+        ms = big.data_ptr() + 4 if bad == 1 else mem.data_ptr()
+        rc = L.rsk_node_reduce(h, ta.data_ptr(), P, S, tpc.data_ptr(), tpm.data_ptr(), N, cnt.data_ptr(), cs, ms,
+                               _lib.RSK_F_DEVICE)
+        assert rc != 0 and name in _lib.last_error()
+    cs = torch.empty(N * S, dtype=torch.int64, device=dev)
+    _lib.check(L.rsk_node_reduce(h, ta.data_ptr(), P, S, tpc.data_ptr(), tpm.data_ptr(), N, cnt.data_ptr(),
+                                 cs.data_ptr(), mem.data_ptr(), _lib.RSK_F_DEVICE))
+    torch.cuda.synchronize(dev)
+    exp = orc.node_reduce(a.reshape(-1), P, S, pc, pm, N)
+    assert np.array_equal(cnt.cpu().numpy(), exp[0]) and np.array_equal(cs.cpu().numpy(), exp[1])
+    assert np.array_equal(mem.cpu().numpy(), exp[2])
