@@ -115,7 +115,11 @@ __global__ __launch_bounds__(kPrep0Threads) void car_prep_small_kernel(const int
 // (non-hazard count, packed max of (rem, ~node)) is reduced in LDS per
 // workgroup first — threads of one workgroup that share a scenario meet in one
 // LDS slot — so a scenario receives one global atomic per workgroup.
-template <int V, bool kCode, bool kKey, int kBlock = 256>
+// kGrp (kBlock 256, SV % 64 == 0): a workgroup takes 64 vector slots x 4 node
+// chunks instead of 256 slots x 1 chunk, so its LDS reduction folds 4 chunks
+// and a scenario's zero-case words receive 4x fewer global atomics (the
+// slots' loads stay 64 consecutive 16-B words per wave).
+template <int V, bool kCode, bool kKey, int kBlock = 256, bool kGrp = false>
 __global__ __launch_bounds__(kBlock) void car_prep_kernel(const int *__restrict__ cap, const typename VecT<V>::I *__restrict__ use,
                                                        const typename VecT<V>::H *__restrict__ haz, int N, int SV,
                                                        int npb, unsigned total, typename VecT<V>::C *__restrict__ code,
@@ -123,11 +127,17 @@ __global__ __launch_bounds__(kBlock) void car_prep_kernel(const int *__restrict_
                                                        int *__restrict__ zc_cnt, unsigned long long *__restrict__ zc_key,
                                                        unsigned *__restrict__ zc_clear, int clear_words) {
     // kBlock 1024 only with SV <= 256: the slots never exceed 256
+    static_assert(!kGrp || kBlock == 256, "grouped prep: 4 waves = 4 chunks");
     __shared__ int lcnt[256 * V];
     __shared__ unsigned long long lkey[256 * V];
     const unsigned t = blockIdx.x * (unsigned)kBlock + threadIdx.x;
-    const unsigned base = (blockIdx.x * (unsigned)kBlock) % (unsigned)SV;  // vector slot of thread 0
-    const int nslot = min(256, SV);
+    // vt: the thread's (chunk * SV + slot) work index; base: the vector slot of its LDS slot 0
+    const unsigned gpr = kGrp ? (unsigned)SV / 64u : 1u;
+    const unsigned vt = kGrp ? ((blockIdx.x / gpr) * 4u + (threadIdx.x >> 6)) * (unsigned)SV +
+                                   (blockIdx.x % gpr) * 64u + (threadIdx.x & 63u)
+                             : t;
+    const unsigned base = kGrp ? (blockIdx.x % gpr) * 64u : (blockIdx.x * (unsigned)kBlock) % (unsigned)SV;
+    const int nslot = kGrp ? 64 : min(256, SV);
     for (int i = threadIdx.x; i < nslot * V; i += kBlock) { lcnt[i] = 0; lkey[i] = 0ull; }
     __syncthreads();
     __shared__ int red[kBlock / 64];
@@ -138,9 +148,9 @@ __global__ __launch_bounds__(kBlock) void car_prep_kernel(const int *__restrict_
         const unsigned z[V] = {};
         code[(size_t)N * SV + t] = cvec_make(z);
     }
-    if (t < total) {
-        const int sv = (int)(t % (unsigned)SV);
-        const int n0 = (int)(t / (unsigned)SV) * npb;
+    if (vt < total) {
+        const int sv = (int)(vt % (unsigned)SV);
+        const int n0 = (int)(vt / (unsigned)SV) * npb;
         const int n1 = min(N, n0 + npb);
         int cnt[V];
         unsigned long long best[V];
@@ -183,24 +193,26 @@ __global__ __launch_bounds__(kBlock) void car_prep_kernel(const int *__restrict_
         }
 }
 
-template <int V, int kBlock = 256>
+template <int V, int kBlock = 256, bool kGrp = false>
 static int prep_launch(hipStream_t stream, const Prep16Args &a, int SV, int npb, unsigned total) {
     typedef typename VecT<V>::I I;
     typedef typename VecT<V>::H H;
     typedef typename VecT<V>::C C;
-    const dim3 grid((unsigned)ceil_div(total, kBlock)), block(kBlock);
+    // kGrp: (SV / 64) workgroups per 4 node chunks
+    const dim3 grid(kGrp ? (unsigned)(SV / 64 * ceil_div(ceil_div(total, SV), 4)) : (unsigned)ceil_div(total, kBlock)),
+        block(kBlock);
     const I *use = reinterpret_cast<const I *>(a.use);
     const H *haz = reinterpret_cast<const H *>(a.haz);
     C *code = reinterpret_cast<C *>(a.code);
     I *key = reinterpret_cast<I *>(a.nodekey);
     if (a.code && a.nodekey)
-        car_prep_kernel<V, true, true, kBlock><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
+        car_prep_kernel<V, true, true, kBlock, kGrp><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
                                                                  a.zc_clear, a.clear_words);
     else if (a.code)
-        car_prep_kernel<V, true, false, kBlock><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
+        car_prep_kernel<V, true, false, kBlock, kGrp><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
                                                                  a.zc_clear, a.clear_words);
     else
-        car_prep_kernel<V, false, true, kBlock><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
+        car_prep_kernel<V, false, true, kBlock, kGrp><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
                                                                  a.zc_clear, a.clear_words);
     RSK_HIP(hipGetLastError());
     return RSK_OK;
@@ -241,6 +253,8 @@ static int launch_prep_main(hipStream_t stream, const Prep16Args &a) {
     const int npb = (int)std::max<int64_t>(1, ceil_div((int64_t)a.N * SV, target_threads));
     const int64_t chunks = ceil_div(a.N, npb);
     const unsigned total = (unsigned)(chunks * SV);
+    if (SV % 64 == 0)
+        return v4 ? prep_launch<4, 256, true>(stream, a, SV, npb, total) : prep_launch<1, 256, true>(stream, a, SV, npb, total);
     return v4 ? prep_launch<4>(stream, a, SV, npb, total) : prep_launch<1>(stream, a, SV, npb, total);
 }
 
