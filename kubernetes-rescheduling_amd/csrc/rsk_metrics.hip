@@ -463,10 +463,12 @@ __device__ __forceinline__ int nr_block(int nblk) {
 }
 
 // launch 1: a wave walks its pods' (batch of 16, chunk) units, the next unit's
-// 16 rows (and the 16 pods' scenario 0 / 21 / 42 words: their keys, one per
-// lane) loaded while one is examined.  A unit's test is one compare and a
-// ballot; only units with deviations (~half of the bench's rows) write
-// entries, into the wave's own eighth of the block's region.  Counters ->
+// 16 rows (wave-uniform row pointers) and the 16 pods' scenario 0 / 21 / 42
+// words (one gather: lane l reads pod l % 16's word l / 16; the majority by
+// two shuffles) loaded while one is examined.  A row's test is one compare
+// folded into a per-lane bit mask, one wave OR per batch; only rows with a
+// deviating lane (~half of the bench's) write entries, into the wave's own
+// eighth of the block's region.  Counters ->
 // bh[j * nblk + b] (the entry bins zeroed when a wave overflowed), the waves'
 // entry counts (-1: the block overflowed) -> ecount[b * 8 + w].
 template <bool kOff32, bool kMaj, int kB = kNrBatch>
