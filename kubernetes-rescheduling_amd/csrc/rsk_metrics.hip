@@ -433,8 +433,8 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(const int *__restrict_
 //    deviation cells are added here, after the stores, by global atomics.
 // podmonitor.py:104-121 (pods grouped by node), nodemonitor.py:24-46 (per-node
 // sums).  Integer sums: the result does not depend on any order.
-constexpr int kNrPods = 4096;     // pods per block of the scan / place / spill launches
-constexpr int kNrThreads = 1024;  // their threads: 16 waves of 256 pods
+constexpr int kNrPods = 2048;     // pods per block of the scan / place / spill launches
+constexpr int kNrThreads = 512;   // their threads: 8 waves of 256 pods
 constexpr int kNrBatch = 16;      // assign rows per batch (two batches in flight per wave)
 constexpr int kNrBucketBits = 5, kNrBucketNodes = 1 << kNrBucketBits;  // nodes per bucket
 constexpr int kNrMaxCounters = 16384;  // buckets + bins: a block's counters in LDS (N < 2^19)
@@ -1447,9 +1447,6 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
         cs<<<(unsigned)ceil_div(nh, 4), 256, 0, ctx->stream>>>(bh, (int)nh, nblk, tot);
         const size_t pl = (size_t)nh * 4 + 8 + (size_t)kNrPods * (d_ms ? 16 : 8);
         auto *pk = d_ms ? &nr_place_kernel<true> : &nr_place_kernel<false>;
-        if (pl > 64 * 1024)
-            RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(pk), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)pl));
         pk<<<g8, kNrThreads, pl, ctx->stream>>>(pkey, P, N, nbk, nchunk, nblk, bh, tot, base, d_cpu, lmem, ent, ecap,
                                                 ecount, rec);
         auto *sk = d_ms ? &nr_sum_kernel<true> : &nr_sum_kernel<false>;
