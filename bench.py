@@ -223,7 +223,7 @@ def alg_bytes(kernel, P, N, S, info, step_bytes=0):
             "car_direct": step_bytes}.get(kernel, 0)
 
 
-def bench_rounds(args, cfg, world, rank, local, dev):
+def bench_rounds(args, cfg, world, rank, local, dev):  # noqa: C901
     """Config 5: one step = one round of detect -> evict -> CAR -> update over
     this rank's S scenarios.  The timed region is ONE rsk_rounds_run call of R =
     --steps rounds (default 256, config 5's R) with the state on the device; the
@@ -298,6 +298,7 @@ def bench_rounds(args, cfg, world, rank, local, dev):
             ms, n = ctx.kernel_time(name)
             if n:
                 kernels[name] = {"avg_ms": ms / n, "launches": n, "per_step_ms": ms / args.steps}
+    line = None
     if rank == 0:
         line = {
             "metric": cfg["metric"],
@@ -317,11 +318,9 @@ def bench_rounds(args, cfg, world, rank, local, dev):
                              f"start state ({parity_s:.1f} s on {cpu_threads()[0]} threads)",
             "rccl_world": args.rccl_world, "env": rsk_env(),
         }
-        print(json.dumps(line), flush=True)
     rounds.close()
     ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
+    return line if rank == 0 else None
 
 
 def main():
@@ -341,6 +340,8 @@ def main():
                     help="time the steps without per-kernel HIP events")
     ap.add_argument("--pmc-json", default=PMC_JSON,
                     help="per-config PMC traffic (tools/pmc_summary.py, FETCH_SIZE x2-corrected)")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="the headline line only (skip the secondary configs 2 / 4 / 5 of the default run)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU-only rehearsal of the multi-rank skeleton over gloo (no GPU, no librsk)")
     args = ap.parse_args()
@@ -376,17 +377,83 @@ def main():
     dev = torch.device("cuda", local)
     args.rccl_world = dist.get_world_size() if world > 1 else 1
 
-    from rsk import _lib, api, synth
-    from rsk import dist as rdist
-
-    cfg = dict(CONFIGS[args.config])
+    cfg = dict(CONFIGS[args.config], key=args.config)
     if args.scenarios:
         cfg["S"] = args.scenarios
-    P, N, S = cfg["P"], cfg["N"], cfg["S"]
+    line = run_config(args, cfg, world, rank, local, dev)
+    # the secondary configs (BASELINE configs 2, 4 and 5, and config 5's per-rank
+    # share at 8 GPUs), each with its own timing, parity and roofline, after the
+    # headline's timed region and parity sample; the headline keys stay the
+    # config-3 line's.  One GPU only: at N > 1 the line is the headline's alone.
+    if args.config == "headline" and not args.scenarios and world == 1 and not args.no_extra:
+        line["configs"] = extra_configs(args, world, rank, local, dev)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# Secondary legs of the default run: (block name, config, overrides).  Steps and
+# warm-up are each config's own defaults (config 5: one call of R = 256 rounds).
+EXTRA_LEGS = (
+    ("config2", "2k64", {}),
+    ("config4", "1m50k", {}),
+    ("config5", "rounds", {}),
+    ("config5_rank_share_8gpu", "rounds", {"S": 128}),
+)
+
+
+def extra_configs(args, world, rank, local, dev):
+    """Run EXTRA_LEGS one after another in this process (inputs regenerated per
+    leg, the previous leg's device memory released first) and return their
+    lines by block name.  A leg that raises is recorded with its error and the
+    others still run."""
+    import copy
+    import gc
+    import traceback
+    import torch
+    out = {}
+    for name, key, over in EXTRA_LEGS:
+        a = copy.copy(args)
+        a.steps, a.warmup, a.no_cpu_baseline, a.row_rounds = 20, 3, True, 256
+        if key == "rounds":
+            a.steps = 256
+        cfg = dict(CONFIGS[key], key=key, **over)
+        t0 = time.perf_counter()
+        try:
+            ln = run_config(a, cfg, world, rank, local, dev)
+        except Exception as e:  # recorded, not fatal: the headline line still prints
+            ln = {"error": f"{type(e).__name__}: {e}", "traceback": traceback.format_exc()[-2000:]}
+        gc.collect()
+        torch.cuda.empty_cache()
+        if ln is not None:
+            ln.pop("env", None)
+            ln["leg_wall_s"] = round(time.perf_counter() - t0, 2)
+            if "S" in over:
+                ln["note"] = (f"config 5 at S = {over['S']} scenarios on one GPU: its per-rank share when the "
+                              "1024 scenarios are sharded over 8 GPUs (DESIGN §6, what the split buys)")
+            out[name] = ln
+        log(f"[bench] leg {name}: {time.perf_counter() - t0:.1f}s")
+    return out
+
+
+def run_config(args, cfg, world, rank, local, dev):
     if cfg.get("rounds"):
         if args.steps_default:
             args.steps = 256   # config 5's R: one rsk_rounds_run call of 256 rounds
         return bench_rounds(args, cfg, world, rank, local, dev)
+    return bench_car(args, cfg, world, rank, local, dev)
+
+
+def bench_car(args, cfg, world, rank, local, dev):  # noqa: C901
+    """One CAR config (headline, 2k64, 1m50k): the timed steps, the per-kernel
+    breakdown, roofline, parity sample and, for config 4, the row-sharded rounds
+    and kernel 3.  Returns rank 0's line (None on other ranks)."""
+    import torch
+    import torch.distributed as dist
+    from rsk import _lib, api, synth
+    from rsk import dist as rdist
+    P, N, S = cfg["P"], cfg["N"], cfg["S"]
     by_rows = (args.shard or cfg.get("shard", "scenarios")) == "rows"
     t0 = time.time()
     if by_rows:  # pod-row sharding: full assign replica, a contiguous row range per rank
@@ -628,7 +695,7 @@ def main():
                 "cut_cost": 4 * (P + 1) + 4 * c.nnz + 4 * P * S + 4 * c.nnz * S}
         try:
             with open(args.pmc_json) as f:
-                pmc3 = json.load(f).get("kernel3", {}).get(args.config, {})
+                pmc3 = json.load(f).get("kernel3", {}).get(cfg['key'], {})
         except (OSError, ValueError):
             pmc3 = {}
         for name in ("node_reduce", "load_std", "cut_cost"):
@@ -652,7 +719,9 @@ def main():
         k3_leg["parity_node_reduce_ok"] = bool(np.array_equal(cnt.cpu().numpy(), ecnt)
                                                and np.array_equal(cs.cpu().numpy(), ecpu)
                                                and np.array_equal(ms_.cpu().numpy(), emem))
-        k3_leg["parity_load_std_max_rel"] = float(np.max(np.abs(std.cpu().numpy() / estd - 1.0)))
+        gstd = std.cpu().numpy()   # relative error; an all-equal batch (std 0) must match exactly
+        k3_leg["parity_load_std_max_rel"] = float(np.max(np.where(estd == 0, np.where(gstd == 0, 0.0, np.inf),
+                                                                  np.abs(gstd - estd) / np.where(estd == 0, 1, estd))))
         k3_leg["parity_cut_cost_ok"] = bool(np.array_equal(cut.cpu().numpy(), ecut))
         k3_leg["parity_sample_ok"] = bool(k3_leg["parity_node_reduce_ok"] and k3_leg["parity_cut_cost_ok"]
                                           and k3_leg["parity_load_std_max_rel"] <= 1e-9)
@@ -672,10 +741,18 @@ def main():
         try:
             with open(args.pmc_json) as f:
                 pmc = json.load(f)
-            entry = pmc.get("configs", {}).get(args.config, {}).get(dom)
+            entry = pmc.get("configs", {}).get(cfg['key'], {}).get(dom)
             if entry and entry.get("S") == S:
                 roof["traffic"] = entry["hbm_bytes_per_launch"]
                 roof["traffic_source"] = f"{os.path.relpath(args.pmc_json, REPO)} ({entry['source']})"
+                roof["traffic_over_algorithmic"] = round(entry["hbm_bytes_per_launch"] / bytes_per_launch, 4)
+                if entry.get("avg_us"):   # the same kernel's rocprofv3 kernel-trace average in the cited profile
+                    roof["rocprof_avg_us"] = entry["avg_us"]
+                    roof["frac_rocprof"] = round(bytes_per_launch / (entry["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+                    roof["frac_note"] = ("frac: algorithmic bytes / this run's HIP-event average of the kernel inside "
+                                         "the timed region; frac_rocprof: the same bytes / rocprof_avg_us, the "
+                                         "rocprofv3 --kernel-trace --stats average in traffic_source (a builder run "
+                                         "of the same library)")
         except (OSError, ValueError, KeyError):
             pass
     for k, v in kernels.items():
@@ -711,6 +788,7 @@ def main():
                "cgroup_cpu_quota": cgroup_cpu_quota(), "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
                "legs": python_legs(c, N, S)}
 
+    line = None
     if rank == 0:
         line = {
             "metric": cfg["metric"], "value": round(value, 1), "unit": "pod×node evals/s", "n_gpus": world,
@@ -731,11 +809,9 @@ def main():
             line["kernel3"] = k3_leg
             line["allgather_ms_per_step"] = None if gather_ms is None else round(gather_ms, 4)
             line["end_to_end_ms_per_step"] = round(ms_step + (gather_ms or 0.0), 4)
-        print(json.dumps(line), flush=True)
     plan.close()
     ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
+    return line
 
 
 if __name__ == "__main__":

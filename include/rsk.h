@@ -178,6 +178,16 @@ int32_t rsk_py_randbelow(uint64_t seed, int32_t n);
 int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, const int32_t *pod_cpu,
                     const int64_t *pod_mem, int32_t N, int32_t *pod_count, int64_t *cpu_sum,
                     int64_t *mem_sum, uint32_t flags);
+/* Device write guards (DESIGN.md §6 "r05v"): launches whose write offsets
+ * come from an earlier launch's counts check them against their buffer and,
+ * on overflow, skip the store and set the context's device error word; the
+ * context's next entry point (a host-pointer call: its own completion) and
+ * rsk_ctx_synchronize return RSK_EHIP naming the kernel.
+ * rsk_selftest_write_guard runs rsk_node_reduce on a small internal batch with
+ * nr_place's record capacity lowered below its pod count: it returns RSK_EHIP
+ * with rsk_last_error() naming nr_place when the guard works, RSK_EINVAL when
+ * it did not fire (test hook; no caller data). */
+int rsk_selftest_write_guard(rsk_ctx *ctx);
 int rsk_cpu_pct(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *cap_cpu, int32_t N, int32_t S,
                 int32_t *out_pct, uint32_t flags);
 int rsk_detect(rsk_ctx *ctx, const int32_t *cpu_pct, int32_t N, int32_t S, int32_t threshold,

@@ -62,6 +62,7 @@ struct rsk_ctx {
     rsk::DevBuf host_stage[12];  // device staging for host-pointer calls
     rsk::DevBuf work[6];         // per-call device workspace
     rsk::PinBuf pin;             // mapped pinned host memory of the single-call paths
+    rsk::PinBuf errw;            // device error word (mapped pinned host memory, rsk::dev_err)
     std::vector<uint8_t> pinned;  // host scratch
 };
 
@@ -84,6 +85,23 @@ int aux_fork(rsk_ctx *ctx, int k);
 int aux_join(rsk_ctx *ctx, int k);
 
 int activate(rsk_ctx *ctx);
+
+// ---- device error word (the r05v fault class) ----
+// A launch whose write offsets come from an earlier launch's counts (nr_place's
+// records, list_fill's base lists) checks every offset against its buffer's
+// capacity; on overflow it skips the store and writes its bit into the
+// context's error word, a plain vector store into mapped pinned host memory
+// (nothing is written on the common path).  activate() — the first step of
+// every entry point — and rsk_ctx_synchronize() read the word: a set bit is
+// RSK_EHIP naming the kernel.  Host-pointer calls read it again after their own
+// completion, so they report their own overflow; a device-pointer call's
+// overflow is reported by the context's next call or synchronize.
+enum DevErr : unsigned {
+    kErrNrPlace = 1u,   // nr_place: a record offset at or past the record buffer
+    kErrListFill = 2u,  // list_fill: a base-list offset at or past P
+};
+unsigned *dev_err(rsk_ctx *ctx);   // the word's device address (allocated on first use; null on failure)
+int check_dev_err(rsk_ctx *ctx);   // RSK_EHIP (and clears the word) when a bit is set
 
 // Host-pointer staging: copy `bytes` from host `src` into context slot `slot`
 // and return the device pointer (or pass a device pointer straight through).

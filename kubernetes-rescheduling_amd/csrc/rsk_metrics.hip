@@ -630,7 +630,8 @@ __global__ __launch_bounds__(kNrThreads) void nr_place_kernel(const int *__restr
                                                               const int *__restrict__ pod_cpu,
                                                               const long long *__restrict__ pod_mem,
                                                               const int2 *__restrict__ ent, size_t ecap,
-                                                              const int *__restrict__ ecount, int4 *__restrict__ rec) {
+                                                              const int *__restrict__ ecount, int4 *__restrict__ rec,
+                                                              int nrec, unsigned *__restrict__ err) {
     extern __shared__ __align__(16) int cur[];
     __shared__ int wsum[kNrThreads / 64];
     const int b = nr_block(nblk);
@@ -678,8 +679,11 @@ __global__ __launch_bounds__(kNrThreads) void nr_place_kernel(const int *__restr
         const int p = p0 + u * kNrThreads + t;
         if (p < p1 && k[u] < N) {
             const int pos = atomicAdd(&cur[k[u] >> kNrBucketBits], 1);
-            rec[pos] = make_int4(k[u] & (kNrBucketNodes - 1), c[u], (int)(unsigned)(unsigned long long)m[u],
-                                 (int)(m[u] >> 32));
+            if ((unsigned)pos < (unsigned)nrec)  // the offsets come from nr_scan's counts: guarded (dev_err)
+                rec[pos] = make_int4(k[u] & (kNrBucketNodes - 1), c[u], (int)(unsigned)(unsigned long long)m[u],
+                                     (int)(m[u] >> 32));
+            else
+                *err = kErrNrPlace;
         }
     }
     // the entries of the block's 8 wave regions, concatenated (-1: overflowed,
@@ -716,11 +720,13 @@ __global__ __launch_bounds__(kNrThreads) void nr_place_kernel(const int *__restr
                 const int mlo = (int)(unsigned)(unsigned long long)mm, mhi = (int)(mm >> 32);
                 if (node < N) {  // + the pod at its node
                     const int pos = atomicAdd(&cur[nbk + (node >> kNrBucketBits) * nchunk + (sc >> 6)], 1);
-                    rec[pos] = make_int4((node & (kNrBucketNodes - 1)) | lane, lc[lp], mlo, mhi);
+                    if ((unsigned)pos < (unsigned)nrec) rec[pos] = make_int4((node & (kNrBucketNodes - 1)) | lane, lc[lp], mlo, mhi);
+                    else *err = kErrNrPlace;
                 }
                 if (key < N) {  // - the pod at its key node
                     const int pos = atomicAdd(&cur[nbk + (key >> kNrBucketBits) * nchunk + (sc >> 6)], 1);
-                    rec[pos] = make_int4((key & (kNrBucketNodes - 1)) | 32 | lane, lc[lp], mlo, mhi);
+                    if ((unsigned)pos < (unsigned)nrec) rec[pos] = make_int4((key & (kNrBucketNodes - 1)) | 32 | lane, lc[lp], mlo, mhi);
+                    else *err = kErrNrPlace;
                 }
             }
         }
@@ -1396,9 +1402,11 @@ int rsk_random_place(rsk_ctx *ctx, const uint8_t *hazard, int32_t N, int32_t S, 
     return RSK_OK;
 }
 
-int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, const int32_t *pod_cpu,
-                    const int64_t *pod_mem, int32_t N, int32_t *pod_count, int64_t *cpu_sum, int64_t *mem_sum,
-                    uint32_t flags) {
+// rec_limit >= 0 (rsk_selftest_write_guard only): nr_place's record capacity
+// lowered to it, so its write guard must fire
+static int node_reduce_impl(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, const int32_t *pod_cpu,
+                            const int64_t *pod_mem, int32_t N, int32_t *pod_count, int64_t *cpu_sum, int64_t *mem_sum,
+                            uint32_t flags, int64_t rec_limit) {
     RSK_TRY(activate(ctx));
     RSK_CHECK(P >= 0 && S > 0 && N > 0 && (int64_t)N * S < INT32_MAX, "bad sizes");
     RSK_CHECK(pod_count && cpu_sum && pod_cpu && (!mem_sum || pod_mem), "null argument");
@@ -1419,12 +1427,14 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
     if (d_mem) RSK_TRY(ws_check_ptr(d_mem, "pod_mem"));
     const int nbk = (int)ceil_div(N, kNrBucketNodes), nchunk = (int)ceil_div(S, 64);
     const int64_t nh = (int64_t)nbk * (1 + nchunk);  // a block's counters: key buckets + entry bins
-    if (PS && S >= 32 && S <= kNrMaxS && nh <= kNrMaxCounters) {  // the deviation form
-        const int nblk = (int)ceil_div(P, kNrPods);
-        const int64_t ncnt = nh * nblk;
-        const size_t ecap = ((size_t)kNrPods * S / kNrEntDiv + 64) & ~(size_t)63;  // a block's entry region (8 waves')
-        const int64_t nrec = (int64_t)P + 2 * (int64_t)nblk * (int64_t)ecap;  // pod records + 2 per entry
-        RSK_CHECK(ncnt < INT32_MAX / 2 && nrec < INT32_MAX, "node_reduce grouping too large");
+    // the deviation form while its counters and records have 32-bit offsets
+    // (larger batches take the atomic form below, which handles any size)
+    const int nblk = (int)ceil_div(P, kNrPods);
+    const int64_t ncnt = nh * nblk;
+    const size_t ecap = ((size_t)kNrPods * S / kNrEntDiv + 64) & ~(size_t)63;  // a block's entry region (8 waves')
+    const int64_t nrec = (int64_t)P + 2 * (int64_t)nblk * (int64_t)ecap;  // pod records + 2 per entry
+    unsigned *derr = dev_err(ctx);
+    if (PS && S >= 32 && S <= kNrMaxS && nh <= kNrMaxCounters && ncnt < INT32_MAX / 2 && nrec < INT32_MAX && derr) {
         const size_t kb = ((size_t)P * 4 + 15) & ~(size_t)15;
         RSK_TRY(ctx->work[0].reserve(kb + (size_t)nrec * 16));  // keys, then the records
         RSK_TRY(ctx->work[1].reserve(((size_t)ncnt + 2 * (size_t)nh + 1 + (size_t)nblk * (kNrThreads / 64)) * 4));
@@ -1440,15 +1450,24 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
         auto *sc = o32 ? (maj ? &nr_scan_kernel<true, true> : &nr_scan_kernel<true, false>)
                        : (maj ? &nr_scan_kernel<false, true> : &nr_scan_kernel<false, false>);
         const unsigned g8 = (unsigned)(8 * ceil_div(nblk, 8));  // (nr_block: XCD runs of consecutive blocks)
-        sc<<<g8, kNrThreads, (size_t)nh * 4, ctx->stream>>>(d_assign, P, S, N, nbk, nchunk, nblk, ecap, pkey, bh, ent,
-                                                             ecount);
+        // dynamic LDS above 64 KiB needs the attribute (nh = 16384 counters: 64 KiB + the static word)
+        const size_t scan_lds = (size_t)nh * 4, pl = (size_t)nh * 4 + 8 + (size_t)kNrPods * (d_ms ? 16 : 8);
+        RSK_CHECK(scan_lds + 64 <= 160 * 1024 && pl + 64 <= 160 * 1024, "node_reduce: %zu / %zu B of LDS", scan_lds, pl);
+        auto *pk = d_ms ? &nr_place_kernel<true> : &nr_place_kernel<false>;
+        if (scan_lds + 64 > 64 * 1024)
+            RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(sc), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)scan_lds));
+        if (pl + 64 > 64 * 1024)
+            RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(pk), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)pl));
+        sc<<<g8, kNrThreads, scan_lds, ctx->stream>>>(d_assign, P, S, N, nbk, nchunk, nblk, ecap, pkey, bh, ent,
+                                                      ecount);
         auto *cs = nblk <= 64 * 8 ? &nr_colscan_kernel<8>
                    : nblk <= 64 * 16 ? &nr_colscan_kernel<16> : &nr_colscan_kernel<0>;
         cs<<<(unsigned)ceil_div(nh, 4), 256, 0, ctx->stream>>>(bh, (int)nh, nblk, tot);
-        const size_t pl = (size_t)nh * 4 + 8 + (size_t)kNrPods * (d_ms ? 16 : 8);
-        auto *pk = d_ms ? &nr_place_kernel<true> : &nr_place_kernel<false>;
         pk<<<g8, kNrThreads, pl, ctx->stream>>>(pkey, P, N, nbk, nchunk, nblk, bh, tot, base, d_cpu, lmem, ent, ecap,
-                                                ecount, rec);
+                                                ecount, rec, (int)(rec_limit >= 0 ? std::min(nrec, rec_limit) : nrec),
+                                                derr);
         auto *sk = d_ms ? &nr_sum_kernel<true> : &nr_sum_kernel<false>;
         sk<<<(unsigned)(nbk * nchunk), kNrSumThreads, 0, ctx->stream>>>(base, nbk, nchunk, rec, N, S, d_cnt, ucs, ums);
         auto *xk = d_ms ? &nr_spill_kernel<true> : &nr_spill_kernel<false>;
@@ -1470,8 +1489,41 @@ int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, c
         RSK_TRY(copy_back(ctx, cpu_sum, d_cs, NS * 8, false));
         if (mem_sum) RSK_TRY(copy_back(ctx, mem_sum, d_ms, NS * 8, false));
         RSK_HIP(hipStreamSynchronize(ctx->stream));
+        RSK_TRY(check_dev_err(ctx));
     }
     return RSK_OK;
+}
+
+int rsk_node_reduce(rsk_ctx *ctx, const int32_t *assign, int32_t P, int32_t S, const int32_t *pod_cpu,
+                    const int64_t *pod_mem, int32_t N, int32_t *pod_count, int64_t *cpu_sum, int64_t *mem_sum,
+                    uint32_t flags) {
+    return node_reduce_impl(ctx, assign, P, S, pod_cpu, pod_mem, N, pod_count, cpu_sum, mem_sum, flags, -1);
+}
+
+int rsk_selftest_write_guard(rsk_ctx *ctx) {
+    RSK_TRY(activate(ctx));
+    constexpr int P = 4096, S = 64, N = 64;
+    std::vector<int32_t> a((size_t)P * S), cpu(P, 1);
+    for (int p = 0; p < P; ++p)
+        for (int s = 0; s < S; ++s) a[(size_t)p * S + s] = (p + (s == 7 && p % 5 == 0)) % N;
+    int32_t *d = nullptr;
+    const size_t ab = (size_t)P * S * 4, ob = (size_t)N * S * 4;
+    RSK_HIP(hipMalloc(&d, ab + (size_t)P * 4 + ob + 2 * ob));
+    int32_t *dc = d + (size_t)P * S, *dn = dc + P;
+    int64_t *ds = reinterpret_cast<int64_t *>(dn + (size_t)N * S);
+    int rc = hipMemcpy(d, a.data(), ab, hipMemcpyHostToDevice) == hipSuccess &&
+                     hipMemcpy(dc, cpu.data(), (size_t)P * 4, hipMemcpyHostToDevice) == hipSuccess
+                 ? RSK_OK
+                 : RSK_EHIP;
+    if (rc == RSK_OK)  // 1,000 records for 4,096 pods: nr_place must skip the rest and raise the word
+        rc = node_reduce_impl(ctx, d, P, S, dc, nullptr, N, dn, ds, nullptr, RSK_F_DEVICE, 1000);
+    if (rc == RSK_OK) rc = hipStreamSynchronize(ctx->stream) == hipSuccess ? check_dev_err(ctx) : RSK_EHIP;
+    (void)hipFree(d);
+    if (rc == RSK_OK) {
+        set_error("rsk_selftest_write_guard: the nr_place guard did not fire");
+        return RSK_EINVAL;
+    }
+    return rc;  // RSK_EHIP naming nr_place: the guard works
 }
 
 int rsk_cpu_pct(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *cap_cpu, int32_t N, int32_t S, int32_t *out_pct,

@@ -423,7 +423,7 @@ __global__ __launch_bounds__(256) void list_fill_kernel(const int *__restrict__ 
                                                         const int *__restrict__ base, int *__restrict__ cur,
                                                         int *__restrict__ pod, int *__restrict__ dcnt,
                                                         const int *__restrict__ pod_cpu, int4 *__restrict__ dlist,
-                                                        int cap) {
+                                                        int cap, unsigned *__restrict__ err) {
     constexpr int kK = 16;  // deviations kept per (wave, lane) in LDS; more: the rows are walked again
     __shared__ int wc[4][64];
     __shared__ int2 keep[4][kK][64];
@@ -434,7 +434,11 @@ __global__ __launch_bounds__(256) void list_fill_kernel(const int *__restrict__ 
     const int ss = min(s, S - 1);
     if (s < 64) {  // the base lists: the first scenario chunk's lanes, a pod each
 #pragma unroll 4
-        for (int p = q0 + lane; p < q1; p += 64) pod[atomicAdd(&cur[base[p]], 1)] = p;
+        for (int p = q0 + lane; p < q1; p += 64) {
+            const int pos = atomicAdd(&cur[base[p]], 1);  // from list_scan's offsets: guarded (dev_err)
+            if ((unsigned)pos < (unsigned)P) pod[pos] = p;
+            else *err = kErrListFill;
+        }
     }
     constexpr int kB = 16;
     int n = 0;
@@ -1269,9 +1273,11 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
             RSK_HIP(hipMemcpyAsync(cntb, r->loff.ptr, (size_t)(N + 1) * 4, hipMemcpyDeviceToDevice, st));
             const int64_t blocks = ceil_div(P, kLF) * ceil_div(S, 64);
             RSK_CHECK(blocks < INT32_MAX, "list grid too large");
+            unsigned *derr = dev_err(ctx);
+            RSK_CHECK(derr, "no device error word (mapped pinned memory)");
             list_fill_kernel<<<(unsigned)blocks, 256, 0, st>>>(d_assign, P, S, N, r->lbase.as<int>(), cntb,
                                                                  r->lpod.as<int>(), r->lcnt.as<int>(),
-                                                                 r->pod_cpu.as<int>(), r->llist.as<int4>(), cap);
+                                                                 r->pod_cpu.as<int>(), r->llist.as<int4>(), cap, derr);
             RSK_HIP(hipGetLastError());
             dl.base = r->lbase.as<int>();
             dl.cnt = r->lcnt.as<int>();
@@ -1343,6 +1349,7 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
             RSK_TRY(copy_back(ctx, out_target, d_target, RS * 4, false));
         }
         RSK_HIP(hipStreamSynchronize(st));
+        RSK_TRY(check_dev_err(ctx));
     }
     return RSK_OK;
 }

@@ -26,7 +26,28 @@ void DevBuf::release() {
 int activate(rsk_ctx *ctx) {
     RSK_CHECK(ctx, "null context");
     RSK_HIP(hipSetDevice(ctx->device));
-    return RSK_OK;
+    return check_dev_err(ctx);
+}
+
+unsigned *dev_err(rsk_ctx *ctx) {
+    if (!ctx->errw.host) {
+        if (ctx->errw.reserve(64) != RSK_OK) return nullptr;
+        *static_cast<volatile unsigned *>(ctx->errw.host) = 0u;
+    }
+    return static_cast<unsigned *>(ctx->errw.dev);
+}
+
+int check_dev_err(rsk_ctx *ctx) {
+    if (!ctx->errw.host) return RSK_OK;
+    volatile unsigned *w = static_cast<volatile unsigned *>(ctx->errw.host);
+    const unsigned e = *w;
+    if (!e) return RSK_OK;
+    *w = 0u;
+    set_error("device write guard: %s%s(offsets from an earlier launch's counts exceeded the buffer; the stores "
+              "were skipped and the results are invalid)",
+              (e & kErrNrPlace) ? "nr_place record offset past its buffer " : "",
+              (e & kErrListFill) ? "list_fill base-list offset past P " : "");
+    return RSK_EHIP;
 }
 
 static hipEvent_t pooled_event(rsk_ctx *ctx) {
@@ -204,6 +225,7 @@ int rsk_ctx_destroy(rsk_ctx *ctx) {
     for (auto &b : ctx->host_stage) b.release();
     for (auto &b : ctx->work) b.release();
     ctx->pin.release();
+    ctx->errw.release();
     for (int i = 0; i < rsk_ctx::kAux; ++i)
         if (ctx->aux[i]) {
             (void)hipStreamSynchronize(ctx->aux[i]);
@@ -225,7 +247,7 @@ int rsk_ctx_set_stream(rsk_ctx *ctx, void *hip_stream) {
 int rsk_ctx_synchronize(rsk_ctx *ctx) {
     RSK_TRY(activate(ctx));
     RSK_HIP(hipStreamSynchronize(ctx->stream));
-    return RSK_OK;
+    return check_dev_err(ctx);
 }
 
 int rsk_ctx_set_profiling(rsk_ctx *ctx, int on) {

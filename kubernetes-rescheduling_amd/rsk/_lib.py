@@ -56,6 +56,7 @@ SIGNATURES = {
     "rsk_random_candidates": (C.c_int, [_vp, _vp, C.c_int32, _vp, _vp]),
     "rsk_random_place": (C.c_int, [_vp, _vp, C.c_int32, C.c_int32, _vp, _vp, C.c_uint32]),
     "rsk_py_randbelow": (C.c_int32, [C.c_uint64, C.c_int32]),
+    "rsk_selftest_write_guard": (C.c_int, [_vp]),
     "rsk_node_reduce": (C.c_int, [_vp, _vp, C.c_int32, C.c_int32, _vp, _vp, C.c_int32, _vp, _vp, _vp, C.c_uint32]),
     "rsk_cpu_pct": (C.c_int, [_vp, _vp, _vp, C.c_int32, C.c_int32, _vp, C.c_uint32]),
     "rsk_detect": (C.c_int, [_vp, _vp, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, C.c_uint32]),

@@ -795,9 +795,10 @@ def test_node_reduce_segmented_vs_oracle(ctx, P, N, S, p_flip):
 def test_node_reduce_deviation_form_edges(ctx, P, N, S):
     """The deviation form of kernel 3's node sums (out = base[key node] +
     per-scenario deviations, podmonitor.py:104-121) against the oracle where
-    its bookkeeping branches: one 4096-pod block with 40 % of its cells
-    redrawn (its entry region overflows: its deviations go through the spill
-    launch) beside blocks that list theirs; pods whose scenario-0 node is
+    its bookkeeping branches: pods 4096-8191 — two of the scan's 2048-pod
+    blocks — with 40 % of their cells redrawn (their entry regions overflow:
+    their deviations go through the spill launch) beside blocks that list
+    theirs; pods whose scenario-0 node is
     redrawn (the key is the majority of scenarios 0 / 21 / 42), pods with no
     key (unscheduled in two of the three), pods unscheduled in scenario 0 only,
     assignments equal to N; 64 chunks per pod (S = 4096) and a partial chunk
@@ -808,7 +809,7 @@ def test_node_reduce_deviation_form_edges(ctx, P, N, S):
     base = rng.integers(0, N, P)
     a = np.repeat(base[:, None], S, axis=1).astype(np.int32)
     flip = rng.random((P, S)) < 0.01
-    flip[4096:8192] = rng.random((4096, S)) < 0.4         # the second block overflows
+    flip[4096:8192] = rng.random((4096, S)) < 0.4         # blocks 2 and 3 (2048 pods each) overflow
     a[flip] = rng.integers(-2, N + 2, int(flip.sum()))
     q = rng.integers(0, P, 300)
     a[q, 0] = rng.integers(0, N, 300)                      # scenario 0 redrawn: key from 21 / 42
@@ -1072,3 +1073,51 @@ def test_node_reduce_rejects_misaligned_u64_outputs(ctx):
     exp = orc.node_reduce(a.reshape(-1), P, S, pc, pm, N)
     assert np.array_equal(cnt.cpu().numpy(), exp[0]) and np.array_equal(cs.cpu().numpy(), exp[1])
     assert np.array_equal(mem.cpu().numpy(), exp[2])
+
+
+@pytest.mark.parametrize("P,N,S", [(20_000, 50_000, 512), (30_000, 150_000, 64)])
+def test_node_reduce_counters_beyond_64k_lds(ctx, P, N, S):
+    """The deviation form with more than 8,192 per-block counters (key buckets
+    + entry bins, nh = ceil(N / 32) * (1 + S / 64)): nh = 14,067 at N = 50k,
+    S = 512 and 9,376 at N = 150k, S = 64, so nr_place's dynamic LDS (4 nh +
+    8 + 2048 * 16 B with memory sums) is 88 KB / 70 KB — above the 64 KB that
+    a launch gets without hipFuncAttributeMaxDynamicSharedMemorySize (ADVICE
+    round 5).  Count / CPU / memory sums against the oracle, with and without
+    memory (podmonitor.py:104-121, nodemonitor.py:24-46)."""
+    from oracle import oracle as orc
+    from rsk import api
+    rng = np.random.default_rng(P + N + S)
+    a = np.repeat(rng.integers(0, N, P)[:, None], S, axis=1).astype(np.int32)
+    flip = rng.random((P, S)) < 0.02
+    a[flip] = rng.integers(-1, N + 1, int(flip.sum()))
+    pod_cpu = rng.integers(1, 900, P).astype(np.int32)
+    pod_mem = rng.integers(1 << 20, 1 << 34, P).astype(np.int64)
+    exp = orc.node_reduce(a.reshape(-1), P, S, pod_cpu, pod_mem, N)
+    for mem in (pod_mem, None):
+        got = api.node_reduce(a.reshape(-1), P, S, pod_cpu, mem, N, ctx=ctx)
+        assert np.array_equal(got[0], exp[0]), "count"
+        assert np.array_equal(got[1], exp[1]), "cpu"
+        if mem is not None:
+            assert np.array_equal(got[2], exp[2]), "mem"
+
+
+def test_write_guard_reports_an_overflowing_scatter(ctx):
+    """The r05v fault class: nr_place writes records at offsets
+    built from nr_scan's counts.  rsk_selftest_write_guard runs node_reduce
+    with the record capacity lowered below the batch's pod count: the guarded
+    stores are skipped (no fault) and the device error word comes back as
+    RSK_EHIP naming nr_place.  The word is cleared once reported: the next call
+    on the same context runs and matches the oracle."""
+    from oracle import oracle as orc
+    from rsk import _lib, api
+    rc = ctx.lib.rsk_selftest_write_guard(ctx.handle)
+    assert rc == _lib.RSK_EHIP, (rc, _lib.last_error())
+    assert "nr_place" in _lib.last_error()
+    P, N, S = 5000, 300, 64
+    rng = np.random.default_rng(5)
+    a = np.repeat(rng.integers(0, N, P)[:, None], S, axis=1).astype(np.int32)
+    a[rng.random((P, S)) < 0.02] = 7
+    pc = rng.integers(1, 500, P).astype(np.int32)
+    got = api.node_reduce(a.reshape(-1), P, S, pc, None, N, ctx=ctx)
+    exp = orc.node_reduce(a.reshape(-1), P, S, pc, np.zeros(P, np.int64), N)
+    assert np.array_equal(got[0], exp[0]) and np.array_equal(got[1], exp[1])

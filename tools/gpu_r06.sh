@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-5 GPU session on one box.  usage: tools/gpu_r05.sh OUTDIR [steps...]
+# GPU session on one box.  usage: tools/gpu_r06.sh OUTDIR [steps...]
 # steps: test (pytest -m gpu), smoke, bench (headline), b2k (config 2),
 #        b1m (config 4), brounds (config 5), prof (rocprof trace + PMC of headline
 #        and 1m50k), profh / prof1m (one config), dropin, nrb (tools/nrbench.py),
 #        nrprof (its kernel trace)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
-out=gpurun_out/${1:-r05}; shift
+out=gpurun_out/${1:-r06}; shift
 mkdir -p "$out"
 export TMPDIR=/tmp
 step() {  # step <name> <seconds> <cmd...>
