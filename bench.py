@@ -328,7 +328,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="headline", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="one config only (default: the headline, config 3, followed by the secondary legs)")
     ap.add_argument("--scenarios", type=int, default=0, help="override S per GPU")
     ap.add_argument("--shard", choices=("scenarios", "rows"), default=None,
                     help="multi-GPU layout (SURVEY §8e): scenario sharding (default; 1m50k: rows)")
@@ -345,6 +346,9 @@ def main():
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU-only rehearsal of the multi-rank skeleton over gloo (no GPU, no librsk)")
     args = ap.parse_args()
+    args.extra = args.config is None and not args.no_extra
+    if args.config is None:
+        args.config = "headline"
     args.steps_default = args.steps is None
     if args.steps is None:
         args.steps = 20
@@ -385,7 +389,7 @@ def main():
     # share at 8 GPUs), each with its own timing, parity and roofline, after the
     # headline's timed region and parity sample; the headline keys stay the
     # config-3 line's.  One GPU only: at N > 1 the line is the headline's alone.
-    if args.config == "headline" and not args.scenarios and world == 1 and not args.no_extra:
+    if args.extra and not args.scenarios and world == 1:
         line["configs"] = extra_configs(args, world, rank, local, dev)
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -308,7 +308,8 @@ struct Tile16Args {
     int img_cells;         // LDS cells of the largest image (rmax * SL); the records follow
     int rec_cap;           // record ints reserved in LDS; the unit counter follows
     int xcd_per;           // tile units per XCD (the XCD-contiguous grid order)
-    int ablate;            // profiling only (RSK_ABLATE_TILE): 1 skip image load, 2 skip scoring
+    int ablate;            // profiling only (RSK_ABLATE_TILE): 1 skip image load, 2 skip scoring, 4 stores only,
+                           // 8 code gathers from one line
     unsigned n_assign, n_out, n_pods, n_recs, n_key;  // element counts (debug bounds build)
 };
 

@@ -595,7 +595,8 @@ __device__ __forceinline__ void t16_rows64(const Tile16Args &a, unsigned *img, i
 #pragma unroll
     for (int u = 0; u < kB; ++u) {
         v[u] = (int)min((unsigned)v[u], N);
-        const unsigned off = __umul24((unsigned)v[u], S2) + sl2;
+        // (profiling ablation 8: every code gather from node 0's line — the code-line traffic by difference)
+        const unsigned off = (RSK_ABL(a) & 8) ? sl2 : __umul24((unsigned)v[u], S2) + sl2;
 #ifdef RSK_DEBUG_BOUNDS
         if (off / 2u >= a.n_key + S) atomicOr(&rsk_dbg16, 8u);
 #endif

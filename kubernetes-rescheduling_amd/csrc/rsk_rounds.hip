@@ -19,6 +19,7 @@
 // ties: the workgroup scans the N nodes of its scenario.
 #include <algorithm>
 #include <climits>
+#include <cstdio>
 #include <vector>
 
 #include "rsk_common.h"
@@ -77,8 +78,46 @@ struct DevLists {
     int cap = 0;
 };
 
+// Per-phase wall clock of the persistent loop (profiling builds only: `make
+// variant NAME=rprof DEFS=-DRSK_ROUNDS_PROF`; the product compiles the marks
+// out).  Thread 0 of a workgroup reads the 100 MHz real-time counter at each
+// phase boundary — after the barrier that ends the phase, so a phase includes
+// waiting for the slowest wave — and accumulates the deltas in LDS; the host
+// prints the sums per (scenario, round) after the call.
+#ifdef RSK_ROUNDS_PROF
+constexpr int kRProfPhases = 10;
+struct PhaseClock {
+    unsigned long long last, acc[kRProfPhases];
+    __device__ __forceinline__ void start() { last = __builtin_amdgcn_s_memrealtime(); }
+    __device__ __forceinline__ void mark(int k) {
+        const unsigned long long n = __builtin_amdgcn_s_memrealtime();
+        acc[k] += n - last;
+        last = n;
+    }
+};
+#define RPROF_MARK(pc, k) do { if ((pc) && threadIdx.x == 0) (pc)->mark(k); } while (0)
+#else
+struct PhaseClock {};
+#define RPROF_MARK(pc, k) ((void)0)
+#endif
+
 __device__ __forceinline__ unsigned long long move_pack(int rem, int n) {  // (rem, -node), 0 = none
     return ((unsigned long long)((unsigned)rem ^ 0x80000000u) << 32) | (unsigned long long)(0x7fffffffu - (unsigned)n);
+}
+
+// wave-wide maxima (every lane active; the result in every lane)
+__device__ __forceinline__ int wv_max(int x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = max(x, __shfl_xor(x, o, 64));
+    return x;
+}
+__device__ __forceinline__ unsigned long long wv_max_u64(unsigned long long x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long y = __shfl_xor(x, o, 64);
+        x = y > x ? y : x;
+    }
+    return x;
 }
 
 // A scenario's node state as car_move_one and blk_update read and update it:
@@ -125,7 +164,8 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
                                              unsigned long long *__restrict__ kdet, int *__restrict__ ev_out,
                                              int *__restrict__ zc_cnt, unsigned long long *__restrict__ zc_key,
                                              int own0, int own1, DevLists dl, int p_direct = -1,
-                                             int old_known = INT_MIN, int cpu_known = INT_MIN) {
+                                             int old_known = INT_MIN, int cpu_known = INT_MIN,
+                                             PhaseClock *pc = nullptr) {
     unsigned *keys = tab, *cnts = tab + H;
     unsigned long long *red64 = reinterpret_cast<unsigned long long *>(tab + 2 * H);  // best
     unsigned *red = tab + 2 * H + 2;                                                   // M, n_at_M, n_free
@@ -147,9 +187,108 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
         return;
     }
     const int b = row_ptr[p], d = row_ptr[p + 1] - b;
+    // the decision (thread 0): the target from the count of nodes at the max
+    // score and the best (rem, -node) among them, then the update
+    auto finish = [&](unsigned nbest, unsigned long long best) {
+        const int rem = (int)((unsigned)(best >> 32) ^ 0x80000000u);
+        const int node = (int)(0x7fffffffu - (unsigned)(best & 0xffffffffu));
+        int t;
+        if (nbest == 0) t = RSK_TARGET_NO_CANDIDATE;  // max() of an empty sequence
+        else if (nbest == 1) t = node;                // the single best, even if overloaded
+        else t = rem >= 0 ? node : RSK_TARGET_NONE;   // largest remaining CPU, None if < 0
+        out_target[s] = t;
+        red[5] = (unsigned)t;  // for the workgroup (the persistent loop), after its next barrier
+        if (kpick) kpick[s] = kdet[s] = 0ull;  // every thread read p long before the last barrier
+        if (zc_cnt) zc_cnt[s] = 0, zc_key[s] = 0ull;
+        if (update && t >= 0) {  // build-defined update: the pod's CPU moves with it
+            const size_t pc = (size_t)p * S + s;
+            // (the persistent loop knows both: the hazard node and the pick key's CPU)
+            const int old = old_known != INT_MIN ? old_known : assign[pc];
+            const int c = cpu_known != INT_MIN ? cpu_known : pod_cpu[p];
+            if ((unsigned)old < (unsigned)N) ns.u(old) -= c;
+            ns.u(t) += c;
+            assign[pc] = t;
+            if (asg16) asg16[pc] = (unsigned short)t;
+            if (dl.base) {  // the pod's entry follows it (one entry per pod off its base node)
+                const int j = *dl.src, q = *dl.cnt;
+                if (q <= dl.cap) {
+                    if (j >= 0) {
+                        dl.list[j].y = t;
+                    } else if (q < dl.cap) {
+                        dl.list[q] = make_int4(p, t, c, 0);
+                        *dl.cnt = q + 1;
+                    } else {
+                        *dl.cnt = dl.cap + 1;  // overflow: full scans from now on
+                    }
+                }
+            }
+        }
+    };
+    // Rows of at most 64 neighbours (a PA tree's pods mostly have 1-3): wave 0
+    // alone, lane = neighbour, no hash and no workgroup barrier — each distinct
+    // candidate node is counted by one ballot (a loop over the distinct nodes),
+    // the max count, the nodes at it and their best (rem, -node) by wave
+    // reductions.  Only a row with no neighbour on a candidate node and no
+    // zero-case words (car_direct, car_move without the loop's detect state)
+    // falls back to the workgroup's scan of every node.
+    if (d <= 64) {  // uniform
+        if (tid < 64) {
+            int x = N;
+            if (d > 0) x = assign[(size_t)col[b + min(tid, d - 1)] * S + s];
+            const bool inN = (unsigned)x < (unsigned)N;
+            const bool v = tid < d && inN && !ns.h(inN ? x : 0);
+            int c = 0;
+            unsigned long long live = __builtin_amdgcn_ballot_w64(v);
+            while (live) {  // uniform: one pass per distinct candidate node
+                const int l = __builtin_ctzll(live);
+                const int xv = __builtin_amdgcn_readlane(x, l);
+                const unsigned long long eq = __builtin_amdgcn_ballot_w64(v && x == xv);
+                if (tid == l) c = __popcll(eq);
+                live &= ~eq;
+            }
+            const int M = wv_max(c);
+            unsigned nb = 0;
+            unsigned long long best = 0ull;
+            if (M > 0) {
+                const bool cand = c == M;
+                nb = (unsigned)__popcll(__builtin_amdgcn_ballot_w64(cand));
+                best = wv_max_u64(cand ? move_pack(cap[x] - ns.u(x), x) : 0ull);
+            } else if (zc_cnt) {  // max score 0: the detect state's zero case of the scenario
+                const unsigned long long z = zc_key[s];
+                nb = (unsigned)zc_cnt[s];
+                best = nb ? move_pack((int)((unsigned)(z >> 32) ^ 0x80000000u), (int)~(unsigned)(z & 0xffffffffull)) : 0ull;
+            }
+            if (M > 0 || zc_cnt) {
+                if (tid == 0) finish(nb, best);
+            } else if (tid == 0) {  // the workgroup's scan below
+                red[1] = 0u;
+                *red64 = 0ull;
+            }
+            if (!zc_cnt && tid == 0) red[3] = M == 0;
+        }
+        if (zc_cnt) return;  // uniform (the caller's barrier publishes red[5] and the update)
+        move_sync<kGlobal>();
+        if (red[3]) {  // uniform: max score 0 and no zero-case words: every non-hazard node ties
+            unsigned long long best = 0;
+            unsigned nb = 0;
+            for (int n = tid; n < N; n += kMoveThreads) {
+                if (ns.h(n)) continue;
+                ++nb;
+                best = max(best, move_pack(cap[n] - ns.u(n), n));
+            }
+            if (nb) {
+                atomicAdd(&red[1], nb);
+                atomicMax(red64, best);
+            }
+            move_sync<kGlobal>();
+            if (tid == 0) finish(red[1], *red64);
+        }
+        return;
+    }
     for (int k = tid; k < 2 * H; k += kMoveThreads) tab[k] = 0u;
     if (tid < 8) tab[2 * H + tid] = 0u;
     move_sync<kGlobal>();
+    RPROF_MARK(pc, 1);
     const unsigned mask = (unsigned)H - 1u;
     // A: count every neighbour on a non-hazard node (kU neighbours per thread
     // in flight: the col, assign and hazard loads of a batch issued together
@@ -178,11 +317,13 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
         }
     }
     move_sync<kGlobal>();
+    RPROF_MARK(pc, 2);
     // B: max count over the slots
     unsigned m = 0;
     for (int h = tid; h < H; h += kMoveThreads) m = max(m, cnts[h]);
     if (m) atomicMax(&red[0], m);
     move_sync<kGlobal>();
+    RPROF_MARK(pc, 3);
     const unsigned M = red[0];
     if (M > 0) {  // C: nodes at the max count -> |best| and the best (rem, -node)
         unsigned long long best = 0;
@@ -219,43 +360,8 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
         }
     }
     move_sync<kGlobal>();
-    if (tid == 0) {
-        const unsigned nbest = red[1];
-        const unsigned long long best = *red64;
-        const int rem = (int)((unsigned)(best >> 32) ^ 0x80000000u);
-        const int node = (int)(0x7fffffffu - (unsigned)(best & 0xffffffffu));
-        int t;
-        if (nbest == 0) t = RSK_TARGET_NO_CANDIDATE;  // max() of an empty sequence
-        else if (nbest == 1) t = node;                // the single best, even if overloaded
-        else t = rem >= 0 ? node : RSK_TARGET_NONE;   // largest remaining CPU, None if < 0
-        out_target[s] = t;
-        red[5] = (unsigned)t;  // for the workgroup (the persistent loop), after its next barrier
-        if (kpick) kpick[s] = kdet[s] = 0ull;  // every thread read p long before the last barrier
-        if (zc_cnt) zc_cnt[s] = 0, zc_key[s] = 0ull;
-        if (update && t >= 0) {  // build-defined update: the pod's CPU moves with it
-            const size_t pc = (size_t)p * S + s;
-            // (the persistent loop knows both: the hazard node and the pick key's CPU)
-            const int old = old_known != INT_MIN ? old_known : assign[pc];
-            const int c = cpu_known != INT_MIN ? cpu_known : pod_cpu[p];
-            if ((unsigned)old < (unsigned)N) ns.u(old) -= c;
-            ns.u(t) += c;
-            assign[pc] = t;
-            if (asg16) asg16[pc] = (unsigned short)t;
-            if (dl.base) {  // the pod's entry follows it (one entry per pod off its base node)
-                const int j = *dl.src, q = *dl.cnt;
-                if (q <= dl.cap) {
-                    if (j >= 0) {
-                        dl.list[j].y = t;
-                    } else if (q < dl.cap) {
-                        dl.list[q] = make_int4(p, t, c, 0);
-                        *dl.cnt = q + 1;
-                    } else {
-                        *dl.cnt = dl.cap + 1;  // overflow: full scans from now on
-                    }
-                }
-            }
-        }
-    }
+    RPROF_MARK(pc, 4);
+    if (tid == 0) finish(red[1], *red64);
 }
 
 // One workgroup per scenario (LDS hash), or kGlobal: a capped grid striding
@@ -723,6 +829,7 @@ struct PersistArgs {
     int blk_lds;                      // the scenario's block row kept in LDS (after the hash when it is there)
     unsigned hash_bytes;              // dynamic LDS of the hash (0: global work areas)
     unsigned cols_off;                // kCols: byte offset of the usage column and hazard bits in the LDS
+    unsigned long long *prof;         // RSK_ROUNDS_PROF builds: [grid][16] per-phase real-time ticks
 };
 
 // kCols: the scenario's usage column and hazard bits live in LDS for its R
@@ -736,6 +843,13 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
     __shared__ int r32[4];
     __shared__ int lsrc, lcnt;  // the scenario's pick source entry and list length
     __shared__ ScnState st;
+#ifdef RSK_ROUNDS_PROF
+    __shared__ PhaseClock pclk;
+    PhaseClock *pc = &pclk;
+    if (threadIdx.x < kRProfPhases) pclk.acc[threadIdx.x] = 0ull;
+#else
+    PhaseClock *pc = nullptr;
+#endif
     unsigned *tab = kGlobal ? gtab + (size_t)blockIdx.x * (size_t)(2 * a.H + 8) : lds;
     const int t = (int)threadIdx.x;
     NodeCols nc;
@@ -797,10 +911,14 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
             a.zc_key[s] = st.zkey;
         }
         auto rounds = [&](const auto &ns) {
+#ifdef RSK_ROUNDS_PROF
+            if (t == 0) pclk.start();
+#endif
             for (int r = 0; r < a.R; ++r) {
                 const unsigned long long kd = st.most;
                 int pcpu;
                 const int p = scn_pick<int>(a.assign, a.pod_cpu, a.P, a.S, s, kd, a.off, a.pod, dl, r64, &lsrc, &pcpu);
+                RPROF_MARK(pc, 0);
                 int *tg_row = a.out_target + (size_t)r * a.S;
                 if (t == 0) a.out_evict[(size_t)r * a.S + s] = p;  // (lsrc: read by car_move_one's thread 0)
                 if (p < 0) {
@@ -810,8 +928,9 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
                 const int o = (int)~(unsigned)(kd & 0xffffffffull);  // the picked pod sits on the hazard node
                 car_move_one<kGlobal>(a.row_ptr, a.col, a.pod_cpu, a.assign, ns, a.cap, nullptr, s, a.S, a.N, a.H, 1,
                                       tg_row, nullptr, tab, nullptr, nullptr, nullptr, a.zc_cnt, a.zc_key, 0, INT_MAX,
-                                      dl, p, o, pcpu);
+                                      dl, p, o, pcpu, pc);
                 move_sync<kGlobal>();  // the move's state update (thread 0) before it is read
+                RPROF_MARK(pc, 5);
                 const int tt = (int)tab[2 * a.H + 7];  // car_move_one's target (red[5])
                 if (tt >= 0) {  // two nodes' CPU changed: their blocks, then the scenario's maxima
                     const int bo = (unsigned)o < (unsigned)a.N ? o / kBlkNodes : -1, bt = tt / kBlkNodes;
@@ -819,7 +938,9 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
                     if (w == 0) blk_update(ns, a.cap, a.N, a.thr, sb, bt, o, tt);
                     if (w == 1 && bo >= 0 && bo != bt) blk_update(ns, a.cap, a.N, a.thr, sb, bo, o, tt);
                     __syncthreads();
+                    RPROF_MARK(pc, 6);
                     scn_reduce(sb, &st, r64, r32);
+                    RPROF_MARK(pc, 7);
                 }
                 if (t == 0) {  // car_move_one zeroes the zero-case words (the launch loop's atomics)
                     a.zc_cnt[s] = st.zcnt;
@@ -827,6 +948,7 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
                 }
                 if (kGlobal) move_sync<true>();  // the area is free before the next round clears it
                 else __syncthreads();
+                RPROF_MARK(pc, 8);
             }
         };
         if constexpr (kCols) {
@@ -837,6 +959,9 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
             rounds(NodeGlobal{a.use, a.haz, a.S, s});
         }
     }
+#ifdef RSK_ROUNDS_PROF
+    if (t < kRProfPhases) a.prof[(size_t)blockIdx.x * 16 + t] = pclk.acc[t];
+#endif
 }
 
 // ---- one-launch CAR for small batches (rsk_car_plan_execute, S <= 4) ----
@@ -1338,8 +1463,36 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         if (lds > 64 * 1024)
             RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)lds));
+#ifdef RSK_ROUNDS_PROF
+        DevBuf profb;
+        RSK_TRY(profb.reserve((size_t)g.grid * 16 * 8));
+        RSK_HIP(hipMemsetAsync(profb.ptr, 0, (size_t)g.grid * 16 * 8, st));
+        pa.prof = profb.as<unsigned long long>();
+#else
+        pa.prof = nullptr;
+#endif
         kern<<<dim3((unsigned)g.grid), dim3(kMoveThreads), lds, st>>>(pa, g.lds ? nullptr : r->gtab.as<unsigned>());
         RSK_HIP(hipGetLastError());
+#ifdef RSK_ROUNDS_PROF
+        {   // the per-phase sums, per (scenario, round), to stderr (experiment builds only)
+            std::vector<unsigned long long> h((size_t)g.grid * 16);
+            RSK_HIP(hipStreamSynchronize(st));
+            RSK_HIP(hipMemcpy(h.data(), profb.ptr, h.size() * 8, hipMemcpyDeviceToHost));
+            static const char *names[kRProfPhases] = {"pick", "move_setup", "move_count", "move_max", "move_best",
+                                                      "move_final", "blk_update", "scn_reduce", "round_tail", "-"};
+            double tot = 0;
+            for (int k = 0; k < kRProfPhases - 1; ++k) {
+                double sum = 0;
+                for (int w = 0; w < g.grid; ++w) sum += (double)h[(size_t)w * 16 + k];
+                const double us = sum * 0.01 / ((double)S * R);  // 100 MHz ticks -> us per (scenario, round)
+                tot += us;
+                fprintf(stderr, "[rounds_prof] %-11s %8.4f us per scenario-round\n", names[k], us);
+            }
+            fprintf(stderr, "[rounds_prof] total       %8.4f us per scenario-round (S=%d R=%d grid=%d)\n", tot, S, R,
+                    g.grid);
+        }
+        profb.release();
+#endif
     }
     if (!dev) {
         if (PS) RSK_TRY(copy_back(ctx, assign, d_assign, PS * 4, false));

@@ -31,6 +31,12 @@ for s in "${@:-test smoke bench}"; do
       abr:*) kv=${w#abr:}; step "abr_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u bench.py --config rounds --no-cpu-baseline ;;
       sb:*) kv=${w#sb:}; step "sb_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_abl.so ${kv//,/ } python -u tools/sidebench.py ;;
       hp:*) step "hostprobe_${w#hp:}" 300 python -u tools/hostprobe.py "${w#hp:}" ;;
+      rprof) step rounds_prof 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_rprof.so python -u bench.py --config rounds --no-cpu-baseline --no-kernel-events ;;
+      rprof128) step rounds_prof128 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_rprof.so python -u bench.py --config rounds --scenarios 128 --no-cpu-baseline --no-kernel-events ;;
+      pmc:*) v=${w#pmc:}; kv=${v#*:}; lib=${v%%:*}; mkdir -p "$out/pmc_$lib"
+             for c in FETCH_SIZE WRITE_SIZE; do
+               step "pmc_${lib}_${c}_${kv//[=,]/_}" 240 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_$lib.so ${kv//,/ } rocprofv3 --pmc $c -d "$out/pmc_$lib/$c${kv//[=,]/_}" -o p -f csv -- python3 bench.py --config headline --steps 10 --warmup 2 --no-cpu-baseline
+             done ;;
       bnoev) step bench_noevents 600 python -u bench.py --no-cpu-baseline --no-kernel-events ;;
       nr:*) kv=${w#nr:}; step "nr_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_abl.so ${kv//,/ } python -u tools/nrbench.py ;;
       nrk:*) kv=${w#nrk:}; step "nrk_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u tools/nrbench.py ;;
