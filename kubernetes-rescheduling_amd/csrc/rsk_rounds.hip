@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "rsk_common.h"
+#include "rsk_wave.h"
 
 struct rsk_rounds {
     rsk_ctx *ctx = nullptr;
@@ -105,20 +106,10 @@ __device__ __forceinline__ unsigned long long move_pack(int rem, int n) {  // (r
     return ((unsigned long long)((unsigned)rem ^ 0x80000000u) << 32) | (unsigned long long)(0x7fffffffu - (unsigned)n);
 }
 
-// wave-wide maxima (every lane active; the result in every lane)
-__device__ __forceinline__ int wv_max(int x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = max(x, __shfl_xor(x, o, 64));
-    return x;
-}
-__device__ __forceinline__ unsigned long long wv_max_u64(unsigned long long x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long y = __shfl_xor(x, o, 64);
-        x = y > x ? y : x;
-    }
-    return x;
-}
+struct ScnState {  // the scenario's detect maxima (LDS)
+    unsigned long long most, zkey;
+    int zcnt;
+};
 
 // A scenario's node state as car_move_one and blk_update read and update it:
 // the global [N][S] usage and hazard arrays at scenario s, or (the persistent
@@ -155,7 +146,7 @@ __device__ __forceinline__ void move_sync() {
 }
 
 template <bool kGlobal, class NS>
-__device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, const int *__restrict__ col,
+__device__ __forceinline__ int car_move_one(const int *__restrict__ row_ptr, const int *__restrict__ col,
                                              const int *__restrict__ pod_cpu, int *assign, const NS &ns,
                                              const int *__restrict__ cap,
                                              const int *__restrict__ evict, int s, int S, int N, int H, int update,
@@ -165,7 +156,10 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
                                              int *__restrict__ zc_cnt, unsigned long long *__restrict__ zc_key,
                                              int own0, int own1, DevLists dl, int p_direct = -1,
                                              int old_known = INT_MIN, int cpu_known = INT_MIN,
-                                             PhaseClock *pc = nullptr) {
+                                             PhaseClock *pc = nullptr, int zs_cnt = -1, unsigned long long zs_key = 0ull) {
+    // returns the target to thread 0 (the persistent loop's wave 0 broadcasts it)
+    // zs_cnt >= 0 (the persistent loop): the scenario's zero case (count, key)
+    // from its LDS detect state instead of the global zc words
     unsigned *keys = tab, *cnts = tab + H;
     unsigned long long *red64 = reinterpret_cast<unsigned long long *>(tab + 2 * H);  // best
     unsigned *red = tab + 2 * H + 2;                                                   // M, n_at_M, n_free
@@ -184,12 +178,12 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
             if (kpick) kpick[s] = kdet[s] = 0ull;  // zeroed for the next round's atomics
             if (zc_cnt) zc_cnt[s] = 0, zc_key[s] = 0ull;
         }
-        return;
+        return kNoEvict;
     }
     const int b = row_ptr[p], d = row_ptr[p + 1] - b;
     // the decision (thread 0): the target from the count of nodes at the max
     // score and the best (rem, -node) among them, then the update
-    auto finish = [&](unsigned nbest, unsigned long long best) {
+    auto finish = [&](unsigned nbest, unsigned long long best) -> int {
         const int rem = (int)((unsigned)(best >> 32) ^ 0x80000000u);
         const int node = (int)(0x7fffffffu - (unsigned)(best & 0xffffffffu));
         int t;
@@ -223,7 +217,10 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
                 }
             }
         }
+        return t;
     };
+    const bool have_zc = zs_cnt >= 0 || zc_cnt;  // the zero case comes from detect state (no all-node scan)
+    int tgt = kNoEvict;
     // Rows of at most 64 neighbours (a PA tree's pods mostly have 1-3): wave 0
     // alone, lane = neighbour, no hash and no workgroup barrier — each distinct
     // candidate node is counted by one ballot (a loop over the distinct nodes),
@@ -246,27 +243,29 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
                 if (tid == l) c = __popcll(eq);
                 live &= ~eq;
             }
-            const int M = wv_max(c);
+            const int M = dpp_max(c);
             unsigned nb = 0;
             unsigned long long best = 0ull;
             if (M > 0) {
                 const bool cand = c == M;
                 nb = (unsigned)__popcll(__builtin_amdgcn_ballot_w64(cand));
-                best = wv_max_u64(cand ? move_pack(cap[x] - ns.u(x), x) : 0ull);
-            } else if (zc_cnt) {  // max score 0: the detect state's zero case of the scenario
-                const unsigned long long z = zc_key[s];
-                nb = (unsigned)zc_cnt[s];
+                const int xc = cand ? x : 0;  // (clamped: an always-valid node for every lane's loads)
+                const unsigned long long k = move_pack(cap[xc] - ns.u(xc), xc);
+                best = dpp_max_u64(cand ? k : 0ull);
+            } else if (have_zc) {  // max score 0: the detect state's zero case of the scenario
+                const unsigned long long z = zs_cnt >= 0 ? zs_key : zc_key[s];
+                nb = zs_cnt >= 0 ? (unsigned)zs_cnt : (unsigned)zc_cnt[s];
                 best = nb ? move_pack((int)((unsigned)(z >> 32) ^ 0x80000000u), (int)~(unsigned)(z & 0xffffffffull)) : 0ull;
             }
-            if (M > 0 || zc_cnt) {
-                if (tid == 0) finish(nb, best);
+            if (M > 0 || have_zc) {
+                if (tid == 0) tgt = finish(nb, best);
             } else if (tid == 0) {  // the workgroup's scan below
                 red[1] = 0u;
                 *red64 = 0ull;
             }
-            if (!zc_cnt && tid == 0) red[3] = M == 0;
+            if (!have_zc && tid == 0) red[3] = M == 0;
         }
-        if (zc_cnt) return;  // uniform (the caller's barrier publishes red[5] and the update)
+        if (have_zc) return tgt;  // uniform (the caller publishes red[5] and the update)
         move_sync<kGlobal>();
         if (red[3]) {  // uniform: max score 0 and no zero-case words: every non-hazard node ties
             unsigned long long best = 0;
@@ -281,9 +280,9 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
                 atomicMax(red64, best);
             }
             move_sync<kGlobal>();
-            if (tid == 0) finish(red[1], *red64);
+            if (tid == 0) tgt = finish(red[1], *red64);
         }
-        return;
+        return tgt;
     }
     for (int k = tid; k < 2 * H; k += kMoveThreads) tab[k] = 0u;
     if (tid < 8) tab[2 * H + tid] = 0u;
@@ -339,10 +338,10 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
             atomicAdd(&red[1], nb);
             atomicMax(red64, best);
         }
-    } else if (zc_cnt) {  // max score 0: the detect kernel's zero case of the scenario
+    } else if (have_zc) {  // max score 0: the detect state's zero case of the scenario
         if (tid == 0) {
-            const unsigned long long z = zc_key[s];
-            red[1] = (unsigned)zc_cnt[s];
+            const unsigned long long z = zs_cnt >= 0 ? zs_key : zc_key[s];
+            red[1] = zs_cnt >= 0 ? (unsigned)zs_cnt : (unsigned)zc_cnt[s];
             *red64 = red[1] ? move_pack((int)((unsigned)(z >> 32) ^ 0x80000000u), (int)~(unsigned)(z & 0xffffffffull)) : 0ull;
         }
     } else {  // max score 0: every non-hazard node ties
@@ -361,7 +360,8 @@ __device__ __forceinline__ void car_move_one(const int *__restrict__ row_ptr, co
     }
     move_sync<kGlobal>();
     RPROF_MARK(pc, 4);
-    if (tid == 0) finish(red[1], *red64);
+    if (tid == 0) tgt = finish(red[1], *red64);
+    return tgt;
 }
 
 // One workgroup per scenario (LDS hash), or kGlobal: a capped grid striding
@@ -674,10 +674,6 @@ __device__ __forceinline__ int wave_sum(int x) {
     return x;
 }
 
-struct ScnState {  // the scenario's detect maxima (LDS)
-    unsigned long long most, zkey;
-    int zcnt;
-};
 
 // the scenario's maxima over its NB block entries (every thread; ends with a barrier)
 // (sb: the scenario's row of the block arrays, in LDS or global memory)
@@ -743,6 +739,65 @@ __device__ __forceinline__ void blk_update(const NS &ns, const int *__restrict__
     }
 }
 
+// The persistent loop's detect update by wave 0 alone (no workgroup barrier):
+// the blocks of the move's two nodes o and t re-reduced — lane = node of each
+// block, both blocks' capacity loads in flight together — then the scenario's
+// maxima over its NB block entries, every reduction through DPP.  Same values
+// as blk_update + scn_reduce (rsk_metrics.hip's detect rule).
+template <class NS>
+__device__ __forceinline__ void blk2_update_wave(const NS &ns, const int *__restrict__ cap, int N, int thr,
+                                                 const BlkArgs &sb, int o, int t) {
+    const int lane = (int)threadIdx.x & 63;
+    const int bt = t / kBlkNodes, bo = (unsigned)o < (unsigned)N ? o / kBlkNodes : -1;
+    const bool two = bo >= 0 && bo != bt;  // uniform
+    const int n1 = bt * kBlkNodes + lane, n2 = (two ? bo : bt) * kBlkNodes + lane;
+    const int c1 = cap[min(n1, N - 1)], c2 = cap[min(n2, N - 1)];
+    auto one = [&](int b, int n, int c) {
+        unsigned long long m = 0ull, z = 0ull;
+        int cnt = 0;
+        if (n < N) {
+            const int u = ns.u(n), v = pct_of(u, c);
+            const bool h = v >= thr;
+            if (n == o || n == t) ns.set_h(n, h);
+            if (h) m = ((unsigned long long)((unsigned)v ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)n);
+            else {
+                cnt = 1;
+                z = ((unsigned long long)((unsigned)(c - u) ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)n);
+            }
+        }
+        m = dpp_max_u64(m);
+        z = dpp_max_u64(z);
+        cnt = dpp_sum(cnt);
+        if (lane == 0) {
+            sb.bm[b] = m;
+            sb.bz[b] = z;
+            sb.bc[b] = cnt;
+        }
+    };
+    one(bt, n1, c1);
+    if (two) one(bo, n2, c2);
+}
+
+__device__ __forceinline__ void scn_reduce_wave(const BlkArgs &sb, ScnState *st) {
+    const int lane = (int)threadIdx.x & 63;
+    unsigned long long m = 0ull, z = 0ull;
+    int c = 0;
+    for (int b = lane; b < sb.NB; b += 64) {
+        const unsigned long long x = sb.bm[b], y = sb.bz[b];
+        m = x > m ? x : m;
+        z = y > z ? y : z;
+        c += sb.bc[b];
+    }
+    m = dpp_max_u64(m);
+    z = dpp_max_u64(z);
+    c = dpp_sum(c);
+    if (lane == 0) {
+        st->most = m;
+        st->zkey = z;
+        st->zcnt = c;
+    }
+}
+
 // delete_replaced_pod.py:41-61 for scenario s by the workgroup: the pods on
 // the most hazardous node m are m's base pods still on m (their assign word
 // checked) and the list entries whose node is m (the entry carries the pod's
@@ -755,9 +810,9 @@ __device__ __forceinline__ void blk_update(const NS &ns, const int *__restrict__
 template <typename T>
 __device__ __forceinline__ int scn_pick(const T *__restrict__ asg, const int *__restrict__ pod_cpu, int P, int S,
                                         int s, unsigned long long kd, const int *__restrict__ off,
-                                        const int *__restrict__ pod, const DevLists &dl, unsigned long long *r64,
-                                        int *lsrc, int *pcpu) {
-    constexpr int kU = 4;
+                                        const int *__restrict__ pod, const DevLists &dl, unsigned long long *wbest,
+                                        int *wsrc, int *src_out, int *pcpu) {
+    constexpr int kU = 8;  // 2,048 ids / entries per pass: config 5's lists (~1.3k entries) in one
     const int t = (int)threadIdx.x;
     if (!kd) return -1;  // uniform
     const int m = (int)~(unsigned)(kd & 0xffffffffull);
@@ -802,25 +857,30 @@ __device__ __forceinline__ int scn_pick(const T *__restrict__ asg, const int *__
             }
         }
     }
-    const unsigned long long mine = best;
-    best = wave_max_u64(best);
-    if ((t & 63) == 0) r64[t >> 6] = best;
-    if (t == 0) *lsrc = -1;
+    // the wave's best and its list entry (at most one entry per pod), then the
+    // workgroup's from the four waves' slots: one barrier, every thread reads
+    // the same winner (the slots are rewritten only after the round's tail barrier)
+    const unsigned long long wb = dpp_max_u64(best);
+    const unsigned long long hit = __builtin_amdgcn_ballot_w64(wb && best == wb && bsrc >= 0);
+    const int ws = hit ? __builtin_amdgcn_readlane(bsrc, __builtin_ctzll(hit)) : -1;
+    if ((t & 63) == 0) {
+        wbest[t >> 6] = wb;
+        wsrc[t >> 6] = ws;
+    }
     __syncthreads();
-    best = r64[0];
-    for (int w = 1; w < 4; ++w) best = r64[w] > best ? r64[w] : best;
-    if (best && mine == best && bsrc >= 0) *lsrc = bsrc;  // the winner's entry (at most one per pod)
-    __syncthreads();
-    *pcpu = (int)((unsigned)(best >> 32) ^ 0x80000000u);  // the winner's CPU (the key's high word)
-    return best ? (int)~(unsigned)(best & 0xffffffffull) : -1;
+    unsigned long long B = wbest[0];
+    for (int w = 1; w < kMoveThreads / 64; ++w) B = wbest[w] > B ? wbest[w] : B;
+    int src = -1;
+    for (int w = 0; w < kMoveThreads / 64; ++w) src = (B && wbest[w] == B && wsrc[w] >= 0) ? wsrc[w] : src;
+    *src_out = src;
+    *pcpu = (int)((unsigned)(B >> 32) ^ 0x80000000u);  // the winner's CPU (the key's high word)
+    return B ? (int)~(unsigned)(B & 0xffffffffull) : -1;
 }
 
 struct PersistArgs {
     const int *row_ptr, *col, *pod_cpu, *cap;
     int *assign, *use;
     uint8_t *haz;
-    int *zc_cnt;                      // [S] the scenario's zero case, as car_move_one reads it
-    unsigned long long *zc_key;
     const int *off, *pod;             // the base nodes' pod lists
     DevLists dl;
     BlkArgs ba;
@@ -843,6 +903,8 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
     __shared__ int r32[4];
     __shared__ int lsrc, lcnt;  // the scenario's pick source entry and list length
     __shared__ ScnState st;
+    __shared__ unsigned long long pk_best[kMoveThreads / 64];  // scn_pick's per-wave winners
+    __shared__ int pk_src[kMoveThreads / 64];
 #ifdef RSK_ROUNDS_PROF
     __shared__ PhaseClock pclk;
     PhaseClock *pc = &pclk;
@@ -906,48 +968,44 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
         dl.list = a.dl.list + (size_t)s * a.dl.cap;
         __syncthreads();
         scn_reduce(sb, &st, r64, r32);
-        if (t == 0) {
-            a.zc_cnt[s] = st.zcnt;
-            a.zc_key[s] = st.zkey;
-        }
+        // A round: the pick (one barrier), the move, then — wave 0 alone —
+        // the detect update of the two changed blocks and the scenario's
+        // maxima; the tail barrier publishes the state for the next round.  A
+        // row of <= 64 neighbours is scored by wave 0 alone (car_move_one), so
+        // such a round holds two workgroup barriers.
         auto rounds = [&](const auto &ns) {
-#ifdef RSK_ROUNDS_PROF
-            if (t == 0) pclk.start();
-#endif
             for (int r = 0; r < a.R; ++r) {
                 const unsigned long long kd = st.most;
-                int pcpu;
-                const int p = scn_pick<int>(a.assign, a.pod_cpu, a.P, a.S, s, kd, a.off, a.pod, dl, r64, &lsrc, &pcpu);
+                int pcpu, src;
+                const int p = scn_pick<int>(a.assign, a.pod_cpu, a.P, a.S, s, kd, a.off, a.pod, dl, pk_best, pk_src,
+                                            &src, &pcpu);
                 RPROF_MARK(pc, 0);
                 int *tg_row = a.out_target + (size_t)r * a.S;
-                if (t == 0) a.out_evict[(size_t)r * a.S + s] = p;  // (lsrc: read by car_move_one's thread 0)
-                if (p < 0) {
+                if (t == 0) {
+                    a.out_evict[(size_t)r * a.S + s] = p;
+                    lsrc = src;  // (read by car_move_one's thread 0)
+                }
+                if (p < 0) {  // uniform: the state is unchanged
                     if (t == 0) tg_row[s] = kNoEvict;
-                    continue;  // uniform: the state is unchanged
+                    __syncthreads();  // the pick's slots are read before the next round rewrites them
+                    continue;
                 }
                 const int o = (int)~(unsigned)(kd & 0xffffffffull);  // the picked pod sits on the hazard node
-                car_move_one<kGlobal>(a.row_ptr, a.col, a.pod_cpu, a.assign, ns, a.cap, nullptr, s, a.S, a.N, a.H, 1,
-                                      tg_row, nullptr, tab, nullptr, nullptr, nullptr, a.zc_cnt, a.zc_key, 0, INT_MAX,
-                                      dl, p, o, pcpu, pc);
-                move_sync<kGlobal>();  // the move's state update (thread 0) before it is read
+                int tt = car_move_one<kGlobal>(a.row_ptr, a.col, a.pod_cpu, a.assign, ns, a.cap, nullptr, s, a.S, a.N,
+                                               a.H, 1, tg_row, nullptr, tab, nullptr, nullptr, nullptr, nullptr,
+                                               nullptr, 0, INT_MAX, dl, p, o, pcpu, pc, st.zcnt, st.zkey);
+                if (kGlobal) move_sync<true>();  // (global work areas: the update through the agent-scope fence)
                 RPROF_MARK(pc, 5);
-                const int tt = (int)tab[2 * a.H + 7];  // car_move_one's target (red[5])
-                if (tt >= 0) {  // two nodes' CPU changed: their blocks, then the scenario's maxima
-                    const int bo = (unsigned)o < (unsigned)a.N ? o / kBlkNodes : -1, bt = tt / kBlkNodes;
-                    const int w = t >> 6;
-                    if (w == 0) blk_update(ns, a.cap, a.N, a.thr, sb, bt, o, tt);
-                    if (w == 1 && bo >= 0 && bo != bt) blk_update(ns, a.cap, a.N, a.thr, sb, bo, o, tt);
-                    __syncthreads();
-                    RPROF_MARK(pc, 6);
-                    scn_reduce(sb, &st, r64, r32);
-                    RPROF_MARK(pc, 7);
+                if (t < 64) {  // wave 0: thread 0's target, the two changed blocks, the scenario's maxima
+                    tt = __builtin_amdgcn_readfirstlane(tt);
+                    if (tt >= 0) {
+                        blk2_update_wave(ns, a.cap, a.N, a.thr, sb, o, tt);
+                        RPROF_MARK(pc, 6);
+                        scn_reduce_wave(sb, &st);
+                        RPROF_MARK(pc, 7);
+                    }
                 }
-                if (t == 0) {  // car_move_one zeroes the zero-case words (the launch loop's atomics)
-                    a.zc_cnt[s] = st.zcnt;
-                    a.zc_key[s] = st.zkey;
-                }
-                if (kGlobal) move_sync<true>();  // the area is free before the next round clears it
-                else __syncthreads();
+                __syncthreads();  // tail: the detect state, usage, lists and hash free for the next round
                 RPROF_MARK(pc, 8);
             }
         };
@@ -1363,12 +1421,9 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         RSK_HIP(hipMemcpyAsync(d_use, use_cpu, NS * 4, hipMemcpyHostToDevice, st));
     }
     RSK_TRY(r->haz.reserve(NS));
-    RSK_TRY(r->key_ws.reserve((size_t)S * 28));  // the detect and pick keys, the zero case
     const MoveGeom g = move_geometry(r, N, S);
     RSK_TRY(g.rc);
     RSK_TRY(ws_check_u64(N, S, g.H));
-    unsigned long long *zkey = r->key_ws.as<unsigned long long>() + 2 * S;
-    int *zcnt = reinterpret_cast<int *>(zkey + S);
     if (R > 0 && r->P == 0) {  // no pod to evict: every round is RSK_TARGET_NO_EVICT
         fill_i32_kernel<<<(unsigned)ceil_div((int64_t)RS, 256), 256, 0, st>>>(d_evict, RS, -1);
         fill_i32_kernel<<<(unsigned)ceil_div((int64_t)RS, 256), 256, 0, st>>>(d_target, RS, kNoEvict);
@@ -1426,8 +1481,6 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
         pa.assign = d_assign;
         pa.use = d_use;
         pa.haz = r->haz.as<uint8_t>();
-        pa.zc_cnt = zcnt;
-        pa.zc_key = zkey;
         pa.off = r->loff.as<int>();
         pa.pod = r->lpod.as<int>();
         pa.dl = dl;

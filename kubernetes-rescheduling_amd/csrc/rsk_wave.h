@@ -1,0 +1,62 @@
+// rsk_wave.h — wave64 reductions through DPP (gfx950): row shifts within each
+// 16-lane row, then the row broadcasts 15 and 31 (gfx9 DPP), so a reduction is
+// six VALU steps with no LDS round trip (HIP's __shfl_xor is a ds_bpermute: an
+// LDS-latency trip per step).  Every lane must be active; the
+// result is lane 63's, read back as a wave-uniform value.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <climits>
+
+namespace rsk {
+
+__device__ __forceinline__ int dpp_max(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ int dpp_min(int v) {
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x111, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x112, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x114, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x118, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x142, 0xa, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x143, 0xc, 0xf, false));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long v) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)v, kCtrl, kRowMask, 0xf, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(v >> 32), kCtrl, kRowMask, 0xf, false);
+    return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ unsigned long long dpp_max_u64(unsigned long long v) {  // identity 0
+    unsigned long long w;
+    w = dpp_u64<0x111, 0xf>(v); v = w > v ? w : v;
+    w = dpp_u64<0x112, 0xf>(v); v = w > v ? w : v;
+    w = dpp_u64<0x114, 0xf>(v); v = w > v ? w : v;
+    w = dpp_u64<0x118, 0xf>(v); v = w > v ? w : v;
+    w = dpp_u64<0x142, 0xa>(v); v = w > v ? w : v;
+    w = dpp_u64<0x143, 0xc>(v); v = w > v ? w : v;
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, 63);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), 63);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+__device__ __forceinline__ int dpp_sum(int v) {  // (the same steps as a wave-wide inclusive scan)
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+}  // namespace rsk

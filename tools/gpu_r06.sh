@@ -3,7 +3,8 @@
 # steps: test (pytest -m gpu), smoke, bench (headline), b2k (config 2),
 #        b1m (config 4), brounds (config 5), prof (rocprof trace + PMC of headline
 #        and 1m50k), profh / prof1m (one config), dropin, nrb (tools/nrbench.py),
-#        nrprof (its kernel trace)
+#        nrprof (its kernel trace), pmc:LIB:CONFIG:ENV (FETCH / WRITE passes of tools/tilebench.py
+#        with librsk_LIB.so — base: the product — and ENV=a=1,b=2 or -)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 out=gpurun_out/${1:-r06}; shift
 mkdir -p "$out"
@@ -33,10 +34,13 @@ for s in "${@:-test smoke bench}"; do
       hp:*) step "hostprobe_${w#hp:}" 300 python -u tools/hostprobe.py "${w#hp:}" ;;
       rprof) step rounds_prof 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_rprof.so python -u bench.py --config rounds --no-cpu-baseline --no-kernel-events ;;
       rprof128) step rounds_prof128 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_rprof.so python -u bench.py --config rounds --scenarios 128 --no-cpu-baseline --no-kernel-events ;;
-      pmc:*) v=${w#pmc:}; kv=${v#*:}; lib=${v%%:*}; mkdir -p "$out/pmc_$lib"
+      pmc:*) v=${w#pmc:}; lib=${v%%:*}; v=${v#*:}; cfg=${v%%:*}; kv=${v#*:}; [ "$kv" = "-" ] && kv=""
+             tag="${lib}_${cfg}_${kv//[=,]/_}"; envs=${kv//,/ }
+             [ "$lib" != base ] && envs="RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_$lib.so $envs"
              for c in FETCH_SIZE WRITE_SIZE; do
-               step "pmc_${lib}_${c}_${kv//[=,]/_}" 240 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_$lib.so ${kv//,/ } rocprofv3 --pmc $c -d "$out/pmc_$lib/$c${kv//[=,]/_}" -o p -f csv -- python3 bench.py --config headline --steps 10 --warmup 2 --no-cpu-baseline
-             done ;;
+               step "pmc_${tag}_$c" 240 env $envs rocprofv3 --pmc $c -d "$out/pmc_$tag/$c" -o p -f csv -- python3 tools/tilebench.py --config $cfg --steps 10
+             done
+             python3 tools/pmc_quick.py "$out/pmc_$tag" | tee "$out/pmc_${tag}_summary.txt" ;;
       bnoev) step bench_noevents 600 python -u bench.py --no-cpu-baseline --no-kernel-events ;;
       nr:*) kv=${w#nr:}; step "nr_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_abl.so ${kv//,/ } python -u tools/nrbench.py ;;
       nrk:*) kv=${w#nrk:}; step "nrk_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u tools/nrbench.py ;;
