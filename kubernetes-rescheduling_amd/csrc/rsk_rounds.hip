@@ -64,7 +64,9 @@ __global__ __launch_bounds__(256) void fill_i32_kernel(int *__restrict__ out, si
 }
 
 // Per-scenario lists of the pods off their base node (base = scenario 0's
-// node), as (pod, its current node, its CPU, 0) entries: every pod that has
+// node), as entries (its current node; pod, its CPU) stored apart — lnode[],
+// the 4-B words the pick scans, and lpc[] (int2), read only for the entries on
+// the picked node (round 6: the scan reads 4 B per entry, not 16): every pod that has
 // left its base node in scenario s has exactly one entry in list s, holding
 // the node it is on now (the move kernel updates it in place, or appends the
 // pod when it first leaves its base node).  In the persistent loop a
@@ -75,7 +77,8 @@ __global__ __launch_bounds__(256) void fill_i32_kernel(int *__restrict__ out, si
 struct DevLists {
     const int *base = nullptr;
     int *cnt = nullptr, *src = nullptr;
-    int4 *list = nullptr;
+    int *lnode = nullptr;   // [S][cap] the entry's current node
+    int2 *lpc = nullptr;    // [S][cap] (pod, its CPU)
     int cap = 0;
 };
 
@@ -192,6 +195,7 @@ __device__ __forceinline__ int car_move_one(const int *__restrict__ row_ptr, con
         else t = rem >= 0 ? node : RSK_TARGET_NONE;   // largest remaining CPU, None if < 0
         out_target[s] = t;
         red[5] = (unsigned)t;  // for the workgroup (the persistent loop), after its next barrier
+        red[4] = (unsigned)rem;  // the target's remaining CPU before the move (the loop's detect update)
         if (kpick) kpick[s] = kdet[s] = 0ull;  // every thread read p long before the last barrier
         if (zc_cnt) zc_cnt[s] = 0, zc_key[s] = 0ull;
         if (update && t >= 0) {  // build-defined update: the pod's CPU moves with it
@@ -207,9 +211,10 @@ __device__ __forceinline__ int car_move_one(const int *__restrict__ row_ptr, con
                 const int j = *dl.src, q = *dl.cnt;
                 if (q <= dl.cap) {
                     if (j >= 0) {
-                        dl.list[j].y = t;
+                        dl.lnode[j] = t;
                     } else if (q < dl.cap) {
-                        dl.list[q] = make_int4(p, t, c, 0);
+                        dl.lnode[q] = t;
+                        dl.lpc[q] = make_int2(p, c);
                         *dl.cnt = q + 1;
                     } else {
                         *dl.cnt = dl.cap + 1;  // overflow: full scans from now on
@@ -528,7 +533,8 @@ constexpr int kLF = 1024;
 __global__ __launch_bounds__(256) void list_fill_kernel(const int *__restrict__ assign, int P, int S, int N,
                                                         const int *__restrict__ base, int *__restrict__ cur,
                                                         int *__restrict__ pod, int *__restrict__ dcnt,
-                                                        const int *__restrict__ pod_cpu, int4 *__restrict__ dlist,
+                                                        const int *__restrict__ pod_cpu, int *__restrict__ lnode,
+                                                        int2 *__restrict__ lpc,
                                                         int cap, unsigned *__restrict__ err) {
     constexpr int kK = 16;  // deviations kept per (wave, lane) in LDS; more: the rows are walked again
     __shared__ int wc[4][64];
@@ -584,7 +590,8 @@ __global__ __launch_bounds__(256) void list_fill_kernel(const int *__restrict__ 
         for (int k = 0; k < n; ++k, ++q)
             if (q < cap) {
                 const int2 e = keep[wv][k][lane];
-                dlist[(size_t)s * cap + q] = make_int4(e.x, e.y, pod_cpu[e.x], 0);
+                lnode[(size_t)s * cap + q] = e.y;
+                lpc[(size_t)s * cap + q] = make_int2(e.x, pod_cpu[e.x]);
             }
         return;
     }
@@ -600,7 +607,10 @@ __global__ __launch_bounds__(256) void list_fill_kernel(const int *__restrict__ 
         for (int u = 0; u < kB; ++u) {
             const int x = (unsigned)a[u] < (unsigned)N ? a[u] : N;
             if (p0 + u < q1 && x != b[u]) {
-                if (q < cap) dlist[(size_t)s * cap + q] = make_int4(p0 + u, x, pod_cpu[p0 + u], 0);
+                if (q < cap) {
+                    lnode[(size_t)s * cap + q] = x;
+                    lpc[(size_t)s * cap + q] = make_int2(p0 + u, pod_cpu[p0 + u]);
+                }
                 ++q;
             }
         }
@@ -739,62 +749,110 @@ __device__ __forceinline__ void blk_update(const NS &ns, const int *__restrict__
     }
 }
 
-// The persistent loop's detect update by wave 0 alone (no workgroup barrier):
-// the blocks of the move's two nodes o and t re-reduced — lane = node of each
-// block, both blocks' capacity loads in flight together — then the scenario's
-// maxima over its NB block entries, every reduction through DPP.  Same values
-// as blk_update + scn_reduce (rsk_metrics.hip's detect rule).
+// The persistent loop's detect update after a move of `cpu` from o (the
+// scenario's most hazardous node: the pick's node) to t (a non-hazard node:
+// CAR never targets a hazard node), by wave 0 alone, incrementally:
+//   o's pct falls: its block's hazard max (bm) is recomputed (lane = node; the
+//     block's capacities were loaded at the round's start, c_bo), and o joins
+//     the block's non-hazard set (bz, bc) when it leaves the hazard set;
+//   t's pct rises: t joins its block's hazard max when it becomes a hazard; its
+//     non-hazard key falls (or leaves), so bz[bt] is recomputed only when t held
+//     it; the count follows;
+//   the scenario's most hazardous node is re-reduced over the blocks (o held
+//     it), its zero-case count follows the two changes and its zero-case key is
+//     re-reduced only when the block that held it lost t's key.
+// A block holding both o and t is recomputed in full.  Every value equals what
+// blk_update + scn_reduce compute from scratch (harzard_detect.py:3-27 with
+// get_resource_usage.py:37's pct; the zero case of rescheduling.py:199-214).
 template <class NS>
-__device__ __forceinline__ void blk2_update_wave(const NS &ns, const int *__restrict__ cap, int N, int thr,
-                                                 const BlkArgs &sb, int o, int t) {
+__device__ __forceinline__ void detect_move_wave(const NS &ns, const int *__restrict__ cap, int N, int thr,
+                                                 const BlkArgs &sb, ScnState *st, int o, int t, int c_bo,
+                                                 int rem_t_old, int cpu) {
     const int lane = (int)threadIdx.x & 63;
-    const int bt = t / kBlkNodes, bo = (unsigned)o < (unsigned)N ? o / kBlkNodes : -1;
-    const bool two = bo >= 0 && bo != bt;  // uniform
-    const int n1 = bt * kBlkNodes + lane, n2 = (two ? bo : bt) * kBlkNodes + lane;
-    const int c1 = cap[min(n1, N - 1)], c2 = cap[min(n2, N - 1)];
-    auto one = [&](int b, int n, int c) {
-        unsigned long long m = 0ull, z = 0ull;
-        int cnt = 0;
-        if (n < N) {
-            const int u = ns.u(n), v = pct_of(u, c);
-            const bool h = v >= thr;
-            if (n == o || n == t) ns.set_h(n, h);
-            if (h) m = ((unsigned long long)((unsigned)v ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)n);
-            else {
-                cnt = 1;
-                z = ((unsigned long long)((unsigned)(c - u) ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)n);
-            }
+    const int bo = o / kBlkNodes, bt = t / kBlkNodes;
+    auto hkey = [](int v, int n) {
+        return ((unsigned long long)((unsigned)v ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)n);
+    };
+    // node t after the move (uniform): rem_t_old = cap[t] - use_old[t]
+    const int ut = ns.u(t), ct = rem_t_old + ut - cpu, vt = pct_of(ut, ct);
+    const bool ht = vt >= thr;
+    const unsigned long long zt_old = hkey(rem_t_old, t);
+    // block bo, lane = node: o's state is new (usage updated), the others unchanged
+    const int n = bo * kBlkNodes + lane;
+    unsigned long long m = 0ull, z = 0ull;
+    int cnt = 0;
+    bool h = false;
+    if (n < N) {
+        const int u = ns.u(n), v = pct_of(u, c_bo);
+        h = v >= thr;
+        if (h) m = hkey(v, n);
+        else {
+            cnt = 1;
+            z = hkey(c_bo - u, n);
         }
+    }
+    const bool ho = __builtin_amdgcn_readlane((int)h, o & 63) != 0;  // o's new hazard flag
+    const unsigned long long zb_old = sb.bz[bo], zt_blk_old = sb.bz[bt], zs_old = st->zkey;
+    bool zs_recompute = false;
+    if (bo == bt) {  // both nodes in one block: the block in full (t's new state is in the lanes too)
         m = dpp_max_u64(m);
         z = dpp_max_u64(z);
         cnt = dpp_sum(cnt);
         if (lane == 0) {
-            sb.bm[b] = m;
-            sb.bz[b] = z;
-            sb.bc[b] = cnt;
+            sb.bm[bo] = m;
+            sb.bz[bo] = z;
+            sb.bc[bo] = cnt;
         }
-    };
-    one(bt, n1, c1);
-    if (two) one(bo, n2, c2);
-}
-
-__device__ __forceinline__ void scn_reduce_wave(const BlkArgs &sb, ScnState *st) {
-    const int lane = (int)threadIdx.x & 63;
-    unsigned long long m = 0ull, z = 0ull;
-    int c = 0;
-    for (int b = lane; b < sb.NB; b += 64) {
-        const unsigned long long x = sb.bm[b], y = sb.bz[b];
-        m = x > m ? x : m;
-        z = y > z ? y : z;
-        c += sb.bc[b];
+        zs_recompute = z < zb_old && zb_old == zs_old;
+    } else {
+        m = dpp_max_u64(m);  // o held its block's hazard max: recomputed
+        unsigned long long zbo = zb_old;
+        const int co = __builtin_amdgcn_readlane(c_bo, o & 63);  // cap[o]
+        if (!ho) zbo = max(zbo, hkey(co - ns.u(o), o));  // o joins its block's non-hazard set
+        unsigned long long zbt = zt_blk_old;
+        if (zt_blk_old == zt_old) {  // t held its block's zero-case key: recomputed (t's key fell or left)
+            const int nt = bt * kBlkNodes + lane;
+            const int cn = cap[min(nt, N - 1)];
+            unsigned long long zz = 0ull;
+            if (nt < N) {
+                const int u = ns.u(nt), v = pct_of(u, cn);
+                if (v < thr) zz = hkey(cn - u, nt);
+            }
+            zbt = dpp_max_u64(zz);
+        } else if (!ht) {
+            zbt = max(zbt, hkey(ct - ut, t));  // (t's key fell and did not hold the max: unchanged max)
+        }
+        if (lane == 0) {
+            sb.bm[bo] = m;
+            sb.bz[bo] = zbo;
+            if (!ho) sb.bc[bo] += 1;
+            if (ht) {
+                sb.bm[bt] = max(sb.bm[bt], hkey(vt, t));
+                sb.bc[bt] -= 1;
+            }
+            sb.bz[bt] = zbt;
+        }
+        zs_recompute = zbt < zt_blk_old && zt_blk_old == zs_old;
     }
-    m = dpp_max_u64(m);
-    z = dpp_max_u64(z);
-    c = dpp_sum(c);
+    if (lane == (o & 63)) ns.set_h(o, ho);
+    if (lane == 0 && ht) ns.set_h(t, true);
+    // the scenario: most hazardous node over the blocks (o held it); the zero case
+    const int dz = (ho ? 0 : 1) - (ht ? 1 : 0);
+    unsigned long long mm = 0ull, zz = 0ull;
+    for (int b = lane; b < sb.NB; b += 64) {
+        const unsigned long long x = sb.bm[b];
+        mm = x > mm ? x : mm;
+        if (zs_recompute) {
+            const unsigned long long y = sb.bz[b];
+            zz = y > zz ? y : zz;
+        }
+    }
+    mm = dpp_max_u64(mm);
+    if (zs_recompute) zz = dpp_max_u64(zz);
     if (lane == 0) {
-        st->most = m;
-        st->zkey = z;
-        st->zcnt = c;
+        st->most = mm;
+        st->zcnt += dz;
+        st->zkey = zs_recompute ? zz : max(zs_old, max(sb.bz[bo], sb.bz[bt]));
     }
 }
 
@@ -819,7 +877,7 @@ __device__ __forceinline__ int scn_pick(const T *__restrict__ asg, const int *__
     const int b0 = off[m], nb = off[m + 1] - b0;
     const int nd = *dl.cnt;
     const bool full = nd > dl.cap;
-    const int4 *l = dl.list;
+    const int *ln = dl.lnode;
     auto key = [](int p, int c) {
         return c >= 0 ? ((unsigned long long)((unsigned)c ^ 0x80000000u) << 32) | (unsigned long long)(~(unsigned)p)
                       : 0ull;
@@ -829,8 +887,7 @@ __device__ __forceinline__ int scn_pick(const T *__restrict__ asg, const int *__
     const int ng = full ? P : nb, nl = full ? 0 : nd;
     const int nmax = max(ng, nl);
     for (int i0 = 0; i0 < nmax; i0 += 256 * kU) {
-        int p[kU], a[kU], c[kU];
-        int4 e[kU];
+        int p[kU], a[kU], c[kU], en[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {  // clamped, always-valid ids (a pod of an empty range: pod 0, masked below)
             const int i = min(i0 + u * 256 + t, max(ng, 1) - 1);
@@ -838,7 +895,7 @@ __device__ __forceinline__ int scn_pick(const T *__restrict__ asg, const int *__
         }
         if (nl > 0) {  // uniform
 #pragma unroll
-            for (int u = 0; u < kU; ++u) e[u] = l[min(i0 + u * 256 + t, nl - 1)];
+            for (int u = 0; u < kU; ++u) en[u] = ln[min(i0 + u * 256 + t, nl - 1)];
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
@@ -850,8 +907,9 @@ __device__ __forceinline__ int scn_pick(const T *__restrict__ asg, const int *__
             const int i = i0 + u * 256 + t;
             const unsigned long long kb = (i < ng && a[u] == m) ? key(p[u], c[u]) : 0ull;
             if (kb > best) best = kb, bsrc = -1;
-            if (nl > 0) {
-                const unsigned long long ke = (i < nl && e[u].y == m) ? key(e[u].x, e[u].z) : 0ull;
+            if (nl > 0 && i < nl && en[u] == m) {  // an entry on m (rare): its pod and CPU
+                const int2 e = dl.lpc[i];
+                const unsigned long long ke = key(e.x, e.y);
                 // >=: an entry of the same pod as a base hit carries the pod's entry index
                 if (ke && ke >= best) best = ke, bsrc = i;
             }
@@ -965,7 +1023,8 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
         DevLists dl = a.dl;
         dl.cnt = &lcnt;
         dl.src = &lsrc;
-        dl.list = a.dl.list + (size_t)s * a.dl.cap;
+        dl.lnode = a.dl.lnode + (size_t)s * a.dl.cap;
+        dl.lpc = a.dl.lpc + (size_t)s * a.dl.cap;
         __syncthreads();
         scn_reduce(sb, &st, r64, r32);
         // A round: the pick (one barrier), the move, then — wave 0 alone —
@@ -974,8 +1033,14 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
         // row of <= 64 neighbours is scored by wave 0 alone (car_move_one), so
         // such a round holds two workgroup barriers.
         auto rounds = [&](const auto &ns) {
+#ifdef RSK_ROUNDS_PROF
+            if (t == 0) pclk.start();
+#endif
             for (int r = 0; r < a.R; ++r) {
                 const unsigned long long kd = st.most;
+                const int o = (int)~(unsigned)(kd & 0xffffffffull);  // the hazard node (the pick's pod sits on it)
+                // wave 0: the capacities of o's block, consumed by the detect update after the move
+                const int c_bo = a.cap[min((kd ? o / kBlkNodes : 0) * kBlkNodes + (t & 63), a.N - 1)];
                 int pcpu, src;
                 const int p = scn_pick<int>(a.assign, a.pod_cpu, a.P, a.S, s, kd, a.off, a.pod, dl, pk_best, pk_src,
                                             &src, &pcpu);
@@ -990,7 +1055,6 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
                     __syncthreads();  // the pick's slots are read before the next round rewrites them
                     continue;
                 }
-                const int o = (int)~(unsigned)(kd & 0xffffffffull);  // the picked pod sits on the hazard node
                 int tt = car_move_one<kGlobal>(a.row_ptr, a.col, a.pod_cpu, a.assign, ns, a.cap, nullptr, s, a.S, a.N,
                                                a.H, 1, tg_row, nullptr, tab, nullptr, nullptr, nullptr, nullptr,
                                                nullptr, 0, INT_MAX, dl, p, o, pcpu, pc, st.zcnt, st.zkey);
@@ -999,10 +1063,8 @@ __global__ __launch_bounds__(kMoveThreads) void rounds_persist_kernel(PersistArg
                 if (t < 64) {  // wave 0: thread 0's target, the two changed blocks, the scenario's maxima
                     tt = __builtin_amdgcn_readfirstlane(tt);
                     if (tt >= 0) {
-                        blk2_update_wave(ns, a.cap, a.N, a.thr, sb, o, tt);
+                        detect_move_wave(ns, a.cap, a.N, a.thr, sb, &st, o, tt, c_bo, (int)tab[2 * a.H + 6], pcpu);
                         RPROF_MARK(pc, 6);
-                        scn_reduce_wave(sb, &st);
-                        RPROF_MARK(pc, 7);
                     }
                 }
                 __syncthreads();  // tail: the detect state, usage, lists and hash free for the next round
@@ -1443,7 +1505,10 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
             RSK_TRY(r->loff.reserve((size_t)(N + 2) * 4 * 2));
             RSK_TRY(r->lpod.reserve((size_t)P * 4));
             RSK_TRY(r->lcnt.reserve((size_t)S * 8));  // counts, then the picks' source entries
-            RSK_TRY(r->llist.reserve((size_t)S * cap * 16));
+            const size_t lpc_off = ((size_t)S * cap * 4 + 15) & ~(size_t)15;  // lnode[S * cap], then lpc
+            RSK_TRY(r->llist.reserve(lpc_off + (size_t)S * cap * 8));
+            int *lnode = r->llist.as<int>();
+            int2 *lpc = reinterpret_cast<int2 *>(r->llist.as<char>() + lpc_off);
             int *cntb = r->loff.as<int>() + (N + 2);  // N + 1 counts, then the fill cursors
             ScopedTimer tm(ctx, "rounds_lists");
             RSK_HIP(hipMemsetAsync(cntb, 0, (size_t)(N + 1) * 4, st));
@@ -1457,12 +1522,13 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
             RSK_CHECK(derr, "no device error word (mapped pinned memory)");
             list_fill_kernel<<<(unsigned)blocks, 256, 0, st>>>(d_assign, P, S, N, r->lbase.as<int>(), cntb,
                                                                  r->lpod.as<int>(), r->lcnt.as<int>(),
-                                                                 r->pod_cpu.as<int>(), r->llist.as<int4>(), cap, derr);
+                                                                 r->pod_cpu.as<int>(), lnode, lpc, cap, derr);
             RSK_HIP(hipGetLastError());
             dl.base = r->lbase.as<int>();
             dl.cnt = r->lcnt.as<int>();
             dl.src = dl.cnt + S;
-            dl.list = r->llist.as<int4>();
+            dl.lnode = lnode;
+            dl.lpc = lpc;
             dl.cap = cap;
         }
         // one launch for all R rounds: the hazard flags and the block maxima

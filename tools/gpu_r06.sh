@@ -44,6 +44,9 @@ for s in "${@:-test smoke bench}"; do
       bnoev) step bench_noevents 600 python -u bench.py --no-cpu-baseline --no-kernel-events ;;
       nr:*) kv=${w#nr:}; step "nr_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_abl.so ${kv//,/ } python -u tools/nrbench.py ;;
       nrk:*) kv=${w#nrk:}; step "nrk_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u tools/nrbench.py ;;
+      nrprof:*) lib=${w#nrprof:}; envs=""; [ "$lib" != base ] && envs="RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_$lib.so"
+                env $envs ./tools/gpu_nrprof.sh "$out/nrprof_${lib}_$RANDOM" > "$out/nrprof_$lib.log" 2>&1 || { tail -5 "$out/nrprof_$lib.log"; exit 1; }
+                cat "$out/nrprof_$lib.log" ;;
       nrb) step nrbench 300 python -u tools/nrbench.py ;;
       nrprof) ./tools/gpu_nrprof.sh "$out/nrprof" > "$out/nrprof.log" 2>&1 || { tail -5 "$out/nrprof.log"; exit 1; }; cat "$out/nrprof.log" ;;
       dropin) step dropin 400 python -u tools/dropin_latency.py --calls 40 --out "$out/dropin.json" ;;
