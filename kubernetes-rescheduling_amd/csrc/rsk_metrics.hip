@@ -500,21 +500,17 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
 #pragma unroll
         for (int u = 0; u < kB; ++u)  // a wave-uniform row base: the load's address is the lane's 32-bit offset
             r[u] = __builtin_nontemporal_load(assign + (size_t)min(pb + u, last) * S + sc);
-        // the keys' words: lane l reads pod pb + l % 16's scenarios 0, 21 and 42
-        // (kMaj; S < 43: scenario 0 only) — lines the row loads fetch anyway —
-        // so the majority is lane-local (no cross-lane shuffle in examine)
+        // the keys' words in one gather: lane l reads pod pb + l % 16's scenario 0
+        // (l < 16), 21 (l < 32) or 42 (kMaj; S < 43: scenario 0 only)
         const unsigned pk = (unsigned)min(pb + (lane & (kB - 1)), last);
-        kr[0] = *reinterpret_cast<const int *>(asg + nr_off<kOff32>(pk, (unsigned)S, 0u));
-        if (kMaj) {
-            kr[1] = *reinterpret_cast<const int *>(asg + nr_off<kOff32>(pk, (unsigned)S, 21u));
-            kr[2] = *reinterpret_cast<const int *>(asg + nr_off<kOff32>(pk, (unsigned)S, 42u));
-        }
+        const unsigned ks = kMaj ? (lane < kB ? 0u : lane < 2 * kB ? 21u : 42u) : 0u;
+        kr[0] = *reinterpret_cast<const int *>(asg + nr_off<kOff32>(pk, (unsigned)S, ks));
     };
     auto examine = [&](int v, const int (&r)[kB], const int (&kr)[3]) {
         const int bt = v / nchunk, c = v - bt * nchunk, pb = q0 + bt * kB, nb = min(kB, q1 - pb);
         int kv = kr[0];  // lane u < 16: pod pb + u's key
         if (kMaj) {
-            const int k1 = kr[1], k2 = kr[2];
+            const int k1 = __shfl(kr[0], lane + kB, 64), k2 = __shfl(kr[0], lane + 2 * kB, 64);
             kv = (kv == k1 || kv == k2) ? kv : (k1 == k2 ? k1 : kv);
         }
         kv = (unsigned)kv < (unsigned)N ? kv : N;
@@ -530,8 +526,14 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
 #pragma unroll
         for (int u = 0; u < kB; ++u) dev |= (unsigned)(r[u] != __builtin_amdgcn_readlane(kv, u)) << u;
         dev = live ? dev : 0u;  // (one select: a per-lane branch per row costs exec-mask juggling)
-        // (the OR over the wave by DPP: VALU steps, no LDS round trips)
+#ifdef RSK_NR_DPP
         const unsigned D = dpp_or(dev) & (nb >= 32 ? 0xffffffffu : (1u << nb) - 1u);
+#else
+        unsigned D = dev;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) D |= (unsigned)__shfl_xor((int)D, o, 64);
+        D = (unsigned)__builtin_amdgcn_readfirstlane((int)D) & (nb >= 32 ? 0xffffffffu : (1u << nb) - 1u);
+#endif
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
             if (!((D >> u) & 1u)) continue;
@@ -553,22 +555,17 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
         }
     };
     if (nv > 0) {
-        // three units' rows in rotation: two in flight while one is examined
-        int ra[kB], rb[kB], rc[kB], ka[3], kb[3], kc[3];
+        int ra[kB], rb[kB], ka[3], kb[3];
         load(0, ra, ka);
-        load(1, rb, kb);
         // (the empty asm after each prefetch: the compiler may not hoist the
-        // examined unit's first uses of its keys above the next units' loads)
-        for (int v = 0; v < nv; v += 3) {
-            load(v + 2, rc, kc);
-            asm volatile("" : "+v"(ka[0]), "+v"(ka[1]), "+v"(ka[2])::"memory");
+        // examined unit's first uses of its keys above the next unit's loads)
+        for (int v = 0; v < nv; v += 2) {
+            load(v + 1, rb, kb);
+            asm volatile("" : "+v"(ka[0])::"memory");
             examine(v, ra, ka);
-            load(v + 3, ra, ka);
-            asm volatile("" : "+v"(kb[0]), "+v"(kb[1]), "+v"(kb[2])::"memory");
+            load(v + 2, ra, ka);
+            asm volatile("" : "+v"(kb[0])::"memory");
             if (v + 1 < nv) examine(v + 1, rb, kb);
-            load(v + 4, rb, kb);
-            asm volatile("" : "+v"(kc[0]), "+v"(kc[1]), "+v"(kc[2])::"memory");
-            if (v + 2 < nv) examine(v + 2, rc, kc);
         }
     }
     if (wover && lane == 0) over = 1;

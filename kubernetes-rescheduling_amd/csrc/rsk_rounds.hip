@@ -884,34 +884,48 @@ __device__ __forceinline__ int scn_pick(const T *__restrict__ asg, const int *__
     };
     unsigned long long best = 0ull;
     int bsrc = -1;  // the list entry of this thread's best (-1: a base pod)
-    const int ng = full ? P : nb, nl = full ? 0 : nd;
-    const int nmax = max(ng, nl);
-    for (int i0 = 0; i0 < nmax; i0 += 256 * kU) {
-        int p[kU], a[kU], c[kU], en[kU];
+    if (full) {  // uniform: an overflowed list — every pod's assign word
+        for (int i0 = 0; i0 < P; i0 += 256 * kU) {
+            int a[kU], c[kU];
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {  // clamped, always-valid ids (a pod of an empty range: pod 0, masked below)
-            const int i = min(i0 + u * 256 + t, max(ng, 1) - 1);
-            p[u] = full ? i : (ng > 0 ? pod[b0 + i] : 0);
+            for (int u = 0; u < kU; ++u) {
+                const int q = min(i0 + u * 256 + t, P - 1);
+                a[u] = (int)asg[(size_t)q * S + s];
+                c[u] = pod_cpu[q];
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int q = i0 + u * 256 + t;
+                const unsigned long long kb = (q < P && a[u] == m) ? key(q, c[u]) : 0ull;
+                if (kb > best) best = kb;
+            }
         }
-        if (nl > 0) {  // uniform
+    } else {
+        // m's base pods (~P/N: one per thread and pass) and the list's node
+        // words (kU per thread and pass) loaded together; a base pod's assign
+        // word and CPU after its id, an entry's (pod, CPU) only when it is on m
+        const int nl = nd;
+        for (int i0 = 0, j0 = 0; i0 < nb || j0 < nl; i0 += 256, j0 += 256 * kU) {
+            const int q = pod[min(b0 + i0 + t, P - 1)];  // (clamped: always a valid id)
+            int en[kU];
+            if (j0 < nl) {  // uniform
 #pragma unroll
-            for (int u = 0; u < kU; ++u) en[u] = ln[min(i0 + u * 256 + t, nl - 1)];
-        }
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            a[u] = (int)asg[(size_t)p[u] * S + s];
-            c[u] = pod_cpu[p[u]];
-        }
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const int i = i0 + u * 256 + t;
-            const unsigned long long kb = (i < ng && a[u] == m) ? key(p[u], c[u]) : 0ull;
+                for (int u = 0; u < kU; ++u) en[u] = ln[min(j0 + u * 256 + t, nl - 1)];
+            }
+            const int a = (int)asg[(size_t)q * S + s], c = pod_cpu[q];
+            const unsigned long long kb = (i0 + t < nb && a == m) ? key(q, c) : 0ull;
             if (kb > best) best = kb, bsrc = -1;
-            if (nl > 0 && i < nl && en[u] == m) {  // an entry on m (rare): its pod and CPU
-                const int2 e = dl.lpc[i];
-                const unsigned long long ke = key(e.x, e.y);
-                // >=: an entry of the same pod as a base hit carries the pod's entry index
-                if (ke && ke >= best) best = ke, bsrc = i;
+            if (j0 < nl) {
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    const int jj = j0 + u * 256 + t;
+                    if (jj < nl && en[u] == m) {  // an entry on m (rare): its pod and CPU
+                        const int2 e = dl.lpc[jj];
+                        const unsigned long long ke = key(e.x, e.y);
+                        // >=: an entry of the same pod as a base hit carries the pod's entry index
+                        if (ke && ke >= best) best = ke, bsrc = jj;
+                    }
+                }
             }
         }
     }
