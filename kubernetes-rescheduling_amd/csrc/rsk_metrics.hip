@@ -526,14 +526,9 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
 #pragma unroll
         for (int u = 0; u < kB; ++u) dev |= (unsigned)(r[u] != __builtin_amdgcn_readlane(kv, u)) << u;
         dev = live ? dev : 0u;  // (one select: a per-lane branch per row costs exec-mask juggling)
-#ifdef RSK_NR_DPP
+        // (the OR over the wave by DPP, VALU steps: 80.5 against 81.5 us with
+        // six ds_swizzle / bpermute round trips, profiles/r06d)
         const unsigned D = dpp_or(dev) & (nb >= 32 ? 0xffffffffu : (1u << nb) - 1u);
-#else
-        unsigned D = dev;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) D |= (unsigned)__shfl_xor((int)D, o, 64);
-        D = (unsigned)__builtin_amdgcn_readfirstlane((int)D) & (nb >= 32 ? 0xffffffffu : (1u << nb) - 1u);
-#endif
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
             if (!((D >> u) & 1u)) continue;

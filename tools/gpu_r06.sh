@@ -41,6 +41,10 @@ for s in "${@:-test smoke bench}"; do
                step "pmc_${tag}_$c" 240 env $envs rocprofv3 --pmc $c -d "$out/pmc_$tag/$c" -o p -f csv -- python3 tools/tilebench.py --config $cfg --steps 10
              done
              python3 tools/pmc_quick.py "$out/pmc_$tag" | tee "$out/pmc_${tag}_summary.txt" ;;
+      abh:*) lib=${w#abh:}; for rep in 1 2; do
+               step "abh_base_$rep" 300 python -u bench.py --config headline --no-cpu-baseline
+               step "abh_${lib}_$rep" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_$lib.so python -u bench.py --config headline --no-cpu-baseline
+             done ;;
       bnoev) step bench_noevents 600 python -u bench.py --no-cpu-baseline --no-kernel-events ;;
       nr:*) kv=${w#nr:}; step "nr_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_abl.so ${kv//,/ } python -u tools/nrbench.py ;;
       nrk:*) kv=${w#nrk:}; step "nrk_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u tools/nrbench.py ;;
