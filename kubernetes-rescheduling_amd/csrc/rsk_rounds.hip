@@ -76,8 +76,6 @@ __global__ __launch_bounds__(256) void fill_i32_kernel(int *__restrict__ out, si
 // is scanned in full from then on.
 struct DevLists {
     const int *base = nullptr;
-    unsigned *mv = nullptr;  // [ceil(P / 32)][S] bit (p, s): p has left its base node in s at some point
-                             // (set by the list setup and by every move, never cleared); clear -> on its base node
     int *cnt = nullptr, *src = nullptr;
     int *lnode = nullptr;   // [S][cap] the entry's current node
     int2 *lpc = nullptr;    // [S][cap] (pod, its CPU)
@@ -209,7 +207,6 @@ __device__ __forceinline__ int car_move_one(const int *__restrict__ row_ptr, con
             ns.u(t) += c;
             assign[pc] = t;
             if (asg16) asg16[pc] = (unsigned short)t;
-            if (dl.mv) dl.mv[(size_t)(p >> 5) * S + s] |= 1u << (p & 31);  // (column s: this thread's alone)
             if (dl.base) {  // the pod's entry follows it (one entry per pod off its base node)
                 const int j = *dl.src, q = *dl.cnt;
                 if (q <= dl.cap) {
@@ -239,17 +236,7 @@ __device__ __forceinline__ int car_move_one(const int *__restrict__ row_ptr, con
     if (d <= 64) {  // uniform
         if (tid < 64) {
             int x = N;
-            if (d > 0) {
-                const int q = col[b + min(tid, d - 1)];
-                if (dl.mv) {  // uniform: a pod that never left its base node is on it (L2-resident
-                              // base and bitmap words instead of the assign column's line)
-                    const int bq = dl.base[q];
-                    const unsigned w = dl.mv[(size_t)(q >> 5) * S + s];
-                    x = ((w >> (q & 31)) & 1u) ? assign[(size_t)q * S + s] : bq;
-                } else {
-                    x = assign[(size_t)q * S + s];
-                }
-            }
+            if (d > 0) x = assign[(size_t)col[b + min(tid, d - 1)] * S + s];
             const bool inN = (unsigned)x < (unsigned)N;
             const bool v = tid < d && inN && !ns.h(inN ? x : 0);
             int c = 0;
@@ -547,7 +534,7 @@ __global__ __launch_bounds__(256) void list_fill_kernel(const int *__restrict__ 
                                                         const int *__restrict__ base, int *__restrict__ cur,
                                                         int *__restrict__ pod, int *__restrict__ dcnt,
                                                         const int *__restrict__ pod_cpu, int *__restrict__ lnode,
-                                                        int2 *__restrict__ lpc, unsigned *__restrict__ mv,
+                                                        int2 *__restrict__ lpc,
                                                         int cap, unsigned *__restrict__ err) {
     constexpr int kK = 16;  // deviations kept per (wave, lane) in LDS; more: the rows are walked again
     __shared__ int wc[4][64];
@@ -565,9 +552,8 @@ __global__ __launch_bounds__(256) void list_fill_kernel(const int *__restrict__ 
             else *err = kErrListFill;
         }
     }
-    constexpr int kB = 16;  // (q0 is a multiple of 256: two batches make one 32-pod bitmap word)
+    constexpr int kB = 16;
     int n = 0;
-    unsigned mbits = 0u;
     for (int p0 = q0; p0 < q1; p0 += kB) {
         int a[kB], b[kB];
 #pragma unroll
@@ -579,17 +565,10 @@ __global__ __launch_bounds__(256) void list_fill_kernel(const int *__restrict__ 
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
             const int x = (unsigned)a[u] < (unsigned)N ? a[u] : N;
-            const bool dv = p0 + u < q1 && x != b[u];
-            if (dv) {
+            if (p0 + u < q1 && x != b[u]) {
                 if (n < kK) keep[wv][n][lane] = make_int2(p0 + u, x);
                 ++n;
             }
-            mbits |= (unsigned)dv << ((p0 + u) & 31);
-        }
-        // the moved bitmap: one word of 32 pods per lane (scenario), 256 B per wave store
-        if (((p0 + kB) & 31) == 0 || p0 + kB >= q1) {
-            if (s < S) mv[(size_t)(p0 >> 5) * S + s] = mbits;
-            mbits = 0u;
         }
     }
     wc[wv][lane] = n;
@@ -933,11 +912,8 @@ __device__ __forceinline__ int scn_pick(const T *__restrict__ asg, const int *__
 #pragma unroll
                 for (int u = 0; u < kU; ++u) en[u] = ln[min(j0 + u * 256 + t, nl - 1)];
             }
-            // a base pod of m is on m iff it never left it (bitmap clear); one that
-            // left has a list entry, found below when it is on m again
-            const unsigned w = dl.mv[(size_t)(q >> 5) * S + s];
-            const int c = pod_cpu[q];
-            const unsigned long long kb = (i0 + t < nb && !((w >> (q & 31)) & 1u)) ? key(q, c) : 0ull;
+            const int a = (int)asg[(size_t)q * S + s], c = pod_cpu[q];
+            const unsigned long long kb = (i0 + t < nb && a == m) ? key(q, c) : 0ull;
             if (kb > best) best = kb, bsrc = -1;
             if (j0 < nl) {
 #pragma unroll
@@ -1544,9 +1520,7 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
             RSK_TRY(r->lpod.reserve((size_t)P * 4));
             RSK_TRY(r->lcnt.reserve((size_t)S * 8));  // counts, then the picks' source entries
             const size_t lpc_off = ((size_t)S * cap * 4 + 15) & ~(size_t)15;  // lnode[S * cap], then lpc
-            const size_t mv_off = (lpc_off + (size_t)S * cap * 8 + 15) & ~(size_t)15;  // then the moved bitmap
-            RSK_TRY(r->llist.reserve(mv_off + (size_t)ceil_div(P, 32) * S * 4));
-            unsigned *mv = reinterpret_cast<unsigned *>(r->llist.as<char>() + mv_off);
+            RSK_TRY(r->llist.reserve(lpc_off + (size_t)S * cap * 8));
             int *lnode = r->llist.as<int>();
             int2 *lpc = reinterpret_cast<int2 *>(r->llist.as<char>() + lpc_off);
             int *cntb = r->loff.as<int>() + (N + 2);  // N + 1 counts, then the fill cursors
@@ -1562,10 +1536,9 @@ int rsk_rounds_run(rsk_rounds *r, int32_t *assign, int32_t S, const int32_t *cap
             RSK_CHECK(derr, "no device error word (mapped pinned memory)");
             list_fill_kernel<<<(unsigned)blocks, 256, 0, st>>>(d_assign, P, S, N, r->lbase.as<int>(), cntb,
                                                                  r->lpod.as<int>(), r->lcnt.as<int>(),
-                                                                 r->pod_cpu.as<int>(), lnode, lpc, mv, cap, derr);
+                                                                 r->pod_cpu.as<int>(), lnode, lpc, cap, derr);
             RSK_HIP(hipGetLastError());
             dl.base = r->lbase.as<int>();
-            dl.mv = mv;
             dl.cnt = r->lcnt.as<int>();
             dl.src = dl.cnt + S;
             dl.lnode = lnode;
