@@ -589,14 +589,6 @@ __device__ __forceinline__ void t16_rows64(const Tile16Args &a, unsigned *img, i
         if ((size_t)qd * S + sl >= a.n_assign) atomicOr(&rsk_dbg16, 4u);
 #endif
         const int *pa = reinterpret_cast<const int *>(asg + cell_off<kOff32>(RSK_B16(qd, a.n_assign / S, 4u), S, sl));
-#ifdef RSK_TILE_LDPOL  // experiment builds: the image loads as buffer loads with cache-policy bits RSK_TILE_LDPOL
-        if (kOff32) {
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<int *>(a.assign), (short)0, (int)(a.n_assign * 4u), 0x00020000);
-            v[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, (unsigned)cell_off<true>(qd, S, sl), 0, RSK_TILE_LDPOL);
-            continue;
-        }
-#endif
         v[u] = (RSK_TILE_NT & 1) ? __builtin_nontemporal_load(pa) : *pa;
     }
     unsigned cd[kB];
