@@ -245,9 +245,9 @@ static int launch_prep_main(hipStream_t stream, const Prep16Args &a) {
     // workgroup (N * SV / 4096 of them), with 4x the loads in flight of 256-thread
     // workgroups at 13 nodes per thread (prep 17 us at 50k nodes x 64).
     if (v4 && SV <= 64) {
-        const int npb = RSK_KNOB(RSK_PREP_NPB_SMALL, 4);
+        // (2 or 1 nodes per thread, or 256-thread workgroups: 0.0186-0.070 against 0.0162 ms, profiles/r06g)
+        const int npb = 4;
         const unsigned total = (unsigned)(ceil_div(a.N, npb) * SV);
-        if (RSK_KNOB(RSK_PREP_BLK256_SMALL, 0)) return prep_launch<4>(stream, a, SV, npb, total);
         return prep_launch<4, 1024>(stream, a, SV, npb, total);
     }
     const int target_threads = (int)std::min<int64_t>(256 * 1024, std::max<int64_t>(65536, 256LL * std::max(SV, 256)));

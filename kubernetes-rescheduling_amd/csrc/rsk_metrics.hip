@@ -811,10 +811,10 @@ __global__ __launch_bounds__(kNrThreads) void nr_spill_kernel(const int *__restr
                                                               int *__restrict__ cnt,
                                                               unsigned long long *__restrict__ cpu,
                                                               unsigned long long *__restrict__ mem) {
-    // a few workgroups striding over the blocks (only an overflowed block has
-    // work: none on the bench batches, where the launch is this check alone)
-    for (int b = (int)blockIdx.x; b < nblk; b += (int)gridDim.x) {
-    if (ecount[b * (kNrThreads / 64)] >= 0) continue;  // (uniform)
+    // (a workgroup per block: 32 workgroups striding over the blocks measured
+    // 4.8 against 4.4 us on the bench batches, where no block has work)
+    const int b = nr_block(nblk);
+    if (b >= nblk || ecount[b * (kNrThreads / 64)] >= 0) return;
     const int p0 = b * kNrPods, p1 = min(P, p0 + kNrPods);
     const size_t n = (size_t)(p1 - p0) * S;
     for (size_t i = threadIdx.x; i < n; i += kNrThreads) {
@@ -834,7 +834,6 @@ __global__ __launch_bounds__(kNrThreads) void nr_spill_kernel(const int *__restr
             atomicAdd(&cpu[o], (unsigned long long)-c);
             if (kMem) atomicAdd(&mem[o], (unsigned long long)-m);
         }
-    }
     }
 }
 
@@ -1469,8 +1468,7 @@ static int node_reduce_impl(rsk_ctx *ctx, const int32_t *assign, int32_t P, int3
         auto *sk = d_ms ? &nr_sum_kernel<true> : &nr_sum_kernel<false>;
         sk<<<(unsigned)(nbk * nchunk), kNrSumThreads, 0, ctx->stream>>>(base, nbk, nchunk, rec, N, S, d_cnt, ucs, ums);
         auto *xk = d_ms ? &nr_spill_kernel<true> : &nr_spill_kernel<false>;
-        xk<<<(unsigned)std::min(nblk, 32), kNrThreads, 0, ctx->stream>>>(d_assign, P, S, N, nblk, pkey, ecount, d_cpu,
-                                                                        lmem, d_cnt, ucs, ums);
+        xk<<<g8, kNrThreads, 0, ctx->stream>>>(d_assign, P, S, N, nblk, pkey, ecount, d_cpu, lmem, d_cnt, ucs, ums);
         RSK_HIP(hipGetLastError());
     } else {
         ScopedTimer tm(ctx, "node_reduce");
