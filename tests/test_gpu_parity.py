@@ -957,6 +957,48 @@ def test_car_direct_small_batches(ctx, S):
         assert (tgt.reshape(-1, S)[:, S - 1] == -2).all()     # no candidate anywhere in the last scenario
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("S", [1, 4])
+def test_car_direct_one_wave_rows_boundary(ctx, S):
+    """Round 6's one-wave path of car_move_one (rows of <= 64 neighbours: a
+    ballot per distinct node instead of the LDS hash) through the small-batch
+    launch, at its boundary: rows of 63, 64 and 65 entries with duplicates and
+    self edges, rows whose every neighbour sits on a hazard node in some
+    scenario (max score 0 with no zero-case words: the workgroup's scan of
+    every node), overloaded single candidates and None ties; every cell against
+    the oracle."""
+    from oracle import oracle as orc
+    from rsk import api
+    rng = np.random.default_rng(640 + S)
+    P, N = 3000, 40
+    rows_l = [rng.integers(0, P, int(rng.integers(0, 5))).tolist() for _ in range(P)]
+    for k in range(300):
+        d = (63, 64, 65)[k % 3]
+        r = rng.integers(0, P, d).tolist()
+        r[0] = k                 # a self edge
+        r[1] = r[2]              # a duplicate
+        rows_l[k] = r
+    rp = np.zeros(P + 1, np.int32)
+    rp[1:] = np.cumsum([len(r) for r in rows_l])
+    ci = np.array([q for r in rows_l for q in r], np.int32)
+    assign = rng.integers(0, N, (P, S)).astype(np.int32)
+    haz = (rng.random((N, S)) < 0.15).astype(np.uint8)
+    for k in range(0, 300, 7):   # every neighbour of row k on a hazard node in scenario k % S
+        s = k % S
+        hn = int(np.nonzero(haz[:, s])[0][0]) if haz[:, s].any() else 0
+        haz[hn, s] = 1
+        assign[[q for q in rows_l[k] if q != k], s] = hn
+    cap = np.full(N, 40000, np.int32)
+    use = rng.integers(20000, 45000, (N, S)).astype(np.int32)   # some rem < 0: None ties and overloaded singles
+    assign, haz, use = assign.reshape(-1), haz.reshape(-1), use.reshape(-1)
+    rpd, cid = _dedup_csr(rp, ci)
+    tgt, _ = api.car_place(rp, ci, assign, S, cap, use, haz, N, ctx=ctx)
+    ot, _ = orc.car(rpd, cid, assign, S, cap, use, haz, N)
+    bad = np.nonzero(tgt != ot)[0]
+    assert bad.size == 0, f"S={S}: {bad.size} differ, first {bad[0]}: gpu {tgt[bad[0]]} oracle {ot[bad[0]]}"
+    assert (ot == -1).any() and (ot >= 0).any()
+
+
 @pytest.mark.parametrize("S,n_hubs", [(64, 6), (256, 40)])
 def test_car_big_rows_beyond_the_fused_grid(ctx, S, n_hubs):
     """Rows whose tables exceed the fused grid's LDS (degree 1,200-1,900 over

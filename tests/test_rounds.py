@@ -186,3 +186,46 @@ def test_gpu_rounds_pod_lists_overflow_mid_run():
     for g, e, name in zip((g_a, g_u, ev, tg), exp, ("assign", "use", "evict", "target")):
         bad = np.nonzero(g != e)[0]
         assert bad.size == 0, f"{name}: {bad.size} differ, first {bad[0]}: gpu {g[bad[0]]} oracle {e[bad[0]]}"
+
+
+@pytest.mark.gpu
+def test_gpu_rounds_one_wave_rows_boundary():
+    """Round 6's one-wave path of car_move_one (rows of <= 64 neighbours: a
+    ballot per distinct node, no hash, no barrier) at its boundary: evicted
+    pods whose rows have 63, 64 and 65 entries (drawn with duplicates, self
+    edges included, so the distinct count differs from the entry count), a row
+    whose neighbours all sit on the hazard node in one scenario (max score 0:
+    the zero case from the loop's LDS detect state) and pods with one or no
+    neighbour; against oracle_rounds, every scenario and round."""
+    from oracle import oracle as orc
+    from rsk import _lib, api
+    rng = np.random.default_rng(64)
+    P, N, S, R = 700, 30, 8, 14
+    rows = [rng.integers(0, P, int(rng.integers(0, 4))).tolist() for _ in range(P)]
+    for k, d in enumerate([63, 64, 65, 64, 65, 1, 0]):
+        r = rng.integers(0, P, d).tolist()
+        if d >= 2:
+            r[0] = k               # a self edge
+            r[1] = r[2 % d]        # a duplicate
+        rows[k] = r
+    rp = np.zeros(P + 1, np.int32)
+    rp[1:] = np.cumsum([len(r) for r in rows])
+    ci = np.array([q for r in rows for q in r], np.int32)
+    assign = rng.integers(1, N, (P, S)).astype(np.int32)
+    assign[:7] = 0                                    # the boundary rows' pods on node 0, the hottest
+    assign[[q for q in rows[1] if q >= 7], 2] = 0     # scenario 2: row 1's neighbours on the hazard node too
+    pod_cpu = rng.integers(1, 400, P).astype(np.int32)
+    pod_cpu[:7] = 50000 - np.arange(7) * 1000         # evicted first, in row order
+    cap = np.full(N, 60000, np.int32)
+    load = np.stack([np.bincount(assign[:, s], weights=pod_cpu, minlength=N) for s in range(S)], axis=1)
+    use = (load + rng.integers(0, 3000, (N, 1))).astype(np.int32).reshape(-1)
+    assign = assign.reshape(-1)
+    exp = orc.rounds(rp, ci, pod_cpu, assign, S, cap, use, N, R, 40)
+    rounds = api.Rounds(rp, ci, pod_cpu, ctx=_lib.default_context())
+    a, u = assign.copy(), use.copy()
+    ev, tg = rounds.run(a, S, cap, u, N, R, threshold=40)
+    rounds.close()
+    assert set(range(5)) <= set(exp[2].tolist())     # the 63 / 64 / 65-entry rows are evicted
+    for g, e, name in zip((a, u, ev, tg), exp, ("assign", "use", "evict", "target")):
+        bad = np.nonzero(g != e)[0]
+        assert bad.size == 0, f"{name}: {bad.size} differ, first {bad[0]}: gpu {g[bad[0]]} oracle {e[bad[0]]}"
