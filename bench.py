@@ -9,6 +9,12 @@ and, at config 4, the largest side rows beside them on a second stream —
 car_side) scores every pod in every scenario against every node — P·N·S
 evaluations — with all inputs resident in HBM.
 
+Secondary configs: with no ``--config`` the line also carries ``configs``:
+config 2, config 4 (its CAR step, the row-sharded loop and kernel 3), config 5
+and config 5 at its 8-GPU per-rank share (S = 128), each run after the
+headline's timed region and parity sample with its own timing, parity check
+and roofline (one GPU only; ``--no-extra`` skips them).
+
 Multi-GPU: ``python bench.py --gpus N`` with no ``WORLD_SIZE`` in the
 environment starts ``torch.distributed.run --nproc-per-node N`` on itself as a
 child process (the parent touches no GPU) and exits with its status; under a
