@@ -207,18 +207,11 @@ __device__ __forceinline__ unsigned code16(int rem, bool haz, int B) {
 
 constexpr int kMaxNodes16 = 65535;  // node ids fit 16 bits, 0xffff stays free as the pad node
 
-// The code table's row stride (elements): S, padded by one 64-scenario line
-// when 2·S bytes is a multiple of 4 KiB, so that one chunk's code lines —
-// n·stride + chunk·128 B — do not all fall at the same offset modulo 4 KiB
-// (the L2's channel / set bits).
-int code_stride(int S);
-
 struct Prep16Args {
     const int *cap, *use;
     const uint8_t *haz;
     int N, S;
-    int cs;                      // the code table's row stride in elements (code_stride(S))
-    unsigned short *code;        // [(N+1)*cs] or null
+    unsigned short *code;        // [N*S] or null
     int *nodekey;                // [N*S] (hazard ? KEY_HAZ : cap - use) or null
     int *zc_cnt;                 // [S] (zero on entry: the previous execute's prep cleared this half)
     unsigned long long *zc_key;  // [S]
@@ -272,7 +265,6 @@ struct Tile16Args {
     int *out_target;
     int *out_score;
     int S, N, T, lsl;      // SL = 1 << lsl scenarios per workgroup (64 when S >= 64); T tiles from tile0
-    int cs;                // the code table's row stride in elements (code_stride(S))
     int tile0;
     int img_cells;         // LDS cells of the largest image (rmax * SL); the records follow
     int rec_cap;           // record ints reserved in LDS; the unit counter follows
@@ -295,7 +287,6 @@ struct SideArgs {
     const unsigned long long *zc_key;
     int *out_target, *out_score;
     int S, N;
-    int cs;                   // the code table's row stride in elements (code_stride(S))
     int H, hshift, K;         // per-team LDS geometry (side16_geometry), word offsets below
     int off_dl, off_ndl, off_dummy, off_fx, off_h2, h2cap;
     unsigned lds_team;

@@ -1098,7 +1098,6 @@ SideArgs side16_class_args(const rsk_car_plan *plan, int c, const SideBufs &b, i
     a.out_score = b.score;
     a.S = S;
     a.N = N;
-    a.cs = code_stride(S);
     a.ablate = sablate;
     return a;
 }
@@ -1292,7 +1291,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     // (S < 2^23: the tile kernel's 24-bit code offsets, rsk_car16.hip t16_rows64)
     // (rows above kMaxDegree neighbours: the side tables count in 16 bits, so
     // such a plan runs the wide path, whose car_bigrow counts in 32)
-    const bool compact = N <= kMaxNodes16 && code_stride(S) < (1 << 23) && plan->max_deg <= kMaxDegree;
+    const bool compact = N <= kMaxNodes16 && S < (1 << 23) && plan->max_deg <= kMaxDegree;
     if (!compact && N >= kPackMaxN && plan->n_sorted_rows > 0) {
         // the wide sorted tile classes pack node << 8 | row into 32 bits: route
         // 17..64 rows through the mid kernel instead (variant built once)
@@ -1338,7 +1337,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         d_key = plan->nodekey.as<int>();
     }
     if (compact) {
-        RSK_TRY(plan->code.reserve(((size_t)N + 1) * (size_t)code_stride(S) * 2));  // + row N, zeroed by the prep kernel
+        RSK_TRY(plan->code.reserve((NS + (size_t)S) * 2));  // + row N, zeroed by the prep kernel
         d_code = plan->code.as<unsigned short>();
     }
     // the zero-case words, double-buffered: half h = zc_key[S] u64, zc_cnt[S],
@@ -1365,7 +1364,6 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
     pa.haz = d_haz;
     pa.N = N;
     pa.S = S;
-    pa.cs = code_stride(S);
     pa.code = d_code;
     pa.nodekey = d_key;
     pa.zc_cnt = d_zcnt;
@@ -1510,7 +1508,6 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         a.recs = plan->recs.as<int>();
         a.assign = d_assign;
         a.code = d_code;
-        a.cs = code_stride(S);
         a.cap = d_cap;
         a.use = d_use;
         a.zc_cnt = d_zcnt;
@@ -1524,7 +1521,7 @@ int rsk_car_plan_execute(rsk_car_plan *plan, const int32_t *assign, int32_t S, c
         a.n_out = (unsigned)std::min<size_t>(QS, UINT32_MAX);
         a.n_pods = (unsigned)plan->n_img_pods;
         a.n_recs = (unsigned)plan->n_recs;
-        a.n_key = (unsigned)std::min<size_t>((size_t)N * (size_t)code_stride(S), UINT32_MAX);  // (row N after)
+        a.n_key = (unsigned)NS;
         const int SL = std::min(next_pow2(S), 64);
         a.lsl = 0;
         while ((1 << a.lsl) < SL) ++a.lsl;

@@ -69,7 +69,7 @@ __global__ __launch_bounds__(kPrep0Threads) void car_prep_small_kernel(const int
                                                                       int *__restrict__ zc_cnt,
                                                                       unsigned long long *__restrict__ zc_key,
                                                                       unsigned *__restrict__ zc_clear,
-                                                                      int clear_words, int cs) {
+                                                                      int clear_words) {
     __shared__ int red[kPrep0Threads / 64];
     __shared__ int lcnt[kPrepSmallS];
     __shared__ unsigned long long lkey[kPrepSmallS];
@@ -88,12 +88,12 @@ __global__ __launch_bounds__(kPrep0Threads) void car_prep_small_kernel(const int
     const int B = max(0, mc - 32766);  // the exact code window (rsk_car.h)
     for (int i = t; i < clear_words; i += kPrep0Threads) zc_clear[i] = 0u;  // the next execute's half
     if (code)
-        for (int i = t; i < S; i += kPrep0Threads) code[(size_t)N * cs + i] = 0;  // row N: no candidate
+        for (int i = t; i < S; i += kPrep0Threads) code[(size_t)N * S + i] = 0;  // row N: no candidate
     for (int i = t; i < N * S; i += kPrep0Threads) {
         const int n = i / S, sc = i - n * S;
         const int rem = cap[n] - use[i];
         const bool h = haz[i] != 0;
-        if (code) code[(size_t)n * cs + sc] = (unsigned short)code16(rem, h, B);
+        if (code) code[i] = (unsigned short)code16(rem, h, B);
         if (nodekey) nodekey[i] = h ? kKeyHaz : rem;
         if (!h) {
             atomicAdd(&lcnt[sc], 1);
@@ -125,9 +125,8 @@ __global__ __launch_bounds__(kBlock) void car_prep_kernel(const int *__restrict_
                                                        int npb, unsigned total, typename VecT<V>::C *__restrict__ code,
                                                        typename VecT<V>::I *__restrict__ nodekey,
                                                        int *__restrict__ zc_cnt, unsigned long long *__restrict__ zc_key,
-                                                       unsigned *__restrict__ zc_clear, int clear_words, int CSV) {
+                                                       unsigned *__restrict__ zc_clear, int clear_words) {
     // kBlock 1024 only with SV <= 256: the slots never exceed 256
-    // (CSV: the code table's row stride in vector units, code_stride(S) / V)
     static_assert(!kGrp || kBlock == 256, "grouped prep: 4 waves = 4 chunks");
     __shared__ int lcnt[256 * V];
     __shared__ unsigned long long lkey[256 * V];
@@ -147,7 +146,7 @@ __global__ __launch_bounds__(kBlock) void car_prep_kernel(const int *__restrict_
         for (int i = (int)threadIdx.x; i < clear_words; i += kBlock) zc_clear[i] = 0u;
     if (kCode && t < (unsigned)SV) {  // code row N: code 0 for every scenario (clamped invalid assignments)
         const unsigned z[V] = {};
-        code[(size_t)N * CSV + t] = cvec_make(z);
+        code[(size_t)N * SV + t] = cvec_make(z);
     }
     if (vt < total) {
         const int sv = (int)(vt % (unsigned)SV);
@@ -175,7 +174,7 @@ __global__ __launch_bounds__(kBlock) void car_prep_kernel(const int *__restrict_
                 best[x] = pk > best[x] ? pk : best[x];
             }
             if (kKey) nodekey[idx] = vec_make(k);
-            if (kCode) code[(size_t)n * CSV + sv] = cvec_make(cd);
+            if (kCode) code[idx] = cvec_make(cd);
         }
         const int slot = (int)(((unsigned)sv + (unsigned)SV - base) % (unsigned)SV);  // < nslot
 #pragma unroll
@@ -208,20 +207,15 @@ static int prep_launch(hipStream_t stream, const Prep16Args &a, int SV, int npb,
     I *key = reinterpret_cast<I *>(a.nodekey);
     if (a.code && a.nodekey)
         car_prep_kernel<V, true, true, kBlock, kGrp><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
-                                                                 a.zc_clear, a.clear_words, a.cs / V);
+                                                                 a.zc_clear, a.clear_words);
     else if (a.code)
         car_prep_kernel<V, true, false, kBlock, kGrp><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
-                                                                 a.zc_clear, a.clear_words, a.cs / V);
+                                                                 a.zc_clear, a.clear_words);
     else
         car_prep_kernel<V, false, true, kBlock, kGrp><<<grid, block, 0, stream>>>(a.cap, use, haz, a.N, SV, npb, total, code, key, a.zc_cnt, a.zc_key,
-                                                                 a.zc_clear, a.clear_words, a.cs / V);
+                                                                 a.zc_clear, a.clear_words);
     RSK_HIP(hipGetLastError());
     return RSK_OK;
-}
-
-int code_stride(int S) {
-    const int pad = RSK_KNOB(RSK_CODE_PAD, 0);  // experiment: scenarios of padding per code row
-    return S + pad;
 }
 
 static int launch_prep_main(hipStream_t stream, const Prep16Args &a);
@@ -230,7 +224,7 @@ int launch_prep(hipStream_t stream, const Prep16Args &a) {
     RSK_CHECK(a.code || a.nodekey, "prep: nothing to write");
     if ((int64_t)a.N * a.S <= kPrepSmallCells && a.S <= kPrepSmallS) {
         car_prep_small_kernel<<<1, kPrep0Threads, 0, stream>>>(a.cap, a.use, a.haz, a.N, a.S, a.code, a.nodekey,
-                                                               a.zc_cnt, a.zc_key, a.zc_clear, a.clear_words, a.cs);
+                                                               a.zc_cnt, a.zc_key, a.zc_clear, a.clear_words);
         RSK_HIP(hipGetLastError());
         return RSK_OK;
     }
@@ -582,7 +576,7 @@ __device__ __forceinline__ void t16_rows64(const Tile16Args &a, unsigned *img, i
     const int lane = threadIdx.x & 63;
     const int s = s0 + lane;
     const unsigned sl = (unsigned)min(s, (int)S - 1);
-    const unsigned S2 = 2u * (unsigned)a.cs, sl2 = 2u * sl;  // (code row stride in bytes)
+    const unsigned S2 = 2u * S, sl2 = 2u * sl;
     const cint_ptr pods = const_ptr(a.img_pods) + img_off + r0;
     const int nr = rend - r0;  // >= 1 except for waves past the image
     if (nr <= 0) return;
@@ -657,7 +651,7 @@ __device__ __forceinline__ void t16_load_image(const Tile16Args &a, unsigned *im
             for (int u = 0; u < kE; ++u) {
                 const int s = s0 + (e[u] & msk);
                 const bool ok = (unsigned)v[u] < N && s < (int)S;
-                cd[u] = ld16(code, RSK_B16(ok ? (unsigned)v[u] * (unsigned)a.cs + (unsigned)s : 0u, a.n_key, 8u));
+                cd[u] = ld16(code, RSK_B16(ok ? (unsigned)v[u] * S + (unsigned)s : 0u, a.n_key, 8u));
             }
 #pragma unroll
             for (int u = 0; u < kE; ++u) {

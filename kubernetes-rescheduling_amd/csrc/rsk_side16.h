@@ -63,7 +63,7 @@ __device__ __forceinline__ void glob_fence(bool glob) {
 // hazard as car_prep computes it (node N and beyond: no candidate).
 template <bool kOTF>
 __device__ __forceinline__ unsigned side_code(const SideArgs &a, unsigned n, unsigned s, int B) {
-    if (!kOTF) return ld16(a.code, n * (unsigned)a.cs + s);  // row N: code 0
+    if (!kOTF) return ld16(a.code, n * (unsigned)a.S + s);  // row N: code 0
     if (n >= (unsigned)a.N) return kCodeHaz;
     const unsigned i = n * (unsigned)a.S + s;
     return code16(a.cap[n] - ld32(a.use, i), a.haz[i] != 0, B);

@@ -45,11 +45,6 @@ for s in "${@:-test smoke bench}"; do
                step "abh_base_$rep" 300 python -u bench.py --config headline --no-cpu-baseline
                step "abh_${lib}_$rep" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_$lib.so python -u bench.py --config headline --no-cpu-baseline
              done ;;
-      abhk:*) kv=${w#abhk:}; for rep in 1 2; do
-               step "abhk_base_$rep" 300 python -u bench.py --config headline --no-cpu-baseline
-               step "abhk_${kv//[=,]/_}_$rep" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u bench.py --config headline --no-cpu-baseline
-             done ;;
-      tk:*) kv=${w#tk:}; step "pytest_knobs_${kv//[=,]/_}" 600 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_headline.py -m gpu -x -v --timeout 300 --timeout-method thread -k "car or config3 or config2" ;;
       bnoev) step bench_noevents 600 python -u bench.py --no-cpu-baseline --no-kernel-events ;;
       nr:*) kv=${w#nr:}; step "nr_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_abl.so ${kv//,/ } python -u tools/nrbench.py ;;
       nrk:*) kv=${w#nrk:}; step "nrk_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u tools/nrbench.py ;;
