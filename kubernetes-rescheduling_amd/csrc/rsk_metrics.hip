@@ -433,8 +433,14 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(const int *__restrict_
 //    deviation cells are added here, after the stores, by global atomics.
 // podmonitor.py:104-121 (pods grouped by node), nodemonitor.py:24-46 (per-node
 // sums).  Integer sums: the result does not depend on any order.
-constexpr int kNrPods = 2048;     // pods per block of the scan / place / spill launches
-constexpr int kNrThreads = 512;   // their threads: 8 waves of 256 pods
+#ifndef RSK_NR_PODS
+#define RSK_NR_PODS 2048
+#endif
+#ifndef RSK_NR_THREADS
+#define RSK_NR_THREADS 512
+#endif
+constexpr int kNrPods = RSK_NR_PODS;       // pods per block of the scan / place / spill launches
+constexpr int kNrThreads = RSK_NR_THREADS;  // their threads: 8 waves of 256 pods
 constexpr int kNrBatch = 16;      // assign rows per batch (two batches in flight per wave)
 constexpr int kNrBucketBits = 5, kNrBucketNodes = 1 << kNrBucketBits;  // nodes per bucket
 constexpr int kNrMaxCounters = 16384;  // buckets + bins: a block's counters in LDS (N < 2^19)

@@ -45,6 +45,9 @@ for s in "${@:-test smoke bench}"; do
                step "abh_base_$rep" 300 python -u bench.py --config headline --no-cpu-baseline
                step "abh_${lib}_$rep" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_$lib.so python -u bench.py --config headline --no-cpu-baseline
              done ;;
+      prof1m:*) lib=${w#prof1m:}; env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_$lib.so ./tools/gpu_prof.sh 1m50k "$out/prof_1m50k_$lib" > "$out/prof_1m50k_$lib.log" 2>&1 || { tail -5 "$out/prof_1m50k_$lib.log"; exit 1; }
+                echo "== prof1m $lib done $(date +%T)" ;;
+      tnr:*) lib=${w#tnr:}; step "pytest_nr_$lib" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_$lib.so python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "node_reduce or kernel3 or write_guard" ;;
       bnoev) step bench_noevents 600 python -u bench.py --no-cpu-baseline --no-kernel-events ;;
       nr:*) kv=${w#nr:}; step "nr_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_abl.so ${kv//,/ } python -u tools/nrbench.py ;;
       nrk:*) kv=${w#nrk:}; step "nrk_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u tools/nrbench.py ;;
