@@ -434,13 +434,14 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(const int *__restrict_
 // podmonitor.py:104-121 (pods grouped by node), nodemonitor.py:24-46 (per-node
 // sums).  Integer sums: the result does not depend on any order.
 #ifndef RSK_NR_PODS
-#define RSK_NR_PODS 2048
+#define RSK_NR_PODS 4096
 #endif
 #ifndef RSK_NR_THREADS
-#define RSK_NR_THREADS 512
+#define RSK_NR_THREADS 1024
 #endif
 constexpr int kNrPods = RSK_NR_PODS;       // pods per block of the scan / place / spill launches
-constexpr int kNrThreads = RSK_NR_THREADS;  // their threads: 8 waves of 256 pods
+constexpr int kNrThreads = RSK_NR_THREADS;  // their threads: 16 waves of 256 pods (r06j: 4096 / 1024
+                                            // 3.5% under 2048 / 512 at 1M x 64: half the colscan blocks)
 constexpr int kNrBatch = 16;      // assign rows per batch (two batches in flight per wave)
 constexpr int kNrBucketBits = 5, kNrBucketNodes = 1 << kNrBucketBits;  // nodes per bucket
 constexpr int kNrMaxCounters = 16384;  // buckets + bins: a block's counters in LDS (N < 2^19)
@@ -893,16 +894,23 @@ __global__ void decode_first_max(const unsigned long long *__restrict__ key, int
 // for equal values, ~1e-15 relative otherwise); then per s a fixed-order Chan
 // merge.  The summation order differs from numpy's pairwise mean and two-pass
 // variance, so the std agrees within tolerance (the tests: 1e-9 relative; the
-// north star: 1e-5), not bit for bit.
+// north star: 1e-5), not bit for bit.  When S divides 256 a workgroup holds
+// F = 256 / S whole chunks for every scenario and folds them (in order, in
+// LDS) into one partial per scenario before writing: F times fewer partials
+// for the merge to read (50k nodes x 64 scenarios: 500 instead of 2,000).
+__device__ __forceinline__ void chan_merge(long long &n, double &mean, double &m2, long long nb, double mb, double m2b);
+
 __global__ __launch_bounds__(256) void std_partial_kernel(const int *__restrict__ use, const int *__restrict__ cap,
-                                                          int N, int S, int npb, unsigned total,
+                                                          int N, int S, int npb, unsigned total, int fold,
                                                           double *__restrict__ pmean, double *__restrict__ pm2,
                                                           int *__restrict__ pcnt) {
 #pragma clang fp contract(off)
+    __shared__ double fm[256], fq[256];
+    __shared__ int fc[256];
     const unsigned t = blockIdx.x * 256u + threadIdx.x;
-    if (t >= total) return;
+    if (!fold && t >= total) return;
     const int s = (int)(t % (unsigned)S), ch = (int)(t / (unsigned)S);
-    const int n0 = ch * npb, n1 = min(N, n0 + npb);
+    const int n0 = ch * npb, n1 = t < total ? min(N, n0 + npb) : n0;  // past the end: an empty chunk
     constexpr int kU = 8;  // loads in flight per thread
     double sum = 0.0, sq = 0.0, K = 0.0;
     int c = 0;
@@ -928,10 +936,26 @@ __global__ __launch_bounds__(256) void std_partial_kernel(const int *__restrict_
     }
     const double mean = c ? K + sum / c : 0.0;
     const double m2 = c ? fmax(0.0, sq - sum * (sum / c)) : 0.0;
-    const size_t o = (size_t)ch * S + s;
-    pmean[o] = mean;
-    pm2[o] = m2;
-    pcnt[o] = c;
+    if (!fold) {
+        const size_t o = (size_t)ch * S + s;
+        pmean[o] = mean;
+        pm2[o] = m2;
+        pcnt[o] = c;
+        return;
+    }
+    const int tl = (int)threadIdx.x;
+    fm[tl] = mean;
+    fq[tl] = m2;
+    fc[tl] = c;
+    __syncthreads();
+    if (tl >= S) return;
+    long long n = 0;
+    double fmean = 0.0, fm2 = 0.0;
+    for (int f = tl; f < 256; f += S) chan_merge(n, fmean, fm2, fc[f], fm[f], fq[f]);
+    const size_t o = (size_t)blockIdx.x * S + tl;
+    pmean[o] = fmean;
+    pm2[o] = fm2;
+    pcnt[o] = (int)n;
 }
 
 // Chan et al.'s pairwise update: (n, mean, m2) of a union from its two parts.
@@ -951,13 +975,19 @@ __device__ __forceinline__ void chan_merge(long long &n, double &mean, double &m
 // states pairwise (xor butterfly, 6 levels), then thread 0 the four waves in
 // order; the result is the same for every run (fixed order).  (One thread per
 // scenario walking every chunk in a chain of fp64 divides took 1.6 ms at 50k
-// nodes x 64 scenarios; one wave per scenario 15 us.)
+// nodes x 64 scenarios; one wave per scenario 15 us.)  Partials are
+// [chunk][scenario], so one 64-B line holds 8 neighbouring scenarios' values:
+// workgroup b takes scenario (b % 8) * S/8 + b / 8, so the workgroups that
+// share an XCD (and its L2) share those lines instead of every XCD fetching
+// every line.
 __global__ __launch_bounds__(256) void std_merge_kernel(const double *__restrict__ pmean, const double *__restrict__ pm2,
                                                         const int *__restrict__ pcnt, int nchunks, int S,
                                                         double *__restrict__ out) {
     __shared__ double wm[4], wq[4];
     __shared__ long long wn[4];
-    const int s = (int)blockIdx.x, t = (int)threadIdx.x, lane = t & 63, w = t >> 6;
+    const int b = (int)blockIdx.x;
+    const int s = (S & 7) ? b : (b & 7) * (S >> 3) + (b >> 3);
+    const int t = (int)threadIdx.x, lane = t & 63, w = t >> 6;
     double mean = 0.0, m2 = 0.0;
     long long n = 0;
     constexpr int kU = 4;
@@ -1597,13 +1627,16 @@ int rsk_load_std(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *cap_cpu, i
     RSK_TRY(ctx->work[1].reserve((size_t)nch * S * 8));
     RSK_TRY(ctx->work[2].reserve((size_t)nch * S * 4));
     const unsigned total = (unsigned)((int64_t)nch * S);
+    const unsigned grid = (unsigned)ceil_div(total, 256);
+    const int fold = 256 % S == 0 && S < 256;  // a workgroup holds 256 / S whole chunks
     {
         ScopedTimer tm(ctx, "load_std");
-        std_partial_kernel<<<(unsigned)ceil_div(total, 256), 256, 0, ctx->stream>>>(
-            d_use, d_cap, N, S, npb, total, ctx->work[0].as<double>(), ctx->work[1].as<double>(),
-            ctx->work[2].as<int>());
-        std_merge_kernel<<<(unsigned)S, 256, 0, ctx->stream>>>(
-            ctx->work[0].as<double>(), ctx->work[1].as<double>(), ctx->work[2].as<int>(), nch, S, d_out);
+        std_partial_kernel<<<grid, 256, 0, ctx->stream>>>(d_use, d_cap, N, S, npb, total, fold,
+                                                          ctx->work[0].as<double>(), ctx->work[1].as<double>(),
+                                                          ctx->work[2].as<int>());
+        std_merge_kernel<<<(unsigned)S, 256, 0, ctx->stream>>>(ctx->work[0].as<double>(), ctx->work[1].as<double>(),
+                                                               ctx->work[2].as<int>(), fold ? (int)grid : nch, S,
+                                                               d_out);
         RSK_HIP(hipGetLastError());
     }
     if (!dev) {

@@ -292,6 +292,28 @@ def test_baselines_ties_and_empty(ctx):
             assert api.spread_place(val, rank, haz, N, 1, ctx=ctx)[0] == orc.spread(val, rank, haz, N, 1)[0]
 
 
+@pytest.mark.parametrize("N,S", [(1, 1), (5, 2), (40_000, 1), (3_001, 8), (20_000, 64), (777, 128), (9_000, 256),
+                                 (1_500, 12), (2_000, 300), (600, 4096)])
+def test_load_std_shapes(ctx, N, S):
+    """rsk_load_std over the partial-kernel shapes: S dividing 256 (a workgroup
+    folds 256 / S whole chunks before writing), S = 256 and S that does not
+    divide it (one partial per chunk), S not a multiple of 8 (the merge's
+    XCD-grouped scenario order falls back to the identity), ragged last
+    chunks and a partly filled last workgroup, cap <= 0 nodes skipped
+    (nodemonitor.py:38-43); within 1e-9 relative of the oracle."""
+    from oracle import oracle as orc
+    from rsk import api
+    rng = np.random.default_rng(N * 7 + S)
+    cap = rng.integers(1_000, 64_000, N).astype(np.int32)
+    if N > 4:
+        cap[rng.choice(N, N // 5, replace=False)] = 0
+        cap[rng.choice(N, N // 9, replace=False)] = -3
+    use = rng.integers(0, 64_000, (N, S)).astype(np.int32).reshape(-1)
+    std = api.load_std(use, cap, N, S, ctx=ctx)
+    ostd = orc.load_std(use, cap, N, S)
+    np.testing.assert_allclose(std, ostd, rtol=1e-9, atol=1e-12)
+
+
 def test_metrics_vs_oracle(ctx):
     from oracle import oracle as orc
     from rsk import api, synth
