@@ -416,9 +416,9 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(const int *__restrict_
 //  1 nr_scan: every assign row read once, coalesced (lane = scenario, the next
 //    16 rows in flight while a batch is examined): the keys (pkey), and per
 //    block of kNrPods pods the count of its keys per 32-node bucket and of its
-//    deviation records per (bucket, 64-scenario chunk) bin (a + at the cell's
+//    deviation records per (64-scenario chunk, bucket) bin (a + at the cell's
 //    node, a - at the key node), one entry per deviation cell (int2: node or
-//    kNrNoNode | (p - p0) << 20, s) into its wave's eighth of the block's
+//    kNrNoNode | (p - p0) << 20, s) into its wave's share of the block's
 //    region of ecap = cells / 8 entries;
 //  2 nr_colscan: per counter (bucket or bin) the exclusive scan of its
 //    per-block counts, laid out [counter][block], and its total;
@@ -439,6 +439,9 @@ __global__ __launch_bounds__(256) void node_reduce_kernel(const int *__restrict_
 #ifndef RSK_NR_THREADS
 #define RSK_NR_THREADS 1024
 #endif
+#ifndef RSK_NR_ABL
+#define RSK_NR_ABL 0  // profiling variants only (results wrong): 1 no row examination (keys and pkey kept;
+#endif                // the rows folded into one word)
 constexpr int kNrPods = RSK_NR_PODS;       // pods per block of the scan / place / spill launches
 constexpr int kNrThreads = RSK_NR_THREADS;  // their threads: 16 waves of 256 pods (r06j: 4096 / 1024
                                             // 3.5% under 2048 / 512 at 1M x 64: half the colscan blocks)
@@ -470,20 +473,23 @@ __device__ __forceinline__ int nr_block(int nblk) {
 }
 
 // launch 1: a wave walks its pods' (batch of 16, chunk) units, the next unit's
-// 16 rows (wave-uniform row pointers) and the 16 pods' scenario 0 / 21 / 42
-// words (one gather: lane l reads pod l % 16's word l / 16; the majority by
-// two shuffles) loaded while one is examined.  A row's test is one compare
-// folded into a per-lane bit mask, one wave OR per batch; only rows with a
-// deviating lane (~half of the bench's) write entries, into the wave's own
-// eighth of the block's region.  Counters ->
-// bh[j * nblk + b] (the entry bins zeroed when a wave overflowed), the waves'
-// entry counts (-1: the block overflowed) -> ecount[b * 8 + w].
+// 16 rows (wave-uniform row pointers) loaded while one is examined; the 16
+// pods' keys are readlanes of their chunk-0 rows (scenarios 0 / 21 / 42, the
+// majority in scalar registers).  (Round 5 gathered those words with a second
+// load per unit: 14 us of the launch's 72, r06q.)  A row's test is one compare
+// into a wave mask (SGPRs); only rows with a deviating lane (~half of the
+// bench's) write entries, into the wave's own share of the block's region.
+// (Round 5's per-lane bit mask folded by a wave OR, then a ballot per flagged
+// row, issued ~28 VALU instructions per row: the scan was issue-bound.)
+// Counters -> bh[j * nblk + b] (the entry bins zeroed when a wave
+// overflowed), the waves' entry counts (-1: the block overflowed) ->
+// ecount[b * waves + w].
 template <bool kOff32, bool kMaj, int kB = kNrBatch>
 __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restrict__ assign, int P, int S, int N,
                                                              int nbk, int nchunk, int nblk, size_t ecap,
                                                              int *__restrict__ pkey, int *__restrict__ bh,
                                                              int2 *__restrict__ ent, int *__restrict__ ecount) {
-    extern __shared__ int lh[];  // [nbk] key buckets, then [nbk * nchunk] entry bins
+    extern __shared__ int lh[];  // [nbk] key buckets, then [nchunk][nbk] entry bins
     __shared__ int over;
     const int b = nr_block(nblk);
     if (b >= nblk) return;
@@ -492,6 +498,7 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
     for (int j = t; j < nh; j += kNrThreads) lh[j] = 0;
     if (t == 0) over = 0;
     __syncthreads();
+    int abl_acc = 0;
     constexpr int kPW = kNrPods / (kNrThreads / 64), kW = kNrThreads / 64;
     const int p0 = b * kNrPods, q0 = p0 + wv * kPW, q1 = min(P, q0 + kPW);
     const int nv = q1 > q0 ? (q1 - q0 + kB - 1) / kB * nchunk : 0;  // the wave's units
@@ -500,80 +507,125 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
     int2 *__restrict__ E = ent + (size_t)b * ecap + (size_t)wv * wcap;
     unsigned wpos = 0u;
     bool wover = false;
-    auto load = [&](int v, int (&r)[kB], int (&kr)[3]) {  // clamped: always valid addresses
-        v = min(v, nv - 1);
-        const int bt = v / nchunk, c = v - bt * nchunk, pb = q0 + bt * kB, last = min(q1, pb + kB) - 1;
-        const unsigned sc = (unsigned)min(c * 64 + lane, S - 1);
-#pragma unroll
-        for (int u = 0; u < kB; ++u)  // a wave-uniform row base: the load's address is the lane's 32-bit offset
-            r[u] = __builtin_nontemporal_load(assign + (size_t)min(pb + u, last) * S + sc);
-        // the keys' words in one gather: lane l reads pod pb + l % 16's scenario 0
-        // (l < 16), 21 (l < 32) or 42 (kMaj; S < 43: scenario 0 only)
-        const unsigned pk = (unsigned)min(pb + (lane & (kB - 1)), last);
-        const unsigned ks = kMaj ? (lane < kB ? 0u : lane < 2 * kB ? 21u : 42u) : 0u;
-        kr[0] = *reinterpret_cast<const int *>(asg + nr_off<kOff32>(pk, (unsigned)S, ks));
-    };
-    auto examine = [&](int v, const int (&r)[kB], const int (&kr)[3]) {
-        const int bt = v / nchunk, c = v - bt * nchunk, pb = q0 + bt * kB, nb = min(kB, q1 - pb);
-        int kv = kr[0];  // lane u < 16: pod pb + u's key
-        if (kMaj) {
-            const int k1 = __shfl(kr[0], lane + kB, 64), k2 = __shfl(kr[0], lane + 2 * kB, 64);
-            kv = (kv == k1 || kv == k2) ? kv : (k1 == k2 ? k1 : kv);
+    auto split = [&](int v, int &bt, int &c) {  // unit v -> (batch, chunk); nchunk = 1 when S <= 64
+        if (nchunk == 1) {
+            bt = v;
+            c = 0;
+        } else {
+            bt = v / nchunk;
+            c = v - bt * nchunk;
         }
-        kv = (unsigned)kv < (unsigned)N ? kv : N;
-        if (c == 0 && lane < nb) {
-            pkey[pb + lane] = kv;
-            if (kv < N) atomicAdd(&lh[kv >> kNrBucketBits], 1);
+    };
+    auto load = [&](int v, int (&r)[kB]) {  // clamped: always valid addresses
+        v = min(v, nv - 1);
+        int bt, c;
+        split(v, bt, c);
+        const int pb = q0 + bt * kB, last = min(q1, pb + kB) - 1;
+        const unsigned sc = (unsigned)min(c * 64 + lane, S - 1);
+        if (kOff32 && last == pb + kB - 1) {  // a full batch: the lane's 32-bit offset plus a row stride
+            const unsigned o0 = ((unsigned)pb * (unsigned)S + sc) << 2, st = (unsigned)S << 2;
+#pragma unroll
+            for (int u = 0; u < kB; ++u)
+                r[u] = __builtin_nontemporal_load(reinterpret_cast<const int *>(asg + (o0 + (unsigned)u * st)));
+        } else {
+#pragma unroll
+            for (int u = 0; u < kB; ++u)  // a wave-uniform row base: the load's address is the lane's 32-bit offset
+                r[u] = __builtin_nontemporal_load(assign + (size_t)min(pb + u, last) * S + sc);
+        }
+    };
+    int kvb = N;  // the current batch's keys (lane u: pod pb + u's), taken from its chunk-0 unit
+    auto examine = [&](int v, const int (&r)[kB]) {
+        int bt, c;
+        split(v, bt, c);
+        const int pb = q0 + bt * kB, nb = min(kB, q1 - pb);
+        if (c == 0) {  // the keys: readlanes of the rows' scenarios 0 / 21 / 42 (the majority; S < 43: 0)
+            int kn = N;
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                int k0 = __builtin_amdgcn_readlane(r[u], 0);
+                if (kMaj) {
+                    const int k1 = __builtin_amdgcn_readlane(r[u], 21), k2 = __builtin_amdgcn_readlane(r[u], 42);
+                    k0 = (k0 == k1 || k0 == k2) ? k0 : (k1 == k2 ? k1 : k0);
+                }
+                k0 = (unsigned)k0 < (unsigned)N ? k0 : N;
+                kn = lane == u ? k0 : kn;
+            }
+            kvb = kn;
+            if (lane < nb) {
+                pkey[pb + lane] = kn;
+                if (kn < N) atomicAdd(&lh[kn >> kNrBucketBits], 1);
+            }
+        }
+        const int kv = kvb;  // lane u < 16: pod pb + u's key
+        if (RSK_NR_ABL & 1) {
+#pragma unroll
+            for (int u = 0; u < kB; ++u) abl_acc ^= r[u] * (u + 1);
+            return;
         }
         const int s = c * 64 + lane;
         const bool live = s < S;
-        // bit u of dev: the lane's cell of unit u is off the pod's key node; D:
-        // the units with any such lane (an OR over the wave)
-        unsigned dev = 0u;
+        const int cb = nbk + c * nbk;  // the chunk's entry bins ([chunk][bucket]: no multiply per cell)
+        // row u: one compare into a wave mask (v_cmp to SGPRs; rows with no
+        // deviating lane skip on it); the deviating lanes write their entries,
+        // lane u of kc collects the row's count for one key-bin add per unit
+        int kc = 0;
+        const unsigned long long liveM = __builtin_amdgcn_ballot_w64(live);
+        auto emit = [&](int u, unsigned long long dm) {
+            const bool inN = (unsigned)r[u] < (unsigned)N;
+            E[wpos + nr_rank(dm)] = make_int2((inN ? r[u] : kNrNoNode) | ((pb + u - p0) << 20), s);
+            if (inN) atomicAdd(&lh[cb + (r[u] >> kNrBucketBits)], 1);
+        };
+        // (llvm.amdgcn.icmp: the compare's own SGPR mask; a ballot of the bool
+        // is materialised through a VGPR, two more VALU per row)
+        if (nb == kB && wpos + (unsigned)(kB * 64) <= wcap) {  // a full batch with room for every cell
 #pragma unroll
-        for (int u = 0; u < kB; ++u) dev |= (unsigned)(r[u] != __builtin_amdgcn_readlane(kv, u)) << u;
-        dev = live ? dev : 0u;  // (one select: a per-lane branch per row costs exec-mask juggling)
-        // (the OR over the wave by DPP, VALU steps: 80.5 against 81.5 us with
-        // six ds_swizzle / bpermute round trips, profiles/r06d)
-        const unsigned D = dpp_or(dev) & (nb >= 32 ? 0xffffffffu : (1u << nb) - 1u);
+            for (int u = 0; u < kB; ++u) {
+                const int k = __builtin_amdgcn_readlane(kv, u);
+                const unsigned long long dm = __builtin_amdgcn_uicmp((unsigned)r[u], (unsigned)k, 33 /* NE */) & liveM;
+                if (!dm) continue;
+                if (live && r[u] != k) emit(u, dm);
+                const unsigned nd = (unsigned)__popcll(dm);
+                kc = lane == u ? (int)nd : kc;
+                wpos += nd;
+            }
+        } else {
 #pragma unroll
-        for (int u = 0; u < kB; ++u) {
-            if (!((D >> u) & 1u)) continue;
-            const int k = __builtin_amdgcn_readlane(kv, u);
-            const bool d = (dev >> u) & 1u;
-            const unsigned long long dm = __builtin_amdgcn_ballot_w64(d);
-            const unsigned nd = (unsigned)__popcll(dm);
-            if (wpos + nd > wcap) {
-                wover = true;  // (the block lists none: nr_spill adds its cells)
-                continue;
+            for (int u = 0; u < kB; ++u) {
+                const int k = __builtin_amdgcn_readlane(kv, u);
+                const unsigned long long dm =
+                    u < nb ? __builtin_amdgcn_uicmp((unsigned)r[u], (unsigned)k, 33 /* NE */) & liveM : 0ull;
+                if (!dm) continue;
+                const unsigned nd = (unsigned)__popcll(dm);
+                if (wpos + nd > wcap) {
+                    wover = true;  // (the block lists none: nr_spill adds its cells)
+                    continue;
+                }
+                if (live && r[u] != k) emit(u, dm);
+                kc = lane == u ? (int)nd : kc;
+                wpos += nd;
             }
-            if (d) {
-                const bool inN = (unsigned)r[u] < (unsigned)N;
-                E[wpos + nr_rank(dm)] = make_int2((inN ? r[u] : kNrNoNode) | ((pb + u - p0) << 20), s);
-                if (inN) atomicAdd(&lh[nbk + (r[u] >> kNrBucketBits) * nchunk + c], 1);
-            }
-            if (k < N && lane == 0) atomicAdd(&lh[nbk + (k >> kNrBucketBits) * nchunk + c], (int)nd);
-            wpos += nd;
         }
+        if (kc && kv < N) atomicAdd(&lh[cb + (kv >> kNrBucketBits)], kc);  // lanes < kB: the key nodes' counts
     };
     if (nv > 0) {
-        int ra[kB], rb[kB], ka[3], kb[3];
-        load(0, ra, ka);
+        int ra[kB], rb[kB];
+        load(0, ra);
         // (the empty asm after each prefetch: the compiler may not hoist the
-        // examined unit's first uses of its keys above the next unit's loads)
+        // examined unit's first uses of its rows above the next unit's loads)
         for (int v = 0; v < nv; v += 2) {
-            load(v + 1, rb, kb);
-            asm volatile("" : "+v"(ka[0])::"memory");
-            examine(v, ra, ka);
-            load(v + 2, ra, ka);
-            asm volatile("" : "+v"(kb[0])::"memory");
-            if (v + 1 < nv) examine(v + 1, rb, kb);
+            load(v + 1, rb);
+            asm volatile("" : "+v"(ra[0])::"memory");
+            examine(v, ra);
+            load(v + 2, ra);
+            asm volatile("" : "+v"(rb[0])::"memory");
+            if (v + 1 < nv) examine(v + 1, rb);
         }
     }
     if (wover && lane == 0) over = 1;
     __syncthreads();
     const bool bo = over != 0;
     for (int j = t; j < nh; j += kNrThreads) bh[(size_t)j * nblk + b] = (bo && j >= nbk) ? 0 : lh[j];
+    if (RSK_NR_ABL) asm volatile("" ::"v"(abl_acc));  // (keeps the ablated rows' loads)
     if (lane == 0) ecount[b * kW + wv] = bo ? -1 : (int)wpos;
 }
 
@@ -721,12 +773,12 @@ __global__ __launch_bounds__(kNrThreads) void nr_place_kernel(const int *__restr
                 const long long mm = kMem ? lm[lp] : 0;
                 const int mlo = (int)(unsigned)(unsigned long long)mm, mhi = (int)(mm >> 32);
                 if (node < N) {  // + the pod at its node
-                    const int pos = atomicAdd(&cur[nbk + (node >> kNrBucketBits) * nchunk + (sc >> 6)], 1);
+                    const int pos = atomicAdd(&cur[nbk + __umul24(sc >> 6, nbk) + (node >> kNrBucketBits)], 1);
                     if ((unsigned)pos < (unsigned)nrec) rec[pos] = make_int4((node & (kNrBucketNodes - 1)) | lane, lc[lp], mlo, mhi);
                     else *err = kErrNrPlace;
                 }
                 if (key < N) {  // - the pod at its key node
-                    const int pos = atomicAdd(&cur[nbk + (key >> kNrBucketBits) * nchunk + (sc >> 6)], 1);
+                    const int pos = atomicAdd(&cur[nbk + __umul24(sc >> 6, nbk) + (key >> kNrBucketBits)], 1);
                     if ((unsigned)pos < (unsigned)nrec) rec[pos] = make_int4((key & (kNrBucketNodes - 1)) | 32 | lane, lc[lp], mlo, mhi);
                     else *err = kErrNrPlace;
                 }
@@ -735,7 +787,7 @@ __global__ __launch_bounds__(kNrThreads) void nr_place_kernel(const int *__restr
     }
 }
 
-// launch 4: a workgroup per bin (bucket b, chunk c)
+// launch 4: a workgroup per bin (chunk c, bucket b)
 constexpr int kNrSumThreads = 256;
 template <bool kMem>
 __global__ __launch_bounds__(kNrSumThreads) void nr_sum_kernel(const int *__restrict__ base, int nbk, int nchunk,
@@ -748,9 +800,9 @@ __global__ __launch_bounds__(kNrSumThreads) void nr_sum_kernel(const int *__rest
     __shared__ unsigned long long bcpu[kNrBucketNodes], bmem[kNrBucketNodes];
     __shared__ int dc[kE];
     __shared__ unsigned long long dcpu[kE], dmem[kMem ? kE : 1];
-    const int t = (int)threadIdx.x, g = (int)blockIdx.x, b = g / nchunk, c = g - b * nchunk;
+    const int t = (int)threadIdx.x, g = (int)blockIdx.x, c = g / nbk, b = g - c * nbk;
     const int lo = base[b], hi = base[b + 1];
-    const int j = nbk + b * nchunk + c, elo = base[j], ehi = base[j + 1];
+    const int j = nbk + g, elo = base[j], ehi = base[j + 1];  // bins [chunk][bucket]
     if (t < kNrBucketNodes) {
         bc[t] = 0;
         bcpu[t] = 0ull;
