@@ -484,25 +484,17 @@ __device__ __forceinline__ int nr_block(int nblk) {
 // Counters -> bh[j * nblk + b] (the entry bins zeroed when a wave
 // overflowed), the waves' entry counts (-1: the block overflowed) ->
 // ecount[b * waves + w].
-template <bool kOff32, bool kMaj, bool kMem, int kB = kNrBatch>
+template <bool kOff32, bool kMaj, int kB = kNrBatch>
 __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restrict__ assign, int P, int S, int N,
                                                              int nbk, int nchunk, int nblk, size_t ecap,
-                                                             int *__restrict__ pkey, int *__restrict__ boff,
-                                                             int2 *__restrict__ ent, int *__restrict__ ecount,
-                                                             const int *__restrict__ pod_cpu,
-                                                             const long long *__restrict__ pod_mem,
-                                                             int4 *__restrict__ rec, size_t rs, int rcap,
-                                                             unsigned *__restrict__ err) {
-    // LDS: [nbk] key buckets, then [nchunk][nbk] entry bins (the counters, then
-    // the cursors); the pods' keys, cpu and (kMem) mem [kNrPods]
-    extern __shared__ __align__(16) int lh[];
-    __shared__ int over, wsum[kNrThreads / 64], wcnt[kNrThreads / 64];
+                                                             int *__restrict__ pkey, int *__restrict__ bh,
+                                                             int2 *__restrict__ ent, int *__restrict__ ecount) {
+    extern __shared__ int lh[];  // [nbk] key buckets, then [nchunk][nbk] entry bins
+    __shared__ int over;
     const int b = nr_block(nblk);
     if (b >= nblk) return;
     const int t = (int)threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);  // (uniform)
     const int nh = nbk * (1 + nchunk);
-    int *lk = lh + ((nh + 3) & ~3), *lc = lk + kNrPods;
-    long long *lm = reinterpret_cast<long long *>(lc + kNrPods);
     for (int j = t; j < nh; j += kNrThreads) lh[j] = 0;
     if (t == 0) over = 0;
     __syncthreads();
@@ -561,7 +553,6 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
             kvb = kn;
             if (lane < nb) {
                 pkey[pb + lane] = kn;
-                lk[pb - p0 + lane] = kn;
                 if (kn < N) atomicAdd(&lh[kn >> kNrBucketBits], 1);
             }
         }
@@ -631,70 +622,135 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
         }
     }
     if (wover && lane == 0) over = 1;
-    if (lane == 0) wcnt[wv] = (int)wpos;
     __syncthreads();
-    const bool bo = over != 0;  // (the block lists none: its bins stay empty, nr_spill adds its cells)
+    const bool bo = over != 0;
+    for (int j = t; j < nh; j += kNrThreads) bh[(size_t)j * nblk + b] = (bo && j >= nbk) ? 0 : lh[j];
     if (RSK_NR_ABL) asm volatile("" ::"v"(abl_acc));  // (keeps the ablated rows' loads)
     if (lane == 0) ecount[b * kW + wv] = bo ? -1 : (int)wpos;
-    // the block's record region: its counters' exclusive scan (thread t: a run
-    // of `per` counters, then a wave scan and the waves' sums), each counter's
-    // offset -> boff[j * nblk + b] (row nh: the region's total) and its cursor
-    const int per = (nh + kNrThreads - 1) / kNrThreads, j0 = min(nh, t * per), j1 = min(nh, j0 + per);
+}
+
+// inclusive scan over a wave (DPP row shifts and broadcasts: no LDS round trips)
+__device__ __forceinline__ int nr_wave_scan(int v, int lane) {
+    (void)lane;
+    return dpp_scan_incl(v);
+}
+
+// launch 2: one wave per counter j: bh[j][0..nblk) -> its exclusive prefix,
+// tot[j] = the sum (kPer > 0: each lane's kPer blocks in registers, one
+// memory trip; 0: nblk > 64 * 8, loops)
+template <int kPer>
+__global__ __launch_bounds__(256) void nr_colscan_kernel(int *__restrict__ bh, int nh, int nblk,
+                                                         int *__restrict__ tot) {
+    const int lane = (int)threadIdx.x & 63, j = (int)blockIdx.x * 4 + ((int)threadIdx.x >> 6);
+    if (j >= nh) return;
+    int *__restrict__ row = bh + (size_t)j * nblk;
+    const int per = kPer ? kPer : (nblk + 63) >> 6, b0 = lane * per, b1 = min(nblk, b0 + per);
     int sum = 0;
-    for (int j = j0; j < j1; ++j) sum += (bo && j >= nbk) ? 0 : lh[j];
-    const int incl = dpp_scan_incl(sum);
-    if (lane == 63) wsum[wv] = incl;
-    __syncthreads();
-    int run = incl - sum, all = 0;
+    if (kPer) {
+        int x[kPer > 0 ? kPer : 1];
 #pragma unroll
-    for (int w = 0; w < kW; ++w) {
-        run += w < wv ? wsum[w] : 0;
-        all += wsum[w];
+        for (int i = 0; i < kPer; ++i) x[i] = row[min(b0 + i, nblk - 1)];
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) sum += b0 + i < b1 ? x[i] : 0;
+        const int incl = nr_wave_scan(sum, lane);
+        int run = incl - sum;
+#pragma unroll
+        for (int i = 0; i < kPer; ++i)
+            if (b0 + i < b1) {
+                row[b0 + i] = run;
+                run += x[i];
+            }
+        if (lane == 63) tot[j] = incl;
+        return;
     }
-    for (int j = j0; j < j1; ++j) {
-        const int x = (bo && j >= nbk) ? 0 : lh[j];
-        lh[j] = run;
-        boff[(size_t)j * nblk + b] = run;
+    for (int i = b0; i < b1; ++i) sum += row[i];
+    const int incl = nr_wave_scan(sum, lane);
+    int run = incl - sum;
+    for (int i = b0; i < b1; ++i) {
+        const int x = row[i];
+        row[i] = run;
         run += x;
     }
-    if (t == 0) boff[(size_t)nh * nblk + b] = all;
-    // the pods: (node & 31, cpu, mem) records into their key bucket's slice
+    if (lane == 63) tot[j] = incl;
+}
+
+// launch 3: LDS = the block's cursors [nh], the pods' cpu [kNrPods], keys
+// [kNrPods] and (kMem) mem [kNrPods]; the counters' bases (exclusive scan of tot) are computed by
+// every block, and written out by block 0 (base[nh] = the total)
+template <bool kMem>
+__global__ __launch_bounds__(kNrThreads) void nr_place_kernel(const int *__restrict__ pkey, int P, int N, int nbk,
+                                                              int nchunk, int nblk, const int *__restrict__ bh,
+                                                              const int *__restrict__ tot, int *__restrict__ base,
+                                                              const int *__restrict__ pod_cpu,
+                                                              const long long *__restrict__ pod_mem,
+                                                              const int2 *__restrict__ ent, size_t ecap,
+                                                              const int *__restrict__ ecount, int4 *__restrict__ rec,
+                                                              int nrec, unsigned *__restrict__ err) {
+    extern __shared__ __align__(16) int cur[];
+    __shared__ int wsum[kNrThreads / 64];
+    const int b = nr_block(nblk);
+    if (b >= nblk) return;
+    const int t = (int)threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);  // (uniform)
+    const int nh = nbk * (1 + nchunk);
+    int *lc = cur + nh, *lk = lc + kNrPods;
+    long long *lm = reinterpret_cast<long long *>(lk + kNrPods + (nh & 1));  // 8-B aligned
+    const int p0 = b * kNrPods, p1 = min(P, p0 + kNrPods);
     constexpr int kU = kNrPods / kNrThreads;
-    int c[kU];
+    int k[kU], c[kU];
     long long m[kU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
+    for (int u = 0; u < kU; ++u) {  // the pods' fields in flight while the bases are scanned
         const int p = min(p0 + u * kNrThreads + t, P - 1);
+        k[u] = pkey[p];
         c[u] = pod_cpu[p];
         m[u] = kMem ? pod_mem[p] : 0;
     }
-    __syncthreads();  // (the cursors)
-    int4 *__restrict__ R = rec + (size_t)b * rs;
+    // bases: thread t scans tot[t * per, ...) after the block's exclusive scan of the threads' sums
+    const int per = (nh + kNrThreads - 1) / kNrThreads, j0 = min(nh, t * per), j1 = min(nh, j0 + per);
+    int s = 0;
+    for (int j = j0; j < j1; ++j) s += tot[j];
+    const int incl = nr_wave_scan(s, lane);
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    int run = incl - s;
+    for (int w = 0; w < wv; ++w) run += wsum[w];
+    for (int j = j0; j < j1; ++j) {
+        const int x = tot[j];
+        cur[j] = run + bh[(size_t)j * nblk + b];
+        if (b == 0) base[j] = run;
+        run += x;
+    }
+    if (b == 0 && t == kNrThreads - 1) base[nh] = run;
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-        const int i = u * kNrThreads + t, k = p0 + i < P ? lk[i] : N;
-        lc[i] = c[u];
-        if (kMem) lm[i] = m[u];
-        if (k < N) {
-            const int pos = atomicAdd(&lh[k >> kNrBucketBits], 1);
-            if ((unsigned)pos < (unsigned)rcap)  // (offsets from this block's counts; guarded all the same)
-                R[pos] = make_int4(k & (kNrBucketNodes - 1), c[u], (int)(unsigned)(unsigned long long)m[u],
-                                   (int)(m[u] >> 32));
+        lc[u * kNrThreads + t] = c[u];
+        lk[u * kNrThreads + t] = k[u];
+        if (kMem) lm[u * kNrThreads + t] = m[u];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        const int p = p0 + u * kNrThreads + t;
+        if (p < p1 && k[u] < N) {
+            const int pos = atomicAdd(&cur[k[u] >> kNrBucketBits], 1);
+            if ((unsigned)pos < (unsigned)nrec)  // the offsets come from nr_scan's counts: guarded (dev_err)
+                rec[pos] = make_int4(k[u] & (kNrBucketNodes - 1), c[u], (int)(unsigned)(unsigned long long)m[u],
+                                     (int)(m[u] >> 32));
             else
                 *err = kErrNrPlace;
         }
     }
-    if (bo) return;
-    __syncthreads();  // (lc / lm)
-    // the entries of the block's wave regions, concatenated: a + record at the
-    // cell's node and a - record at the pod's key node, in the cell's bins
+    // the entries of the block's 8 wave regions, concatenated (-1: overflowed,
+    // nr_spill adds the block's deviations)
+    constexpr int kW = kNrThreads / 64;
     int wc[kW], ne = 0;
 #pragma unroll
     for (int w = 0; w < kW; ++w) {
-        wc[w] = wcnt[w];
+        wc[w] = max(0, ecount[b * kW + w]);
         ne += wc[w];
     }
-    const int2 *__restrict__ Eb = ent + (size_t)b * ecap;
+    const size_t wcap = ecap / kW;
+    const int2 *__restrict__ E = ent + (size_t)b * ecap;
     constexpr int kV = 4;
     for (int i0 = 0; i0 < ne; i0 += kNrThreads * kV) {
         int2 e[kV];
@@ -707,53 +763,46 @@ __global__ __launch_bounds__(kNrThreads) void nr_scan_kernel(const int *__restri
                     i -= wc[x];
                     w = x + 1;
                 }
-            e[v] = Eb[(size_t)w * wcap + i];
+            e[v] = E[(size_t)w * wcap + i];
         }
 #pragma unroll
         for (int v = 0; v < kV; ++v) {
             if (i0 + v * kNrThreads + t < ne) {
                 const int node = e[v].x & kNrNoNode, lp = (int)((unsigned)e[v].x >> 20), sc = e[v].y;
-                const int key = lk[lp], sl = (sc & 63) << 6, cbin = nbk + __umul24(sc >> 6, nbk);
+                const int key = lk[lp], lane = (sc & 63) << 6;
                 const long long mm = kMem ? lm[lp] : 0;
                 const int mlo = (int)(unsigned)(unsigned long long)mm, mhi = (int)(mm >> 32);
                 if (node < N) {  // + the pod at its node
-                    const int pos = atomicAdd(&lh[cbin + (node >> kNrBucketBits)], 1);
-                    if ((unsigned)pos < (unsigned)rcap)
-                        R[pos] = make_int4((node & (kNrBucketNodes - 1)) | sl, lc[lp], mlo, mhi);
-                    else
-                        *err = kErrNrPlace;
+                    const int pos = atomicAdd(&cur[nbk + __umul24(sc >> 6, nbk) + (node >> kNrBucketBits)], 1);
+                    if ((unsigned)pos < (unsigned)nrec) rec[pos] = make_int4((node & (kNrBucketNodes - 1)) | lane, lc[lp], mlo, mhi);
+                    else *err = kErrNrPlace;
                 }
                 if (key < N) {  // - the pod at its key node
-                    const int pos = atomicAdd(&lh[cbin + (key >> kNrBucketBits)], 1);
-                    if ((unsigned)pos < (unsigned)rcap)
-                        R[pos] = make_int4((key & (kNrBucketNodes - 1)) | 32 | sl, lc[lp], mlo, mhi);
-                    else
-                        *err = kErrNrPlace;
+                    const int pos = atomicAdd(&cur[nbk + __umul24(sc >> 6, nbk) + (key >> kNrBucketBits)], 1);
+                    if ((unsigned)pos < (unsigned)nrec) rec[pos] = make_int4((key & (kNrBucketNodes - 1)) | 32 | lane, lc[lp], mlo, mhi);
+                    else *err = kErrNrPlace;
                 }
             }
         }
     }
 }
 
-// launch 2: a workgroup per bin (chunk c, bucket b).  A counter's records
-// lie in every block's region: block bb's slice of counter j is
-// [boff[j][bb], boff[j + 1][bb]) of region bb.  The workgroup scans the
-// slices' lengths (256 blocks a round) and walks them as one range, each
-// record's slice found by a binary search of the scan in LDS.
+// launch 4: a workgroup per bin (chunk c, bucket b)
 constexpr int kNrSumThreads = 256;
 template <bool kMem>
-__global__ __launch_bounds__(kNrSumThreads) void nr_sum_kernel(const int *__restrict__ boff, int nbk, int nblk,
-                                                               const int4 *__restrict__ rec, size_t rs, int N, int S,
+__global__ __launch_bounds__(kNrSumThreads) void nr_sum_kernel(const int *__restrict__ base, int nbk, int nchunk,
+                                                               const int4 *__restrict__ rec, int N, int S,
                                                                int *__restrict__ cnt,
                                                                unsigned long long *__restrict__ cpu,
                                                                unsigned long long *__restrict__ mem) {
-    constexpr int kE = kNrBucketNodes * 64, kW = kNrSumThreads / 64;
+    constexpr int kE = kNrBucketNodes * 64;
     __shared__ int bc[kNrBucketNodes];
     __shared__ unsigned long long bcpu[kNrBucketNodes], bmem[kNrBucketNodes];
     __shared__ int dc[kE];
     __shared__ unsigned long long dcpu[kE], dmem[kMem ? kE : 1];
-    __shared__ int spre[kNrSumThreads], sst[kNrSumThreads], wsum[kW];
-    const int t = (int)threadIdx.x, lane = t & 63, w = t >> 6, g = (int)blockIdx.x, c = g / nbk, b = g - c * nbk;
+    const int t = (int)threadIdx.x, g = (int)blockIdx.x, c = g / nbk, b = g - c * nbk;
+    const int lo = base[b], hi = base[b + 1];
+    const int j = nbk + g, elo = base[j], ehi = base[j + 1];  // bins [chunk][bucket]
     if (t < kNrBucketNodes) {
         bc[t] = 0;
         bcpu[t] = 0ull;
@@ -764,62 +813,41 @@ __global__ __launch_bounds__(kNrSumThreads) void nr_sum_kernel(const int *__rest
         dcpu[e] = 0ull;
         if (kMem) dmem[e] = 0ull;
     }
-    auto walk = [&](int j, auto &&add) {
-        for (int bb0 = 0; bb0 < nblk; bb0 += kNrSumThreads) {
-            const int bb = bb0 + t;
-            int st = 0, n = 0;
-            if (bb < nblk) {
-                st = boff[(size_t)j * nblk + bb];
-                n = boff[(size_t)(j + 1) * nblk + bb] - st;
+    __syncthreads();
+    constexpr int kV = 4;
+    for (int i0 = lo; i0 < hi; i0 += kNrSumThreads * kV) {  // the bucket's pods: base
+        int4 r[kV];
+#pragma unroll
+        for (int v = 0; v < kV; ++v) r[v] = rec[min(i0 + v * kNrSumThreads + t, hi - 1)];
+#pragma unroll
+        for (int v = 0; v < kV; ++v) {
+            if (i0 + v * kNrSumThreads + t < hi) {
+                const int n = r[v].x;
+                atomicAdd(&bc[n], 1);
+                atomicAdd(&bcpu[n], (unsigned long long)(long long)r[v].y);
+                if (kMem) atomicAdd(&bmem[n], ((unsigned long long)(unsigned)r[v].w << 32) | (unsigned)r[v].z);
             }
-            const int incl = dpp_scan_incl(n);
-            __syncthreads();  // (the previous round's readers of spre / sst; the zeroed sums)
-            if (lane == 63) wsum[w] = incl;
-            __syncthreads();
-            int ex = incl - n, total = 0;
+        }
+    }
+    for (int i0 = elo; i0 < ehi; i0 += kNrSumThreads * kV) {  // the bin's deviation entries
+        int4 r[kV];
 #pragma unroll
-            for (int x = 0; x < kW; ++x) {
-                ex += x < w ? wsum[x] : 0;
-                total += wsum[x];
-            }
-            spre[t] = ex;
-            sst[t] = st;
-            __syncthreads();
-            constexpr int kV = 4;
-            for (int i0 = 0; i0 < total; i0 += kNrSumThreads * kV) {
-                int4 r[kV];
+        for (int v = 0; v < kV; ++v) r[v] = rec[min(i0 + v * kNrSumThreads + t, ehi - 1)];
 #pragma unroll
-                for (int v = 0; v < kV; ++v) {
-                    const int i = min(i0 + v * kNrSumThreads + t, total - 1);
-                    int q = 0;  // the last slice starting at or before i (empty slices share starts)
-#pragma unroll
-                    for (int step = kNrSumThreads / 2; step > 0; step >>= 1)
-                        if (spre[q + step] <= i) q += step;
-                    r[v] = rec[(size_t)(bb0 + q) * rs + (size_t)(sst[q] + (i - spre[q]))];
+        for (int v = 0; v < kV; ++v) {
+            if (i0 + v * kNrSumThreads + t < ehi) {
+                const int x = r[v].x, e = (x & (kNrBucketNodes - 1)) * 64 + ((x >> 6) & 63);
+                const bool neg = (x >> 5) & 1;
+                const long long cv = r[v].y;
+                atomicAdd(&dc[e], neg ? -1 : 1);
+                atomicAdd(&dcpu[e], (unsigned long long)(neg ? -cv : cv));
+                if (kMem) {
+                    const unsigned long long mv = ((unsigned long long)(unsigned)r[v].w << 32) | (unsigned)r[v].z;
+                    atomicAdd(&dmem[e], neg ? 0ull - mv : mv);
                 }
-#pragma unroll
-                for (int v = 0; v < kV; ++v)
-                    if (i0 + v * kNrSumThreads + t < total) add(r[v]);
             }
         }
-    };
-    walk(b, [&](const int4 &r) {  // the bucket's pods: base
-        const int n = r.x;
-        atomicAdd(&bc[n], 1);
-        atomicAdd(&bcpu[n], (unsigned long long)(long long)r.y);
-        if (kMem) atomicAdd(&bmem[n], ((unsigned long long)(unsigned)r.w << 32) | (unsigned)r.z);
-    });
-    walk(nbk + g, [&](const int4 &r) {  // the bin's deviation records (bins [chunk][bucket])
-        const int x = r.x, e = (x & (kNrBucketNodes - 1)) * 64 + ((x >> 6) & 63);
-        const bool neg = (x >> 5) & 1;
-        const long long cv = r.y;
-        atomicAdd(&dc[e], neg ? -1 : 1);
-        atomicAdd(&dcpu[e], (unsigned long long)(neg ? -cv : cv));
-        if (kMem) {
-            const unsigned long long mv = ((unsigned long long)(unsigned)r.w << 32) | (unsigned)r.z;
-            atomicAdd(&dmem[e], neg ? 0ull - mv : mv);
-        }
-    });
+    }
     __syncthreads();
     for (int e = t; e < kE; e += kNrSumThreads) {
         const int l = e >> 6, n = b * kNrBucketNodes + l, s = c * 64 + (e & 63);
@@ -831,7 +859,7 @@ __global__ __launch_bounds__(kNrSumThreads) void nr_sum_kernel(const int *__rest
     }
 }
 
-// launch 3: the deviation cells of the blocks that overflowed, by atomics on
+// launch 5: the deviation cells of the blocks that overflowed, by atomics on
 // the stored sums (none on the bench batches: every block exits at once)
 template <bool kMem>
 __global__ __launch_bounds__(kNrThreads) void nr_spill_kernel(const int *__restrict__ assign, int P, int S, int N,
@@ -1487,44 +1515,47 @@ static int node_reduce_impl(rsk_ctx *ctx, const int32_t *assign, int32_t P, int3
     // the deviation form while its counters and records have 32-bit offsets
     // (larger batches take the atomic form below, which handles any size)
     const int nblk = (int)ceil_div(P, kNrPods);
-    const int64_t ncnt = (nh + 1) * nblk;
-    const size_t ecap = ((size_t)kNrPods * S / kNrEntDiv + 64) & ~(size_t)63;  // a block's entry region (its waves')
-    const size_t rs = (size_t)kNrPods + 2 * ecap;  // a block's record region: its pods + 2 per entry
+    const int64_t ncnt = nh * nblk;
+    const size_t ecap = ((size_t)kNrPods * S / kNrEntDiv + 64) & ~(size_t)63;  // a block's entry region (8 waves')
+    const int64_t nrec = (int64_t)P + 2 * (int64_t)nblk * (int64_t)ecap;  // pod records + 2 per entry
     unsigned *derr = dev_err(ctx);
-    if (PS && S >= 32 && S <= kNrMaxS && nh <= kNrMaxCounters && ncnt < INT32_MAX / 2 && rs < INT32_MAX && derr) {
+    if (PS && S >= 32 && S <= kNrMaxS && nh <= kNrMaxCounters && ncnt < INT32_MAX / 2 && nrec < INT32_MAX && derr) {
         const size_t kb = ((size_t)P * 4 + 15) & ~(size_t)15;
-        RSK_TRY(ctx->work[0].reserve(kb + (size_t)nblk * rs * 16));  // keys, then the block regions
-        RSK_TRY(ctx->work[1].reserve(((size_t)ncnt + (size_t)nblk * (kNrThreads / 64)) * 4));
+        RSK_TRY(ctx->work[0].reserve(kb + (size_t)nrec * 16));  // keys, then the records
+        RSK_TRY(ctx->work[1].reserve(((size_t)ncnt + 2 * (size_t)nh + 1 + (size_t)nblk * (kNrThreads / 64)) * 4));
         RSK_TRY(ctx->work[2].reserve((size_t)nblk * ecap * 8));
         int *pkey = ctx->work[0].as<int>();
         int4 *rec = reinterpret_cast<int4 *>(ctx->work[0].as<char>() + kb);
-        int *boff = ctx->work[1].as<int>(), *ecount = boff + ncnt;
+        int *bh = ctx->work[1].as<int>(), *tot = bh + ncnt, *base = tot + nh, *ecount = base + nh + 1;
         int2 *ent = ctx->work[2].as<int2>();
         auto *ucs = reinterpret_cast<unsigned long long *>(d_cs), *ums = reinterpret_cast<unsigned long long *>(d_ms);
         const auto *lmem = reinterpret_cast<const long long *>(d_mem);
         ScopedTimer tm(ctx, "node_reduce");
-        const bool o32 = PS * 4 < ((size_t)1 << 32), maj = S >= 43, km = d_ms != nullptr;
-        using ScanFn = decltype(&nr_scan_kernel<true, true, true>);
-        const ScanFn scans[8] = {&nr_scan_kernel<false, false, false>, &nr_scan_kernel<false, false, true>,
-                                 &nr_scan_kernel<false, true, false>,  &nr_scan_kernel<false, true, true>,
-                                 &nr_scan_kernel<true, false, false>,  &nr_scan_kernel<true, false, true>,
-                                 &nr_scan_kernel<true, true, false>,   &nr_scan_kernel<true, true, true>};
-        auto *sc = scans[(o32 ? 4 : 0) + (maj ? 2 : 0) + (km ? 1 : 0)];
+        const bool o32 = PS * 4 < ((size_t)1 << 32), maj = S >= 43;
+        auto *sc = o32 ? (maj ? &nr_scan_kernel<true, true> : &nr_scan_kernel<true, false>)
+                       : (maj ? &nr_scan_kernel<false, true> : &nr_scan_kernel<false, false>);
         const unsigned g8 = (unsigned)(8 * ceil_div(nblk, 8));  // (nr_block: XCD runs of consecutive blocks)
-        // LDS: the counters (16-B aligned), the pods' keys and cpu, and mem; above
-        // 64 KiB the launch needs the attribute
-        const size_t scan_lds = (size_t)((nh + 3) & ~3) * 4 + (size_t)kNrPods * (km ? 16 : 8);
-        RSK_CHECK(scan_lds + 128 <= 160 * 1024, "node_reduce: %zu B of LDS", scan_lds);
-        if (scan_lds + 128 > 64 * 1024)
+        // dynamic LDS above 64 KiB needs the attribute (nh = 16384 counters: 64 KiB + the static word)
+        const size_t scan_lds = (size_t)nh * 4, pl = (size_t)nh * 4 + 8 + (size_t)kNrPods * (d_ms ? 16 : 8);
+        RSK_CHECK(scan_lds + 64 <= 160 * 1024 && pl + 64 <= 160 * 1024, "node_reduce: %zu / %zu B of LDS", scan_lds, pl);
+        auto *pk = d_ms ? &nr_place_kernel<true> : &nr_place_kernel<false>;
+        if (scan_lds + 64 > 64 * 1024)
             RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(sc), hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)scan_lds));
-        const int rcap = (int)(rec_limit >= 0 ? std::min<int64_t>((int64_t)rs, rec_limit) : (int64_t)rs);
-        sc<<<g8, kNrThreads, scan_lds, ctx->stream>>>(d_assign, P, S, N, nbk, nchunk, nblk, ecap, pkey, boff, ent,
-                                                      ecount, d_cpu, lmem, rec, rs, rcap, derr);
-        auto *sk = km ? &nr_sum_kernel<true> : &nr_sum_kernel<false>;
-        sk<<<(unsigned)(nbk * nchunk), kNrSumThreads, 0, ctx->stream>>>(boff, nbk, nblk, rec, rs, N, S, d_cnt, ucs,
-                                                                        ums);
-        auto *xk = km ? &nr_spill_kernel<true> : &nr_spill_kernel<false>;
+        if (pl + 64 > 64 * 1024)
+            RSK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(pk), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)pl));
+        sc<<<g8, kNrThreads, scan_lds, ctx->stream>>>(d_assign, P, S, N, nbk, nchunk, nblk, ecap, pkey, bh, ent,
+                                                      ecount);
+        auto *cs = nblk <= 64 * 8 ? &nr_colscan_kernel<8>
+                   : nblk <= 64 * 16 ? &nr_colscan_kernel<16> : &nr_colscan_kernel<0>;
+        cs<<<(unsigned)ceil_div(nh, 4), 256, 0, ctx->stream>>>(bh, (int)nh, nblk, tot);
+        pk<<<g8, kNrThreads, pl, ctx->stream>>>(pkey, P, N, nbk, nchunk, nblk, bh, tot, base, d_cpu, lmem, ent, ecap,
+                                                ecount, rec, (int)(rec_limit >= 0 ? std::min(nrec, rec_limit) : nrec),
+                                                derr);
+        auto *sk = d_ms ? &nr_sum_kernel<true> : &nr_sum_kernel<false>;
+        sk<<<(unsigned)(nbk * nchunk), kNrSumThreads, 0, ctx->stream>>>(base, nbk, nchunk, rec, N, S, d_cnt, ucs, ums);
+        auto *xk = d_ms ? &nr_spill_kernel<true> : &nr_spill_kernel<false>;
         xk<<<g8, kNrThreads, 0, ctx->stream>>>(d_assign, P, S, N, nblk, pkey, ecount, d_cpu, lmem, d_cnt, ucs, ums);
         RSK_HIP(hipGetLastError());
     } else {
