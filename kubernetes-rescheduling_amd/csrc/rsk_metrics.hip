@@ -1670,17 +1670,24 @@ int rsk_load_std(rsk_ctx *ctx, const int32_t *use_cpu, const int32_t *cap_cpu, i
     RSK_TRY(stage_in(ctx, 0, use_cpu, NS * 4, dev, reinterpret_cast<const void **>(&d_use)));
     RSK_TRY(stage_in(ctx, 1, cap_cpu, (size_t)N * 4, dev, reinterpret_cast<const void **>(&d_cap)));
     RSK_TRY(stage_out(ctx, 2, out_std, (size_t)S * 8, dev, reinterpret_cast<void **>(&d_out)));
-    // nodes per thread: at least 16, and at most 2,048 chunks for the merge
-    // workgroups to walk (50k nodes x 64 scenarios: 25 nodes, 2,000 chunks)
-    constexpr int max_chunks = 2048;
-    const int npb = std::max({chunk_for(N, S), 16, (int)ceil_div(N, max_chunks)});
+    // nodes per thread: at least RSK_STD_MIN (two batches of loads), and at
+    // most 2,048 partials for the merge workgroups to walk (a folding
+    // workgroup writes one partial per 256 / S chunks).  50k nodes x 64
+    // scenarios: 16 nodes, 3,125 chunks, 782 partials — 14.3 us for the two
+    // launches against 17.5 at 8 or 4 nodes (more partials to merge, no
+    // faster partial pass) and 15.6 at 25 nodes / 500 partials (r06w, r06k)
+#ifndef RSK_STD_MIN
+#define RSK_STD_MIN 16
+#endif
+    const int fold = 256 % S == 0 && S < 256;  // a workgroup holds 256 / S whole chunks
+    const int64_t max_chunks = 2048 * (fold ? 256 / S : 1);
+    const int npb = std::max({chunk_for(N, S), RSK_STD_MIN, (int)ceil_div(N, max_chunks)});
     const int nch = (int)ceil_div(N, npb);
     RSK_TRY(ctx->work[0].reserve((size_t)nch * S * 8));
     RSK_TRY(ctx->work[1].reserve((size_t)nch * S * 8));
     RSK_TRY(ctx->work[2].reserve((size_t)nch * S * 4));
     const unsigned total = (unsigned)((int64_t)nch * S);
     const unsigned grid = (unsigned)ceil_div(total, 256);
-    const int fold = 256 % S == 0 && S < 256;  // a workgroup holds 256 / S whole chunks
     {
         ScopedTimer tm(ctx, "load_std");
         std_partial_kernel<<<grid, 256, 0, ctx->stream>>>(d_use, d_cap, N, S, npb, total, fold,

@@ -216,9 +216,9 @@ def test_rounds_hub_above_4096_neighbours(ctx, P, N, deg):
 
 def test_kernel3_config4_1m50k_s64(ctx):
     """North-star kernel 3 at config 4's shape (1M pods x 50k nodes x 64
-    scenarios): rsk_load_std (2,000 node chunks of 25 nodes per scenario,
-    folded four to a workgroup into 500 partials, two per merge lane before
-    the butterfly) with 700 nodes of cap <= 0
+    scenarios): rsk_load_std (3,125 node chunks of 16 nodes per scenario,
+    folded four to a workgroup into 782 partials, up to four per merge lane
+    before the butterfly) with 700 nodes of cap <= 0
     mixed in, and a near-constant-pct batch that stresses the shifted sums;
     rsk_cut_cost over all 1M rows (with and without `missing`) and
     rsk_node_reduce over all 64 M cells, against the oracle
