@@ -817,10 +817,10 @@ def test_node_reduce_segmented_vs_oracle(ctx, P, N, S, p_flip):
 def test_node_reduce_deviation_form_edges(ctx, P, N, S):
     """The deviation form of kernel 3's node sums (out = base[key node] +
     per-scenario deviations, podmonitor.py:104-121) against the oracle where
-    its bookkeeping branches: pods 4096-8191 — two of the scan's 2048-pod
-    blocks — with 40 % of their cells redrawn (their entry regions overflow:
-    their deviations go through the spill launch) beside blocks that list
-    theirs; pods whose scenario-0 node is
+    its bookkeeping branches: pods 4096-8191 — block 1 of the scan's
+    4,096-pod blocks — with 40 % of their cells redrawn (its entry region
+    overflows: its deviations go through the spill launch) beside blocks that
+    list theirs; pods whose scenario-0 node is
     redrawn (the key is the majority of scenarios 0 / 21 / 42), pods with no
     key (unscheduled in two of the three), pods unscheduled in scenario 0 only,
     assignments equal to N; 64 chunks per pod (S = 4096) and a partial chunk
@@ -831,7 +831,7 @@ def test_node_reduce_deviation_form_edges(ctx, P, N, S):
     base = rng.integers(0, N, P)
     a = np.repeat(base[:, None], S, axis=1).astype(np.int32)
     flip = rng.random((P, S)) < 0.01
-    flip[4096:8192] = rng.random((4096, S)) < 0.4         # blocks 2 and 3 (2048 pods each) overflow
+    flip[4096:8192] = rng.random((4096, S)) < 0.4         # block 1 (4,096 pods) overflows
     a[flip] = rng.integers(-2, N + 2, int(flip.sum()))
     q = rng.integers(0, P, 300)
     a[q, 0] = rng.integers(0, N, 300)                      # scenario 0 redrawn: key from 21 / 42
