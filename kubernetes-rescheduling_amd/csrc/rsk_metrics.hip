@@ -705,20 +705,33 @@ __global__ __launch_bounds__(kNrThreads) void nr_place_kernel(const int *__restr
         c[u] = pod_cpu[p];
         m[u] = kMem ? pod_mem[p] : 0;
     }
-    // bases: thread t scans tot[t * per, ...) after the block's exclusive scan of the threads' sums
+    // bases: thread t scans tot[t * per, ...) after the block's exclusive scan
+    // of the threads' sums; its totals and column prefixes are loaded at once
+    // into registers (predicated; a loop of loads waited on each in turn)
+    constexpr int kPer = (kNrMaxCounters + kNrThreads - 1) / kNrThreads;
     const int per = (nh + kNrThreads - 1) / kNrThreads, j0 = min(nh, t * per), j1 = min(nh, j0 + per);
+    int tv[kPer], hv[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+        const bool in = j0 + i < j1;
+        tv[i] = in ? tot[j0 + i] : 0;
+        hv[i] = in ? bh[(size_t)(j0 + i) * nblk + b] : 0;
+    }
     int s = 0;
-    for (int j = j0; j < j1; ++j) s += tot[j];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) s += tv[i];
     const int incl = nr_wave_scan(s, lane);
     if (lane == 63) wsum[wv] = incl;
     __syncthreads();
     int run = incl - s;
     for (int w = 0; w < wv; ++w) run += wsum[w];
-    for (int j = j0; j < j1; ++j) {
-        const int x = tot[j];
-        cur[j] = run + bh[(size_t)j * nblk + b];
-        if (b == 0) base[j] = run;
-        run += x;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+        if (j0 + i < j1) {
+            cur[j0 + i] = run + hv[i];
+            if (b == 0) base[j0 + i] = run;
+        }
+        run += tv[i];
     }
     if (b == 0 && t == kNrThreads - 1) base[nh] = run;
 #pragma unroll
