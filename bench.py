@@ -737,7 +737,7 @@ def bench_car(args, cfg, world, rank, local, dev):  # noqa: C901
                                           and k3_leg["parity_load_std_max_rel"] <= 1e-9)
         k3_leg["parity_sample"] = f"all {S} scenarios of the batch: node_reduce / cut_cost exact, load_std 1e-9 rel"
         k3_leg["note"] = ("algorithmic bytes: node_reduce reads assign + pod cpu/mem and writes the N*S count/cpu/mem"
-                          " words; load_std reads use and cap (its 20 B per (node chunk, scenario) partials not counted); cut_cost reads CSR + assign + one gather per edge")
+                          " words; load_std reads use and cap (its 20-B partials, one per (workgroup, scenario) after the in-LDS fold, not counted); cut_cost reads CSR + assign + one gather per edge")
 
     alg = {k: alg_bytes(k, P, N, S, info, B) for k in kernels}
     roof = None
