@@ -1253,7 +1253,10 @@ int launch_fused16(hipStream_t stream, const Tile16Args &a, const SideArgs &sa, 
     const int64_t cells = (int64_t)da.Q * da.S;
     RSK_CHECK(cells == 0 || (!score && da.H > 0 && (size_t)(da.H + 4) * 4 <= lds && cells < INT32_MAX),
               "direct cells in the fused grid: targets only, a table within the tile's LDS");
-    constexpr int spread = 2;  // side rows over the first half of the tile rows (1 / 4 of them: slower)
+#ifndef RSK_FUSE_SPREAD
+#define RSK_FUSE_SPREAD 2
+#endif
+    constexpr int spread = RSK_FUSE_SPREAD;  // side rows over the first half of the tile rows (1 / 4 of them: slower)
     FuseMap f;
     f.direct_blocks = (int)(8 * ceil_div(cells, 8));  // (XCD alignment of the blocks after them)
     f.big_blocks = (int)(8 * ceil_div((int64_t)ba.n_rows * ba.nchunk, 8));
