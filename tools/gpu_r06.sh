@@ -28,7 +28,6 @@ for s in "${@:-test smoke bench}"; do
       b1m) step bench_1m50k 600 python -u bench.py --config 1m50k --no-cpu-baseline ;;
       brounds) step bench_rounds 300 python -u bench.py --config rounds --no-cpu-baseline ;;
       ab:*) kv=${w#ab:}; step "ab_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u bench.py --no-cpu-baseline ;;
-      ab1m:*) kv=${w#ab1m:}; step "ab1m_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u bench.py --config 1m50k --no-cpu-baseline --row-rounds 0 ;;
       abr:*) kv=${w#abr:}; step "abr_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_knobs.so ${kv//,/ } python -u bench.py --config rounds --no-cpu-baseline ;;
       sb:*) kv=${w#sb:}; step "sb_${kv//[=,]/_}" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_abl.so ${kv//,/ } python -u tools/sidebench.py ;;
       hp:*) step "hostprobe_${w#hp:}" 300 python -u tools/hostprobe.py "${w#hp:}" ;;
@@ -41,6 +40,10 @@ for s in "${@:-test smoke bench}"; do
                step "pmc_${tag}_$c" 240 env $envs rocprofv3 --pmc $c -d "$out/pmc_$tag/$c" -o p -f csv -- python3 tools/tilebench.py --config $cfg --steps 10
              done
              python3 tools/pmc_quick.py "$out/pmc_$tag" | tee "$out/pmc_${tag}_summary.txt" ;;
+      ab1m:*) lib=${w#ab1m:}; for rep in 1 2; do
+               step "ab1m_base_$rep" 300 python -u bench.py --config 1m50k --no-cpu-baseline
+               step "ab1m_${lib}_$rep" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_$lib.so python -u bench.py --config 1m50k --no-cpu-baseline
+             done ;;
       abh:*) lib=${w#abh:}; for rep in 1 2; do
                step "abh_base_$rep" 300 python -u bench.py --config headline --no-cpu-baseline
                step "abh_${lib}_$rep" 300 env RSK_LIB=kubernetes-rescheduling_amd/rsk/librsk_$lib.so python -u bench.py --config headline --no-cpu-baseline
